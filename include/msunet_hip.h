@@ -1,0 +1,132 @@
+/* msunet_hip.h -- C ABI of libmsunet_hip.so, the gfx950 (MI355X) kernels of the MS-UNet /
+ * Swin training hot path.
+ *
+ * Plain pointers + sizes only (no torch types).  Every launch goes to `stream` (a
+ * hipStream_t passed as void*), allocates nothing and never synchronises, so calls can be
+ * captured into a hipGraph.  Device pointers are HIP device memory; scalars are host
+ * values.  Return value: 0 on success, -2 bad shape/arguments, -3 unsupported mode,
+ * -4 LDS budget exceeded, -1 launch error.
+ *
+ * dtype: 0 = f32 activations (parity mode), 1 = bf16 activations (training mode).
+ * Parameters, statistics and parameter gradients are always f32.
+ *
+ * The reference path is Python (network/model_parts.py, torchvision SwinTransformerBlock,
+ * loss/DynamicLoss.py); each entry point names the reference operation it replaces.  The
+ * reference has no FFI of its own -- the Python binding is semantic_segmentation_of_stylegan2_artifacts_amd/_lib.py
+ * (ctypes) and INTEGRATION.md shows how a reference checkout would bind it.
+ */
+#ifndef MSUNET_HIP_H
+#define MSUNET_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- LayerNorm family
+ * nn.LayerNorm(C) over rows, with fused input addressing (mode):
+ *   0 plain     torchvision block norm1/norm2 (model_parts.py:143-151 -> torchvision),
+ *               PatchEmbed.norm (model_parts.py:213,224), MSUNetSys.norm / norm_up (:740-741,
+ *               :813, :827)
+ *   1 add       s = x + bscale[row / rows_per_sample] * b, y = LN(s); s stored to s_out.
+ *               torchvision block residual `x + stochastic_depth(branch)` fused with the
+ *               next norm
+ *   2 merge     PatchMerging cat(x0,x1,x2,x3) + norm(4C) (model_parts.py:87-94); x is
+ *               [B,H,W,Cin], C = 4*Cin
+ *   3 d2s2      PatchExpand rearrange 'b h w (p1 p2 c) -> b (h p1) (w p2) c' + norm
+ *               (model_parts.py:403-405); x is [B,H,W,4C]
+ * mean / rstd: [rows] f32 saved for backward. */
+int msu_layernorm_fwd(int dtype, int mode, const void* x, const void* b, const float* bscale,
+                      long rows_per_sample, void* s_out, const float* gamma, const float* beta,
+                      void* y, float* mean, float* rstd, long rows, int C, int H, int W, int Cin,
+                      float eps, void* stream);
+/* Backward: dx (scattered for merge / d2s2), optional dres added to dx (plain / add modes),
+ * db = dx * bscale (add mode), dgamma/dbeta via nparts partial rows in `part`
+ * ([nparts, 2, C] f32; nparts from msu_ln_part_blocks). */
+int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const void* dres,
+                      const float* gamma, const float* mean, const float* rstd, void* dx,
+                      void* db, const float* bscale, long rows_per_sample, float* part,
+                      int nparts, float* dgamma, float* dbeta, long rows, int C, int H, int W,
+                      int Cin, void* stream);
+int msu_ln_part_blocks(long rows, int C);
+int msu_reduce_rows(const float* part, int nparts, int n, long stride, float* out,
+                    int accumulate, void* stream);
+
+/* FinalPatchExpand_X4_V2.norm (model_parts.py:475) + bias-free 1x1 `output` conv
+ * (model_parts.py:751, :846), num_classes == 1: logit[r] = <LN(z[r]), w> (f32). */
+int msu_head_fwd(int dtype, const void* z, const float* gamma, const float* beta,
+                 const float* w, float* logit, float* mean, float* rstd, long rows, int C,
+                 float eps, void* stream);
+int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gamma,
+                 const float* beta, const float* w, const float* mean, const float* rstd,
+                 void* dz, float* part, int nparts, float* dgamma, float* dbeta, float* dw,
+                 long rows, int C, void* stream);
+
+/* ---------------------------------------------------------------- window attention
+ * torchvision shifted_window_attention core (called from SwinTransformerBlock at
+ * model_parts.py:170 / :538): pad to 7 -> roll(-shift) -> 7x7 windows -> softmax(q k^T *
+ * 32^-0.5 + B_rel + shift mask(-100)) -> dropout(p) -> @v -> reverse.  qkv: [B,H,W,3C]
+ * (q|k|v, heads contiguous, head_dim 32), out: [B,H,W,C]; table [169, nh] f32 is
+ * relative_position_bias_table; qkv_bias [3C] f32 supplies padded tokens' q,k,v. */
+long msu_win_count(int B, int H, int W);
+int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
+                     void* out, int B, int H, int W, int C, int nh, int shift, float p_drop,
+                     unsigned long long seed, void* stream);
+long msu_win_attn_bwd_workspace(int nblk, int C, int nh);
+/* dqkv [B,H,W,3C]; dtable [169,nh] (overwritten); dqkv_bias_pad [3C]: padded tokens'
+ * contribution to the qkv-bias gradient (overwritten). */
+int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
+                     const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
+                     float* workspace, int nblk, int B, int H, int W, int C, int nh, int shift,
+                     float p_drop, unsigned long long seed, void* stream);
+
+/* ---------------------------------------------------------------- refine convs
+ * FinalPatchExpand_X4_V2.refine1 / refine2 (model_parts.py:447-448, :468-471): 3x3, pad 1,
+ * NHWC implicit GEMM on MFMA.  in_mode bit0: GELU on the loaded input (model_parts.py:460,
+ * :469); bit1: input is the pre-depth-to-space [B,H/4,W/4,16*Cin] expand output
+ * (model_parts.py:464-465).  Wt: [9][Cout][roundup(Cin,32)] in the activation dtype. */
+int msu_conv3x3_fwd(int dtype, int in_mode, const void* X, const void* Wt, const float* bias,
+                    void* Y, int B, int H, int W, int Cin, int Cout, void* stream);
+/* dX = conv(dY, Wflip) * GELU'(S) through the same input map (out_mode as in_mode);
+ * Wflip [9][Cin][roundup(Cout,32)], Wflip[t][ci][co] = W[co][ci][8-t]. */
+int msu_conv3x3_dgrad(int dtype, int out_mode, const void* dY, const void* Wflip, const void* S,
+                      void* dX, int B, int H, int W, int Cin, int Cout, void* stream);
+long msu_conv3x3_wgrad_workspace(int nchunk, int Cin, int Cout, int dtype, int unused);
+/* dW [Cout][Cin][3][3] f32, db [Cout] f32 (deterministic partial-sum reduction). */
+int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, float* dW, float* db,
+                      float* workspace, void* unused, int nchunk, int B, int H, int W, int Cin,
+                      int Cout, void* stream);
+
+/* ---------------------------------------------------------------- streaming ops
+ * nn.GELU() (exact erf): torchvision MLP activation, FinalPatchExpand_X4_V2.act. */
+int msu_gelu_fwd(int dtype, const void* x, void* y, long n, void* stream);
+int msu_gelu_bwd(int dtype, const void* x, const void* dy, void* dx, long n, void* stream);
+/* PatchEmbed.proj im2col (model_parts.py:211, :222): img [B,Cin,H,W] f32 ->
+ * [B*(H/p)*(W/p), Cin*p*p] in (c, ky, kx) order. */
+int msu_patchify(int dtype, const float* img, void* out, int B, int Cin, int H, int W, int p,
+                 void* stream);
+
+/* DynamicLoss (loss/DynamicLoss.py:82-111): per-sample BCE-with-logits mean + Tversky
+ * (smooth 1e-6) on non-empty masks, mixed (1-m)*bce + m*tversky, mean over samples;
+ * binarise target at 127.5 iff max(target) > 1.  logits [B,N], target [B,N] f32.
+ * loss[0] = loss, loss[1] = binarised flag; coef [4B] and part [B*nblk*12] scratch. */
+int msu_dynloss_nblk(long N);
+int msu_dynloss_fwd(int dtype, const void* logits, const float* target, int B, long N,
+                    float alpha, float beta, float mix, float* part, int nblk, float* loss,
+                    float* coef, void* stream);
+/* dlogits [B,N] f32 = gout[0] * d loss / d logits (gout may be null = 1). */
+int msu_dynloss_bwd(int dtype, const void* logits, const float* target, const float* coef,
+                    const float* loss, const float* gout, int B, long N, float alpha, float beta,
+                    float mix, float* dlogits, void* stream);
+
+/* AdamW step (trainer.py:143-152; torch.optim.AdamW, amsgrad=False) over a flat f32
+ * parameter range; optional grad unscale (inv_scale) and skip-on-found_inf (GradScaler). */
+int msu_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
+              float beta2, float eps, float weight_decay, int step, const float* inv_scale,
+              const float* found_inf, void* stream);
+int msu_nonfinite(const float* x, long n, float* flag, void* stream);
+int msu_cast(int dtype, const float* x, void* y, long n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSUNET_HIP_H */

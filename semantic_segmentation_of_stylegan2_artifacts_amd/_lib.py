@@ -1,0 +1,73 @@
+"""ctypes binding of the C-ABI in ``include/msunet_hip.h`` (``libmsunet_hip.so``).
+
+There is no CPU fallback: if the library is missing or fails to load, every op raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmsunet_hip.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+U64 = ctypes.c_ulonglong
+
+# name -> (restype, argtypes); must match include/msunet_hip.h
+SIGNATURES = {
+    "msu_ln_part_blocks": (I, [L, I]),
+    "msu_layernorm_fwd": (I, [I, I, P, P, P, L, P, P, P, P, P, P, L, I, I, I, I, F, P]),
+    "msu_layernorm_bwd": (I, [I, I, P, P, P, P, P, P, P, P, P, L, P, I, P, P, L, I, I, I, I, P]),
+    "msu_reduce_rows": (I, [P, I, I, L, P, I, P]),
+    "msu_head_fwd": (I, [I, P, P, P, P, P, P, P, L, I, F, P]),
+    "msu_head_bwd": (I, [I, P, P, P, P, P, P, P, P, P, I, P, P, P, L, I, P]),
+    "msu_win_count": (L, [I, I, I]),
+    "msu_win_attn_fwd": (I, [I, P, P, P, P, I, I, I, I, I, I, F, U64, P]),
+    "msu_win_attn_bwd_workspace": (L, [I, I, I]),
+    "msu_win_attn_bwd": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, F, U64, P]),
+    "msu_gelu_fwd": (I, [I, P, P, L, P]),
+    "msu_gelu_bwd": (I, [I, P, P, P, L, P]),
+    "msu_patchify": (I, [I, P, P, I, I, I, I, I, P]),
+    "msu_dynloss_nblk": (I, [L]),
+    "msu_dynloss_fwd": (I, [I, P, P, I, L, F, F, F, P, I, P, P, P]),
+    "msu_dynloss_bwd": (I, [I, P, P, P, P, P, I, L, F, F, F, P, P]),
+    "msu_adamw": (I, [P, P, P, P, L, F, F, F, F, F, I, P, P, P]),
+    "msu_nonfinite": (I, [P, L, P, P]),
+    "msu_cast": (I, [I, P, P, L, P]),
+    "msu_conv3x3_fwd": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),
+    "msu_conv3x3_dgrad": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),
+    "msu_conv3x3_wgrad_workspace": (L, [I, I, I, I, I]),
+    "msu_conv3x3_wgrad": (I, [I, I, P, P, P, P, P, P, I, I, I, I, I, I, P]),
+}
+
+_lib = None
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the HIP library; raise loudly when it is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HipLibraryError(
+            f"{LIB_PATH} not found: build it with "
+            "`python -m semantic_segmentation_of_stylegan2_artifacts_amd.build` (no CPU fallback)")
+    h = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(h, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = h
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise HipLibraryError(f"{name} failed with code {rc}")
+    return rc

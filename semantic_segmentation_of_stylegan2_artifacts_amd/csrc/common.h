@@ -1,0 +1,92 @@
+// Shared device helpers for the MS-UNet gfx950 kernels.
+// Activations are either f32 (parity mode) or bf16 (training mode); every reduction and
+// every normalisation statistic is computed in f32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define MSU_DEV __device__ __forceinline__
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t bf16_t;  // storage type of a bf16 activation
+
+enum MsuDtype { MSU_F32 = 0, MSU_BF16 = 1 };
+
+// ------------------------------------------------------------------ scalar conversion
+MSU_DEV float to_f32(float v) { return v; }
+MSU_DEV float to_f32(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+template <typename T> MSU_DEV T from_f32(float v);
+template <> MSU_DEV float from_f32<float>(float v) { return v; }
+template <> MSU_DEV bf16_t from_f32<bf16_t>(float v) {
+  __hip_bfloat16 h = __float2bfloat16(v);  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+  return *reinterpret_cast<bf16_t*>(&h);
+}
+
+// ------------------------------------------------------------------ 4-wide vector I/O
+// f32: one 16-B load; bf16: one 8-B load.
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+  static MSU_DEV void load(const float* p, float (&v)[4]) {
+    float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
+  static MSU_DEV void store(float* p, const float (&v)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <> struct Vec4<bf16_t> {
+  static MSU_DEV void load(const bf16_t* p, float (&v)[4]) {
+    uint2 q = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+  }
+  static MSU_DEV void store(bf16_t* p, const float (&v)[4]) {
+    uint2 q;
+    q.x = (uint32_t)from_f32<bf16_t>(v[0]) | ((uint32_t)from_f32<bf16_t>(v[1]) << 16);
+    q.y = (uint32_t)from_f32<bf16_t>(v[2]) | ((uint32_t)from_f32<bf16_t>(v[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = q;
+  }
+};
+
+// ------------------------------------------------------------------ reductions
+template <int W> MSU_DEV float group_sum(float v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int W> MSU_DEV float group_max(float v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ------------------------------------------------------------------ activations
+MSU_DEV float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+MSU_DEV float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// ------------------------------------------------------------------ counter-based RNG
+// Philox-free 32-bit hash (splitmix-style) of (seed, index): uniform in [0, 1).
+MSU_DEV float hash_uniform(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+// XCD-aware bijective block remap: blocks b and b+8 share an XCD under round-robin
+// dispatch; give each XCD group a contiguous range of work items (speed only).
+MSU_DEV int xcd_remap(int b, int nb) {
+  const int x = b & 7, local = b >> 3;
+  const int q = nb >> 3, r = nb & 7;
+  const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return start + local;
+}
+
+#define MSU_CHECK_LAUNCH() (hipGetLastError() == hipSuccess ? 0 : -1)

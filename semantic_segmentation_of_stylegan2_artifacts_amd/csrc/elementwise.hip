@@ -1,0 +1,313 @@
+// Streaming kernels of the MS-UNet step: GELU fwd/bwd (torchvision MLP activation,
+// FinalPatchExpand_X4_V2.act), the 4x4/s4 patch-embed im2col (PatchEmbed.proj,
+// model_parts.py:211,222), DynamicLoss fwd/bwd (loss/DynamicLoss.py:82-111) and the fused
+// AdamW step over flat parameter buffers (trainer.py:143-152, torch.optim.AdamW semantics).
+// All HBM-bound: vectorised 4-wide, grid-stride, f32 math.
+#include "common.h"
+
+namespace {
+
+template <typename T>
+__global__ void __launch_bounds__(256) gelu_fwd_kernel(const T* x, T* y, long n4) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float v[4];
+    Vec4<T>::load(x + 4 * i, v);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+    Vec4<T>::store(y + 4 * i, v);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gelu_bwd_kernel(const T* x, const T* dy, T* dx, long n4) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float v[4], d[4];
+    Vec4<T>::load(x + 4 * i, v);
+    Vec4<T>::load(dy + 4 * i, d);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[e] *= gelu_grad_f(v[e]);
+    Vec4<T>::store(dx + 4 * i, d);
+  }
+}
+
+// img [B, Cin, H, W] f32 -> cols [B*(H/p)*(W/p), Cin*p*p] in (c, ky, kx) order = conv weight order
+template <typename T>
+__global__ void __launch_bounds__(256) patchify_kernel(const float* img, T* out, int B, int Cin,
+                                                       int H, int W, int p) {
+  const int Ho = H / p, Wo = W / p;
+  const int K = Cin * p * p;
+  const long total = (long)B * Ho * Wo * K;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long tok = i / K;
+    const int k = (int)(i - tok * K);
+    const int c = k / (p * p), r = k - c * p * p, ky = r / p, kx = r - (r / p) * p;
+    const long b = tok / ((long)Ho * Wo);
+    const int t = (int)(tok - b * Ho * Wo);
+    const int oy = t / Wo, ox = t - (t / Wo) * Wo;
+    out[i] = from_f32<T>(img[((b * Cin + c) * H + oy * p + ky) * (long)W + ox * p + kx]);
+  }
+}
+
+// ---------------------------------------------------------------- DynamicLoss
+// Per (sample, block) partial sums, for both the raw target and the >127.5-binarised one
+// (the reference binarises iff target.max() > 1 over the WHOLE batch, DynamicLoss.py:87-88).
+// part layout [B][nblk][12]: raw {bce, tp, fp, fn, tsum}, bin {bce, tp, fp, fn, tsum}, tmax, pad
+constexpr int NS = 12;
+
+template <typename T>
+__global__ void __launch_bounds__(256) dynloss_partial_kernel(const T* logits, const float* target,
+                                                              long N, int nblk, float* part) {
+  const int b = blockIdx.y;
+  const T* x = logits + (long)b * N;
+  const float* t = target + (long)b * N;
+  float acc[11];
+#pragma unroll
+  for (int k = 0; k < 11; ++k) acc[k] = 0.f;
+  acc[10] = -INFINITY;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < N; i += (long)nblk * 256) {
+    const float xv = to_f32(x[i]);
+    const float tr = t[i];
+    const float p = 1.f / (1.f + __expf(-xv));
+    const float sp = fmaxf(xv, 0.f) + log1pf(__expf(-fabsf(xv)));  // softplus(x) = max(x,0)+log1p(e^-|x|)
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const float tv = m == 0 ? tr : (tr > 127.5f ? 1.f : 0.f);
+      acc[m * 5 + 0] += sp - xv * tv;
+      acc[m * 5 + 1] += p * tv;
+      acc[m * 5 + 2] += p * (1.f - tv);
+      acc[m * 5 + 3] += (1.f - p) * tv;
+      acc[m * 5 + 4] += tv;
+    }
+    acc[10] = fmaxf(acc[10], tr);
+  }
+  __shared__ float red[4][11];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    const float s = group_sum<64>(acc[k]);
+    if (lane == 0) red[wv][k] = s;
+  }
+  const float mx = group_max<64>(acc[10]);
+  if (lane == 0) red[wv][10] = mx;
+  __syncthreads();
+  if (threadIdx.x < 11) {
+    const int k = threadIdx.x;
+    float v = red[0][k];
+    for (int w = 1; w < 4; ++w) v = k == 10 ? fmaxf(v, red[w][k]) : v + red[w][k];
+    part[((long)b * nblk + blockIdx.x) * NS + k] = v;
+  }
+}
+
+// One block: finalise per-sample loss terms.  coef[b] = {w_bce, has_tv, num, den}; flags[0]=binarise
+__global__ void __launch_bounds__(64) dynloss_final_kernel(const float* part, int B, int nblk, long N,
+                                                           float alpha, float beta, float mix,
+                                                           float smooth, float* loss, float* coef) {
+  __shared__ int binarise;
+  if (threadIdx.x == 0) {
+    float mx = -INFINITY;
+    for (int b = 0; b < B; ++b)
+      for (int k = 0; k < nblk; ++k) mx = fmaxf(mx, part[((long)b * nblk + k) * NS + 10]);
+    binarise = mx > 1.f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int o = binarise ? 5 : 0;
+    double total = 0.0;
+    for (int b = 0; b < B; ++b) {
+      double s[5] = {0, 0, 0, 0, 0};
+      for (int k = 0; k < nblk; ++k)
+        for (int q = 0; q < 5; ++q) s[q] += part[((long)b * nblk + k) * NS + o + q];
+      const double bce = s[0] / (double)N;
+      float* c = coef + 4 * b;
+      if (s[4] != 0.0) {
+        const double num = s[1] + smooth;
+        const double den = s[1] + alpha * s[2] + beta * s[3] + smooth;
+        total += (1.0 - mix) * bce + mix * (1.0 - num / den);
+        c[0] = (float)((1.0 - mix) / (double)N);
+        c[1] = 1.f;
+        c[2] = (float)num;
+        c[3] = (float)den;
+      } else {
+        total += bce;
+        c[0] = (float)(1.0 / (double)N);
+        c[1] = 0.f; c[2] = 1.f; c[3] = 1.f;
+      }
+    }
+    loss[0] = (float)(total / B);
+    loss[1] = (float)binarise;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dynloss_bwd_kernel(const T* logits, const float* target,
+                                                          const float* coef, const float* flags,
+                                                          const float* gout, long N, int B,
+                                                          float alpha, float beta, float mix,
+                                                          float* dlogits) {
+  const long total = N * B;
+  const bool bin = flags[1] != 0.f;
+  const float g = gout ? gout[0] / B : 1.f / B;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int b = (int)(i / N);
+    const float* c = coef + 4 * b;
+    const float xv = to_f32(logits[i]);
+    float tv = target[i];
+    if (bin) tv = tv > 127.5f ? 1.f : 0.f;
+    const float p = 1.f / (1.f + __expf(-xv));
+    float d = c[0] * (p - tv);
+    if (c[1] != 0.f) {
+      const float num = c[2], den = c[3];
+      const float dti = (tv * den - num * (tv + alpha * (1.f - tv) - beta * tv)) / (den * den);
+      d -= mix * dti * p * (1.f - p);
+    }
+    dlogits[i] = g * d;
+  }
+}
+
+// ---------------------------------------------------------------- AdamW (torch semantics)
+__global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, long n,
+                                                    float lr, float b1, float b2, float eps, float wd,
+                                                    float bc1, float bc2_sqrt, const float* inv_scale,
+                                                    const float* found_inf) {
+  if (found_inf && found_inf[0] != 0.f) return;
+  const float is = inv_scale ? inv_scale[0] : 1.f;
+  const float step_size = lr / bc1;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float gi = g[i] * is;
+    float pi = p[i] * (1.f - lr * wd);
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    pi -= step_size * mi / (sqrtf(vi) / bc2_sqrt + eps);
+    p[i] = pi;
+  }
+}
+
+// any non-finite in x -> flag[0] = 1 (flag must be zeroed by the caller)
+__global__ void __launch_bounds__(256) nonfinite_kernel(const float* x, long n, float* flag) {
+  bool bad = false;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    bad |= !isfinite(x[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) flag[0] = 1.f;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) cast_kernel(const float* x, T* y, long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    y[i] = from_f32<T>(x[i]);
+}
+
+inline unsigned grid_for(long n, long per_block = 256, long cap = 8192) {
+  long nb = (n + per_block - 1) / per_block;
+  if (nb > cap) nb = cap;
+  return (unsigned)(nb < 1 ? 1 : nb);
+}
+
+}  // namespace
+
+extern "C" {
+
+int msu_gelu_fwd(int dtype, const void* x, void* y, long n, void* stream) {
+  if (n % 4) return -2;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MSU_BF16)
+    hipLaunchKernelGGL(gelu_fwd_kernel<bf16_t>, dim3(grid_for(n / 4)), dim3(256), 0, st,
+                       (const bf16_t*)x, (bf16_t*)y, n / 4);
+  else
+    hipLaunchKernelGGL(gelu_fwd_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, st,
+                       (const float*)x, (float*)y, n / 4);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_gelu_bwd(int dtype, const void* x, const void* dy, void* dx, long n, void* stream) {
+  if (n % 4) return -2;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MSU_BF16)
+    hipLaunchKernelGGL(gelu_bwd_kernel<bf16_t>, dim3(grid_for(n / 4)), dim3(256), 0, st,
+                       (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)dx, n / 4);
+  else
+    hipLaunchKernelGGL(gelu_bwd_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, st,
+                       (const float*)x, (const float*)dy, (float*)dx, n / 4);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_patchify(int dtype, const float* img, void* out, int B, int Cin, int H, int W, int p,
+                 void* stream) {
+  if (H % p || W % p) return -2;
+  hipStream_t st = (hipStream_t)stream;
+  const long n = (long)B * Cin * H * W;
+  if (dtype == MSU_BF16)
+    hipLaunchKernelGGL(patchify_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, img,
+                       (bf16_t*)out, B, Cin, H, W, p);
+  else
+    hipLaunchKernelGGL(patchify_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, img,
+                       (float*)out, B, Cin, H, W, p);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_dynloss_nblk(long N) {
+  long nb = (N + 256 * 16 - 1) / (256 * 16);
+  if (nb > 256) nb = 256;
+  return (int)(nb < 1 ? 1 : nb);
+}
+
+// loss[0] = loss value, loss[1] = binarised flag; coef [B*4]; part [B*nblk*12]
+int msu_dynloss_fwd(int dtype, const void* logits, const float* target, int B, long N,
+                    float alpha, float beta, float mix, float* part, int nblk, float* loss,
+                    float* coef, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MSU_BF16)
+    hipLaunchKernelGGL(dynloss_partial_kernel<bf16_t>, dim3(nblk, B), dim3(256), 0, st,
+                       (const bf16_t*)logits, target, N, nblk, part);
+  else
+    hipLaunchKernelGGL(dynloss_partial_kernel<float>, dim3(nblk, B), dim3(256), 0, st,
+                       (const float*)logits, target, N, nblk, part);
+  hipLaunchKernelGGL(dynloss_final_kernel, dim3(1), dim3(64), 0, st, part, B, nblk, N, alpha, beta,
+                     mix, 1e-6f, loss, coef);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_dynloss_bwd(int dtype, const void* logits, const float* target, const float* coef,
+                    const float* loss, const float* gout, int B, long N, float alpha, float beta,
+                    float mix, float* dlogits, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long n = (long)B * N;
+  if (dtype == MSU_BF16)
+    hipLaunchKernelGGL(dynloss_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st,
+                       (const bf16_t*)logits, target, coef, loss, gout, N, B, alpha, beta, mix, dlogits);
+  else
+    hipLaunchKernelGGL(dynloss_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st,
+                       (const float*)logits, target, coef, loss, gout, N, B, alpha, beta, mix, dlogits);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
+              float beta2, float eps, float weight_decay, int step, const float* inv_scale,
+              const float* found_inf, void* stream) {
+  if (n == 0) return 0;
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream,
+                     p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, (float)bc1,
+                     (float)sqrt(bc2), inv_scale, found_inf);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_nonfinite(const float* x, long n, float* flag, void* stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(nonfinite_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, flag);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_cast(int dtype, const float* x, void* y, long n, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MSU_BF16)
+    hipLaunchKernelGGL(cast_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, x, (bf16_t*)y, n);
+  else
+    hipLaunchKernelGGL(cast_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, x, (float*)y, n);
+  return MSU_CHECK_LAUNCH();
+}
+
+}  // extern "C"

@@ -1,0 +1,523 @@
+// Row LayerNorm family (eps, per-row f32 mean/rstd saved for backward) with fused input
+// addressing.  Replaces every nn.LayerNorm on the MS-UNet path:
+//   * plain            block norm1/norm2, PatchEmbed.norm, norm, norm_up
+//                      (model_parts.py:213,224,740-741; torchvision block)
+//   * residual add     x + dp[b]*branch -> LN (torchvision block residual + StochasticDepth,
+//                      fused with the following norm)
+//   * 2x2 merge gather PatchMerging x0..x3 cat + norm (model_parts.py:87-94)
+//   * 2x2 d2s          PatchExpand rearrange + norm (model_parts.py:403-405)
+//   * head             FinalPatchExpand_X4_V2.norm + 1x1 output conv (model_parts.py:475,846)
+// One row is owned by TPR lanes; each lane holds KMAX 4-wide chunks in registers.
+#include "common.h"
+
+namespace {
+
+enum InMode { IN_PLAIN = 0, IN_ADD = 1, IN_MERGE = 2, IN_D2S2 = 3 };
+
+struct LnArgs {
+  const void* x;      // IN_PLAIN/MERGE/D2S2: source; IN_ADD: residual stream a
+  const void* b;      // IN_ADD: branch output (may be null)
+  const float* bscale;  // IN_ADD: per-sample stochastic-depth scale (null = 1)
+  void* s_out;        // IN_ADD: a + scale*b (null = not stored)
+  const float* gamma;
+  const float* beta;
+  void* y;
+  float* mean;
+  float* rstd;
+  long rows;
+  int C;              // normalised width (row length of y)
+  int H, W;           // MERGE: input grid; D2S2: input grid (output grid is 2H x 2W)
+  int Cin;            // MERGE: input channels (C = 4*Cin)
+  long rows_per_sample;
+  float eps;
+};
+
+// element offset of column `col` of logical row `r` in the source tensor
+template <int MODE>
+MSU_DEV long src_off(const LnArgs& a, long r, int col) {
+  if constexpr (MODE == IN_MERGE) {
+    const int H2 = a.H >> 1, W2 = a.W >> 1;
+    const long b = r / ((long)H2 * W2);
+    const int rem = (int)(r - b * (long)H2 * W2);
+    const int i = rem / W2, j = rem - (rem / W2) * W2;
+    const int q = col / a.Cin, off = col - q * a.Cin;
+    const int dy = q & 1, dx = q >> 1;  // x0 (0,0) x1 (1,0) x2 (0,1) x3 (1,1)
+    return (((b * a.H + 2 * i + dy) * a.W) + 2 * j + dx) * (long)a.Cin + off;
+  } else if constexpr (MODE == IN_D2S2) {
+    const int OH = a.H * 2, OW = a.W * 2;
+    const long b = r / ((long)OH * OW);
+    const int rem = (int)(r - b * (long)OH * OW);
+    const int oh = rem / OW, ow = rem - (rem / OW) * OW;
+    const long tok = (b * a.H + (oh >> 1)) * a.W + (ow >> 1);
+    return tok * (4L * a.C) + (long)(((oh & 1) * 2 + (ow & 1)) * a.C) + col;
+  } else {
+    return r * (long)a.C + col;
+  }
+}
+
+template <typename T, int MODE, int TPR, int KMAX>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs a) {
+  const int lane = threadIdx.x % TPR;
+  const int grp = threadIdx.x / TPR;
+  constexpr int GPB = 256 / TPR;
+  const int nchunk = a.C >> 2;
+  const T* X = reinterpret_cast<const T*>(a.x);
+  const T* Bv = reinterpret_cast<const T*>(a.b);
+  for (long r = (long)blockIdx.x * GPB + grp; r < a.rows; r += (long)gridDim.x * GPB) {
+    float v[KMAX][4];
+    float sum = 0.f;
+    float sc = 1.f;
+    if constexpr (MODE == IN_ADD) {
+      if (a.bscale) sc = a.bscale[r / a.rows_per_sample];
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        const long off = src_off<MODE>(a, r, ch * 4);
+        Vec4<T>::load(X + off, v[k]);
+        if constexpr (MODE == IN_ADD) {
+          if (Bv) {
+            float w[4];
+            Vec4<T>::load(Bv + off, w);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[k][e] += sc * w[e];
+          }
+          // round the residual stream to storage precision first: the stored value is
+          // what later layers (and backward) see, so normalise exactly that value
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[k][e] = to_f32(from_f32<T>(v[k][e]));
+          if (a.s_out) Vec4<T>::store(reinterpret_cast<T*>(a.s_out) + off, v[k]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sum += v[k][e];
+      }
+    }
+    sum = group_sum<TPR>(sum);
+    const float mu = sum / a.C;
+    float var = 0.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { const float d = v[k][e] - mu; var += d * d; }
+      }
+    }
+    var = group_sum<TPR>(var);
+    const float rs = rsqrtf(var / a.C + a.eps);
+    T* Y = reinterpret_cast<T*>(a.y);
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        float o[4];
+        const float4 g = *reinterpret_cast<const float4*>(a.gamma + ch * 4);
+        const float4 bt = *reinterpret_cast<const float4*>(a.beta + ch * 4);
+        o[0] = (v[k][0] - mu) * rs * g.x + bt.x;
+        o[1] = (v[k][1] - mu) * rs * g.y + bt.y;
+        o[2] = (v[k][2] - mu) * rs * g.z + bt.z;
+        o[3] = (v[k][3] - mu) * rs * g.w + bt.w;
+        Vec4<T>::store(Y + r * (long)a.C + ch * 4, o);
+      }
+    }
+    if (lane == 0) { a.mean[r] = mu; a.rstd[r] = rs; }
+  }
+}
+
+struct LnBwdArgs {
+  const void* dy;       // [rows, C]
+  const void* x;        // the normalised input (IN_ADD: the stored s; others: source)
+  const void* dres;     // extra gradient into s (IN_ADD / IN_PLAIN; null = none)
+  const float* gamma;
+  const float* mean;
+  const float* rstd;
+  void* dx;             // gradient wrt the normalised input (scattered for MERGE / D2S2)
+  void* db;             // IN_ADD: gradient wrt branch = dx * bscale (null = not needed)
+  const float* bscale;
+  float* part;          // [gridDim.x, 2, C] partial dgamma / dbeta
+  long rows;
+  int C, H, W, Cin;
+  long rows_per_sample;
+};
+
+template <typename T, int MODE, int TPR, int KMAX>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
+  const int lane = threadIdx.x % TPR;
+  const int grp = threadIdx.x / TPR;
+  constexpr int GPB = 256 / TPR;
+  const int nchunk = a.C >> 2;
+  const T* X = reinterpret_cast<const T*>(a.x);
+  const T* DY = reinterpret_cast<const T*>(a.dy);
+  float accg[KMAX][4], accb[KMAX][4];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { accg[k][e] = 0.f; accb[k][e] = 0.f; }
+  LnArgs fa;
+  fa.C = a.C; fa.H = a.H; fa.W = a.W; fa.Cin = a.Cin;
+  for (long r = (long)blockIdx.x * GPB + grp; r < a.rows; r += (long)gridDim.x * GPB) {
+    const float mu = a.mean[r], rs = a.rstd[r];
+    float xh[KMAX][4], g[KMAX][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        float xv[4], dv[4];
+        Vec4<T>::load(X + src_off<MODE>(fa, r, ch * 4), xv);
+        Vec4<T>::load(DY + r * (long)a.C + ch * 4, dv);
+        const float4 gm = *reinterpret_cast<const float4*>(a.gamma + ch * 4);
+        const float gg[4] = {gm.x, gm.y, gm.z, gm.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[k][e] = (xv[e] - mu) * rs;
+          g[k][e] = dv[e] * gg[e];
+          s1 += g[k][e];
+          s2 += g[k][e] * xh[k][e];
+          accg[k][e] += dv[e] * xh[k][e];
+          accb[k][e] += dv[e];
+        }
+      }
+    }
+    s1 = group_sum<TPR>(s1) / a.C;
+    s2 = group_sum<TPR>(s2) / a.C;
+    float sc = 1.f;
+    if constexpr (MODE == IN_ADD) {
+      if (a.bscale) sc = a.bscale[r / a.rows_per_sample];
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rs * (g[k][e] - s1 - xh[k][e] * s2);
+        const long off = src_off<MODE>(fa, r, ch * 4);
+        if constexpr (MODE == IN_ADD || MODE == IN_PLAIN) {
+          if (a.dres) {
+            float dr[4];
+            Vec4<T>::load(reinterpret_cast<const T*>(a.dres) + off, dr);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] += dr[e];
+          }
+        }
+        Vec4<T>::store(reinterpret_cast<T*>(a.dx) + off, o);
+        if constexpr (MODE == IN_ADD) {
+          if (a.db) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] *= sc;
+            Vec4<T>::store(reinterpret_cast<T*>(a.db) + off, o);
+          }
+        }
+      }
+    }
+  }
+  // block reduction of the per-lane parameter-gradient partials: groups share columns
+  __shared__ float red[2][2048 / 4][4];
+  // reduce in two passes over groups to bound LDS: accumulate group-by-group
+  for (int gsel = 0; gsel < GPB; ++gsel) {
+    if (grp == gsel) {
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        const int ch = lane + k * TPR;
+        if (ch < nchunk) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (gsel == 0) { red[0][ch][e] = accg[k][e]; red[1][ch][e] = accb[k][e]; }
+            else { red[0][ch][e] += accg[k][e]; red[1][ch][e] += accb[k][e]; }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* P = a.part + (long)blockIdx.x * 2 * a.C;
+  for (int i = threadIdx.x; i < a.C; i += 256) {
+    P[i] = red[0][i >> 2][i & 3];
+    P[a.C + i] = red[1][i >> 2][i & 3];
+  }
+}
+
+// Sum `nparts` rows of [nparts, n] f32 partials into out[n] (deterministic order).
+__global__ void __launch_bounds__(256) reduce_rows_kernel(const float* part, int nparts, int n,
+                                                          long stride, float* out, int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(long)p * stride + i];
+  out[i] = accumulate ? out[i] + s : s;
+}
+
+template <typename T, int MODE>
+int launch_fwd(const LnArgs& a, hipStream_t st, int max_blocks) {
+  const int nchunk = a.C / 4;
+  auto go = [&](auto kern, int tpr) {
+    const long gpb = 256 / tpr;
+    long nb = (a.rows + gpb - 1) / gpb;
+    if (nb > max_blocks) nb = max_blocks;
+    if (nb < 1) nb = 1;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, st, a);
+    return MSU_CHECK_LAUNCH();
+  };
+  if (nchunk <= 8 * 4) return go(ln_fwd_kernel<T, MODE, 8, 4>, 8);
+  if (nchunk <= 16 * 4) return go(ln_fwd_kernel<T, MODE, 16, 4>, 16);
+  if (nchunk <= 32 * 4) return go(ln_fwd_kernel<T, MODE, 32, 4>, 32);
+  if (nchunk <= 64 * 4) return go(ln_fwd_kernel<T, MODE, 64, 4>, 64);
+  if (nchunk <= 64 * 8) return go(ln_fwd_kernel<T, MODE, 64, 8>, 64);
+  return -2;
+}
+
+template <typename T, int MODE>
+int launch_bwd(const LnBwdArgs& a, hipStream_t st, int nblocks) {
+  const int nchunk = a.C / 4;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(256), 0, st, a);
+    return MSU_CHECK_LAUNCH();
+  };
+  if (nchunk <= 8 * 4) return go(ln_bwd_kernel<T, MODE, 8, 4>);
+  if (nchunk <= 16 * 4) return go(ln_bwd_kernel<T, MODE, 16, 4>);
+  if (nchunk <= 32 * 4) return go(ln_bwd_kernel<T, MODE, 32, 4>);
+  if (nchunk <= 64 * 4) return go(ln_bwd_kernel<T, MODE, 64, 4>);
+  if (nchunk <= 64 * 8) return go(ln_bwd_kernel<T, MODE, 64, 8>);
+  return -2;
+}
+
+template <int MODE>
+int fwd_dispatch(int dtype, const LnArgs& a, hipStream_t st) {
+  if (a.C % 4 != 0 || a.C > 2048) return -2;
+  if (a.rows == 0) return 0;
+  return dtype == MSU_BF16 ? launch_fwd<bf16_t, MODE>(a, st, 4096) : launch_fwd<float, MODE>(a, st, 4096);
+}
+
+template <int MODE>
+int bwd_dispatch(int dtype, const LnBwdArgs& a, float* dgamma, float* dbeta, int nparts,
+                 hipStream_t st) {
+  if (a.C % 4 != 0 || a.C > 2048) return -2;
+  if (a.rows == 0) return 0;
+  int rc = dtype == MSU_BF16 ? launch_bwd<bf16_t, MODE>(a, st, nparts) : launch_bwd<float, MODE>(a, st, nparts);
+  if (rc) return rc;
+  const int nb = (a.C + 255) / 256;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(nb), dim3(256), 0, st, a.part, nparts, a.C,
+                     (long)2 * a.C, dgamma, 0);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(nb), dim3(256), 0, st, a.part + a.C, nparts, a.C,
+                     (long)2 * a.C, dbeta, 0);
+  return MSU_CHECK_LAUNCH();
+}
+
+// ----------------------------------------------------------------------------- head
+// FinalPatchExpand_X4_V2.norm (model_parts.py:475) fused with the bias-free 1x1 `output`
+// conv (:751, :846) for num_classes == 1: logit[r] = sum_c LN(z[r])_c * w_c (f32 logits).
+template <typename T, int KMAX>
+__global__ void __launch_bounds__(256) head_fwd_kernel(const T* z, const float* gamma, const float* beta,
+                                                       const float* w, float* logit, float* mean,
+                                                       float* rstd, long rows, int C, float eps) {
+  constexpr int TPR = 8, GPB = 32;
+  const int lane = threadIdx.x % TPR, grp = threadIdx.x / TPR;
+  const int nchunk = C >> 2;
+  for (long r = (long)blockIdx.x * GPB + grp; r < rows; r += (long)gridDim.x * GPB) {
+    float v[KMAX][4];
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        Vec4<T>::load(z + r * (long)C + ch * 4, v[k]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sum += v[k][e];
+      }
+    }
+    const float mu = group_sum<TPR>(sum) / C;
+    float var = 0.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { const float d = v[k][e] - mu; var += d * d; }
+      }
+    }
+    const float rs = rsqrtf(group_sum<TPR>(var) / C + eps);
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = ch * 4 + e;
+          dot += ((v[k][e] - mu) * rs * gamma[c] + beta[c]) * w[c];
+        }
+      }
+    }
+    dot = group_sum<TPR>(dot);
+    if (lane == 0) { logit[r] = dot; mean[r] = mu; rstd[r] = rs; }
+  }
+}
+
+template <typename T, int KMAX>
+__global__ void __launch_bounds__(256) head_bwd_kernel(const float* dlogit, const T* z, const float* gamma,
+                                                       const float* beta, const float* w,
+                                                       const float* mean, const float* rstd, T* dz,
+                                                       float* part /* [grid, 3, C] */, long rows, int C) {
+  constexpr int TPR = 8, GPB = 32;
+  const int lane = threadIdx.x % TPR, grp = threadIdx.x / TPR;
+  const int nchunk = C >> 2;
+  float ag[KMAX][4], ab[KMAX][4], aw[KMAX][4];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { ag[k][e] = 0.f; ab[k][e] = 0.f; aw[k][e] = 0.f; }
+  for (long r = (long)blockIdx.x * GPB + grp; r < rows; r += (long)gridDim.x * GPB) {
+    const float mu = mean[r], rs = rstd[r], dl = dlogit[r];
+    float xh[KMAX][4], g[KMAX][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        float xv[4];
+        Vec4<T>::load(z + r * (long)C + ch * 4, xv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = ch * 4 + e;
+          const float dy = dl * w[c];
+          xh[k][e] = (xv[e] - mu) * rs;
+          g[k][e] = dy * gamma[c];
+          s1 += g[k][e];
+          s2 += g[k][e] * xh[k][e];
+          ag[k][e] += dy * xh[k][e];
+          ab[k][e] += dy;
+          aw[k][e] += dl * (xh[k][e] * gamma[c] + beta[c]);
+        }
+      }
+    }
+    s1 = group_sum<TPR>(s1) / C;
+    s2 = group_sum<TPR>(s2) / C;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rs * (g[k][e] - s1 - xh[k][e] * s2);
+        Vec4<T>::store(dz + r * (long)C + ch * 4, o);
+      }
+    }
+  }
+  __shared__ float red[3][256 / 4][4];
+  for (int gsel = 0; gsel < GPB; ++gsel) {
+    if (grp == gsel) {
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        const int ch = lane + k * TPR;
+        if (ch < nchunk) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (gsel == 0) { red[0][ch][e] = ag[k][e]; red[1][ch][e] = ab[k][e]; red[2][ch][e] = aw[k][e]; }
+            else { red[0][ch][e] += ag[k][e]; red[1][ch][e] += ab[k][e]; red[2][ch][e] += aw[k][e]; }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* P = part + (long)blockIdx.x * 3 * C;
+  for (int i = threadIdx.x; i < C; i += 256) {
+    P[i] = red[0][i >> 2][i & 3];
+    P[C + i] = red[1][i >> 2][i & 3];
+    P[2 * C + i] = red[2][i >> 2][i & 3];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int msu_head_fwd(int dtype, const void* z, const float* gamma, const float* beta, const float* w,
+                 float* logit, float* mean, float* rstd, long rows, int C, float eps, void* stream) {
+  if (C % 4 || C > 256) return -2;
+  if (rows == 0) return 0;
+  long nb = (rows + 31) / 32;
+  if (nb > 8192) nb = 8192;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MSU_BF16) {
+    if (C <= 128) hipLaunchKernelGGL((head_fwd_kernel<bf16_t, 4>), dim3(nb), dim3(256), 0, st, (const bf16_t*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps);
+    else hipLaunchKernelGGL((head_fwd_kernel<bf16_t, 8>), dim3(nb), dim3(256), 0, st, (const bf16_t*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps);
+  } else {
+    if (C <= 128) hipLaunchKernelGGL((head_fwd_kernel<float, 4>), dim3(nb), dim3(256), 0, st, (const float*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps);
+    else hipLaunchKernelGGL((head_fwd_kernel<float, 8>), dim3(nb), dim3(256), 0, st, (const float*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps);
+  }
+  return MSU_CHECK_LAUNCH();
+}
+
+// grads: dgamma, dbeta, dw (each [C]); part [nparts, 3, C]
+int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gamma,
+                 const float* beta, const float* w, const float* mean, const float* rstd, void* dz,
+                 float* part, int nparts, float* dgamma, float* dbeta, float* dw, long rows, int C,
+                 void* stream) {
+  if (C % 4 || C > 256) return -2;
+  if (rows == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MSU_BF16) {
+    if (C <= 128) hipLaunchKernelGGL((head_bwd_kernel<bf16_t, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const bf16_t*)z, gamma, beta, w, mean, rstd, (bf16_t*)dz, part, rows, C);
+    else hipLaunchKernelGGL((head_bwd_kernel<bf16_t, 8>), dim3(nparts), dim3(256), 0, st, dlogit, (const bf16_t*)z, gamma, beta, w, mean, rstd, (bf16_t*)dz, part, rows, C);
+  } else {
+    if (C <= 128) hipLaunchKernelGGL((head_bwd_kernel<float, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const float*)z, gamma, beta, w, mean, rstd, (float*)dz, part, rows, C);
+    else hipLaunchKernelGGL((head_bwd_kernel<float, 8>), dim3(nparts), dim3(256), 0, st, dlogit, (const float*)z, gamma, beta, w, mean, rstd, (float*)dz, part, rows, C);
+  }
+  const int nb = (C + 255) / 256;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(nb), dim3(256), 0, st, part, nparts, C, (long)3 * C, dgamma, 0);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(nb), dim3(256), 0, st, part + C, nparts, C, (long)3 * C, dbeta, 0);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(nb), dim3(256), 0, st, part + 2 * C, nparts, C, (long)3 * C, dw, 0);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_ln_part_blocks(long rows, int C) {
+  (void)C;
+  long nb = (rows + 31) / 32;
+  if (nb > 1024) nb = 1024;
+  return nb < 1 ? 1 : (int)nb;
+}
+
+int msu_layernorm_fwd(int dtype, int mode, const void* x, const void* b, const float* bscale,
+                      long rows_per_sample, void* s_out, const float* gamma, const float* beta,
+                      void* y, float* mean, float* rstd, long rows, int C, int H, int W, int Cin,
+                      float eps, void* stream) {
+  LnArgs a{x, b, bscale, s_out, gamma, beta, y, mean, rstd, rows, C, H, W, Cin,
+           rows_per_sample > 0 ? rows_per_sample : 1, eps};
+  hipStream_t st = (hipStream_t)stream;
+  switch (mode) {
+    case IN_PLAIN: return fwd_dispatch<IN_PLAIN>(dtype, a, st);
+    case IN_ADD: return fwd_dispatch<IN_ADD>(dtype, a, st);
+    case IN_MERGE: return fwd_dispatch<IN_MERGE>(dtype, a, st);
+    case IN_D2S2: return fwd_dispatch<IN_D2S2>(dtype, a, st);
+  }
+  return -3;
+}
+
+int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const void* dres,
+                      const float* gamma, const float* mean, const float* rstd, void* dx,
+                      void* db, const float* bscale, long rows_per_sample, float* part,
+                      int nparts, float* dgamma, float* dbeta, long rows, int C, int H, int W,
+                      int Cin, void* stream) {
+  LnBwdArgs a{dy, x, dres, gamma, mean, rstd, dx, db, bscale, part, rows, C, H, W, Cin,
+              rows_per_sample > 0 ? rows_per_sample : 1};
+  hipStream_t st = (hipStream_t)stream;
+  switch (mode) {
+    case IN_PLAIN: return bwd_dispatch<IN_PLAIN>(dtype, a, dgamma, dbeta, nparts, st);
+    case IN_ADD: return bwd_dispatch<IN_ADD>(dtype, a, dgamma, dbeta, nparts, st);
+    case IN_MERGE: return bwd_dispatch<IN_MERGE>(dtype, a, dgamma, dbeta, nparts, st);
+    case IN_D2S2: return bwd_dispatch<IN_D2S2>(dtype, a, dgamma, dbeta, nparts, st);
+  }
+  return -3;
+}
+
+int msu_reduce_rows(const float* part, int nparts, int n, long stride, float* out,
+                    int accumulate, void* stream) {
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, part, nparts, n, stride, out, accumulate);
+  return MSU_CHECK_LAUNCH();
+}
+
+}  // extern "C"

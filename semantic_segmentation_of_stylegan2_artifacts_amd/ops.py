@@ -1,0 +1,452 @@
+"""Autograd wrappers over the HIP C-ABI (``include/msunet_hip.h``).
+
+Every op here launches hand-written gfx950 kernels from ``libmsunet_hip.so`` on the
+current HIP stream of its input's device.  There is no CPU / eager fallback: a CPU tensor
+or a missing library raises.  Activations are float32 (parity mode) or bfloat16 (training
+mode, chosen by ``torch.autocast``); statistics, parameters and parameter gradients are
+float32.
+"""
+import math
+
+import torch
+
+from . import _lib
+
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+# ----------------------------------------------------------------------------- helpers
+def _dt(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported activation dtype {t.dtype} (float32 / bfloat16)") from None
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("msunet HIP ops need tensors on a HIP device (no CPU fallback)")
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _s(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def act_dtype(device_type="cuda"):
+    """Activation dtype for the current context: autocast dtype if enabled, else float32."""
+    if torch.is_autocast_enabled(device_type):
+        return torch.get_autocast_dtype(device_type)
+    return torch.float32
+
+
+def _f32(t):
+    return t if (t.dtype == torch.float32 and t.is_contiguous()) else t.float().contiguous()
+
+
+def _as(t, dtype):
+    t = t if t.dtype == dtype else t.to(dtype)
+    return t.contiguous()
+
+
+def _ln_parts(rows, C, device):
+    n = _lib.lib().msu_ln_part_blocks(rows, C)
+    return n, torch.empty(n * 3 * C, device=device, dtype=torch.float32)
+
+
+IN_PLAIN, IN_ADD, IN_MERGE, IN_D2S2 = 0, 1, 2, 3
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        _need_cuda(x)
+        x = x.contiguous()
+        C = x.shape[-1]
+        rows = x.numel() // C
+        y = torch.empty_like(x)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        _lib.call("msu_layernorm_fwd", _dt(x), IN_PLAIN, _p(x), None, None, 1, None, _p(w), _p(b),
+                  _p(y), _p(mean), _p(rstd), rows, C, 0, 0, 0, eps, _s(x))
+        ctx.save_for_backward(x, w, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        dy = _as(dy, x.dtype)
+        C = x.shape[-1]
+        rows = x.numel() // C
+        dx = torch.empty_like(x)
+        dw = torch.empty(C, device=x.device, dtype=torch.float32)
+        db = torch.empty_like(dw)
+        n, part = _ln_parts(rows, C, x.device)
+        _lib.call("msu_layernorm_bwd", _dt(x), IN_PLAIN, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
+                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, C, 0, 0, 0, _s(x))
+        return dx, dw, db, None
+
+
+def layer_norm(x, weight, bias, eps=1e-5):
+    """nn.LayerNorm(C) over the last dim; x keeps its dtype."""
+    return _LayerNorm.apply(_as(x, act_dtype()), _f32(weight), _f32(bias), eps)
+
+
+class _AddLayerNorm(torch.autograd.Function):
+    """s = a + scale[b] * branch ; y = LN(s).  Returns (s, y)."""
+
+    @staticmethod
+    def forward(ctx, a, branch, scale, w, b, eps):
+        _need_cuda(a, branch)
+        a, branch = a.contiguous(), branch.contiguous()
+        C = a.shape[-1]
+        rows = a.numel() // C
+        rps = rows // a.shape[0]
+        s = torch.empty_like(a)
+        y = torch.empty_like(a)
+        mean = torch.empty(rows, device=a.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        _lib.call("msu_layernorm_fwd", _dt(a), IN_ADD, _p(a), _p(branch), _p(scale), rps, _p(s), _p(w),
+                  _p(b), _p(y), _p(mean), _p(rstd), rows, C, 0, 0, 0, eps, _s(a))
+        ctx.save_for_backward(s, w, mean, rstd, scale)
+        ctx.rps = rps
+        ctx.set_materialize_grads(False)
+        return s, y
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        s, w, mean, rstd, scale = ctx.saved_tensors
+        C = s.shape[-1]
+        rows = s.numel() // C
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dy = _as(dy, s.dtype)
+        ds = None if ds is None else _as(ds, s.dtype)
+        da = torch.empty_like(s)
+        dbr = torch.empty_like(s) if scale is not None else None
+        dw = torch.empty(C, device=s.device, dtype=torch.float32)
+        dbb = torch.empty_like(dw)
+        n, part = _ln_parts(rows, C, s.device)
+        _lib.call("msu_layernorm_bwd", _dt(s), IN_ADD, _p(dy), _p(s), _p(ds), _p(w), _p(mean), _p(rstd),
+                  _p(da), _p(dbr), _p(scale), ctx.rps, _p(part), n, _p(dw), _p(dbb), rows, C, 0, 0, 0, _s(s))
+        return da, (dbr if dbr is not None else da), None, dw, dbb, None
+
+
+def add_layer_norm(a, branch, scale, weight, bias, eps=1e-5):
+    dt = act_dtype()
+    sc = None if scale is None else _f32(scale)
+    return _AddLayerNorm.apply(_as(a, dt), _as(branch, dt), sc, _f32(weight), _f32(bias), eps)
+
+
+class _MergeLayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        _need_cuda(x)
+        x = x.contiguous()
+        B, H, W, C = x.shape
+        rows = B * (H // 2) * (W // 2)
+        y = torch.empty(B, rows // B, 4 * C, device=x.device, dtype=x.dtype)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        _lib.call("msu_layernorm_fwd", _dt(x), IN_MERGE, _p(x), None, None, 1, None, _p(w), _p(b),
+                  _p(y), _p(mean), _p(rstd), rows, 4 * C, H, W, C, eps, _s(x))
+        ctx.save_for_backward(x, w, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        B, H, W, C = x.shape
+        rows = B * (H // 2) * (W // 2)
+        dy = _as(dy, x.dtype)
+        dx = torch.empty_like(x)
+        dw = torch.empty(4 * C, device=x.device, dtype=torch.float32)
+        db = torch.empty_like(dw)
+        n, part = _ln_parts(rows, 4 * C, x.device)
+        _lib.call("msu_layernorm_bwd", _dt(x), IN_MERGE, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
+                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, 4 * C, H, W, C, _s(x))
+        return dx, dw, db, None
+
+
+def merge_layer_norm(x, weight, bias, eps=1e-5):
+    """PatchMerging gather (x0,x1,x2,x3 order) + LayerNorm(4C): [B,H,W,C] -> [B,HW/4,4C]."""
+    return _MergeLayerNorm.apply(_as(x, act_dtype()), _f32(weight), _f32(bias), eps)
+
+
+class _D2SLayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        _need_cuda(x)
+        x = x.contiguous()
+        B, H, W, C4 = x.shape
+        c = C4 // 4
+        rows = B * 4 * H * W
+        y = torch.empty(B, 4 * H * W, c, device=x.device, dtype=x.dtype)
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        _lib.call("msu_layernorm_fwd", _dt(x), IN_D2S2, _p(x), None, None, 1, None, _p(w), _p(b),
+                  _p(y), _p(mean), _p(rstd), rows, c, H, W, 0, eps, _s(x))
+        ctx.save_for_backward(x, w, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        B, H, W, C4 = x.shape
+        c = C4 // 4
+        rows = B * 4 * H * W
+        dy = _as(dy, x.dtype)
+        dx = torch.empty_like(x)
+        dw = torch.empty(c, device=x.device, dtype=torch.float32)
+        db = torch.empty_like(dw)
+        n, part = _ln_parts(rows, c, x.device)
+        _lib.call("msu_layernorm_bwd", _dt(x), IN_D2S2, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
+                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, c, H, W, 0, _s(x))
+        return dx, dw, db, None
+
+
+def d2s_layer_norm(x, weight, bias, eps=1e-5):
+    """PatchExpand rearrange 'b h w (p1 p2 c) -> b (h p1) (w p2) c' (p=2) + LayerNorm(c)."""
+    return _D2SLayerNorm.apply(_as(x, act_dtype()), _f32(weight), _f32(bias), eps)
+
+
+# ----------------------------------------------------------------------------- attention
+class _WindowAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, qkv_bias, table, num_heads, shift, p_drop, seed):
+        _need_cuda(qkv)
+        qkv = qkv.contiguous()
+        B, H, W, C3 = qkv.shape
+        C = C3 // 3
+        out = torch.empty(B, H, W, C, device=qkv.device, dtype=qkv.dtype)
+        _lib.call("msu_win_attn_fwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(out), B, H, W, C,
+                  num_heads, shift, float(p_drop), seed, _s(qkv))
+        ctx.save_for_backward(qkv, qkv_bias, table)
+        ctx.cfg = (num_heads, shift, float(p_drop), seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, qkv_bias, table = ctx.saved_tensors
+        nh, shift, p_drop, seed = ctx.cfg
+        B, H, W, C3 = qkv.shape
+        C = C3 // 3
+        dout = _as(dout, qkv.dtype)
+        L = _lib.lib()
+        nwin = L.msu_win_count(B, H, W)
+        nblk = int(max(1, min(nwin, 2048 // nh)))
+        ws = torch.empty(L.msu_win_attn_bwd_workspace(nblk, C, nh), device=qkv.device, dtype=torch.float32)
+        dqkv = torch.empty_like(qkv)
+        dtable = torch.empty_like(table)
+        dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
+        _lib.call("msu_win_attn_bwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
+                  _p(dtable), _p(dbias), _p(ws), nblk, B, H, W, C, nh, shift, p_drop, seed, _s(qkv))
+        return dqkv, dbias, dtable, None, None, None, None
+
+
+def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0):
+    """torchvision shifted_window_attention core between the qkv and proj Linears.
+    qkv: [B, H, W, 3C] (unpadded tokens) -> [B, H, W, C]."""
+    C3 = qkv.shape[-1]
+    if C3 % 3 or (C3 // 3) != num_heads * 32:
+        raise ValueError(f"head_dim must be 32 (C={C3 // 3}, heads={num_heads})")
+    return _WindowAttention.apply(_as(qkv, act_dtype()), _f32(qkv_bias), _f32(table), int(num_heads),
+                                  int(shift), float(p_drop), int(seed) & ((1 << 63) - 1))
+
+
+# ----------------------------------------------------------------------------- GELU
+class _Gelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        _need_cuda(x)
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        _lib.call("msu_gelu_fwd", _dt(x), _p(x), _p(y), x.numel(), _s(x))
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = _as(dy, x.dtype)
+        dx = torch.empty_like(x)
+        _lib.call("msu_gelu_bwd", _dt(x), _p(x), _p(dy), _p(dx), x.numel(), _s(x))
+        return dx
+
+
+def gelu(x):
+    """Exact (erf) GELU, nn.GELU()."""
+    return _Gelu.apply(_as(x, act_dtype()))
+
+
+# ----------------------------------------------------------------------------- head
+class _HeadNormOut(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, gamma, beta, w, eps):
+        _need_cuda(z)
+        z = z.contiguous()
+        B, H, W, C = z.shape
+        rows = B * H * W
+        logit = torch.empty(B, 1, H, W, device=z.device, dtype=torch.float32)
+        mean = torch.empty(rows, device=z.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        _lib.call("msu_head_fwd", _dt(z), _p(z), _p(gamma), _p(beta), _p(w), _p(logit), _p(mean),
+                  _p(rstd), rows, C, eps, _s(z))
+        ctx.save_for_backward(z, gamma, beta, w, mean, rstd)
+        return logit
+
+    @staticmethod
+    def backward(ctx, dlogit):
+        z, gamma, beta, w, mean, rstd = ctx.saved_tensors
+        B, H, W, C = z.shape
+        rows = B * H * W
+        dlogit = _f32(dlogit)
+        dz = torch.empty_like(z)
+        dg = torch.empty(C, device=z.device, dtype=torch.float32)
+        db, dw = torch.empty_like(dg), torch.empty_like(dg)
+        n, part = _ln_parts(rows, C, z.device)
+        _lib.call("msu_head_bwd", _dt(z), _p(dlogit), _p(z), _p(gamma), _p(beta), _p(w), _p(mean),
+                  _p(rstd), _p(dz), _p(part), n, _p(dg), _p(db), _p(dw), rows, C, _s(z))
+        return dz, dg, db, dw, None
+
+
+def head_norm_output(z, gamma, beta, out_weight, eps=1e-5):
+    """FinalPatchExpand_X4_V2.norm + bias-free 1x1 output conv (num_classes == 1).
+    z: [B, H, W, C] -> f32 logits [B, 1, H, W]."""
+    if out_weight.shape[0] != 1:
+        raise ValueError("fused head supports num_classes == 1")
+    C = z.shape[-1]
+    w = _f32(out_weight.reshape(C))
+    return _HeadNormOut.apply(_as(z, act_dtype()), _f32(gamma), _f32(beta), w, eps)
+
+
+# ----------------------------------------------------------------------------- conv 3x3
+def _pad_to(t, dim, mult):
+    n = t.shape[dim]
+    p = (n + mult - 1) // mult * mult - n
+    if p == 0:
+        return t
+    shape = list(t.shape)
+    shape[dim] = p
+    return torch.cat([t, t.new_zeros(shape)], dim)
+
+
+class _RefineConv(torch.autograd.Function):
+    """z = conv3x3(GELU(map(x)), W) + b, NHWC; map = identity or the 4x4 depth-to-space of
+    FinalPatchExpand_X4_V2 (x: [B, H/4, W/4, 16*Cin])."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, d2s, out_hw):
+        _need_cuda(x)
+        x = x.contiguous()
+        Cout, Cin = weight.shape[0], weight.shape[1]
+        B = x.shape[0]
+        H, W = out_hw
+        dt = x.dtype
+        wt = _pad_to(weight.permute(2, 3, 0, 1).reshape(9, Cout, Cin), 2, 32).to(dt).contiguous()
+        z = torch.empty(B, H, W, Cout, device=x.device, dtype=dt)
+        _lib.call("msu_conv3x3_fwd", _dt(x), 1 | (2 if d2s else 0), _p(x), _p(wt), _p(bias), _p(z),
+                  B, H, W, Cin, Cout, _s(x))
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (d2s, H, W)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, weight = ctx.saved_tensors
+        d2s, H, W = ctx.cfg
+        Cout, Cin = weight.shape[0], weight.shape[1]
+        B = x.shape[0]
+        dz = _as(dz, x.dtype)
+        mode = 1 | (2 if d2s else 0)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wf = _pad_to(weight.flip(2, 3).permute(2, 3, 1, 0).reshape(9, Cin, Cout), 2, 32)
+            wf = wf.to(x.dtype).contiguous()
+            dx = torch.empty_like(x)
+            _lib.call("msu_conv3x3_dgrad", _dt(x), mode, _p(dz), _p(wf), _p(x), _p(dx), B, H, W, Cin, Cout, _s(x))
+        L = _lib.lib()
+        nchunk = 256
+        ws = torch.empty(L.msu_conv3x3_wgrad_workspace(nchunk, Cin, Cout, 0, 0), device=x.device,
+                         dtype=torch.float32)
+        dw = torch.empty(Cout, Cin, 3, 3, device=x.device, dtype=torch.float32)
+        db = torch.empty(Cout, device=x.device, dtype=torch.float32)
+        _lib.call("msu_conv3x3_wgrad", _dt(x), mode, _p(x), _p(dz), _p(dw), _p(db), _p(ws), None, nchunk,
+                  B, H, W, Cin, Cout, _s(x))
+        return dx, dw, db, None, None
+
+
+def refine_conv(x, weight, bias, d2s, out_hw):
+    return _RefineConv.apply(_as(x, act_dtype()), _f32(weight), _f32(bias), bool(d2s), tuple(out_hw))
+
+
+# ----------------------------------------------------------------------------- patch embed
+def patchify(img, patch, dtype):
+    """[B, Cin, H, W] f32 image -> [B*(H/p)*(W/p), Cin*p*p] im2col rows (no grad)."""
+    _need_cuda(img)
+    img = _f32(img)
+    B, Cin, H, W = img.shape
+    out = torch.empty(B * (H // patch) * (W // patch), Cin * patch * patch, device=img.device, dtype=dtype)
+    _lib.call("msu_patchify", _DT[dtype], _p(img), _p(out), B, Cin, H, W, patch, _s(img))
+    return out
+
+
+# ----------------------------------------------------------------------------- loss
+class _DynamicLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, alpha, beta, mix):
+        _need_cuda(logits, target)
+        logits = logits.contiguous()
+        target = _f32(target)
+        B = logits.shape[0]
+        N = logits[0].numel()
+        L = _lib.lib()
+        nblk = L.msu_dynloss_nblk(N)
+        part = torch.empty(B * nblk * 12, device=logits.device, dtype=torch.float32)
+        out = torch.empty(2, device=logits.device, dtype=torch.float32)
+        coef = torch.empty(B * 4, device=logits.device, dtype=torch.float32)
+        _lib.call("msu_dynloss_fwd", _dt(logits), _p(logits), _p(target), B, N, alpha, beta, mix,
+                  _p(part), nblk, _p(out), _p(coef), _s(logits))
+        ctx.save_for_backward(logits, target, coef, out)
+        ctx.cfg = (alpha, beta, mix)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, target, coef, out = ctx.saved_tensors
+        alpha, beta, mix = ctx.cfg
+        B = logits.shape[0]
+        N = logits[0].numel()
+        g = _f32(g.reshape(1))
+        dl = torch.empty(logits.shape, device=logits.device, dtype=torch.float32)
+        _lib.call("msu_dynloss_bwd", _dt(logits), _p(logits), _p(target), _p(coef), _p(out), _p(g), B, N,
+                  alpha, beta, mix, _p(dl), _s(logits))
+        return dl.to(logits.dtype), None, None, None, None
+
+
+def dynamic_loss(logits, target, alpha, beta, mix):
+    if target.dim() == 3:
+        target = target.unsqueeze(1)
+    if logits.shape[0] != target.shape[0]:
+        raise ValueError(f"Batchsize from ouptut {logits.shape[0]} not equal to batchsize target {target.shape[0]}")
+    if logits.shape[1:] != target.shape[1:]:
+        raise ValueError(f"target shape {tuple(target.shape)} does not match output {tuple(logits.shape)}")
+    return _DynamicLoss.apply(logits, target, float(alpha), float(beta), float(mix))
+
+
+# ----------------------------------------------------------------------------- optimizer
+def adamw_(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step,
+           inv_scale=None, found_inf=None):
+    """In-place torch.optim.AdamW update over flat f32 buffers (one launch)."""
+    _need_cuda(param)
+    _lib.call("msu_adamw", _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), lr, beta1,
+              beta2, eps, weight_decay, int(step), _p(inv_scale), _p(found_inf), _s(param))
+
+
+def nonfinite_(x, flag):
+    _lib.call("msu_nonfinite", _p(x), x.numel(), _p(flag), _s(x))

@@ -1,0 +1,341 @@
+"""GPU parity of every HIP op against the CPU oracle / a plain fp32 PyTorch reference.
+
+fp32 mode: tolerance 1e-4 relative (kernels compute in f32; only summation order differs).
+bf16 mode: tolerance stated per test (bf16 storage has 8 significant bits).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from oracle import swin_block as osb  # noqa: E402
+from oracle import msunet as om  # noqa: E402
+from oracle import dynamic_loss as odl  # noqa: E402
+
+DEV = "cuda"
+
+
+def _ops():
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    return ops
+
+
+def _close(a, b, rtol, atol, what=""):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item()
+    assert err <= atol + rtol * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def _g(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 3e-2)])
+@pytest.mark.parametrize("C,rows", [(96, 1000), (32, 64), (384, 333), (1536, 77)])
+def test_layer_norm(dtype, tol, C, rows):
+    ops = _ops()
+    g = _g(C)
+    x = (torch.randn(rows, C, generator=g) * 2 + 0.5)
+    w = 1 + 0.1 * torch.randn(C, generator=g)
+    b = 0.1 * torch.randn(C, generator=g)
+    dy = torch.randn(rows, C, generator=g)
+    xr = x.clone().requires_grad_(True); wr = w.clone().requires_grad_(True); br = b.clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (C,), wr, br, 1e-5)
+    yr.backward(dy)
+    xg = x.to(DEV, dtype).requires_grad_(True)
+    wg = w.to(DEV).requires_grad_(True)
+    bg = b.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        y = ops.layer_norm(xg, wg, bg)
+    y.backward(dy.to(DEV, dtype))
+    _close(y, yr, tol, tol, "y")
+    _close(xg.grad, xr.grad, tol, tol, "dx")
+    _close(wg.grad, wr.grad, tol, tol * rows ** 0.5, "dw")
+    _close(bg.grad, br.grad, tol, tol * rows ** 0.5, "db")
+
+
+@pytest.mark.parametrize("use_scale", [False, True])
+def test_add_layer_norm(use_scale):
+    ops = _ops()
+    g = _g(7)
+    B, H, W, C = 3, 5, 6, 192
+    a = torch.randn(B, H, W, C, generator=g)
+    br = torch.randn(B, H, W, C, generator=g)
+    sc = torch.tensor([0.0, 1.25, 1.25]) if use_scale else None
+    w = 1 + 0.1 * torch.randn(C, generator=g)
+    bb = 0.1 * torch.randn(C, generator=g)
+    ds_up = torch.randn(B, H, W, C, generator=g)
+    dy_up = torch.randn(B, H, W, C, generator=g)
+    ar, brr, wr, bbr = [t.clone().requires_grad_(True) for t in (a, br, w, bb)]
+    s_ref = ar + brr * (sc.view(B, 1, 1, 1) if sc is not None else 1.0)
+    y_ref = F.layer_norm(s_ref, (C,), wr, bbr, 1e-5)
+    (s_ref * ds_up + y_ref * dy_up).sum().backward()
+    ag, bgg, wg, bbg = [t.to(DEV).requires_grad_(True) for t in (a, br, w, bb)]
+    s, y = ops.add_layer_norm(ag, bgg, sc.to(DEV) if sc is not None else None, wg, bbg)
+    (s * ds_up.to(DEV) + y * dy_up.to(DEV)).sum().backward()
+    _close(s, s_ref, 1e-5, 1e-5, "s")
+    _close(y, y_ref, 1e-4, 1e-4, "y")
+    _close(ag.grad, ar.grad, 1e-4, 1e-4, "da")
+    _close(bgg.grad, brr.grad, 1e-4, 1e-4, "dbranch")
+    _close(wg.grad, wr.grad, 1e-4, 1e-3, "dw")
+    _close(bbg.grad, bbr.grad, 1e-4, 1e-3, "db")
+
+
+@pytest.mark.parametrize("B,H,W,C", [(2, 8, 8, 16), (1, 14, 10, 96), (2, 64, 64, 96)])
+def test_merge_layer_norm(B, H, W, C):
+    ops = _ops()
+    g = _g(H * W)
+    x = torch.randn(B, H, W, C, generator=g)
+    w = 1 + 0.1 * torch.randn(4 * C, generator=g)
+    b = 0.1 * torch.randn(4 * C, generator=g)
+    xr = x.clone().requires_grad_(True)
+    x0, x1, x2, x3 = xr[:, 0::2, 0::2], xr[:, 1::2, 0::2], xr[:, 0::2, 1::2], xr[:, 1::2, 1::2]
+    yr = F.layer_norm(torch.cat([x0, x1, x2, x3], -1).view(B, -1, 4 * C), (4 * C,), w, b, 1e-5)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    xg = x.to(DEV).requires_grad_(True)
+    y = ops.merge_layer_norm(xg, w.to(DEV), b.to(DEV))
+    y.backward(dy.to(DEV))
+    _close(y, yr, 1e-4, 1e-4, "y")
+    _close(xg.grad, xr.grad, 1e-4, 1e-4, "dx")
+
+
+@pytest.mark.parametrize("B,H,W,c", [(2, 4, 4, 16), (1, 7, 5, 48), (2, 32, 32, 96)])
+def test_d2s_layer_norm(B, H, W, c):
+    from einops import rearrange
+    ops = _ops()
+    g = _g(c)
+    x = torch.randn(B, H, W, 4 * c, generator=g)
+    w = 1 + 0.1 * torch.randn(c, generator=g)
+    b = 0.1 * torch.randn(c, generator=g)
+    xr = x.clone().requires_grad_(True)
+    yr = F.layer_norm(rearrange(xr, "b h w (p1 p2 c)-> b (h p1) (w p2) c", p1=2, p2=2, c=c).reshape(B, -1, c),
+                      (c,), w, b, 1e-5)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    xg = x.to(DEV).requires_grad_(True)
+    y = ops.d2s_layer_norm(xg, w.to(DEV), b.to(DEV))
+    y.backward(dy.to(DEV))
+    _close(y, yr, 1e-4, 1e-4, "y")
+    _close(xg.grad, xr.grad, 1e-4, 1e-4, "dx")
+
+
+ATTN_CASES = [
+    # B, H, W, heads, shift
+    (2, 8, 8, 1, 3),     # pad 8 -> 14, shifted
+    (1, 14, 14, 2, 0),   # no pad, no shift
+    (1, 14, 14, 2, 3),   # no pad, shifted
+    (2, 7, 7, 3, 3),     # window covers the map -> torchvision zeroes the shift
+    (1, 10, 12, 2, 3),   # non-square, padded both axes
+    (2, 28, 28, 3, 3),
+    (1, 16, 16, 4, 0),   # pad 16 -> 21, padded tokens attend unmasked
+]
+
+
+@pytest.mark.parametrize("B,H,W,nh,shift", ATTN_CASES)
+def test_window_attention_fp32(B, H, W, nh, shift):
+    """ops.window_attention (qkv Linear outside) == torchvision v1 restatement, fwd + bwd."""
+    ops = _ops()
+    C = 32 * nh
+    g = _g(B * H * W + nh)
+    x = torch.randn(B, H, W, C, generator=g)
+    qw = torch.randn(3 * C, C, generator=g) / math.sqrt(C)
+    qb = 0.3 * torch.randn(3 * C, generator=g)
+    table = torch.randn(169, nh, generator=g)
+    index = osb.relative_position_index(7)
+    eye, zero = torch.eye(C), torch.zeros(C)
+    xr, qwr, qbr, tr = [t.clone().requires_grad_(True) for t in (x, qw, qb, table)]
+    yr = osb.shifted_window_attention(xr, qwr, qbr, eye, zero, tr, index, 7, nh, shift)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    xg, qwg, qbg, tg = [t.to(DEV).requires_grad_(True) for t in (x, qw, qb, table)]
+    qkv = F.linear(xg, qwg, qbg)
+    y = ops.window_attention(qkv, qbg, tg, nh, shift)
+    y.backward(dy.to(DEV))
+    _close(y, yr, 1e-4, 1e-5, "out")
+    _close(xg.grad, xr.grad, 1e-4, 1e-5, "dx")
+    _close(qwg.grad, qwr.grad, 1e-4, 1e-5, "dWqkv")
+    _close(qbg.grad, qbr.grad, 1e-4, 1e-5, "dbqkv (incl. padded tokens)")
+    _close(tg.grad, tr.grad, 1e-4, 1e-5, "d relative_position_bias_table")
+
+
+@pytest.mark.parametrize("B,H,W,nh,shift", [(2, 8, 8, 1, 3), (1, 28, 28, 3, 3), (2, 64, 64, 3, 0)])
+def test_window_attention_bf16(B, H, W, nh, shift):
+    ops = _ops()
+    C = 32 * nh
+    g = _g(3 + H)
+    qkv = torch.randn(B, H, W, 3 * C, generator=g)
+    qb = 0.3 * torch.randn(3 * C, generator=g)
+    table = torch.randn(169, nh, generator=g)
+    y32 = ops.window_attention(qkv.to(DEV), qb.to(DEV), table.to(DEV), nh, shift)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y16 = ops.window_attention(qkv.to(DEV), qb.to(DEV), table.to(DEV), nh, shift)
+    assert y16.dtype == torch.bfloat16
+    _close(y16, y32, 3e-2, 3e-2, "bf16 vs f32")
+
+
+def test_window_attention_dropout_statistics():
+    """p=0 is exact; with p>0 the kept fraction is ~1-p and output is unbiased; fwd/bwd use
+    the same mask (checked via linearity: <dy, y> == <dqkv_v, v> for the v-part)."""
+    ops = _ops()
+    B, H, W, nh, C = 2, 28, 28, 2, 64
+    g = _g(99)
+    qkv = torch.randn(B, H, W, 3 * C, generator=g).to(DEV)
+    qb = torch.zeros(3 * C, device=DEV)
+    table = torch.zeros(169, nh, device=DEV)
+    y0 = ops.window_attention(qkv, qb, table, nh, 0, 0.0, 1)
+    ys = torch.stack([ops.window_attention(qkv, qb, table, nh, 0, 0.25, s) for s in range(64)])
+    rel = ((ys.mean(0) - y0).norm() / y0.norm()).item()
+    assert rel < 0.1, rel
+    assert not torch.equal(ys[0], ys[1])
+    q = qkv.clone().requires_grad_(True)
+    y = ops.window_attention(q, qb, table, nh, 0, 0.5, 1234)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    v = q[..., 2 * C:]
+    lhs = (dy * y).sum()
+    rhs = (q.grad[..., 2 * C:] * v).sum()
+    assert abs(lhs.item() - rhs.item()) <= 1e-3 * abs(lhs.item()) + 1e-3
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+def test_gelu(dtype, tol):
+    ops = _ops()
+    x = torch.randn(4096, generator=_g(1)) * 3
+    xr = x.clone().requires_grad_(True)
+    yr = F.gelu(xr)
+    yr.backward(torch.ones_like(x))
+    xg = x.to(DEV, dtype).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        y = ops.gelu(xg)
+    y.backward(torch.ones_like(y))
+    _close(y, yr, tol, tol, "gelu")
+    _close(xg.grad, xr.grad, tol, tol, "gelu'")
+
+
+CONV_CASES = [
+    # B, H, W (output), C, d2s
+    (2, 24, 24, 16, True),
+    (1, 32, 20, 32, True),
+    (1, 20, 36, 32, False),
+    (2, 64, 64, 96, True),
+    (1, 48, 32, 96, False),
+    (1, 32, 32, 128, True),
+]
+
+
+def _conv_ref(x, w, b, d2s, H, W):
+    from einops import rearrange
+    C = w.shape[1]
+    if d2s:
+        x = rearrange(x, "b h w (p1 p2 c) -> b (h p1) (w p2) c", p1=4, p2=4, c=C)
+    x = F.gelu(x).permute(0, 3, 1, 2)
+    return F.conv2d(x, w, b, padding=1).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("B,H,W,C,d2s", CONV_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_refine_conv(B, H, W, C, d2s, dtype):
+    ops = _ops()
+    g = _g(H * W + C)
+    xs = (B, H // 4, W // 4, 16 * C) if d2s else (B, H, W, C)
+    x = torch.randn(xs, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    b = 0.1 * torch.randn(C, generator=g)
+    dz = torch.randn(B, H, W, C, generator=g)
+    xr, wr, br = [t.clone().requires_grad_(True) for t in (x, w, b)]
+    zr = _conv_ref(xr, wr, br, d2s, H, W)
+    zr.backward(dz)
+    xg = x.to(DEV, dtype).requires_grad_(True)
+    wg, bg = w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        z = ops.refine_conv(xg, wg, bg, d2s, (H, W))
+    z.backward(dz.to(DEV, dtype))
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    _close(z, zr, tol, tol, "z")
+    _close(xg.grad, xr.grad, tol, tol, "dx")
+    _close(wg.grad, wr.grad, tol, tol, "dW")
+    _close(bg.grad, br.grad, tol, tol, "db")
+
+
+def test_head_norm_output():
+    ops = _ops()
+    g = _g(5)
+    B, H, W, C = 2, 16, 12, 96
+    z = torch.randn(B, H, W, C, generator=g)
+    gm = 1 + 0.1 * torch.randn(C, generator=g)
+    bt = 0.1 * torch.randn(C, generator=g)
+    wo = torch.randn(1, C, 1, 1, generator=g) / math.sqrt(C)
+    zr, gr, btr, wr = [t.clone().requires_grad_(True) for t in (z, gm, bt, wo)]
+    yr = F.conv2d(F.layer_norm(zr, (C,), gr, btr, 1e-5).permute(0, 3, 1, 2), wr)
+    dl = torch.randn(yr.shape, generator=g)
+    yr.backward(dl)
+    zg, gg, bg, wg = [t.to(DEV).requires_grad_(True) for t in (z, gm, bt, wo)]
+    y = ops.head_norm_output(zg, gg, bg, wg)
+    y.backward(dl.to(DEV))
+    _close(y, yr, 1e-4, 1e-5, "logits")
+    _close(zg.grad, zr.grad, 1e-4, 1e-5, "dz")
+    _close(gg.grad, gr.grad, 1e-4, 1e-4, "dgamma")
+    _close(bg.grad, btr.grad, 1e-4, 1e-4, "dbeta")
+    _close(wg.grad, wr.grad, 1e-4, 1e-4, "dw_out")
+
+
+def test_patchify_matches_conv():
+    ops = _ops()
+    g = _g(6)
+    img = torch.rand(2, 3, 32, 48, generator=g)
+    w = torch.randn(96, 3, 4, 4, generator=g)
+    b = torch.randn(96, generator=g)
+    ref = F.conv2d(img, w, b, stride=4).flatten(2).transpose(1, 2).reshape(-1, 96)
+    cols = ops.patchify(img.to(DEV), 4, torch.float32)
+    out = F.linear(cols, w.to(DEV).reshape(96, -1), b.to(DEV))
+    _close(out, ref, 1e-5, 1e-5, "patch embed")
+
+
+def test_dynamic_loss_golden(golden_dir):
+    import os
+    import cases
+    from semantic_segmentation_of_stylegan2_artifacts_amd.loss import DynamicLoss
+    z = np.load(os.path.join(golden_dir, "dynamic_loss.npz"))
+    for name, (logits, target, kw) in cases.loss_cases().items():
+        lossf = DynamicLoss(alpha=kw["alpha"], beta=kw["beta"], tversky_bce_mix=kw["mix"])
+        x = logits.to(DEV).requires_grad_(True)
+        loss = lossf(x, target.to(DEV))
+        loss.backward()
+        ref = float(z[f"{name}.loss"])
+        assert abs(loss.item() - ref) <= 1e-5 * max(1, abs(ref)), name
+        _close(x.grad, torch.from_numpy(z[f"{name}.grad"]), 1e-4, 1e-9, name)
+
+
+def test_dynamic_loss_bf16_logits():
+    from semantic_segmentation_of_stylegan2_artifacts_amd.loss import DynamicLoss
+    import cases
+    logits, target, kw = cases.loss_cases()["mixed3d"]
+    lb = logits.to(torch.bfloat16)
+    ref = odl.dynamic_loss(lb.float(), target, **kw)
+    out = DynamicLoss(alpha=kw["alpha"], beta=kw["beta"], tversky_bce_mix=kw["mix"])(lb.to(DEV), target.to(DEV))
+    assert abs(out.item() - ref.item()) < 1e-5
+
+
+def test_adamw_matches_torch():
+    ops = _ops()
+    g = _g(8)
+    n = 10007
+    p0 = torch.randn(n, generator=g)
+    grads = [torch.randn(n, generator=g) for _ in range(5)]
+    pr = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([pr], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
+    pg = p0.to(DEV)
+    m = torch.zeros_like(pg)
+    v = torch.zeros_like(pg)
+    for step, gr in enumerate(grads, 1):
+        pr.grad = gr.clone()
+        opt.step()
+        ops.adamw_(pg, gr.to(DEV), m, v, 1e-3, 0.9, 0.999, 1e-8, 0.01, step)
+    _close(pg, pr, 1e-6, 1e-6, "adamw")
