@@ -1,0 +1,175 @@
+"""Training step of ``trainer.py:295-336`` re-planned for MI355X data parallelism.
+
+Reference step (per batch): autocast fp16 -> model -> DynamicLoss -> GradScaler backward ->
+AdamW (two param groups, ``trainer.py:130-152``) -> ``loss.item()``; multi-GPU via
+``nn.DataParallel`` (``trainer.py:96-97``; unusable for N_GPU > 1 because the batch
+sampler requires batch_size == 2).
+
+Here:
+* one process per GPU (torchrun env), bf16 autocast (no loss scaling needed), no host
+  synchronisation inside the step (the loss stays on the device);
+* trainable parameters and their gradients live in two flat f32 buffers (weight-decay /
+  no-decay, the reference's split rule) laid out in reverse registration order, so
+  gradients become ready roughly front-to-back during backward;
+* DP: the gradient buffers are cut into ~``bucket_mb`` buckets; when every parameter of a
+  bucket has accumulated its gradient (post-accumulate hooks) the bucket is all-reduced
+  (RCCL over xGMI, ``async_op``) while backward continues; the 1/world average is folded
+  into the fused AdamW kernel;
+* AdamW = one fused HIP launch per group over the flat buffer;
+* parameters whose outputs the reference discards (dead central-decoder branches) never
+  receive gradients there; they are excluded here, matching torch AdamW's skip of
+  ``grad is None``.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .loss import DynamicLoss
+
+
+def is_no_decay(name, param):
+    """``trainer.py:137``: 1-D params, biases and anything with 'norm' in its name."""
+    return param.ndim == 1 or name.endswith(".bias") or "norm" in name.lower()
+
+
+def cosine_lr(epoch, base_lr, warmup_epochs, max_epochs, warmup_lr, min_lr, warmup_prefix=True):
+    """timm CosineLRScheduler(t_initial=lr_epochs - warmup, warmup_prefix, cycle_limit=1),
+    stepped per epoch as in ``trainer.py:155-169, :412`` (lr_epochs = max(60, max_epochs))."""
+    lr_epochs = max(60, max_epochs)
+    t_initial = lr_epochs - warmup_epochs
+    if epoch < warmup_epochs:
+        return warmup_lr + epoch * (base_lr - warmup_lr) / warmup_epochs
+    t = epoch - warmup_epochs if warmup_prefix else epoch
+    if t >= t_initial:
+        return min_lr
+    return min_lr + 0.5 * (base_lr - min_lr) * (1 + math.cos(math.pi * t / t_initial))
+
+
+class FlatGroup:
+    """Parameters (and grads) of one optimizer group re-homed into flat f32 buffers."""
+
+    def __init__(self, named_params, weight_decay, device):
+        self.names = [n for n, _ in named_params]
+        self.params = [p for _, p in named_params]
+        self.weight_decay = weight_decay
+        n = sum(p.numel() for p in self.params)
+        self.numel = n
+        self.data = torch.empty(n, device=device, dtype=torch.float32)
+        self.grad = torch.zeros(n, device=device, dtype=torch.float32)
+        self.exp_avg = torch.zeros_like(self.data)
+        self.exp_avg_sq = torch.zeros_like(self.data)
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            self.data[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.data[off:off + k].view_as(p)
+            p.grad = self.grad[off:off + k].view_as(p)
+            self.offsets.append(off)
+            off += k
+
+
+class GradBucketer:
+    """Bucketed, backward-overlapped gradient all-reduce over flat gradient buffers."""
+
+    def __init__(self, groups, bucket_bytes, process_group=None):
+        self.pg = process_group
+        self.buckets = []       # (group, start, end, n_params)
+        self.param_bucket = {}  # id(param) -> bucket index
+        for g in groups:
+            start = 0
+            count = 0
+            for p, off in zip(g.params, g.offsets):
+                end = off + p.numel()
+                self.param_bucket[id(p)] = len(self.buckets)
+                count += 1
+                if (end - start) * 4 >= bucket_bytes:
+                    self.buckets.append([g, start, end, count])
+                    start, count = end, 0
+            if count:
+                self.buckets.append([g, start, g.numel, count])
+        self.pending = [0] * len(self.buckets)
+        self.works = []
+        self.handles = []
+        for g in groups:
+            for p in g.params:
+                self.handles.append(p.register_post_accumulate_grad_hook(self._hook))
+
+    def _hook(self, p):
+        b = self.param_bucket[id(p)]
+        self.pending[b] += 1
+        if self.pending[b] == self.buckets[b][3]:
+            g, s, e, _ = self.buckets[b]
+            self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+
+    def finish(self):
+        for b, (g, s, e, n) in enumerate(self.buckets):
+            if self.pending[b] != n:  # parameters that did not receive a gradient this step
+                self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg,
+                                                  async_op=True))
+        for w in self.works:
+            w.wait()
+        self.works = []
+        self.pending = [0] * len(self.buckets)
+
+
+class Trainer:
+    def __init__(self, model, config, device, lr=None, amp_dtype=torch.bfloat16, bucket_mb=32,
+                 world_size=1, process_group=None):
+        self.model = model
+        self.device = device
+        self.amp_dtype = amp_dtype
+        core = model.ms_unet if hasattr(model, "ms_unet") else model
+        dead = set()
+        if hasattr(core, "dead_modules"):
+            for m in core.dead_modules():
+                dead.update(id(p) for p in m.parameters())
+        decay, no_decay = [], []
+        for name, p in model.named_parameters():
+            if not p.requires_grad or id(p) in dead:
+                continue
+            (no_decay if is_no_decay(name, p) else decay).append((name, p))
+        # reverse registration order ~ gradient-ready order during backward
+        self.groups = [FlatGroup(decay[::-1], config.TRAIN.WEIGHT_DECAY, device),
+                       FlatGroup(no_decay[::-1], 0.0, device)]
+        opt = config.TRAIN.OPTIMIZER
+        self.betas = tuple(opt.BETAS)
+        self.eps = float(opt.EPS)
+        self.lr = float(config.TRAIN.BASE_LR if lr is None else lr)
+        t = config.TRAIN
+        self.loss_fn = DynamicLoss(alpha=t.TVERSKY_LOSS_ALPHA, beta=t.TVERSKY_LOSS_BETA,
+                                   tversky_bce_mix=t.LOSS_TVERSKY_BCE_MIX)
+        self.world_size = world_size
+        self.step_count = 0
+        self.inv_world = torch.full((1,), 1.0 / world_size, device=device, dtype=torch.float32)
+        self.reducer = GradBucketer(self.groups, bucket_mb << 20, process_group) if world_size > 1 else None
+
+    def num_params(self):
+        return sum(g.numel for g in self.groups)
+
+    def set_epoch(self, epoch, config):
+        t = config.TRAIN
+        self.lr = cosine_lr(epoch, t.BASE_LR, t.WARMUP_EPOCHS, t.MAX_EPOCHS, t.WARMUP_LR, t.MIN_LR,
+                            t.LR_SCHEDULER.WARMUP_PREFIX)
+
+    def forward_loss(self, images, labels):
+        with torch.autocast("cuda", dtype=self.amp_dtype, enabled=self.amp_dtype != torch.float32):
+            out = self.model(images)
+            return self.loss_fn(out, labels)
+
+    def step(self, images, labels):
+        """One training step; returns the (device) loss of this rank's batch."""
+        self.model.train()
+        loss = self.forward_loss(images, labels)
+        loss.backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        self.step_count += 1
+        inv = self.inv_world if self.world_size > 1 else None
+        for g in self.groups:
+            ops.adamw_(g.data, g.grad, g.exp_avg, g.exp_avg_sq, self.lr, self.betas[0], self.betas[1],
+                       self.eps, g.weight_decay, self.step_count, inv_scale=inv)
+            g.grad.zero_()
+        return loss.detach()
