@@ -96,6 +96,17 @@ int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, flo
                       float* workspace, void* unused, int nchunk, int B, int H, int W, int Cin,
                       int Cout, void* stream);
 
+/* ---------------------------------------------------------------- Linear weight gradient
+ * Every nn.Linear on the path (torchvision block qkv / proj / mlp.0 / mlp.3,
+ * PatchMerging.reduction model_parts.py:72, PatchExpand.expand :379, concat_back_dim
+ * :639-641, FinalPatchExpand_X4_V2.expand :443, PatchEmbed.proj :211 as im2col GEMM):
+ * dW[N][K] = sum_m dY[m][n] X[m][k], db[n] = sum_m dY[m][n] (db may be null), split over M
+ * on MFMA; workspace f32 elements from msu_wgrad_workspace. */
+int msu_wgrad_splits(long M, int N, int K);
+long msu_wgrad_workspace(long M, int N, int K);
+int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float* db, float* workspace,
+                     long M, int N, int K, int accumulate, void* stream);
+
 /* ---------------------------------------------------------------- streaming ops
  * nn.GELU() (exact erf): torchvision MLP activation, FinalPatchExpand_X4_V2.act. */
 int msu_gelu_fwd(int dtype, const void* x, void* y, long n, void* stream);

@@ -39,6 +39,9 @@ SIGNATURES = {
     "msu_conv3x3_dgrad": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),
     "msu_conv3x3_wgrad_workspace": (L, [I, I, I, I, I]),
     "msu_conv3x3_wgrad": (I, [I, I, P, P, P, P, P, P, I, I, I, I, I, I, P]),
+    "msu_wgrad_splits": (I, [L, I, I]),
+    "msu_wgrad_workspace": (L, [L, I, I]),
+    "msu_linear_wgrad": (I, [I, P, P, P, P, P, L, I, I, I, P]),
 }
 
 _lib = None

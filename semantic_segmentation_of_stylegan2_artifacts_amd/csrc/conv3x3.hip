@@ -12,11 +12,9 @@
 // weights).  wgrad reads both operands k-strided from natural [pixel][channel] LDS images
 // with ds_read_b64_tr_b16 (bf16) and writes deterministic per-block partials.
 #include "common.h"
+#include "mfma_frag.h"
 
 namespace {
-
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef short v4s __attribute__((ext_vector_type(4)));
 
 constexpr int TW = 16;  // output tile width (pixels) = one MFMA M tile
 
@@ -210,36 +208,6 @@ __global__ void __launch_bounds__(64 * (TH / MT)) conv3x3_kernel(const T* __rest
 // dW[dy][co][dx][ci] partial per block: sum over the block's pixel tiles of
 //   DY[pixel][co] * Xt[pixel + (dy-1, dx-1)][ci];  one block = one dy, NT waves (one per
 //   co tile), each wave 3 * CinP/16 n-tiles.  dbias partial from the dy == 0 blocks.
-template <typename T> struct TR;
-template <> struct TR<bf16_t> {
-  // 16x16x32 operand fragment from a [k rows][cols] bf16 LDS image, rows given per lane
-  // by row_ptr (element pointer of row k), columns col0 .. col0+15 (ds_read_b64_tr_b16).
-  template <typename RowFn>
-  static MSU_DEV bf16x8 frag(RowFn row_ptr, int kbase, int col0, int lane) {
-    const int gq = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-    const bf16_t* a0 = row_ptr(kbase + 8 * gq + q) + col0 + 4 * p;
-    const bf16_t* a1 = row_ptr(kbase + 8 * gq + 4 + q) + col0 + 4 * p;
-    typedef __attribute__((address_space(3))) v4s lds_v4s;
-    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a0));
-    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a1));
-    v4s both[2] = {lo, hi};
-    return *reinterpret_cast<bf16x8*>(both);
-  }
-  template <typename RA, typename RB>
-  static MSU_DEV void mma(f32x4& acc, RA ra, int colA, RB rb, int colB, int kbase, int lane) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(ra, kbase, colA, lane), frag(rb, kbase, colB, lane), acc, 0, 0, 0);
-  }
-};
-template <> struct TR<float> {
-  template <typename RA, typename RB>
-  static MSU_DEV void mma(f32x4& acc, RA ra, int colA, RB rb, int colB, int kbase, int lane) {
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int k = kbase + 4 * s + (lane >> 4);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra(k)[colA + (lane & 15)], rb(k)[colB + (lane & 15)], acc, 0, 0, 0);
-    }
-  }
-};
 
 template <typename T, int NT, int NTI, int TH, bool IN_D2S, bool IN_GELU>
 __global__ void __launch_bounds__(64 * NT) conv3x3_wgrad_kernel(const T* __restrict__ X,

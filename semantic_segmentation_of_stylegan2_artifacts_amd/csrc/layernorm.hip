@@ -9,6 +9,7 @@
 //   * head             FinalPatchExpand_X4_V2.norm + 1x1 output conv (model_parts.py:475,846)
 // One row is owned by TPR lanes; each lane holds KMAX 4-wide chunks in registers.
 #include "common.h"
+#include "reduce.h"
 
 namespace {
 
@@ -239,15 +240,6 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
   }
 }
 
-// Sum `nparts` rows of [nparts, n] f32 partials into out[n] (deterministic order).
-__global__ void __launch_bounds__(256) reduce_rows_kernel(const float* part, int nparts, int n,
-                                                          long stride, float* out, int accumulate) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(long)p * stride + i];
-  out[i] = accumulate ? out[i] + s : s;
-}
 
 template <typename T, int MODE>
 int launch_fwd(const LnArgs& a, hipStream_t st, int max_blocks) {
@@ -297,11 +289,8 @@ int bwd_dispatch(int dtype, const LnBwdArgs& a, float* dgamma, float* dbeta, int
   if (a.rows == 0) return 0;
   int rc = dtype == MSU_BF16 ? launch_bwd<bf16_t, MODE>(a, st, nparts) : launch_bwd<float, MODE>(a, st, nparts);
   if (rc) return rc;
-  const int nb = (a.C + 255) / 256;
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(nb), dim3(256), 0, st, a.part, nparts, a.C,
-                     (long)2 * a.C, dgamma, 0);
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(nb), dim3(256), 0, st, a.part + a.C, nparts, a.C,
-                     (long)2 * a.C, dbeta, 0);
+  colsum(a.part, nparts, a.C, (long)2 * a.C, dgamma, 0, st);
+  colsum(a.part + a.C, nparts, a.C, (long)2 * a.C, dbeta, 0, st);
   return MSU_CHECK_LAUNCH();
 }
 
@@ -466,10 +455,9 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
     if (C <= 128) hipLaunchKernelGGL((head_bwd_kernel<float, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const float*)z, gamma, beta, w, mean, rstd, (float*)dz, part, rows, C);
     else hipLaunchKernelGGL((head_bwd_kernel<float, 8>), dim3(nparts), dim3(256), 0, st, dlogit, (const float*)z, gamma, beta, w, mean, rstd, (float*)dz, part, rows, C);
   }
-  const int nb = (C + 255) / 256;
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(nb), dim3(256), 0, st, part, nparts, C, (long)3 * C, dgamma, 0);
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(nb), dim3(256), 0, st, part + C, nparts, C, (long)3 * C, dbeta, 0);
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(nb), dim3(256), 0, st, part + 2 * C, nparts, C, (long)3 * C, dw, 0);
+  colsum(part, nparts, C, (long)3 * C, dgamma, 0, st);
+  colsum(part + C, nparts, C, (long)3 * C, dbeta, 0, st);
+  colsum(part + 2 * C, nparts, C, (long)3 * C, dw, 0, st);
   return MSU_CHECK_LAUNCH();
 }
 
@@ -515,8 +503,7 @@ int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const 
 
 int msu_reduce_rows(const float* part, int nparts, int n, long stride, float* out,
                     int accumulate, void* stream) {
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((n + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, part, nparts, n, stride, out, accumulate);
+  colsum(part, nparts, n, stride, out, accumulate, (hipStream_t)stream);
   return MSU_CHECK_LAUNCH();
 }
 

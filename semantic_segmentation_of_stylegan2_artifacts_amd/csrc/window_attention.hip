@@ -16,6 +16,7 @@
 // k-contiguous (one 16-B read per fragment) or k-strided (8 scalar reads) so no transposed
 // copies are staged; softmax runs in registers one 16-row block at a time.
 #include "common.h"
+#include "reduce.h"
 
 namespace {
 
@@ -358,13 +359,6 @@ __global__ void __launch_bounds__(64, 2) win_attn_bwd_kernel(
     }
 }
 
-__global__ void __launch_bounds__(256) sum_parts_kernel(const float* part, int nparts, long n, float* out) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(long)p * n + i];
-  out[i] = s;
-}
 
 // dB [nh, 49*49] -> d_table [169, nh]: gather the (i, j) pairs of each relative offset
 __global__ void __launch_bounds__(256) rel_table_grad_kernel(const float* dB, int nh, float* dtable) {
@@ -455,12 +449,10 @@ int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const fl
                        (const float*)qkv, qkv_bias, table, (const float*)dout, (float*)dqkv,
                        dB_part, qb_part, g, scale, p_drop, (uint64_t)seed, nblk);
   const long nB = (long)nh * NT * NT;
-  hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)((nB + 255) / 256)), dim3(256), 0, st,
-                     dB_part, nblk, nB, dB);
+  colsum(dB_part, nblk, nB, nB, dB, 0, st);
   hipLaunchKernelGGL(rel_table_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, st,
                      dB, nh, dtable);
-  hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)((3L * C + 255) / 256)), dim3(256), 0, st,
-                     qb_part, nblk, 3L * C, dqkv_bias_pad);
+  colsum(qb_part, nblk, 3L * C, 3L * C, dqkv_bias_pad, 0, st);
   return MSU_CHECK_LAUNCH();
 }
 

@@ -93,13 +93,13 @@ class ShiftedWindowAttention(nn.Module):
 
     def forward(self, x):
         """x: [B, H, W, C] (already norm1-ed)."""
-        qkv = F.linear(x, self.qkv.weight, self.qkv.bias)
+        qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
         qb = self.qkv.bias if self.qkv.bias is not None else torch.zeros(
             3 * x.shape[-1], device=x.device, dtype=torch.float32)
         p = self.attention_dropout if self.training else 0.0
         o = ops.window_attention(qkv, qb, self.relative_position_bias_table, self.num_heads,
                                  self.shift_size[0], p, _next_seed() if p > 0 else 0)
-        o = F.linear(o, self.proj.weight, self.proj.bias)
+        o = ops.linear(o, self.proj.weight, self.proj.bias)
         if self.dropout > 0 and self.training:
             o = F.dropout(o, self.dropout, True)
         return o
@@ -140,10 +140,10 @@ class SwinTransformerBlock(nn.Module):
         sc1 = _drop_path_scale(self.stochastic_depth_prob, self.training, B, x.device)
         x1, xn2 = ops.add_layer_norm(x, a, sc1, self.norm2.weight, self.norm2.bias, self.norm2.eps)
         fc1, fc2 = self.mlp[0], self.mlp[3]
-        h = ops.gelu(F.linear(xn2, fc1.weight, fc1.bias))
+        h = ops.gelu(ops.linear(xn2, fc1.weight, fc1.bias))
         if self.dropout > 0 and self.training:
             h = F.dropout(h, self.dropout, True)
-        m = F.linear(h, fc2.weight, fc2.bias)
+        m = ops.linear(h, fc2.weight, fc2.bias)
         if self.dropout > 0 and self.training:
             m = F.dropout(m, self.dropout, True)
         sc2 = _drop_path_scale(self.stochastic_depth_prob, self.training, B, x.device)
@@ -182,7 +182,7 @@ class PatchMerging(nn.Module):
         assert Wi == W, "input feature has wrong size"
         assert H % 2 == 0 and W % 2 == 0, f"x size ({H}*{W}) are not even."
         x = ops.merge_layer_norm(x, self.norm.weight, self.norm.bias, self.norm.eps)
-        return F.linear(x, self.reduction.weight)
+        return ops.linear(x, self.reduction.weight)
 
     def extra_repr(self):
         return f"input_resolution={self.input_resolution}, dim={self.dim}"
@@ -252,7 +252,7 @@ class PatchEmbed(nn.Module):
         if self.patch_size[0] != self.patch_size[1]:
             raise ValueError("square patches only")
         cols = ops.patchify(x, self.patch_size[0], ops.act_dtype())
-        t = F.linear(cols, self.proj.weight.reshape(self.embed_dim, -1), self.proj.bias)
+        t = ops.linear(cols, self.proj.weight.reshape(self.embed_dim, -1), self.proj.bias)
         t = t.view(B, self.num_patches, self.embed_dim)
         if self.norm is not None:
             t = ops.layer_norm(t, self.norm.weight, self.norm.bias, self.norm.eps)
@@ -280,7 +280,7 @@ class PatchExpand(nn.Module):
         else:
             raise ValueError(f"Unexpected dimensionality: x.dim()={x.dim()}")
         x = x.reshape(B, H, W, C_in)
-        x = self.expand(x) if isinstance(self.expand, nn.Identity) else F.linear(x, self.expand.weight)
+        x = self.expand(x) if isinstance(self.expand, nn.Identity) else ops.linear(x, self.expand.weight)
         C = x.shape[-1]
         if C % 4 != 0:
             raise ValueError(f"channels C={C} are not divisible by 4 (required for ×2 upsampling).")
@@ -310,7 +310,7 @@ class FinalPatchExpand_X4_V2(nn.Module):
         H, W = self.input_resolution
         B, L, C = x.shape
         assert L == H * W, "input feature has wrong size"
-        e = F.linear(x, self.expand.weight).view(B, H, W, 16 * C)
+        e = ops.linear(x, self.expand.weight).view(B, H, W, 16 * C)
         z1 = ops.refine_conv(e, self.refine1.weight, self.refine1.bias, True, (4 * H, 4 * W))
         return ops.refine_conv(z1, self.refine2.weight, self.refine2.bias, False, (4 * H, 4 * W))
 
@@ -362,7 +362,7 @@ def _skip_fuse(lin, x, skip):
     """``torch.cat([x, skip], -1)`` -> ``concat_back_dim[k]`` (model_parts.py:792-793 etc.)."""
     B = x.shape[0]
     x = torch.cat([x.reshape(B, -1, x.shape[-1]), skip.reshape(B, -1, skip.shape[-1]).to(x.dtype)], -1)
-    return F.linear(x, lin.weight, lin.bias)
+    return ops.linear(x, lin.weight, lin.bias)
 
 
 # ============================================================================ MSUNetSys
@@ -539,7 +539,7 @@ class MSUNetSys(nn.Module):
             return ops.head_norm_output(z2, self.up.norm.weight, self.up.norm.bias, self.output.weight,
                                         self.up.norm.eps)
         y = ops.layer_norm(z2, self.up.norm.weight, self.up.norm.bias, self.up.norm.eps)
-        return F.linear(y, self.output.weight.reshape(self.num_classes, -1)).permute(0, 3, 1, 2)
+        return ops.linear(y, self.output.weight.reshape(self.num_classes, -1)).permute(0, 3, 1, 2)
 
     def forward(self, x):
         x, xd = self.forward_features(x)

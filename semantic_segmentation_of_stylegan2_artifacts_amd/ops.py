@@ -259,6 +259,50 @@ def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0)
                                   int(shift), float(p_drop), int(seed) & ((1 << 63) - 1))
 
 
+# ----------------------------------------------------------------------------- Linear
+def linear(x, weight, bias=None):
+    """nn.functional.linear with the HIP weight-gradient kernel (activation dtype per autocast)."""
+    _need_cuda(x)
+    dt = act_dtype()
+    x = _as(x, dt)
+    N, K = weight.shape
+    if K % 4 or N % 4:
+        return torch.nn.functional.linear(x, weight.to(dt), None if bias is None else bias.to(dt))
+    return _LinearParams.apply(x, weight, bias, dt)
+
+
+class _LinearParams(torch.autograd.Function):
+    """Casts the f32 master weight/bias to the activation dtype inside the op so that the
+    returned parameter gradients are the f32 ones computed by the wgrad kernel."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, dt):
+        w = weight.to(dt)
+        b = None if bias is None else bias.to(dt)
+        with torch.autocast("cuda", enabled=False):
+            y = torch.nn.functional.linear(x, w, b)
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = _as(dy, x.dtype)
+        N, K = w.shape
+        M = dy.numel() // N
+        dx = None
+        if ctx.needs_input_grad[0]:
+            with torch.autocast("cuda", enabled=False):
+                dx = dy.matmul(w)
+        L = _lib.lib()
+        ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
+        dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
+        db = torch.empty(N, device=x.device, dtype=torch.float32) if ctx.has_bias else None
+        _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(dw), _p(db), _p(ws), M, N, K, 0, _s(x))
+        return dx, dw, db, None
+
+
 # ----------------------------------------------------------------------------- GELU
 class _Gelu(torch.autograd.Function):
     @staticmethod
