@@ -68,15 +68,17 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
  * (q|k|v, heads contiguous, head_dim 32), out: [B,H,W,C]; table [169, nh] f32 is
  * relative_position_bias_table; qkv_bias [3C] f32 supplies padded tokens' q,k,v. */
 long msu_win_count(int B, int H, int W);
+/* f32 workspace elements (bf16: the per-head relative-bias image in MFMA C layout). */
+long msu_win_attn_fwd_workspace(int dtype, int C, int nh);
 int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
-                     void* out, int B, int H, int W, int C, int nh, int shift, float p_drop,
-                     unsigned long long seed, void* stream);
-long msu_win_attn_bwd_workspace(int nblk, int C, int nh);
+                     void* out, float* workspace, int B, int H, int W, int C, int nh, int shift,
+                     float p_drop, unsigned long long seed, void* stream);
+long msu_win_attn_bwd_workspace(int dtype, int B, int H, int W, int C, int nh);
 /* dqkv [B,H,W,3C]; dtable [169,nh] (overwritten); dqkv_bias_pad [3C]: padded tokens'
  * contribution to the qkv-bias gradient (overwritten). */
 int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                      const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
-                     float* workspace, int nblk, int B, int H, int W, int C, int nh, int shift,
+                     float* workspace, int B, int H, int W, int C, int nh, int shift,
                      float p_drop, unsigned long long seed, void* stream);
 
 /* ---------------------------------------------------------------- refine convs

@@ -2,53 +2,56 @@
 //
 // Every nn.Linear on the MS-UNet path (torchvision block qkv / proj / mlp.0 / mlp.3,
 // PatchMerging.reduction, PatchExpand.expand, concat_back_dim, FinalPatchExpand_X4_V2.expand,
-// PatchEmbed.proj as im2col GEMM) has M = tokens (up to 8 x 65536 at 1024^2) and N, K <= a
-// few thousand: a tall-skinny "TN" product whose reduction runs over M.  Library kernels
-// tile it with far too few workgroups (hipBLASLt picked MT64x64x256 at ~0.76 ms/call).
-// Here the M range is split across S workgroups per 64x64 output tile (S chosen to fill
-// the 256 CUs), operands are staged row-major in LDS and read k-strided with
-// ds_read_b64_tr_b16 into v_mfma_f32_16x16x32_bf16, and the S partial tiles are reduced
-// deterministically (colsum).  The bias gradient rides along on the k-tile-0 workgroups.
+// PatchEmbed.proj as im2col GEMM) has M = tokens (up to 8 x 65536 at 1024^2) and N, K = a
+// small multiple of the embed width (96 / 128): a tall-skinny "TN" product whose reduction
+// runs over M.  Library kernels tile it with far too few workgroups (hipBLASLt picked
+// MT64x64x256 at ~0.76 ms/call).  Here:
+//   * output tile BT x BT with BT = 96 (Swin-T/S widths) or 128 (Swin-B), 4 waves in 2x2,
+//     each wave (BT/2)^2 = 3x3 or 4x4 v_mfma_f32_16x16x32_bf16 tiles;
+//   * the M range is split across S workgroups per output tile (S fills the 256 CUs);
+//   * operands are staged row-major ([m][n], [m][k]) in LDS, 64 rows per stage, double
+//     buffered, and read k-strided with ds_read_b64_tr_b16;
+//   * S partial tiles are reduced deterministically (colsum); the bias gradient rides along
+//     on the k-tile-0 workgroups.
 #include "common.h"
 #include "mfma_frag.h"
 #include "reduce.h"
 
 namespace {
 
-constexpr int BM = 32;       // rows of M per step (one MFMA K)
-constexpr int BT = 64;       // output tile: 64 (n) x 64 (k)
-constexpr int LDT = BT + 8;  // LDS row stride (elements), 16-B aligned rows
+constexpr int BM = 64;  // rows of M per LDS stage (two MFMA k-steps)
 
-template <typename T>
+template <typename T, int NTW>
 __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ dY, const T* __restrict__ X,
                                                     float* __restrict__ part, float* __restrict__ dbpart,
-                                                    long M, int N, int K, int S, long mchunk) {
+                                                    long M, int N, int K, long mchunk) {
+  constexpr int WT = 16 * NTW;    // wave tile
+  constexpr int BT = 2 * WT;      // block tile
+  constexpr int LDT = BT + 8;     // LDS row stride (elements): rows stay 16-B aligned
+  constexpr int VEC = 4;          // elements per staging chunk
+  constexpr int CPR = BT / VEC;   // chunks per row
   __shared__ __attribute__((aligned(16))) T sA[2][BM * LDT];  // dY rows  [m][n]
   __shared__ __attribute__((aligned(16))) T sB[2][BM * LDT];  // X rows   [m][k]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntk = (K + BT - 1) / BT;
-  const int tile = blockIdx.x, split = blockIdx.y;
-  const int tn = tile / ntk, tk = tile - (tile / ntk) * ntk;
+  const int tn = blockIdx.x / ntk, tk = blockIdx.x - (blockIdx.x / ntk) * ntk;
   const int n0 = tn * BT, k0 = tk * BT;
-  const long m_begin = (long)split * mchunk;
+  const long m_begin = (long)blockIdx.y * mchunk;
   long m_end = m_begin + mchunk;
   if (m_end > M) m_end = M;
-  const int wn = (wave >> 1) * 32, wk = (wave & 1) * 32;  // wave sub-tile 32 x 32
+  const int wn = (wave >> 1) * WT, wk = (wave & 1) * WT;
 
-  f32x4 acc[2][2];
+  f32x4 acc[NTW][NTW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NTW; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float dbacc = 0.f;
   const bool do_bias = dbpart != nullptr && tk == 0;
 
-  // staging: 32 rows x 64 cols = 512 4-element chunks per operand, 2 per thread
   auto stage = [&](int buf, long m0) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int idx = tid + c * 256;
-      const int r = idx >> 4, col = (idx & 15) * 4;
+    for (int idx = tid; idx < BM * CPR; idx += 256) {
+      const int r = idx / CPR, col = (idx - r * CPR) * VEC;
       const long m = m0 + r;
       float va[4] = {0.f, 0.f, 0.f, 0.f}, vb[4] = {0.f, 0.f, 0.f, 0.f};
       if (m < m_end) {
@@ -70,9 +73,11 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ dY, co
     auto ra = [&](int k) { return A + k * LDT; };
     auto rb = [&](int k) { return B + k * LDT; };
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int ks = 0; ks < BM; ks += 32)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) TR<T>::mma(acc[i][j], ra, wn + 16 * i, rb, wk + 16 * j, 0, lane);
+      for (int i = 0; i < NTW; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) TR<T>::mma(acc[i][j], ra, wn + 16 * i, rb, wk + 16 * j, ks, lane);
     if (do_bias && tid < BT) {
 #pragma unroll 8
       for (int r = 0; r < BM; ++r) dbacc += to_f32(A[r * LDT + tid]);
@@ -80,25 +85,27 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ dY, co
     __syncthreads();
     buf ^= 1;
   }
-  // partial tile -> part[split][n][k]
-  float* out = part + (long)split * N * K;
+  float* out = part + (long)blockIdx.y * N * K;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NTW; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NTW; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + wn + 16 * i + (lane >> 4) * 4 + r;
         const int k = k0 + wk + 16 * j + (lane & 15);
         if (n < N && k < K) out[(long)n * K + k] = acc[i][j][r];
       }
-  if (do_bias && tid < BT && n0 + tid < N) dbpart[(long)split * N + n0 + tid] = dbacc;
+  if (do_bias && tid < BT && n0 + tid < N) dbpart[(long)blockIdx.y * N + n0 + tid] = dbacc;
 }
 
+inline int tile_of(int N, int K) { return (N % 128 == 0 && K % 128 == 0) ? 128 : 96; }
+
 inline int pick_splits(long M, int N, int K) {
-  const long tiles = (long)((N + BT - 1) / BT) * ((K + BT - 1) / BT);
-  long s = (2048 + tiles - 1) / tiles;
-  const long max_s = (M + 255) / 256;  // keep >= 256 rows per split
+  const int bt = tile_of(N, K);
+  const long tiles = (long)((N + bt - 1) / bt) * ((K + bt - 1) / bt);
+  long s = (1024 + tiles - 1) / tiles;
+  const long max_s = (M + 511) / 512;  // keep >= 512 rows per split
   if (s > max_s) s = max_s;
   if (s < 1) s = 1;
   return (int)s;
@@ -130,13 +137,23 @@ int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float*
   mchunk = (mchunk + BM - 1) / BM * BM;
   float* part = workspace;
   float* dbpart = db ? workspace + (long)S * N * K : nullptr;
-  const dim3 grid((unsigned)(((N + BT - 1) / BT) * ((K + BT - 1) / BT)), (unsigned)S);
-  if (dtype == MSU_BF16)
-    hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)dY, (const bf16_t*)X,
-                       part, dbpart, M, N, K, S, mchunk);
-  else
-    hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, (const float*)dY, (const float*)X,
-                       part, dbpart, M, N, K, S, mchunk);
+  const int bt = tile_of(N, K);
+  const dim3 grid((unsigned)(((N + bt - 1) / bt) * ((K + bt - 1) / bt)), (unsigned)S);
+  if (dtype == MSU_BF16) {
+    if (bt == 96)
+      hipLaunchKernelGGL((wgrad_kernel<bf16_t, 3>), grid, dim3(256), 0, st, (const bf16_t*)dY,
+                         (const bf16_t*)X, part, dbpart, M, N, K, mchunk);
+    else
+      hipLaunchKernelGGL((wgrad_kernel<bf16_t, 4>), grid, dim3(256), 0, st, (const bf16_t*)dY,
+                         (const bf16_t*)X, part, dbpart, M, N, K, mchunk);
+  } else {
+    if (bt == 96)
+      hipLaunchKernelGGL((wgrad_kernel<float, 3>), grid, dim3(256), 0, st, (const float*)dY,
+                         (const float*)X, part, dbpart, M, N, K, mchunk);
+    else
+      hipLaunchKernelGGL((wgrad_kernel<float, 4>), grid, dim3(256), 0, st, (const float*)dY,
+                         (const float*)X, part, dbpart, M, N, K, mchunk);
+  }
   colsum(part, S, (long)N * K, (long)N * K, dW, accumulate, st);
   if (db) colsum(dbpart, S, N, N, db, accumulate, st);
   return MSU_CHECK_LAUNCH();

@@ -393,61 +393,77 @@ WinGeom make_geom(int B, int H, int W, int C, int nh, int shift) {
 
 }  // namespace
 
+// bf16 training path: window_attention_mfma.hip
+int msu_attn_mfma_fwd(const void* qkv, const float* qkv_bias, const float* table, void* out, int B,
+                      int H, int W, int C, int nh, int shift, float p_drop, unsigned long long seed,
+                      float* bias_img, hipStream_t st);
+int msu_attn_mfma_bwd(const void* qkv, const float* qkv_bias, const float* table, const void* dout,
+                      void* dqkv, float* dtable, float* dqkv_bias_pad, float* ws, int B, int H, int W,
+                      int C, int nh, int shift, float p_drop, unsigned long long seed, hipStream_t st);
+long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh);
+
+namespace {
+int f32_bwd_blocks(long nwin, int nh) {
+  long n = 2048 / nh;
+  if (n > nwin) n = nwin;
+  return (int)(n < 1 ? 1 : n);
+}
+}  // namespace
+
 extern "C" {
 
 long msu_win_count(int B, int H, int W) { return make_geom(B, H, W, 32, 1, 0).nwin; }
 
+long msu_win_attn_fwd_workspace(int dtype, int C, int nh) {
+  (void)C;
+  return dtype == MSU_BF16 ? (long)nh * 4096 : 1;
+}
+
 int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
-                     void* out, int B, int H, int W, int C, int nh, int shift, float p_drop,
-                     unsigned long long seed, void* stream) {
+                     void* out, float* workspace, int B, int H, int W, int C, int nh, int shift,
+                     float p_drop, unsigned long long seed, void* stream) {
   if (C != nh * HD) return -2;
   const WinGeom g = make_geom(B, H, W, C, nh, shift);
   if ((long)B * H * W >= (1L << 31)) return -2;
   const long items = g.nwin * nh;
   if (items == 0) return 0;
-  const float scale = 1.0f / sqrtf((float)HD);
-  const long nb = items < 262144 ? items : 262144;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == MSU_BF16)
-    hipLaunchKernelGGL(win_attn_fwd_kernel<bf16_t>, dim3((unsigned)nb), dim3(64), 0, st,
-                       (const bf16_t*)qkv, qkv_bias, table, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed);
-  else
-    hipLaunchKernelGGL(win_attn_fwd_kernel<float>, dim3((unsigned)nb), dim3(64), 0, st,
-                       (const float*)qkv, qkv_bias, table, (float*)out, g, scale, p_drop, (uint64_t)seed);
+    return msu_attn_mfma_fwd(qkv, qkv_bias, table, out, B, H, W, C, nh, shift, p_drop, seed, workspace, st);
+  const float scale = 1.0f / sqrtf((float)HD);
+  const long nb = items < 262144 ? items : 262144;
+  hipLaunchKernelGGL(win_attn_fwd_kernel<float>, dim3((unsigned)nb), dim3(64), 0, st,
+                     (const float*)qkv, qkv_bias, table, (float*)out, g, scale, p_drop, (uint64_t)seed);
   return MSU_CHECK_LAUNCH();
 }
 
-// f32 workspace elements needed by msu_win_attn_bwd for `nblk` blocks per head
-long msu_win_attn_bwd_workspace(int nblk, int C, int nh) {
-  return (long)nblk * nh * NT * NT + (long)nh * NT * NT + (long)nblk * 3 * C;
+long msu_win_attn_bwd_workspace(int dtype, int B, int H, int W, int C, int nh) {
+  const WinGeom g = make_geom(B, H, W, C, nh, 0);
+  if (dtype == MSU_BF16) return msu_attn_mfma_bwd_workspace(g.nwin, C, nh);
+  const long nblk = f32_bwd_blocks(g.nwin, nh);
+  return nblk * nh * NT * NT + (long)nh * NT * NT + nblk * 3 * C;
 }
 
 int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                      const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
-                     float* workspace, int nblk, int B, int H, int W, int C, int nh, int shift,
+                     float* workspace, int B, int H, int W, int C, int nh, int shift,
                      float p_drop, unsigned long long seed, void* stream) {
-  if (C != nh * HD || nblk < 1) return -2;
+  if (C != nh * HD) return -2;
   if ((long)B * H * W >= (1L << 31)) return -2;
   const WinGeom g = make_geom(B, H, W, C, nh, shift);
   hipStream_t st = (hipStream_t)stream;
   if (g.nwin == 0) return 0;
+  if (dtype == MSU_BF16)
+    return msu_attn_mfma_bwd(qkv, qkv_bias, table, dout, dqkv, dtable, dqkv_bias_pad, workspace, B, H, W,
+                             C, nh, shift, p_drop, seed, st);
+  const int nblk = f32_bwd_blocks(g.nwin, nh);
   const float scale = 1.0f / sqrtf((float)HD);
   float* dB_part = workspace;
   float* dB = dB_part + (long)nblk * nh * NT * NT;
   float* qb_part = dB + (long)nh * NT * NT;
-  // blocks beyond nwin would leave their partial rows unwritten: clear the partials
-  if (nblk > g.nwin) {
-    hipMemsetAsync(dB_part, 0, sizeof(float) * (long)nblk * nh * NT * NT, st);
-    hipMemsetAsync(qb_part, 0, sizeof(float) * (long)nblk * 3 * C, st);
-  }
-  if (dtype == MSU_BF16)
-    hipLaunchKernelGGL(win_attn_bwd_kernel<bf16_t>, dim3(nblk, nh), dim3(64), 0, st,
-                       (const bf16_t*)qkv, qkv_bias, table, (const bf16_t*)dout, (bf16_t*)dqkv,
-                       dB_part, qb_part, g, scale, p_drop, (uint64_t)seed, nblk);
-  else
-    hipLaunchKernelGGL(win_attn_bwd_kernel<float>, dim3(nblk, nh), dim3(64), 0, st,
-                       (const float*)qkv, qkv_bias, table, (const float*)dout, (float*)dqkv,
-                       dB_part, qb_part, g, scale, p_drop, (uint64_t)seed, nblk);
+  hipLaunchKernelGGL(win_attn_bwd_kernel<float>, dim3(nblk, nh), dim3(64), 0, st,
+                     (const float*)qkv, qkv_bias, table, (const float*)dout, (float*)dqkv,
+                     dB_part, qb_part, g, scale, p_drop, (uint64_t)seed, nblk);
   const long nB = (long)nh * NT * NT;
   colsum(dB_part, nblk, nB, nB, dB, 0, st);
   hipLaunchKernelGGL(rel_table_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, st,

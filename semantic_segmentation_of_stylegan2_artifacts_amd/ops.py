@@ -224,8 +224,10 @@ class _WindowAttention(torch.autograd.Function):
         B, H, W, C3 = qkv.shape
         C = C3 // 3
         out = torch.empty(B, H, W, C, device=qkv.device, dtype=qkv.dtype)
-        _lib.call("msu_win_attn_fwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(out), B, H, W, C,
-                  num_heads, shift, float(p_drop), seed, _s(qkv))
+        ws = torch.empty(_lib.lib().msu_win_attn_fwd_workspace(_dt(qkv), C, num_heads), device=qkv.device,
+                         dtype=torch.float32)
+        _lib.call("msu_win_attn_fwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(out), _p(ws), B, H, W,
+                  C, num_heads, shift, float(p_drop), seed, _s(qkv))
         ctx.save_for_backward(qkv, qkv_bias, table)
         ctx.cfg = (num_heads, shift, float(p_drop), seed)
         return out
@@ -238,14 +240,13 @@ class _WindowAttention(torch.autograd.Function):
         C = C3 // 3
         dout = _as(dout, qkv.dtype)
         L = _lib.lib()
-        nwin = L.msu_win_count(B, H, W)
-        nblk = int(max(1, min(nwin, 2048 // nh)))
-        ws = torch.empty(L.msu_win_attn_bwd_workspace(nblk, C, nh), device=qkv.device, dtype=torch.float32)
+        ws = torch.empty(L.msu_win_attn_bwd_workspace(_dt(qkv), B, H, W, C, nh), device=qkv.device,
+                         dtype=torch.float32)
         dqkv = torch.empty_like(qkv)
         dtable = torch.empty_like(table)
         dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
         _lib.call("msu_win_attn_bwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
-                  _p(dtable), _p(dbias), _p(ws), nblk, B, H, W, C, nh, shift, p_drop, seed, _s(qkv))
+                  _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _s(qkv))
         return dqkv, dbias, dtable, None, None, None, None
 
 

@@ -365,3 +365,83 @@ def test_linear(M, N, K, dtype):
     _close(xg.grad, xr.grad, tol, tol, "dx")
     _close(wg.grad, wr.grad, tol, tol, "dW")
     _close(bg.grad, br.grad, tol, tol, "db")
+
+
+@pytest.mark.parametrize("B,H,W,nh,shift", ATTN_CASES)
+def test_window_attention_bf16_grad(B, H, W, nh, shift):
+    """bf16 MFMA attention (32x32x16, transposed scores) fwd + bwd vs the fp32 torchvision
+    restatement; tolerance 3e-2 of the max magnitude (bf16 operands)."""
+    ops = _ops()
+    C = 32 * nh
+    g = _g(5 * B * H * W + nh)
+    qkv = torch.randn(B, H, W, 3 * C, generator=g)
+    qb = 0.3 * torch.randn(3 * C, generator=g)
+    table = torch.randn(169, nh, generator=g)
+    dy = torch.randn(B, H, W, C, generator=g)
+    q16 = qkv.to(torch.bfloat16).float()  # reference sees the same bf16-rounded inputs
+    qr, qbr, tr = [t.clone().requires_grad_(True) for t in (q16, qb, table)]
+    # restatement driven directly with qkv: identity qkv projection
+    index = osb.relative_position_index(7)
+    x_eye = qr  # [B,H,W,3C] -> apply shifted_window_attention to q,k,v via a block-diagonal trick
+    yr = _attn_ref_from_qkv(qr, qbr, tr, index, nh, shift)
+    yr.backward(dy)
+    qg = qkv.to(DEV, torch.bfloat16).requires_grad_(True)
+    qbg, tg = qb.to(DEV).requires_grad_(True), table.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.window_attention(qg, qbg, tg, nh, shift)
+    y.backward(dy.to(DEV, torch.bfloat16))
+    _close(y, yr, 3e-2, 3e-2, "out")
+    _close(qg.grad, qr.grad, 3e-2, 3e-2, "dqkv")
+    _close(qbg.grad, qbr.grad, 3e-2, 3e-2, "dbias (padded tokens)")
+    _close(tg.grad, tr.grad, 3e-2, 3e-2, "dtable")
+
+
+def _attn_ref_from_qkv(qkv, qkv_bias, table, index, nh, shift):
+    """torchvision semantics given the post-Linear qkv of real tokens; padded tokens take
+    qkv_bias (= Linear of the zero pad)."""
+    B, H, W, C3 = qkv.shape
+    C = C3 // 3
+    ws = 7
+    pad_r, pad_b = (ws - W % ws) % ws, (ws - H % ws) % ws
+    x = torch.nn.functional.pad(qkv - qkv_bias, (0, 0, 0, pad_r, 0, pad_b)) + qkv_bias
+    _, pH, pW, _ = x.shape
+    _, _, sh = osb.effective_shift(H, W, ws, shift)
+    if sum(sh) > 0:
+        x = torch.roll(x, shifts=(-sh[0], -sh[1]), dims=(1, 2))
+    nW = (pH // ws) * (pW // ws)
+    x = x.view(B, pH // ws, ws, pW // ws, ws, C3).permute(0, 1, 3, 2, 4, 5).reshape(B * nW, ws * ws, C3)
+    qkv_ = x.reshape(x.size(0), x.size(1), 3, nh, C // nh).permute(2, 0, 3, 1, 4)
+    q, k, v = qkv_[0] * (C // nh) ** -0.5, qkv_[1], qkv_[2]
+    attn = q.matmul(k.transpose(-2, -1)) + osb.relative_position_bias(table, index, ws)
+    if sum(sh) > 0:
+        mask = osb.shift_mask(pH, pW, ws, sh)
+        attn = attn.view(B, nW, nh, ws * ws, ws * ws) + mask.unsqueeze(1).unsqueeze(0)
+        attn = attn.view(-1, nh, ws * ws, ws * ws)
+    attn = torch.softmax(attn, -1)
+    o = attn.matmul(v).transpose(1, 2).reshape(B * nW, ws * ws, C)
+    o = o.view(B, pH // ws, pW // ws, ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B, pH, pW, C)
+    if sum(sh) > 0:
+        o = torch.roll(o, shifts=(sh[0], sh[1]), dims=(1, 2))
+    return o[:, :H, :W, :]
+
+
+def test_window_attention_bf16_dropout_consistency():
+    ops = _ops()
+    B, H, W, nh, C = 2, 28, 28, 2, 64
+    g = _g(77)
+    qkv = torch.randn(B, H, W, 3 * C, generator=g).to(DEV, torch.bfloat16)
+    qb = torch.zeros(3 * C, device=DEV)
+    table = torch.zeros(169, nh, device=DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y0 = ops.window_attention(qkv, qb, table, nh, 3, 0.0, 1).float()
+        ys = torch.stack([ops.window_attention(qkv, qb, table, nh, 3, 0.25, s).float() for s in range(64)])
+    rel = ((ys.mean(0) - y0).norm() / y0.norm()).item()
+    assert rel < 0.1, rel
+    q = qkv.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.window_attention(q, qb, table, nh, 3, 0.5, 1234)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    lhs = (dy.float() * y.float()).sum().item()
+    rhs = (q.grad[..., 2 * C:].float() * q[..., 2 * C:].float()).sum().item()
+    assert abs(lhs - rhs) <= 2e-2 * abs(lhs) + 1e-2, (lhs, rhs)
