@@ -28,8 +28,9 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ dY, co
   constexpr int WT = 16 * NTW;    // wave tile
   constexpr int BT = 2 * WT;      // block tile
   constexpr int LDT = BT + 8;     // LDS row stride (elements): rows stay 16-B aligned
-  constexpr int VEC = 4;          // elements per staging chunk
-  constexpr int CPR = BT / VEC;   // chunks per row
+  constexpr int EPC = 16 / (int)sizeof(T);  // elements per 16-B staging chunk
+  constexpr int CPR = BT / EPC;   // chunks per row
+  constexpr int CH = BM * CPR / 256;  // chunks per thread per operand
   __shared__ __attribute__((aligned(16))) T sA[2][BM * LDT];  // dY rows  [m][n]
   __shared__ __attribute__((aligned(16))) T sB[2][BM * LDT];  // X rows   [m][k]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -49,39 +50,54 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ dY, co
   float dbacc = 0.f;
   const bool do_bias = dbpart != nullptr && tk == 0;
 
-  auto stage = [&](int buf, long m0) {
-    for (int idx = tid; idx < BM * CPR; idx += 256) {
-      const int r = idx / CPR, col = (idx - r * CPR) * VEC;
+  // register-staged pipeline: issue the next stage's 16-B loads, compute the current
+  // stage from LDS, then write the registers to the other LDS buffer (T14 split)
+  uint4 ra[CH], rb[CH];
+  auto load_regs = [&](long m0) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = tid + 256 * c;
+      const int r = idx / CPR, col = (idx - r * CPR) * EPC;
       const long m = m0 + r;
-      float va[4] = {0.f, 0.f, 0.f, 0.f}, vb[4] = {0.f, 0.f, 0.f, 0.f};
-      if (m < m_end) {
-        if (n0 + col < N) Vec4<T>::load(dY + m * (long)N + n0 + col, va);
-        if (k0 + col < K) Vec4<T>::load(X + m * (long)K + k0 + col, vb);
-      }
-      Vec4<T>::store(&sA[buf][r * LDT + col], va);
-      Vec4<T>::store(&sB[buf][r * LDT + col], vb);
+      const bool ok = m < m_end;
+      ra[c] = (ok && n0 + col < N) ? *reinterpret_cast<const uint4*>(dY + m * (long)N + n0 + col) : make_uint4(0, 0, 0, 0);
+      rb[c] = (ok && k0 + col < K) ? *reinterpret_cast<const uint4*>(X + m * (long)K + k0 + col) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_regs = [&](int buf) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = tid + 256 * c;
+      const int r = idx / CPR, col = (idx - r * CPR) * EPC;
+      *reinterpret_cast<uint4*>(&sA[buf][r * LDT + col]) = ra[c];
+      *reinterpret_cast<uint4*>(&sB[buf][r * LDT + col]) = rb[c];
     }
   };
 
   int buf = 0;
-  if (m_begin < m_end) stage(0, m_begin);
+  if (m_begin < m_end) {
+    load_regs(m_begin);
+    store_regs(0);
+  }
   __syncthreads();
   for (long m0 = m_begin; m0 < m_end; m0 += BM) {
-    if (m0 + BM < m_end) stage(buf ^ 1, m0 + BM);
+    const bool more = m0 + BM < m_end;
+    if (more) load_regs(m0 + BM);
     const T* A = sA[buf];
     const T* B = sB[buf];
-    auto ra = [&](int k) { return A + k * LDT; };
-    auto rb = [&](int k) { return B + k * LDT; };
+    auto rowA = [&](int k) { return A + k * LDT; };
+    auto rowB = [&](int k) { return B + k * LDT; };
 #pragma unroll
     for (int ks = 0; ks < BM; ks += 32)
 #pragma unroll
       for (int i = 0; i < NTW; ++i)
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) TR<T>::mma(acc[i][j], ra, wn + 16 * i, rb, wk + 16 * j, ks, lane);
+        for (int j = 0; j < NTW; ++j) TR<T>::mma(acc[i][j], rowA, wn + 16 * i, rowB, wk + 16 * j, ks, lane);
     if (do_bias && tid < BT) {
 #pragma unroll 8
       for (int r = 0; r < BM; ++r) dbacc += to_f32(A[r * LDT + tid]);
     }
+    if (more) store_regs(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
@@ -125,7 +141,7 @@ long msu_wgrad_workspace(long M, int N, int K) {
 // dW [N][K] f32 (overwritten, or accumulated when accumulate != 0), db [N] f32 (may be null).
 int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float* db, float* workspace,
                      long M, int N, int K, int accumulate, void* stream) {
-  if (N % 4 || K % 4 || M < 0) return -2;
+  if (N % 8 || K % 8 || M < 0) return -2;  // 16-B staging chunks
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) {
     if (!accumulate) hipMemsetAsync(dW, 0, sizeof(float) * (long)N * K, st);

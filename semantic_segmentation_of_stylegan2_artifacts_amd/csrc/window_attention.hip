@@ -401,6 +401,7 @@ int msu_attn_mfma_bwd(const void* qkv, const float* qkv_bias, const float* table
                       void* dqkv, float* dtable, float* dqkv_bias_pad, float* ws, int B, int H, int W,
                       int C, int nh, int shift, float p_drop, unsigned long long seed, hipStream_t st);
 long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh);
+long msu_attn_mfma_fwd_workspace(int C, int nh);
 
 namespace {
 int f32_bwd_blocks(long nwin, int nh) {
@@ -416,7 +417,7 @@ long msu_win_count(int B, int H, int W) { return make_geom(B, H, W, 32, 1, 0).nw
 
 long msu_win_attn_fwd_workspace(int dtype, int C, int nh) {
   (void)C;
-  return dtype == MSU_BF16 ? (long)nh * 4096 : 1;
+  return dtype == MSU_BF16 ? msu_attn_mfma_fwd_workspace(C, nh) : 1;
 }
 
 int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,

@@ -4,14 +4,18 @@
 // window_attention.hip for the pad / roll / partition folding and the f32 parity kernel).
 //
 // Per (window, head) item, one wave:
-//   S^T[j][i] = K Q^T + B_rel^T (+ -100 shift mask)   8 x v_mfma_f32_32x32x16_bf16, the
+//   S^T[j][i] = K Q^T (+ B_rel^T / scale, + -100/scale shift mask); softmax uses
+//              exp(scale * (s - max)), i.e. q * hd^-1/2 is folded into the exponent.  The
 //              accumulators start from a per-head bias image laid out in the MFMA C layout
-//              (-inf on padded key rows), so the bias add costs nothing;
+//              (-inf on padded key rows), so the bias add costs nothing.  K and Q operand
+//              fragments are loaded straight from HBM (one 16-B load per lane each);
 //   softmax over j: each lane owns one query column -> in-register max/sum + one xor-32
 //              shuffle; dropout by a counter hash;
 //   O^T[d][i] = V^T P^T: P^T stays in registers and is the B operand directly (sum over
 //              the accumulator's row index); V^T comes from the staged V rows with
 //              ds_read_b64_tr_b16 in the matching permuted k order.
+// All global loads of an item are issued together before first use (the HBM latency is
+// paid once per item, not once per row).
 // Backward recomputes S^T / P^T, forms dP^T = V dO^T, dS^T = P^T (dP^T - delta), stores
 // Pd and dS once as [i][j] LDS images (8-byte stores) and runs dV = Pd^T dO,
 // dQ = dS K, dK = dS^T Q with tr-read operands; relative-bias gradients accumulate in
@@ -24,6 +28,7 @@ namespace {
 constexpr int WS = 7, NT = 49, HD = 32;
 constexpr int LD = 40;   // staged [64 x 32] rows: 32 + 8 pad (80 B)
 constexpr int LDP = 72;  // [64 x 64] images: 64 + 8 pad (144 B)
+constexpr int TOK_PAD = -1, TOK_ZERO = -2;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -76,65 +81,59 @@ MSU_DEV constexpr int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h
 
 MSU_DEV int region(int p, int P, int s) { return s == 0 ? 0 : (p < P - WS ? 0 : (p < P - s ? 1 : 2)); }
 
-struct WinInfo {
-  bool boundary;  // window touches the shifted wrap-around (mask non-trivial)
-};
-
-// Token table of the window (sTok: source token or -1 = padded, sReg: mask region)
-MSU_DEV WinInfo window_tokens(const Geom& g, long win, int* sTok, int* sReg, int lane) {
+// Token table of the window: sTok = source token, TOK_PAD (padded) or TOK_ZERO (t >= 49);
+// sReg = mask region.  Returns whether the mask is non-trivial for this window.
+MSU_DEV bool window_tokens(const Geom& g, long win, int* sTok, int* sReg, int lane) {
   const int nw = g.nWy * g.nWx;
-  const long b = win / nw;
-  const int wr = (int)(win - b * nw);
+  const int b = (int)(win / nw);
+  const int wr = (int)(win - (long)b * nw);
   const int wy = wr / g.nWx, wx = wr - (wr / g.nWx) * g.nWx;
-  int tok = -1, reg = 0;
+  int tok = TOK_ZERO, reg = 0;
   if (lane < NT) {
     const int py = wy * WS + lane / WS, px = wx * WS + lane % WS;
     int sy = py + g.sh; if (sy >= g.Hp) sy -= g.Hp;
     int sx = px + g.sw; if (sx >= g.Wp) sx -= g.Wp;
-    if (sy < g.H && sx < g.W) tok = (int)((b * g.H + sy) * (long)g.W + sx);
+    tok = (sy < g.H && sx < g.W) ? (b * g.H + sy) * g.W + sx : TOK_PAD;
     reg = region(py, g.Hp, g.sh) * 3 + region(px, g.Wp, g.sw);
   }
   sTok[lane] = tok;
   sReg[lane] = reg;
-  WinInfo w;
-  w.boundary = (g.sh + g.sw) > 0 && (wy == g.nWy - 1 || wx == g.nWx - 1);
-  return w;
+  return (g.sh + g.sw) > 0 && (wy == g.nWy - 1 || wx == g.nWx - 1);
 }
 
-// stage rows t < 49 of a head slice (32 bf16 = 4 x 16 B) into sX[t][LD]; rows >= 49 zero.
-// Padded tokens take the bf16-rounded bias (or zero when bias == nullptr).
-MSU_DEV void stage(const int* sTok, const bf16_t* src, long stride, int col0, const float* bias,
-                   float mul, bf16_t* sX, int lane) {
+MSU_DEV const bf16_t* row_ptr(int tok, const bf16_t* base, long stride, const bf16_t* padrow,
+                              const bf16_t* zrow) {
+  return tok >= 0 ? base + (long)tok * stride : (tok == TOK_PAD ? padrow : zrow);
+}
+
+// fragment straight from HBM: lane l -> window row row0 + (l&31), k = k0 + 8(l>>5) .. +7
+MSU_DEV bf16x8 frag_global(const int* sTok, int row0, const bf16_t* base, long stride,
+                           const bf16_t* padrow, const bf16_t* zrow, int k0, int lane) {
+  const bf16_t* p = row_ptr(sTok[row0 + (lane & 31)], base, stride, padrow, zrow);
+  return *reinterpret_cast<const bf16x8*>(p + k0 + 8 * (lane >> 5));
+}
+
+// Stage NS head slices (rows t = 0..63, 32 bf16 each) into LDS; all 4*NS loads issued first.
+template <int NS>
+MSU_DEV void stage_rows(const int* sTok, const bf16_t* const (&base)[NS], const long (&stride)[NS],
+                        const bf16_t* const (&padrow)[NS], const bf16_t* zrow,
+                        bf16_t* const (&dst)[NS], int lane) {
+  uint4 raw[NS][4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int idx = lane + 64 * c;
     const int t = idx >> 2, q = idx & 3;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (t < NT) {
-      const int tok = sTok[t];
-      float f[8];
-      if (tok >= 0) {
-        const uint4 raw = *reinterpret_cast<const uint4*>(src + (long)tok * stride + col0 + q * 8);
-        const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+    const int tok = sTok[t];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          f[2 * e] = __uint_as_float(w[e] << 16);
-          f[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
-        }
-      } else {
+    for (int s = 0; s < NS; ++s)
+      raw[s][c] = *reinterpret_cast<const uint4*>(row_ptr(tok, base[s], stride[s], padrow[s], zrow) + q * 8);
+  }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = bias ? to_f32(from_f32<bf16_t>(bias[col0 + q * 8 + e])) : 0.f;
-      }
-      if (mul != 1.f) {
+  for (int c = 0; c < 4; ++c) {
+    const int idx = lane + 64 * c;
+    const int t = idx >> 2, q = idx & 3;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] *= mul;
-      }
-      v.x = (uint32_t)from_f32<bf16_t>(f[0]) | ((uint32_t)from_f32<bf16_t>(f[1]) << 16);
-      v.y = (uint32_t)from_f32<bf16_t>(f[2]) | ((uint32_t)from_f32<bf16_t>(f[3]) << 16);
-      v.z = (uint32_t)from_f32<bf16_t>(f[4]) | ((uint32_t)from_f32<bf16_t>(f[5]) << 16);
-      v.w = (uint32_t)from_f32<bf16_t>(f[6]) | ((uint32_t)from_f32<bf16_t>(f[7]) << 16);
-    }
-    *reinterpret_cast<uint4*>(sX + t * LD + q * 8) = v;
+    for (int s = 0; s < NS; ++s) *reinterpret_cast<uint4*>(dst[s] + t * LD + q * 8) = raw[s][c];
   }
 }
 
@@ -143,9 +142,15 @@ MSU_DEV float drop_keep(uint64_t seed, long win, int h, int nh, int i, int j, fl
   return hash_uniform(seed, idx) >= p ? 1.0f / (1.0f - p) : 0.0f;
 }
 
-// S^T tiles (jt, it) of one item, bias-initialised, masked, softmax-ed over j -> P^T
-MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16_t* sQ, const bf16_t* sK, const float* bimg,
-                     const int* sReg, bool boundary, int lane) {
+MSU_DEV void lds_sync() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+}
+
+// S^T tiles (jt, it): bias image init + K Q^T from fragments ka[jt][ks], qb[it][ks];
+// mask; softmax over j with exp(scale * (s - max)) -> P^T
+MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (&qb)[2][2],
+                     const float* bimg, const int* sReg, bool boundary, float scale, int lane) {
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
@@ -158,30 +163,22 @@ MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16_t* sQ, const bf16_t* sK, cons
       }
     }
 #pragma unroll
-  for (int ks = 0; ks < HD; ks += 16) {
-    bf16x8 a[2], b[2];
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt) a[jt] = frag_rows(sK, LD, jt * 32, ks, lane);
-#pragma unroll
-    for (int it = 0; it < 2; ++it) b[it] = frag_rows(sQ, LD, it * 32, ks, lane);
+  for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-      for (int it = 0; it < 2; ++it) P[jt][it] = mfma32(a[jt], b[it], P[jt][it]);
-  }
+      for (int it = 0; it < 2; ++it) P[jt][it] = mfma32(ka[jt][ks], qb[it][ks], P[jt][it]);
   const int h = lane >> 5;
   if (boundary) {
+    const float mval = -100.0f / scale;
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      const int i = it * 32 + (lane & 31);
-      const int ri = sReg[i];
+      const int ri = sReg[it * 32 + (lane & 31)];
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int j = jt * 32 + crow(r, h);
-          if (sReg[j] != ri) P[jt][it][r] += -100.0f;
-        }
+        for (int r = 0; r < 16; ++r)
+          if (sReg[jt * 32 + crow(r, h)] != ri) P[jt][it][r] += mval;
     }
   }
 #pragma unroll
@@ -192,12 +189,13 @@ MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16_t* sQ, const bf16_t* sK, cons
 #pragma unroll
       for (int r = 0; r < 16; ++r) m = fmaxf(m, P[jt][it][r]);
     m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float ms = m * scale;
     float s = 0.f;
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float e = __expf(P[jt][it][r] - m);
+        const float e = __expf(fmaf(P[jt][it][r], scale, -ms));
         P[jt][it][r] = e;
         s += e;
       }
@@ -210,17 +208,21 @@ MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16_t* sQ, const bf16_t* sK, cons
   }
 }
 
+struct Aux {
+  const float* bimg;      // [nh][4096] bias image / scale
+  const bf16_t* biasrow;  // [3C] bf16 qkv bias (padded tokens' q|k|v)
+  const bf16_t* zrow;     // [64] zeros
+};
+
 struct FwdLds {
-  bf16_t q[64 * LD], k[64 * LD], v[64 * LD];
+  bf16_t v[64 * LD];
   int tok[64], reg[64];
 };
 
 template <int WAVES>
-__global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __restrict__ qkv,
-                                                            const float* __restrict__ qkv_bias,
-                                                            const float* __restrict__ bimg_all,
-                                                            bf16_t* __restrict__ out, Geom g,
-                                                            float scale, float p_drop, uint64_t seed) {
+__global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __restrict__ qkv, Aux aux,
+                                                               bf16_t* __restrict__ out, Geom g, float scale,
+                                                               float p_drop, uint64_t seed) {
   __shared__ __attribute__((aligned(16))) FwdLds lds_all[WAVES];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   FwdLds& L = lds_all[wave];
@@ -228,20 +230,32 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
   const long C3 = 3L * g.C;
   const long nblk = gridDim.x;
   const long b0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int hh = lane >> 5;
   for (long it0 = b0 * WAVES; it0 < nitems; it0 += nblk * WAVES) {
     const long item = it0 + wave;
-    if (item >= nitems) break;  // no block-wide barriers below: waves are independent
+    if (item >= nitems) break;  // no block-wide barriers: waves are independent
     const long win = item / g.nh;
     const int h = (int)(item - win * g.nh);
-    const WinInfo wi = window_tokens(g, win, L.tok, L.reg, lane);
-    stage(L.tok, qkv, C3, h * HD, qkv_bias, scale, L.q, lane);
-    stage(L.tok, qkv, C3, g.C + h * HD, qkv_bias, 1.f, L.k, lane);
-    stage(L.tok, qkv, C3, 2 * g.C + h * HD, qkv_bias, 1.f, L.v, lane);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes of this wave done
-    __builtin_amdgcn_wave_barrier();
+    const bool boundary = window_tokens(g, win, L.tok, L.reg, lane);
+    lds_sync();
+    const int cq = h * HD, ck = g.C + h * HD, cv = 2 * g.C + h * HD;
+    bf16x8 ka[2][2], qb[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        ka[t][ks] = frag_global(L.tok, 32 * t, qkv + ck, C3, aux.biasrow + ck, aux.zrow, 16 * ks, lane);
+        qb[t][ks] = frag_global(L.tok, 32 * t, qkv + cq, C3, aux.biasrow + cq, aux.zrow, 16 * ks, lane);
+      }
+    {
+      const bf16_t* const base[1] = {qkv + cv};
+      const long strd[1] = {C3};
+      const bf16_t* const pad[1] = {aux.biasrow + cv};
+      bf16_t* const dst[1] = {L.v};
+      stage_rows<1>(L.tok, base, strd, pad, aux.zrow, dst, lane);
+    }
     f32x16 P[2][2];
-    probs_T(P, L.q, L.k, bimg_all + (long)h * 4 * 64 * 16, L.reg, wi.boundary, lane);
-    const int hh = lane >> 5;
+    probs_T(P, ka, qb, aux.bimg + (long)h * 4096, L.reg, boundary, scale, lane);
     if (p_drop > 0.f) {
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
@@ -251,6 +265,7 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
           for (int r = 0; r < 16; ++r)
             P[jt][it][r] *= drop_keep(seed, win, h, g.nh, it * 32 + (lane & 31), jt * 32 + crow(r, hh), p_drop);
     }
+    lds_sync();
     // O^T[d][i] = sum_j V[j][d] P^T[j][i]
     f32x16 O[2];
     O[0] = f32x16{0}; O[1] = f32x16{0};
@@ -262,11 +277,11 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
 #pragma unroll
         for (int it = 0; it < 2; ++it) O[it] = mfma32(a, pack8(P[jt][it], s), O[it]);
       }
-    // store: lane -> query i, registers 4g..4g+3 -> d = 8g + 4hh .. +3 (8-byte stores)
+    // store: lane -> query i, registers 4gq..4gq+3 -> d = 8gq + 4hh .. +3 (8-byte stores)
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int i = it * 32 + (lane & 31);
-      const int tok = i < NT ? L.tok[i] : -1;
+      const int tok = L.tok[i];
       if (tok >= 0) {
         bf16_t* dst = out + (long)tok * g.C + h * HD;
 #pragma unroll
@@ -283,16 +298,16 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
 }
 
 struct BwdLds {
-  bf16_t q[64 * LD], k[64 * LD], v[64 * LD], dO[64 * LD];
+  bf16_t q[64 * LD], k[64 * LD], dO[64 * LD];
   bf16_t P[64 * LDP], dS[64 * LDP];  // [i][j] images
   int tok[64], reg[64];
 };
 
 template <int WAVES>
 __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
-    const bf16_t* __restrict__ qkv, const float* __restrict__ qkv_bias, const float* __restrict__ bimg_all,
-    const bf16_t* __restrict__ dout, bf16_t* __restrict__ dqkv, float* __restrict__ dB_part,
-    float* __restrict__ qb_part, Geom g, float scale, float p_drop, uint64_t seed, int nblk) {
+    const bf16_t* __restrict__ qkv, Aux aux, const bf16_t* __restrict__ dout, bf16_t* __restrict__ dqkv,
+    float* __restrict__ dB_part, float* __restrict__ qb_part, Geom g, float scale, float p_drop,
+    uint64_t seed, int nblk) {
   // grid (nblk, nh): block owns head h, waves walk windows win = (blk*WAVES + wave) + k*nblk*WAVES
   __shared__ __attribute__((aligned(16))) BwdLds lds_all[WAVES];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -300,7 +315,8 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
   const int h = blockIdx.y;
   const long C3 = 3L * g.C;
   const int hh = lane >> 5;
-  const float* bimg = bimg_all + (long)h * 4 * 64 * 16;
+  const float* bimg = aux.bimg + (long)h * 4096;
+  const int cq = h * HD, ck = g.C + h * HD, cv = 2 * g.C + h * HD;
   f32x16 dB[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -309,15 +325,32 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
   float padacc[3] = {0.f, 0.f, 0.f};  // column d = lane&31 of padded tokens' dq, dk, dv (per half)
   const long stride = (long)nblk * WAVES;
   for (long win = (long)blockIdx.x * WAVES + wave; win < g.nwin; win += stride) {
-    const WinInfo wi = window_tokens(g, win, L.tok, L.reg, lane);
-    stage(L.tok, qkv, C3, h * HD, qkv_bias, scale, L.q, lane);
-    stage(L.tok, qkv, C3, g.C + h * HD, qkv_bias, 1.f, L.k, lane);
-    stage(L.tok, qkv, C3, 2 * g.C + h * HD, qkv_bias, 1.f, L.v, lane);
-    stage(L.tok, dout, g.C, h * HD, nullptr, 1.f, L.dO, lane);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+    const bool boundary = window_tokens(g, win, L.tok, L.reg, lane);
+    lds_sync();
+    bf16x8 va[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        va[t][ks] = frag_global(L.tok, 32 * t, qkv + cv, C3, aux.biasrow + cv, aux.zrow, 16 * ks, lane);
+    {
+      const bf16_t* const base[3] = {qkv + cq, qkv + ck, dout + h * HD};
+      const long strd[3] = {C3, C3, (long)g.C};
+      const bf16_t* const pad[3] = {aux.biasrow + cq, aux.biasrow + ck, aux.zrow};
+      bf16_t* const dst[3] = {L.q, L.k, L.dO};
+      stage_rows<3>(L.tok, base, strd, pad, aux.zrow, dst, lane);
+    }
+    lds_sync();
+    bf16x8 ka[2][2], qb[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        ka[t][ks] = frag_rows(L.k, LD, 32 * t, 16 * ks, lane);
+        qb[t][ks] = frag_rows(L.q, LD, 32 * t, 16 * ks, lane);
+      }
     f32x16 P[2][2];
-    probs_T(P, L.q, L.k, bimg, L.reg, wi.boundary, lane);
+    probs_T(P, ka, qb, bimg, L.reg, boundary, scale, lane);
     // dPd^T[j][i] = sum_d V[j][d] dO[i][d]
     f32x16 D[2][2];
 #pragma unroll
@@ -325,33 +358,30 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
 #pragma unroll
       for (int b = 0; b < 2; ++b) D[a][b] = f32x16{0};
 #pragma unroll
-    for (int ks = 0; ks < HD; ks += 16) {
-      bf16x8 a[2], b[2];
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 b[2];
 #pragma unroll
-      for (int jt = 0; jt < 2; ++jt) a[jt] = frag_rows(L.v, LD, jt * 32, ks, lane);
-#pragma unroll
-      for (int it = 0; it < 2; ++it) b[it] = frag_rows(L.dO, LD, it * 32, ks, lane);
+      for (int it = 0; it < 2; ++it) b[it] = frag_rows(L.dO, LD, it * 32, 16 * ks, lane);
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-        for (int it = 0; it < 2; ++it) D[jt][it] = mfma32(a[jt], b[it], D[jt][it]);
+        for (int it = 0; it < 2; ++it) D[jt][it] = mfma32(va[jt][ks], b[it], D[jt][it]);
     }
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int i = it * 32 + (lane & 31);
+      float keep[2][16];
       float delta = 0.f;
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float keep = 1.f;
-          if (p_drop > 0.f) keep = drop_keep(seed, win, h, g.nh, i, jt * 32 + crow(r, hh), p_drop);
-          D[jt][it][r] *= keep;                  // dP = dPd * keep/(1-p)
+          keep[jt][r] = p_drop > 0.f ? drop_keep(seed, win, h, g.nh, i, jt * 32 + crow(r, hh), p_drop) : 1.f;
+          D[jt][it][r] *= keep[jt][r];  // dP = dPd * keep/(1-p)
           delta += P[jt][it][r] * D[jt][it][r];
-          if (p_drop > 0.f) D[jt][it][r] = D[jt][it][r];  // keep in D; Pd written below
         }
       delta += __shfl_xor(delta, 32, 64);
-      // Pd (dropped probabilities) and dS images [i][j], 4 consecutive j per 8-byte store
+      // Pd and dS images [i][j], 4 consecutive j per 8-byte store
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
@@ -361,12 +391,9 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
             const float p = P[jt][it][r];
-            const float dsv = p * (D[jt][it][r] - delta);
-            float keep = 1.f;
-            if (p_drop > 0.f) keep = drop_keep(seed, win, h, g.nh, i, jt * 32 + crow(r, hh), p_drop);
-            pd[e] = p * keep;
-            ds[e] = dsv;
-            dB[jt][it][r] += dsv;
+            ds[e] = p * (D[jt][it][r] - delta);
+            pd[e] = p * keep[jt][r];
+            dB[jt][it][r] += ds[e];
           }
           const int j0 = jt * 32 + 8 * gq + 4 * hh;
           uint2 wp, wd;
@@ -378,9 +405,9 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
           *reinterpret_cast<uint2*>(L.dS + i * LDP + j0) = wd;
         }
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    // dV[j][d] = sum_i Pd[i][j] dO[i][d]; dK[j][d] = sum_i dS[i][j] Q[i][d]; dQ[i][d] = sum_j dS[i][j] K[j][d]
+    lds_sync();
+    // dV[j][d] = sum_i Pd[i][j] dO[i][d]; dK[j][d] = scale sum_i dS[i][j] Q[i][d];
+    // dQ[i][d] = scale sum_j dS[i][j] K[j][d]   (scores = scale * q k^T)
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 av = f32x16{0}, ak = f32x16{0}, aq = f32x16{0};
@@ -393,31 +420,27 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
         ak = mfma32(frag_tr(L.dS, LDP, ks, mt * 32, lane), bq, ak);
         aq = mfma32(frag_rows(L.dS, LDP, mt * 32, ks, lane), bk, aq);
       }
-      // rows t = mt*32 + crow(r, hh), column d = lane & 31
       const int d = lane & 31;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int t = mt * 32 + crow(r, hh);
-        if (t < NT) {
-          const int tok = L.tok[t];
-          if (tok >= 0) {
-            bf16_t* row = dqkv + (long)tok * C3 + h * HD + d;
-            row[0] = from_f32<bf16_t>(aq[r] * scale);
-            row[g.C] = from_f32<bf16_t>(ak[r]);
-            row[2 * g.C] = from_f32<bf16_t>(av[r]);
-          } else {
-            padacc[0] += aq[r] * scale;
-            padacc[1] += ak[r];
-            padacc[2] += av[r];
-          }
+        const int tok = L.tok[t];
+        if (tok >= 0) {
+          bf16_t* row = dqkv + (long)tok * C3 + h * HD + d;
+          row[0] = from_f32<bf16_t>(aq[r] * scale);
+          row[g.C] = from_f32<bf16_t>(ak[r] * scale);
+          row[2 * g.C] = from_f32<bf16_t>(av[r]);
+        } else if (tok == TOK_PAD) {
+          padacc[0] += aq[r] * scale;
+          padacc[1] += ak[r] * scale;
+          padacc[2] += av[r];
         }
       }
     }
     __builtin_amdgcn_wave_barrier();
   }
-  // per-wave partials: relative-bias gradient image [part][h][4 tiles][64 lanes][16]
   const long part = (long)blockIdx.x * WAVES + wave;
-  float* db = dB_part + (part * g.nh + h) * (4 * 64 * 16);
+  float* db = dB_part + (part * g.nh + h) * 4096;
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
@@ -434,10 +457,16 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
   }
 }
 
-// bias image [nh][4 tiles (jt*2+it)][64 lanes][16 regs]: value for (j, i) = table[idx(i,j)][h]
-// (i, j < 49), -inf for padded keys j >= 49, 0 for padded queries i >= 49.
-__global__ void __launch_bounds__(256) bias_image_kernel(const float* table, int nh, float* img) {
+// bias image [nh][4 tiles (jt*2+it)][64 lanes][16 regs] = table[idx(i,j)][h] / scale
+// (i, j < 49), -inf for padded keys j >= 49, 0 for padded queries i >= 49.  Block 0 also
+// writes the bf16 qkv-bias row and the zero row.
+__global__ void __launch_bounds__(256) aux_kernel(const float* table, const float* qkv_bias, int nh, int C3,
+                                                  float inv_scale, float* img, bf16_t* biasrow, bf16_t* zrow) {
   const int e = blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C3; c += 256) biasrow[c] = from_f32<bf16_t>(qkv_bias[c]);
+    if (threadIdx.x < 64) zrow[threadIdx.x] = 0;
+  }
   if (e >= nh * 4096) return;
   const int h = e / 4096, rem = e % 4096;
   const int t = rem / 1024, lane = (rem / 16) % 64, r = rem % 16;
@@ -446,11 +475,11 @@ __global__ void __launch_bounds__(256) bias_image_kernel(const float* table, int
   float v;
   if (j >= NT) v = -INFINITY;
   else if (i >= NT) v = 0.f;
-  else v = table[((i / WS - j / WS + WS - 1) * (2 * WS - 1) + (i % WS - j % WS + WS - 1)) * nh + h];
+  else v = table[((i / WS - j / WS + WS - 1) * (2 * WS - 1) + (i % WS - j % WS + WS - 1)) * nh + h] * inv_scale;
   img[e] = v;
 }
 
-// d bias image [nh][4096] -> d table [169][nh]
+// d bias image [nh][4096] (dS, in the image layout) -> d table [169][nh]
 __global__ void __launch_bounds__(256) bias_image_grad_kernel(const float* dimg, int nh, float* dtable) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= 169 * nh) return;
@@ -487,11 +516,21 @@ Geom make_geom(int B, int H, int W, int C, int nh, int shift) {
 
 constexpr int FWD_WAVES = 4, BWD_WAVES = 2;
 
-}  // namespace
+// aux workspace (f32 units): bias image nh*4096, bf16 bias row (3C bf16), zero row (64 bf16)
+long aux_floats(int C, int nh) { return (long)nh * 4096 + (3L * C + 64 + 1) / 2 + 4; }
 
-// entry points used by window_attention.hip for dtype == bf16
-int msu_attn_mfma_bwd_parts(long nwin, int nh) {
-  // per head: waves = nblk * BWD_WAVES, aim for ~2048 waves in total
+Aux carve_aux(float* ws, int C, int nh, float** img_out, bf16_t** brow, bf16_t** zrow) {
+  Aux a;
+  *img_out = ws;
+  *brow = reinterpret_cast<bf16_t*>(ws + (long)nh * 4096);
+  *zrow = *brow + 3L * C;
+  a.bimg = *img_out;
+  a.biasrow = *brow;
+  a.zrow = *zrow;
+  return a;
+}
+
+int bwd_blocks(long nwin, int nh) {
   long nblk = 1024 / ((long)nh * BWD_WAVES);
   if (nblk < 1) nblk = 1;
   const long maxb = (nwin + BWD_WAVES - 1) / BWD_WAVES;
@@ -499,23 +538,31 @@ int msu_attn_mfma_bwd_parts(long nwin, int nh) {
   return (int)nblk;
 }
 
+}  // namespace
+
+// entry points used by window_attention.hip for dtype == bf16
+long msu_attn_mfma_fwd_workspace(int C, int nh) { return aux_floats(C, nh); }
+
 long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh) {
-  const long parts = (long)msu_attn_mfma_bwd_parts(nwin, nh) * BWD_WAVES;
-  return parts * nh * 4096 + (long)nh * 4096 * 2 + parts * 3L * C;
+  const long parts = (long)bwd_blocks(nwin, nh) * BWD_WAVES;
+  return aux_floats(C, nh) + parts * nh * 4096 + (long)nh * 4096 + parts * 3L * C;
 }
 
 int msu_attn_mfma_fwd(const void* qkv, const float* qkv_bias, const float* table, void* out, int B,
                       int H, int W, int C, int nh, int shift, float p_drop, unsigned long long seed,
-                      float* bias_img, hipStream_t st) {
+                      float* ws, hipStream_t st) {
   const Geom g = make_geom(B, H, W, C, nh, shift);
   const long items = g.nwin * nh;
   if (items == 0) return 0;
-  hipLaunchKernelGGL(bias_image_kernel, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, nh, bias_img);
+  const float scale = 1.0f / sqrtf((float)HD);
+  float* img; bf16_t* brow; bf16_t* zrow;
+  const Aux aux = carve_aux(ws, C, nh, &img, &brow, &zrow);
+  hipLaunchKernelGGL(aux_kernel, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
+                     1.0f / scale, img, brow, zrow);
   long nb = (items + FWD_WAVES - 1) / FWD_WAVES;
   if (nb > 65536) nb = 65536;
   hipLaunchKernelGGL(attn_fwd_mfma<FWD_WAVES>, dim3((unsigned)nb), dim3(64 * FWD_WAVES), 0, st,
-                     (const bf16_t*)qkv, qkv_bias, bias_img, (bf16_t*)out, g, 1.0f / sqrtf((float)HD),
-                     p_drop, (uint64_t)seed);
+                     (const bf16_t*)qkv, aux, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed);
   return MSU_CHECK_LAUNCH();
 }
 
@@ -524,16 +571,19 @@ int msu_attn_mfma_bwd(const void* qkv, const float* qkv_bias, const float* table
                       int C, int nh, int shift, float p_drop, unsigned long long seed, hipStream_t st) {
   const Geom g = make_geom(B, H, W, C, nh, shift);
   if (g.nwin == 0) return 0;
-  const int nblk = msu_attn_mfma_bwd_parts(g.nwin, nh);
+  const float scale = 1.0f / sqrtf((float)HD);
+  const int nblk = bwd_blocks(g.nwin, nh);
   const long parts = (long)nblk * BWD_WAVES;
-  float* dB_part = ws;
-  float* img = dB_part + parts * nh * 4096;
-  float* dimg = img + (long)nh * 4096;
+  float* img; bf16_t* brow; bf16_t* zrow;
+  const Aux aux = carve_aux(ws, C, nh, &img, &brow, &zrow);
+  float* dB_part = ws + aux_floats(C, nh);
+  float* dimg = dB_part + parts * nh * 4096;
   float* qb_part = dimg + (long)nh * 4096;
-  hipLaunchKernelGGL(bias_image_kernel, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, nh, img);
+  hipLaunchKernelGGL(aux_kernel, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
+                     1.0f / scale, img, brow, zrow);
   hipLaunchKernelGGL(attn_bwd_mfma<BWD_WAVES>, dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
-                     (const bf16_t*)qkv, qkv_bias, img, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part,
-                     g, 1.0f / sqrtf((float)HD), p_drop, (uint64_t)seed, nblk);
+                     (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
+                     p_drop, (uint64_t)seed, nblk);
   colsum(dB_part, (int)parts, (long)nh * 4096, (long)nh * 4096, dimg, 0, st);
   hipLaunchKernelGGL(bias_image_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, st, dimg, nh, dtable);
   colsum(qb_part, (int)parts, 3L * C, 3L * C, dqkv_bias_pad, 0, st);

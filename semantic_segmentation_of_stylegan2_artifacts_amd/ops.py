@@ -267,7 +267,7 @@ def linear(x, weight, bias=None):
     dt = act_dtype()
     x = _as(x, dt)
     N, K = weight.shape
-    if K % 4 or N % 4:
+    if K % 8 or N % 8:
         return torch.nn.functional.linear(x, weight.to(dt), None if bias is None else bias.to(dt))
     return _LinearParams.apply(x, weight, bias, dt)
 

@@ -1,0 +1,119 @@
+"""Per-op microbenchmarks at the Swin-T 1024^2 bs=8 training shapes (bf16).
+
+    python tools/kbench.py [attn|wgrad|conv|ln|all]
+
+Times each HIP op with HIP events on the current stream (median of N launches) and prints
+achieved GB/s or TFLOP/s next to the algorithmic work.  Used to pick what to optimise.
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from semantic_segmentation_of_stylegan2_artifacts_amd import ops  # noqa: E402
+
+DEV = "cuda"
+B = 8
+
+
+def timeit(fn, n=10):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def attn():
+    for stage, (res, nh) in enumerate([(256, 3), (128, 6), (64, 12), (32, 24)]):
+        C = 32 * nh
+        qkv = torch.randn(B, res, res, 3 * C, device=DEV, dtype=torch.bfloat16)
+        qb = torch.randn(3 * C, device=DEV)
+        tb = torch.randn(169, nh, device=DEV)
+        nwin = B * ((res + 6) // 7) ** 2
+        byts = B * res * res * (3 * C + C) * 2
+        for p in (0.0, 0.05):
+            for shift in (0, 3):
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    f = lambda: ops.window_attention(qkv, qb, tb, nh, shift, p, 1)
+                    ms = timeit(f)
+                    q = qkv.clone().requires_grad_(True)
+                    y = ops.window_attention(q, qb, tb, nh, shift, p, 1)
+                    dy = torch.randn_like(y)
+
+                    def bw():
+                        torch.autograd.grad(y, q, dy, retain_graph=True)
+                    msb = timeit(bw)
+                print(f"attn stage{stage} res{res} nh{nh} p={p} shift={shift}: fwd {ms*1e3:7.1f} us "
+                      f"({byts/ms/1e6:6.0f} GB/s, {nwin*nh/ms/1e3:6.1f} Mitem/s)  bwd {msb*1e3:7.1f} us")
+
+
+def wgrad():
+    from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
+    shapes = [(B * 65536, 288, 96), (B * 65536, 96, 96), (B * 65536, 384, 96), (B * 65536, 96, 384),
+              (B * 65536, 1536, 96), (B * 16384, 576, 192), (B * 16384, 768, 192), (B * 16384, 192, 768),
+              (B * 4096, 1152, 384), (B * 4096, 1536, 384), (B * 1024, 3072, 768)]
+    for M, N, K in shapes:
+        dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+        x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+        L = _lib.lib()
+        ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=DEV)
+        dw = torch.empty(N, K, device=DEV)
+        db = torch.empty(N, device=DEV)
+        s = torch.cuda.current_stream().cuda_stream
+        f = lambda: _lib.call("msu_linear_wgrad", 1, dy.data_ptr(), x.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                              ws.data_ptr(), M, N, K, 0, s)
+        ms = timeit(f)
+        fl = 2.0 * M * N * K
+        byts = M * (N + K) * 2
+        mt = timeit(lambda: dy.t().matmul(x))
+        print(f"wgrad M={M:8d} N={N:5d} K={K:5d}: {ms*1e3:7.1f} us {fl/ms/1e9:7.1f} TF/s "
+              f"{byts/ms/1e6:6.0f} GB/s (min bytes)   hipBLASLt dY^T X {mt*1e3:7.1f} us")
+
+
+def conv():
+    C, H = 96, 1024
+    x = torch.randn(B, H // 4, H // 4, 16 * C, device=DEV, dtype=torch.bfloat16)
+    z1 = torch.randn(B, H, H, C, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(C, C, 3, 3, device=DEV) * 0.03
+    b = torch.randn(C, device=DEV)
+    fl = 2.0 * B * H * H * C * C * 9
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        for name, inp, d2s in (("conv1(d2s)", x, True), ("conv2", z1, False)):
+            ms = timeit(lambda: ops.refine_conv(inp, w, b, d2s, (H, H)), 5)
+            q = inp.clone().requires_grad_(True)
+            wq = w.clone().requires_grad_(True)
+            z = ops.refine_conv(q, wq, b, d2s, (H, H))
+            dz = torch.randn_like(z)
+            msb = timeit(lambda: torch.autograd.grad(z, (q, wq), dz, retain_graph=True), 5)
+            print(f"{name}: fwd {ms:.3f} ms ({fl/ms/1e9:.0f} TF/s)  bwd(dgrad+wgrad) {msb:.3f} ms ({2*fl/msb/1e9:.0f} TF/s)")
+
+
+def ln():
+    for rows, C in ((B * 65536, 96), (B * 16384, 192), (B * 4096, 384), (B * 1048576, 96)):
+        x = torch.randn(rows, C, device=DEV, dtype=torch.bfloat16)
+        w = torch.randn(C, device=DEV)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            ms = timeit(lambda: ops.layer_norm(x, w, w))
+            q = x.clone().requires_grad_(True)
+            y = ops.layer_norm(q, w, w)
+            dy = torch.randn_like(y)
+            msb = timeit(lambda: torch.autograd.grad(y, q, dy, retain_graph=True))
+        print(f"LN rows={rows} C={C}: fwd {ms*1e3:.1f} us ({2*rows*C*2/ms/1e6:.0f} GB/s) "
+              f"bwd {msb*1e3:.1f} us ({3*rows*C*2/msb/1e6:.0f} GB/s)")
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    for name, fn in (("attn", attn), ("wgrad", wgrad), ("conv", conv), ("ln", ln)):
+        if what in (name, "all"):
+            fn()
