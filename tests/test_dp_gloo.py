@@ -1,0 +1,95 @@
+"""CPU (gloo, world_size 2): the bucketed, backward-overlapped gradient all-reduce of
+trainer.GradBucketer over flat gradient buffers gives exactly the gradient of the global
+batch (sum over ranks), for any bucket size, and leaves every rank with identical
+gradients -- the data-parallel semantics of the reference's nn.DataParallel
+(trainer.py:96-97: loss = mean over the global batch, grads reduced)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn as nn
+
+from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import FlatGroup, GradBucketer, is_no_decay, cosine_lr
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model():
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Linear(16, 32), nn.LayerNorm(32), nn.GELU(), nn.Linear(32, 8))
+
+
+def _data(rank, n=6):
+    g = torch.Generator().manual_seed(100 + rank)
+    return torch.randn(n, 16, generator=g), torch.randn(n, 8, generator=g)
+
+
+def _worker(rank, world, port, bucket_bytes, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = _model()
+    named = list(m.named_parameters())
+    decay = [(n, p) for n, p in named if not is_no_decay(n, p)][::-1]
+    nodecay = [(n, p) for n, p in named if is_no_decay(n, p)][::-1]
+    groups = [FlatGroup(decay, 0.01, "cpu"), FlatGroup(nodecay, 0.0, "cpu")]
+    red = GradBucketer(groups, bucket_bytes)
+    for step in range(2):
+        x, y = _data(rank + 10 * step)
+        loss = ((m(x) - y) ** 2).mean() / world  # each rank's share of the global mean
+        loss.backward()
+        red.finish()
+        grads = torch.cat([g.grad.clone() for g in groups])
+        out[(rank, step)] = grads
+        for g in groups:
+            g.grad.zero_()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bucket_bytes", [64, 1 << 20])
+def test_bucketed_allreduce_equals_global_batch(bucket_bytes):
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), bucket_bytes, out), nprocs=world, join=True)
+    for step in range(2):
+        m = _model()
+        named = list(m.named_parameters())
+        xs, ys = zip(*[_data(r + 10 * step) for r in range(world)])
+        loss = ((m(torch.cat(xs)) - torch.cat(ys)) ** 2).mean()
+        loss.backward()
+        decay = [p for n, p in named if not is_no_decay(n, p)][::-1]
+        nodecay = [p for n, p in named if is_no_decay(n, p)][::-1]
+        ref = torch.cat([p.grad.reshape(-1) for p in decay + nodecay])
+        g0, g1 = out[(0, step)], out[(1, step)]
+        assert torch.equal(g0, g1), "ranks disagree"
+        torch.testing.assert_close(g0, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_no_decay_rule_matches_reference():
+    """trainer.py:137: 1-D params, '.bias' names and names containing 'norm' -> no decay."""
+    p2 = torch.zeros(3, 3)
+    p1 = torch.zeros(3)
+    assert not is_no_decay("layers.0.blocks.0.attn.qkv.weight", p2)
+    assert is_no_decay("layers.0.blocks.0.attn.qkv.bias", p1)
+    assert is_no_decay("layers.0.blocks.0.norm1.weight", p1)
+    assert is_no_decay("layers.0.blocks.0.attn.relative_position_bias_table", torch.zeros(169, 3)) is False
+    assert is_no_decay("up.norm.weight", p1)
+
+
+def test_cosine_schedule_matches_timm_semantics():
+    """timm CosineLRScheduler(t_initial=60-20, warmup_t=20, warmup_prefix=True) per epoch."""
+    base, wlr, mn = 1e-5, 1e-6, 1e-6
+    assert cosine_lr(0, base, 20, 60, wlr, mn) == pytest.approx(wlr)
+    assert cosine_lr(10, base, 20, 60, wlr, mn) == pytest.approx(wlr + 10 * (base - wlr) / 20)
+    assert cosine_lr(20, base, 20, 60, wlr, mn) == pytest.approx(base)
+    assert cosine_lr(40, base, 20, 60, wlr, mn) == pytest.approx(mn + 0.5 * (base - mn))
+    assert cosine_lr(70, base, 20, 60, wlr, mn) == pytest.approx(mn)
