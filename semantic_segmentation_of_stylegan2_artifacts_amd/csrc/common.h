@@ -80,6 +80,16 @@ MSU_DEV float hash_uniform(uint64_t seed, uint64_t idx) {
   return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
 }
 
+// Cheap 32-bit counter hash (murmur3 fmix32 of idx*golden + seed): uniform in [0, 1).
+// Used for dropout masks that forward and backward regenerate identically.
+MSU_DEV float hash_uniform32(uint32_t seed, uint32_t idx) {
+  uint32_t x = idx * 0x9E3779B9u + seed;
+  x ^= x >> 16; x *= 0x85EBCA6Bu;
+  x ^= x >> 13; x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return (float)(x >> 8) * (1.0f / 16777216.0f);
+}
+
 // XCD-aware bijective block remap: blocks b and b+8 share an XCD under round-robin
 // dispatch; give each XCD group a contiguous range of work items (speed only).
 MSU_DEV int xcd_remap(int b, int nb) {

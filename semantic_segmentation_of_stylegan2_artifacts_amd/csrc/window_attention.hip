@@ -168,7 +168,8 @@ MSU_DEV void softmax_block(f32x4 (&S)[4]) {
 
 MSU_DEV float drop_keep(uint64_t seed, long win, int h, int nh, int i, int j, float p) {
   const uint64_t idx = ((((uint64_t)win * nh + h) * 64 + i) * 64 + j);
-  return hash_uniform(seed, idx) >= p ? 1.0f / (1.0f - p) : 0.0f;
+  const uint32_t s = (uint32_t)seed ^ (uint32_t)(seed >> 32);
+  return hash_uniform32(s, (uint32_t)idx) >= p ? 1.0f / (1.0f - p) : 0.0f;
 }
 
 template <typename T>

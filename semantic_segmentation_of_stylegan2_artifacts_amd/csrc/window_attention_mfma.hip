@@ -138,8 +138,9 @@ MSU_DEV void stage_rows(const int* sTok, const bf16_t* const (&base)[NS], const 
 }
 
 MSU_DEV float drop_keep(uint64_t seed, long win, int h, int nh, int i, int j, float p) {
-  const uint64_t idx = ((((uint64_t)win * nh + h) * 64 + i) * 64 + j);
-  return hash_uniform(seed, idx) >= p ? 1.0f / (1.0f - p) : 0.0f;
+  const uint32_t idx = ((((uint32_t)win * nh + h) * 64 + i) * 64 + j);
+  const uint32_t s = (uint32_t)seed ^ (uint32_t)(seed >> 32);
+  return hash_uniform32(s, idx) >= p ? 1.0f / (1.0f - p) : 0.0f;
 }
 
 MSU_DEV void lds_sync() {
