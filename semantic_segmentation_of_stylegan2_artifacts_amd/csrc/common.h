@@ -10,6 +10,9 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // register-resident 16-B chunk
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t bf16_t;  // storage type of a bf16 activation
 
 enum MsuDtype { MSU_F32 = 0, MSU_BF16 = 1 };
@@ -68,6 +71,26 @@ MSU_DEV float gelu_grad_f(float x) {
   const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
   const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
   return cdf + x * pdf;
+}
+
+// bf16-path GELU: erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16
+// rounding of every consumer), one v_rcp + one v_exp; gelu' reuses the same exponential.
+MSU_DEV float erf_fast(float x, float& e_neg_x2) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  const float p = fmaf(fmaf(fmaf(fmaf(1.061405429f, t, -1.453152027f), t, 1.421413741f), t, -0.284496736f), t,
+                       0.254829592f) * t;
+  e_neg_x2 = __expf(-ax * ax);
+  return copysignf(fmaf(-p, e_neg_x2, 1.0f), x);
+}
+MSU_DEV float gelu_fast(float x) {
+  float e;
+  return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f, e));
+}
+MSU_DEV float gelu_grad_fast(float x) {
+  float e;  // e = exp(-x^2 / 2)
+  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f, e));
+  return fmaf(x * 0.39894228040143268f, e, cdf);
 }
 
 // ------------------------------------------------------------------ counter-based RNG

@@ -30,7 +30,6 @@ constexpr int LD = 40;   // staged [64 x 32] rows: 32 + 8 pad (80 B)
 constexpr int LDP = 72;  // [64 x 64] images: 64 + 8 pad (144 B)
 constexpr int TOK_PAD = -1, TOK_ZERO = -2;
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 

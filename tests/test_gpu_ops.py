@@ -227,6 +227,8 @@ CONV_CASES = [
     (2, 64, 64, 96, True),
     (1, 48, 32, 96, False),
     (1, 32, 32, 128, True),
+    (1, 40, 56, 96, True),     # partial 8x32 tiles of the persistent bf16 kernel
+    (2, 20, 36, 96, False),
 ]
 
 
