@@ -122,4 +122,25 @@ MSU_DEV int xcd_remap(int b, int nb) {
   return start + local;
 }
 
+// ------------------------------------------------------------------ LDS-DMA helpers
+// global_load_lds_dwordx4: each lane's 16 B land at lds_base + 16 * lane (lds_base is
+// wave-uniform); counted by vmcnt like any global load.
+typedef __attribute__((address_space(3))) void msu_lds_void;
+typedef __attribute__((address_space(1))) void msu_glb_void;
+MSU_DEV void glds16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((msu_glb_void*)src, (msu_lds_void*)lds_base, 16, 0, 0);
+}
+// s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0], expcnt[6:4], lgkmcnt[11:8], vmcnt_hi[15:14])
+template <int N> MSU_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
+// Zero source for DMA slots that must read zeros (rows / pixels outside the tensor): 4 KB,
+// addressed by slot so the requests spread over L2 channels instead of hammering one line.
+// Pure pad slots should re-read a real address of the same row instead.
+namespace {
+__device__ __attribute__((aligned(16))) uint32_t g_zero_region[1024];
+}
+MSU_DEV const void* zero_src(int slot) { return g_zero_region + 4 * (slot & 255); }
+
 #define MSU_CHECK_LAUNCH() (hipGetLastError() == hipSuccess ? 0 : -1)

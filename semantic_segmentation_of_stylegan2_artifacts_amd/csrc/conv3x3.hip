@@ -593,8 +593,6 @@ __global__ void __launch_bounds__(64 * NT) conv3x3_wgrad_kernel(const T* __restr
 // DMAs land (vmcnt), each wave GELU-converts the halo slots it wrote, in place, so no
 // registers are held across the tile and no extra barrier is needed.
 // Partials: [block][dy][co][dx][ci] + db [block][co], the layout wgrad_reduce_kernel sums.
-__device__ __attribute__((aligned(16))) uint32_t g_zero16[4];
-
 template <bool IN_D2S, bool IN_GELU>
 __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __restrict__ X,
                                                                const bf16_t* __restrict__ DY,
@@ -638,18 +636,17 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
       const int k = wave + NW * r;
       if (k < NINS) {
         const int s = 64 * k + ln;
-        const int pix = s / SLOTS, ch = s - (s / SLOTS) * SLOTS;
-        const void* src = g_zero16;
-        if (ch < SLOTS - 1) {
-          if (pix < HPIX) {
-            const int row = pix / HWD, col = pix - (pix / HWD) * HWD;
-            const int y = y0 - 1 + row, x = x0 - 1 + col;
-            if (y >= 0 && y < g.H && x >= 0 && x < g.W) src = X + pix_off32<IN_D2S>(b, y, x, g.H, g.W, C) + ch * 8;
-          } else if (pix < HPIX + DPIX) {
-            const int dp = pix - HPIX;
-            const int y = y0 + dp / TWV, x = x0 + dp % TWV;
-            if (y < g.H && x < g.W) src = DY + pix_off32<false>(b, y, x, g.H, g.W, C) + ch * 8;
-          }
+        const int pix = s / SLOTS, ch0 = s - (s / SLOTS) * SLOTS;
+        const int ch = ch0 < SLOTS - 1 ? ch0 : 0;  // pad slot: re-read chunk 0 of the pixel
+        const void* src = zero_src(s);
+        if (pix < HPIX) {
+          const int row = pix / HWD, col = pix - (pix / HWD) * HWD;
+          const int y = y0 - 1 + row, x = x0 - 1 + col;
+          if (y >= 0 && y < g.H && x >= 0 && x < g.W) src = X + pix_off32<IN_D2S>(b, y, x, g.H, g.W, C) + ch * 8;
+        } else if (pix < HPIX + DPIX) {
+          const int dp = pix - HPIX;
+          const int y = y0 + dp / TWV, x = x0 + dp % TWV;
+          if (y < g.H && x < g.W) src = DY + pix_off32<false>(b, y, x, g.H, g.W, C) + ch * 8;
         }
         __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(lds + buf * BUF + 64 * 8 * k), 16, 0, 0);
       }

@@ -13,13 +13,23 @@
 //     buffered, and read k-strided with ds_read_b64_tr_b16;
 //   * S partial tiles are reduced deterministically (colsum); the bias gradient rides along
 //     on the k-tile-0 workgroups.
+#include <stdlib.h>
+
 #include "common.h"
 #include "mfma_frag.h"
 #include "reduce.h"
 
 namespace {
 
-constexpr int BM = 64;  // rows of M per LDS stage (two MFMA k-steps)
+constexpr int BM = 64;
+
+MSU_DEV void unpack8(const u32x4& q, float (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(q[i] << 16);
+    v[2 * i + 1] = __uint_as_float(q[i] & 0xffff0000u);
+  }
+}  // rows of M per LDS stage (two MFMA k-steps)
 
 template <typename T, int NTW>
 __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ dY, const T* __restrict__ X,
@@ -115,6 +125,245 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ dY, co
   if (do_bias && tid < BT && n0 + tid < N) dbpart[(long)blockIdx.y * N + n0 + tid] = dbacc;
 }
 
+// bf16: wave-sized output tiles.  Each wave owns a full WT x WT output tile (WT = 96 or
+// 128, 36 / 64 accumulators of 16x16) so every fragment read from LDS feeds NTW MFMAs;
+// the 4 waves split either N (WN waves along N, sharing the X rows of the stage) or the
+// rows of the stage (WM = 4 / WN waves, each its own partial slab).  Staging is LDS-DMA:
+// a stage is RS = 32 * WM rows of dY [RS][BN+8] and X [RS][WT+8] written lane-linearly by
+// global_load_lds_dwordx4 (pad slots re-read chunk 0 of their row; rows past the block's
+// range read the spread zero region); a ring of NST stages keeps NST-1 in flight; raw
+// s_barrier + counted vmcnt keep the prefetch alive across barriers.
+template <int NTW, int WN, int NST>
+__global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
+                                                         float* __restrict__ part, float* __restrict__ dbpart,
+                                                         long M, int N, int K, long mchunk) {
+  constexpr int WM = 4 / WN, WT = 16 * NTW, BN = WN * WT, RS = 32 * WM;
+  constexpr int SA = (BN + 8) / 8, SB = (WT + 8) / 8;  // 16-B slots per row
+  constexpr int LA = 8 * SA, LB = 8 * SB;              // row strides (elements)
+  constexpr int SLOTS = RS * (SA + SB);
+  constexpr int INS = ((SLOTS + 63) / 64 + 3) / 4 * 4;
+  constexpr int PER_WAVE = INS / 4;
+  constexpr int STG = INS * 64 * 8;
+  static_assert(PER_WAVE * (NST - 2) < 64, "vmcnt");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem_raw);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wni = wave % WN, wmi = wave / WN;
+  const int ntk = K / WT;
+  const int tn = blockIdx.x / ntk, tk = blockIdx.x - (blockIdx.x / ntk) * ntk;
+  const int n0 = tn * BN, k0 = tk * WT;
+  const long m_begin = (long)blockIdx.y * mchunk;
+  long m_end = m_begin + mchunk;
+  if (m_end > M) m_end = M;
+  const int nstage = m_end > m_begin ? (int)((m_end - m_begin + RS - 1) / RS) : 0;
+
+  // per-lane DMA slot geometry, fixed across stages: row within the stage, element offset
+  // from the stage's first row of dY (A slots) or X (B slots); pad slots re-read chunk 0
+  int srow[PER_WAVE], soff[PER_WAVE];
+  bool sisA[PER_WAVE];
+#pragma unroll
+  for (int r = 0; r < PER_WAVE; ++r) {
+    const int s = 64 * (wave + 4 * r) + lane;
+    if (s < RS * SA) {
+      const int row = s / SA, c = s - (s / SA) * SA;
+      srow[r] = row;
+      soff[r] = row * N + n0 + (c < SA - 1 ? 8 * c : 0);
+      sisA[r] = true;
+    } else {
+      const int t = s < SLOTS ? s - RS * SA : 0;
+      const int row = t / SB, c = t - (t / SB) * SB;
+      srow[r] = s < SLOTS ? row : RS;  // slots past the image: always the zero region
+      soff[r] = row * K + k0 + (c < SB - 1 ? 8 * c : 0);
+      sisA[r] = false;
+    }
+  }
+  auto issue = [&](int st) __attribute__((always_inline)) {
+    bf16_t* buf = lds + (st % NST) * STG;
+    const long m0 = m_begin + (long)st * RS;
+    const long rem = m_end - m0;
+    const int valid = rem > RS ? RS : (rem < 0 ? 0 : (int)rem);
+    const bf16_t* baseA = dY + m0 * N;
+    const bf16_t* baseB = X + m0 * K;
+#pragma unroll
+    for (int r = 0; r < PER_WAVE; ++r) {
+      const bf16_t* src = (sisA[r] ? baseA : baseB) + soff[r];
+      glds16(srow[r] < valid ? (const void*)src : zero_src(64 * r + lane), buf + 64 * 8 * (wave + 4 * r));
+    }
+  };
+
+  f32x4 acc[NTW][NTW];
+  f32x4 accb[NTW];  // bias: dY rows times a ones operand
+#pragma unroll
+  for (int i = 0; i < NTW; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bool do_bias = dbpart != nullptr && tk == 0;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  // lane part of a k-strided fragment read (ds_read_b64_tr_b16): rows 8(lane>>4) + q,
+  // columns 4p; the second half of the fragment is 4 rows further
+  const int q = (lane & 15) >> 2, p4 = 4 * (lane & 3), r0 = wmi * 32 + 8 * (lane >> 4) + q;
+  const int laneA = r0 * LA + wni * WT + p4, laneB = RS * LA + r0 * LB + p4;
+  auto tr8 = [](const bf16_t* p, int second) {
+    typedef __attribute__((address_space(3))) msu_v4s lds_v4s;
+    const msu_v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
+    const msu_v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p + second));
+    msu_v4s both[2] = {lo, hi};
+    return *reinterpret_cast<bf16x8*>(both);
+  };
+
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st) issue(st);
+  for (int st = 0; st < nstage; ++st) {
+    wait_vmcnt<PER_WAVE * (NST - 2)>();
+    __builtin_amdgcn_s_barrier();
+    issue(st + NST - 1);  // into the buffer computed in the previous iteration
+    const bf16_t* buf = lds + (st % NST) * STG;
+    const bf16_t* pa = buf + laneA;
+    const bf16_t* pb = buf + laneB;
+    bf16x8 bf[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) bf[j] = tr8(pb + 16 * j, 4 * LB);
+#pragma unroll
+    for (int i = 0; i < NTW; ++i) {
+      const bf16x8 af = tr8(pa + 16 * i, 4 * LA);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
+      accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, ones, accb[i], 0, 0, 0);  // unconditional: no branch
+    }
+  }
+  wait_vmcnt<0>();  // every DMA has landed: the ring may be reused
+  // row-waves of the same output tile are summed in LDS first: one slab per split
+  if constexpr (WM > 1) {
+    float* red = reinterpret_cast<float*>(smem_raw);  // [WM][NTW*NTW*4][64] per N-wave
+    __syncthreads();
+    constexpr int PW = (NTW * NTW * 4 + NTW * 4) * 64;  // floats per wave
+    static_assert((size_t)WN * (WM - 1) * PW * 4 <= 160 * 1024, "LDS reduction");
+    float* mine = red + ((long)wni * (WM - 1) + (wmi > 0 ? wmi - 1 : 0)) * PW;
+    if (wmi > 0) {
+#pragma unroll
+    for (int i = 0; i < NTW; ++i) {
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mine[((i * NTW + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mine[(NTW * NTW * 4 + i * 4 + r) * 64 + lane] = accb[i][r];
+    }
+    }
+    __syncthreads();
+    if (wmi == 0) {
+#pragma unroll
+      for (int w = 1; w < WM; ++w) {
+        const float* other = red + ((long)wni * (WM - 1) + w - 1) * PW;
+#pragma unroll
+        for (int i = 0; i < NTW; ++i) {
+#pragma unroll
+          for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][j][r] += other[((i * NTW + j) * 4 + r) * 64 + lane];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) accb[i][r] += other[(NTW * NTW * 4 + i * 4 + r) * 64 + lane];
+        }
+      }
+    }
+  }
+  if (wmi != 0) return;
+  float* out = part + (long)blockIdx.y * N * K;
+#pragma unroll
+  for (int i = 0; i < NTW; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wni * WT + 16 * i + (lane >> 4) * 4 + r;
+        const int k = k0 + 16 * j + (lane & 15);
+        out[(long)n * K + k] = acc[i][j][r];
+      }
+  if (do_bias && (lane & 15) == 0) {
+    // every column of accb holds the row sums
+#pragma unroll
+    for (int i = 0; i < NTW; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        dbpart[(long)blockIdx.y * N + n0 + wni * WT + 16 * i + (lane >> 4) * 4 + r] = accb[i][r];
+  }
+}
+
+// bf16 plan: wave tile, waves along N, ring depth, splits (each split writes WM slabs)
+struct WavePlan {
+  int ntw = 0, wn = 1, nst = 3, S = 1;
+  int slabs() const { return S; }
+};
+
+inline WavePlan wave_plan(long M, int N, int K) {
+  WavePlan p;
+  if (N % 96 == 0 && K % 96 == 0) p.ntw = 6;
+  else if (N % 128 == 0 && K % 128 == 0) p.ntw = 8;
+  else return p;  // not supported: generic kernel
+  const int wt = 16 * p.ntw, nt = N / wt;
+  p.wn = nt % 4 == 0 ? 4 : (nt % 2 == 0 ? 2 : 1);
+  const int wm = 4 / p.wn, rs = 32 * wm;
+  const int sa = (p.wn * wt + 8) / 8, sb = (wt + 8) / 8;
+  const int ins = ((rs * (sa + sb) + 63) / 64 + 3) / 4 * 4;
+  const long stage_bytes = (long)ins * 64 * 16;
+  p.nst = (int)((160L * 1024) / stage_bytes);
+  if (p.nst > 6) p.nst = 6;
+  if (p.nst < 3) {  // ring too shallow: generic kernel
+    p.ntw = 0;
+    return p;
+  }
+  const long tiles = (long)(N / (p.wn * wt)) * (K / wt);
+  long s = 256 / tiles;  // at most one workgroup per CU (no tail wave), long row ranges
+  const long max_s = (M + 8 * rs - 1) / (8 * rs);  // at least 8 stages per split
+  if (s > max_s) s = max_s;
+  if (s < 1) s = 1;
+  p.S = (int)s;
+  return p;
+}
+
+template <int NTW, int WN, int NST>
+void launch_wave(dim3 grid, const bf16_t* dY, const bf16_t* X, float* part, float* dbpart, long M, int N, int K,
+                 long mchunk, hipStream_t st) {
+  constexpr int WM = 4 / WN, WT = 16 * NTW, RS = 32 * WM;
+  constexpr int SLOTS = RS * ((WN * WT + 8) / 8 + (WT + 8) / 8);
+  constexpr int INS = ((SLOTS + 63) / 64 + 3) / 4 * 4;
+  constexpr size_t lds = (size_t)NST * INS * 64 * 16;
+  if constexpr (lds <= 160 * 1024) {  // ring depths the plan never picks are not instantiated
+    auto kern = wgrad_wave_kernel<NTW, WN, NST>;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, dY, X, part, dbpart, M, N, K, mchunk);
+  }
+}
+
+int run_wave(const WavePlan& p, const bf16_t* dY, const bf16_t* X, float* part, float* dbpart, long M, int N, int K,
+             hipStream_t st) {
+  const int wt = 16 * p.ntw, wm = 4 / p.wn, rs = 32 * wm;
+  long mchunk = (M + p.S - 1) / p.S;
+  mchunk = (mchunk + rs - 1) / rs * rs;
+  const dim3 grid((unsigned)((N / (p.wn * wt)) * (K / wt)), (unsigned)p.S);
+#define MSU_WAVE(NTW, WN)                                                                                   \
+  if (p.ntw == NTW && p.wn == WN) {                                                                         \
+    switch (p.nst) {                                                                                        \
+      case 3: launch_wave<NTW, WN, 3>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;            \
+      case 4: launch_wave<NTW, WN, 4>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;            \
+      case 5: launch_wave<NTW, WN, 5>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;            \
+      case 6: launch_wave<NTW, WN, 6>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;            \
+    }                                                                                                       \
+  }
+  MSU_WAVE(6, 1) MSU_WAVE(6, 2) MSU_WAVE(6, 4) MSU_WAVE(8, 1) MSU_WAVE(8, 2) MSU_WAVE(8, 4)
+#undef MSU_WAVE
+  return -3;
+}
+
 inline int tile_of(int N, int K) { return (N % 128 == 0 && K % 128 == 0) ? 128 : 96; }
 
 inline int pick_splits(long M, int N, int K) {
@@ -135,7 +384,13 @@ int msu_wgrad_splits(long M, int N, int K) { return pick_splits(M, N, K); }
 
 long msu_wgrad_workspace(long M, int N, int K) {
   const int S = pick_splits(M, N, K);
-  return (long)S * N * K + (long)S * N;
+  long ws = (long)S * N * K + (long)S * N;
+  const WavePlan p = wave_plan(M, N, K);
+  if (p.ntw) {
+    const long w2 = (long)p.slabs() * N * K + (long)p.slabs() * N;
+    if (w2 > ws) ws = w2;
+  }
+  return ws;
 }
 
 // dW [N][K] f32 (overwritten, or accumulated when accumulate != 0), db [N] f32 (may be null).
@@ -147,6 +402,19 @@ int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float*
     if (!accumulate) hipMemsetAsync(dW, 0, sizeof(float) * (long)N * K, st);
     if (db && !accumulate) hipMemsetAsync(db, 0, sizeof(float) * N, st);
     return MSU_CHECK_LAUNCH();
+  }
+  static const bool generic_only = getenv("MSU_WGRAD_GENERIC") != nullptr;  // A/B timing switch
+  if (dtype == MSU_BF16 && !generic_only) {
+    const WavePlan p = wave_plan(M, N, K);
+    if (p.ntw) {
+      float* part = workspace;
+      float* dbpart = db ? workspace + (long)p.slabs() * N * K : nullptr;
+      const int rc = run_wave(p, (const bf16_t*)dY, (const bf16_t*)X, part, dbpart, M, N, K, st);
+      if (rc) return rc;
+      colsum(part, p.slabs(), (long)N * K, (long)N * K, dW, accumulate, st);
+      if (db) colsum(dbpart, p.slabs(), N, N, db, accumulate, st);
+      return MSU_CHECK_LAUNCH();
+    }
   }
   const int S = pick_splits(M, N, K);
   long mchunk = (M + S - 1) / S;
