@@ -41,12 +41,13 @@ int msu_layernorm_fwd(int dtype, int mode, const void* x, const void* b, const f
                       float eps, void* stream);
 /* Backward: dx (scattered for merge / d2s2), optional dres added to dx (plain / add modes),
  * db = dx * bscale (add mode), dgamma/dbeta via nparts partial rows in `part`
- * ([nparts, 2, C] f32; nparts from msu_ln_part_blocks). */
+ * ([nparts, 2, C] f32; nparts from msu_ln_part_blocks), written or (accumulate != 0) added
+ * to dgamma/dbeta -- the latter lets a trainer accumulate straight into .grad. */
 int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const void* dres,
                       const float* gamma, const float* mean, const float* rstd, void* dx,
                       void* db, const float* bscale, long rows_per_sample, float* part,
                       int nparts, float* dgamma, float* dbeta, long rows, int C, int H, int W,
-                      int Cin, void* stream);
+                      int Cin, int accumulate, void* stream);
 int msu_ln_part_blocks(long rows, int C);
 int msu_reduce_rows(const float* part, int nparts, int n, long stride, float* out,
                     int accumulate, void* stream);

@@ -18,7 +18,7 @@ U64 = ctypes.c_ulonglong
 SIGNATURES = {
     "msu_ln_part_blocks": (I, [L, I]),
     "msu_layernorm_fwd": (I, [I, I, P, P, P, L, P, P, P, P, P, P, L, I, I, I, I, F, P]),
-    "msu_layernorm_bwd": (I, [I, I, P, P, P, P, P, P, P, P, P, L, P, I, P, P, L, I, I, I, I, P]),
+    "msu_layernorm_bwd": (I, [I, I, P, P, P, P, P, P, P, P, P, L, P, I, P, P, L, I, I, I, I, I, P]),
     "msu_reduce_rows": (I, [P, I, I, L, P, I, P]),
     "msu_head_fwd": (I, [I, P, P, P, P, P, P, P, L, I, F, P]),
     "msu_head_bwd": (I, [I, P, P, P, P, P, P, P, P, P, I, P, P, P, L, I, P]),

@@ -99,24 +99,45 @@ __global__ void __launch_bounds__(256) dynloss_partial_kernel(const T* logits, c
 }
 
 // One block: finalise per-sample loss terms.  coef[b] = {w_bce, has_tv, num, den}; flags[0]=binarise
-__global__ void __launch_bounds__(64) dynloss_final_kernel(const float* part, int B, int nblk, long N,
-                                                           float alpha, float beta, float mix,
-                                                           float smooth, float* loss, float* coef) {
+// Per-sample totals over the nblk partial rows: one wave per (sample, quantity), lanes
+// stride over the partial rows, fixed-order double-precision shuffle tree (deterministic).
+MSU_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(512) dynloss_final_kernel(const float* part, int B, int nblk, long N,
+                                                            float alpha, float beta, float mix,
+                                                            float smooth, float* loss, float* coef) {
   __shared__ int binarise;
+  __shared__ double sums[64][5];  // B <= 64
+  __shared__ float wmax[8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float mx = -INFINITY;
+  for (long i = threadIdx.x; i < (long)B * nblk; i += 512) mx = fmaxf(mx, part[i * NS + 10]);
+  mx = group_max<64>(mx);
+  if (lane == 0) wmax[wave] = mx;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    float mx = -INFINITY;
-    for (int b = 0; b < B; ++b)
-      for (int k = 0; k < nblk; ++k) mx = fmaxf(mx, part[((long)b * nblk + k) * NS + 10]);
-    binarise = mx > 1.f;
+    float m = wmax[0];
+    for (int w = 1; w < 8; ++w) m = fmaxf(m, wmax[w]);
+    binarise = m > 1.f;
+  }
+  __syncthreads();
+  const int o = binarise ? 5 : 0;
+  for (int bq = wave; bq < B * 5; bq += 8) {
+    const int b = bq / 5, q = bq - (bq / 5) * 5;
+    double v = 0.0;
+    for (int k = lane; k < nblk; k += 64) v += part[((long)b * nblk + k) * NS + o + q];
+    v = wave_sum_d(v);
+    if (lane == 0) sums[b][q] = v;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int o = binarise ? 5 : 0;
     double total = 0.0;
     for (int b = 0; b < B; ++b) {
-      double s[5] = {0, 0, 0, 0, 0};
-      for (int k = 0; k < nblk; ++k)
-        for (int q = 0; q < 5; ++q) s[q] += part[((long)b * nblk + k) * NS + o + q];
+      const double* s = sums[b];
       const double bce = s[0] / (double)N;
       float* c = coef + 4 * b;
       if (s[4] != 0.0) {
@@ -264,7 +285,8 @@ int msu_dynloss_fwd(int dtype, const void* logits, const float* target, int B, l
   else
     hipLaunchKernelGGL(dynloss_partial_kernel<float>, dim3(nblk, B), dim3(256), 0, st,
                        (const float*)logits, target, N, nblk, part);
-  hipLaunchKernelGGL(dynloss_final_kernel, dim3(1), dim3(64), 0, st, part, B, nblk, N, alpha, beta,
+  if (B > 64) return -2;
+  hipLaunchKernelGGL(dynloss_final_kernel, dim3(1), dim3(512), 0, st, part, B, nblk, N, alpha, beta,
                      mix, 1e-6f, loss, coef);
   return MSU_CHECK_LAUNCH();
 }

@@ -283,14 +283,18 @@ int fwd_dispatch(int dtype, const LnArgs& a, hipStream_t st) {
 }
 
 template <int MODE>
-int bwd_dispatch(int dtype, const LnBwdArgs& a, float* dgamma, float* dbeta, int nparts,
+int bwd_dispatch(int dtype, const LnBwdArgs& a, float* dgamma, float* dbeta, int nparts, int accumulate,
                  hipStream_t st) {
   if (a.C % 4 != 0 || a.C > 2048) return -2;
   if (a.rows == 0) return 0;
   int rc = dtype == MSU_BF16 ? launch_bwd<bf16_t, MODE>(a, st, nparts) : launch_bwd<float, MODE>(a, st, nparts);
   if (rc) return rc;
-  colsum(a.part, nparts, a.C, (long)2 * a.C, dgamma, 0, st);
-  colsum(a.part + a.C, nparts, a.C, (long)2 * a.C, dbeta, 0, st);
+  if (dbeta == dgamma + a.C) {  // contiguous [dgamma | dbeta]: one reduction launch
+    colsum(a.part, nparts, 2L * a.C, 2L * a.C, dgamma, accumulate, st);
+  } else {
+    colsum(a.part, nparts, a.C, (long)2 * a.C, dgamma, accumulate, st);
+    colsum(a.part + a.C, nparts, a.C, (long)2 * a.C, dbeta, accumulate, st);
+  }
   return MSU_CHECK_LAUNCH();
 }
 
@@ -419,6 +423,144 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* dlogit, cons
   }
 }
 
+// bf16, C % 32 == 0: 4 lanes per row, 16-B loads (KC chunks of 8 channels per lane), the
+// lane's gamma*w / beta*w slices held in registers, two rows per iteration for ILP.
+MSU_DEV uint32_t pack2bf(float a, float b) {
+  return (uint32_t)from_f32<bf16_t>(a) | ((uint32_t)from_f32<bf16_t>(b) << 16);
+}
+
+template <int KC>
+__global__ void __launch_bounds__(256) head_fwd16_kernel(const bf16_t* z, const float* gamma, const float* beta,
+                                                         const float* w, float* logit, float* mean,
+                                                         float* rstd, long rows, float eps) {
+  constexpr int TPR = 4, C = 32 * KC, RPB = 256 / TPR;
+  const int lane = threadIdx.x % TPR, grp = threadIdx.x / TPR;
+  float gw[KC][8];
+  float bwsum = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = (lane + TPR * k) * 8 + e;
+      gw[k][e] = gamma[c] * w[c];
+      bwsum += beta[c] * w[c];
+    }
+  bwsum = group_sum<TPR>(bwsum);
+  for (long r0 = ((long)blockIdx.x * RPB + grp) * 2; r0 < rows; r0 += (long)gridDim.x * RPB * 2) {
+    float v[2][KC][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long r = r0 + h < rows ? r0 + h : r0;
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        const u32x4 q = *reinterpret_cast<const u32x4*>(z + r * C + (lane + TPR * k) * 8);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[h][k][2 * i] = __uint_as_float(q[i] << 16);
+          v[h][k][2 * i + 1] = __uint_as_float(q[i] & 0xffff0000u);
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sum += v[h][k][e];
+      const float mu = group_sum<TPR>(sum) * (1.0f / C);
+      float var = 0.f, dot = 0.f;
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = v[h][k][e] - mu;
+          var += d * d;
+          dot += d * gw[k][e];
+        }
+      const float rs = rsqrtf(group_sum<TPR>(var) * (1.0f / C) + eps);
+      dot = group_sum<TPR>(dot) * rs + bwsum;
+      if (lane == 0 && r0 + h < rows) {
+        logit[r0 + h] = dot;
+        mean[r0 + h] = mu;
+        rstd[r0 + h] = rs;
+      }
+    }
+  }
+}
+
+// dgamma_c = w_c A_c, dbeta_c = w_c D, dw_c = gamma_c A_c + beta_c D with A_c = sum_r dl xh_c,
+// D = sum_r dl: per block only A (per channel) and D are accumulated, reduced over the
+// block's 64 row groups in fixed order through LDS, and expanded into the [3][C] partial.
+template <int KC>
+__global__ void __launch_bounds__(256) head_bwd16_kernel(const float* dlogit, const bf16_t* z, const float* gamma,
+                                                         const float* beta, const float* w, const float* mean,
+                                                         const float* rstd, bf16_t* dz,
+                                                         float* part /* [grid, 3, C] */, long rows) {
+  constexpr int TPR = 4, C = 32 * KC, RPB = 256 / TPR;
+  __shared__ float redA[RPB][C + 1];
+  __shared__ float redD[RPB];
+  const int lane = threadIdx.x % TPR, grp = threadIdx.x / TPR;
+  float gw[KC][8], acc[KC][8];
+  float adl = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = (lane + TPR * k) * 8 + e;
+      gw[k][e] = gamma[c] * w[c];
+      acc[k][e] = 0.f;
+    }
+  for (long r = (long)blockIdx.x * RPB + grp; r < rows; r += (long)gridDim.x * RPB) {
+    const float mu = mean[r], rs = rstd[r], dl = dlogit[r];
+    float xh[KC][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const u32x4 q = *reinterpret_cast<const u32x4*>(z + r * C + (lane + TPR * k) * 8);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        xh[k][2 * i] = (__uint_as_float(q[i] << 16) - mu) * rs;
+        xh[k][2 * i + 1] = (__uint_as_float(q[i] & 0xffff0000u) - mu) * rs;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g = dl * gw[k][e];
+        s1 += g;
+        s2 += g * xh[k][e];
+        acc[k][e] += dl * xh[k][e];
+      }
+    }
+    adl += dl;
+    s1 = group_sum<TPR>(s1) * (1.0f / C);
+    s2 = group_sum<TPR>(s2) * (1.0f / C);
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = rs * (dl * gw[k][e] - s1 - xh[k][e] * s2);
+      *reinterpret_cast<u32x4*>(dz + r * C + (lane + TPR * k) * 8) =
+          u32x4{pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7])};
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < KC; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) redA[grp][(lane + TPR * k) * 8 + e] = acc[k][e];
+  if (lane == 0) redD[grp] = adl;
+  __syncthreads();
+  float D = 0.f;
+  for (int g = 0; g < RPB; ++g) D += redD[g];
+  float* P = part + (long)blockIdx.x * 3 * C;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float A = 0.f;
+    for (int g = 0; g < RPB; ++g) A += redA[g][c];
+    P[c] = w[c] * A;
+    P[C + c] = w[c] * D;
+    P[2 * C + c] = gamma[c] * A + beta[c] * D;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -430,6 +572,13 @@ int msu_head_fwd(int dtype, const void* z, const float* gamma, const float* beta
   long nb = (rows + 31) / 32;
   if (nb > 8192) nb = 8192;
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == MSU_BF16 && (C == 96 || C == 128)) {
+    long g = (rows + 127) / 128;
+    if (g > 4096) g = 4096;
+    if (C == 96) hipLaunchKernelGGL((head_fwd16_kernel<3>), dim3(g), dim3(256), 0, st, (const bf16_t*)z, gamma, beta, w, logit, mean, rstd, rows, eps);
+    else hipLaunchKernelGGL((head_fwd16_kernel<4>), dim3(g), dim3(256), 0, st, (const bf16_t*)z, gamma, beta, w, logit, mean, rstd, rows, eps);
+    return MSU_CHECK_LAUNCH();
+  }
   if (dtype == MSU_BF16) {
     if (C <= 128) hipLaunchKernelGGL((head_fwd_kernel<bf16_t, 4>), dim3(nb), dim3(256), 0, st, (const bf16_t*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps);
     else hipLaunchKernelGGL((head_fwd_kernel<bf16_t, 8>), dim3(nb), dim3(256), 0, st, (const bf16_t*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps);
@@ -448,16 +597,24 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
   if (C % 4 || C > 256) return -2;
   if (rows == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MSU_BF16) {
+  if (dtype == MSU_BF16 && C == 96)
+    hipLaunchKernelGGL((head_bwd16_kernel<3>), dim3(nparts), dim3(256), 0, st, dlogit, (const bf16_t*)z, gamma, beta, w, mean, rstd, (bf16_t*)dz, part, rows);
+  else if (dtype == MSU_BF16 && C == 128)
+    hipLaunchKernelGGL((head_bwd16_kernel<4>), dim3(nparts), dim3(256), 0, st, dlogit, (const bf16_t*)z, gamma, beta, w, mean, rstd, (bf16_t*)dz, part, rows);
+  else if (dtype == MSU_BF16) {
     if (C <= 128) hipLaunchKernelGGL((head_bwd_kernel<bf16_t, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const bf16_t*)z, gamma, beta, w, mean, rstd, (bf16_t*)dz, part, rows, C);
     else hipLaunchKernelGGL((head_bwd_kernel<bf16_t, 8>), dim3(nparts), dim3(256), 0, st, dlogit, (const bf16_t*)z, gamma, beta, w, mean, rstd, (bf16_t*)dz, part, rows, C);
   } else {
     if (C <= 128) hipLaunchKernelGGL((head_bwd_kernel<float, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const float*)z, gamma, beta, w, mean, rstd, (float*)dz, part, rows, C);
     else hipLaunchKernelGGL((head_bwd_kernel<float, 8>), dim3(nparts), dim3(256), 0, st, dlogit, (const float*)z, gamma, beta, w, mean, rstd, (float*)dz, part, rows, C);
   }
-  colsum(part, nparts, C, (long)3 * C, dgamma, 0, st);
-  colsum(part + C, nparts, C, (long)3 * C, dbeta, 0, st);
-  colsum(part + 2 * C, nparts, C, (long)3 * C, dw, 0, st);
+  if (dbeta == dgamma + C && dw == dgamma + 2 * C) {  // contiguous [dgamma | dbeta | dw]
+    colsum(part, nparts, 3L * C, 3L * C, dgamma, 0, st);
+  } else {
+    colsum(part, nparts, C, (long)3 * C, dgamma, 0, st);
+    colsum(part + C, nparts, C, (long)3 * C, dbeta, 0, st);
+    colsum(part + 2 * C, nparts, C, (long)3 * C, dw, 0, st);
+  }
   return MSU_CHECK_LAUNCH();
 }
 
@@ -488,15 +645,15 @@ int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const 
                       const float* gamma, const float* mean, const float* rstd, void* dx,
                       void* db, const float* bscale, long rows_per_sample, float* part,
                       int nparts, float* dgamma, float* dbeta, long rows, int C, int H, int W,
-                      int Cin, void* stream) {
+                      int Cin, int accumulate, void* stream) {
   LnBwdArgs a{dy, x, dres, gamma, mean, rstd, dx, db, bscale, part, rows, C, H, W, Cin,
               rows_per_sample > 0 ? rows_per_sample : 1};
   hipStream_t st = (hipStream_t)stream;
   switch (mode) {
-    case IN_PLAIN: return bwd_dispatch<IN_PLAIN>(dtype, a, dgamma, dbeta, nparts, st);
-    case IN_ADD: return bwd_dispatch<IN_ADD>(dtype, a, dgamma, dbeta, nparts, st);
-    case IN_MERGE: return bwd_dispatch<IN_MERGE>(dtype, a, dgamma, dbeta, nparts, st);
-    case IN_D2S2: return bwd_dispatch<IN_D2S2>(dtype, a, dgamma, dbeta, nparts, st);
+    case IN_PLAIN: return bwd_dispatch<IN_PLAIN>(dtype, a, dgamma, dbeta, nparts, accumulate, st);
+    case IN_ADD: return bwd_dispatch<IN_ADD>(dtype, a, dgamma, dbeta, nparts, accumulate, st);
+    case IN_MERGE: return bwd_dispatch<IN_MERGE>(dtype, a, dgamma, dbeta, nparts, accumulate, st);
+    case IN_D2S2: return bwd_dispatch<IN_D2S2>(dtype, a, dgamma, dbeta, nparts, accumulate, st);
   }
   return -3;
 }

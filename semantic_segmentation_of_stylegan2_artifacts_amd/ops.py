@@ -53,6 +53,39 @@ def _as(t, dtype):
     return t.contiguous()
 
 
+# ----------------------------------------------------------------------------- direct grads
+# A trainer that keeps parameters and gradients in flat buffers (trainer.FlatGroup) marks
+# its parameters ``_msu_direct``: the backward kernels then add straight into the
+# preallocated ``.grad`` views (no temporary + AccumulateGrad add per parameter) and report
+# each parameter to ``_grad_ready`` (the bucketed all-reduce) themselves.
+_grad_ready = None
+
+
+def set_grad_ready_callback(fn):
+    global _grad_ready
+    _grad_ready = fn
+
+
+def _direct(*params):
+    return all(p is not None and getattr(p, "_msu_direct", False) and p.grad is not None for p in params)
+
+
+def _notify(*params):
+    if _grad_ready is not None:
+        for p in params:
+            if p is not None:
+                _grad_ready(p)
+
+
+def _ln_grads(ctx, C, device):
+    """(dgamma, dbeta, accumulate, direct) buffers for a LayerNorm backward."""
+    w, b = ctx.affine
+    if _direct(w, b):
+        return w.grad, b.grad, 1, True
+    dw, db = torch.empty(2, C, device=device, dtype=torch.float32)  # contiguous: one reduction
+    return dw, db, 0, False
+
+
 def _ln_parts(rows, C, device):
     n = _lib.lib().msu_ln_part_blocks(rows, C)
     return n, torch.empty(n * 3 * C, device=device, dtype=torch.float32)
@@ -75,6 +108,7 @@ class _LayerNorm(torch.autograd.Function):
         _lib.call("msu_layernorm_fwd", _dt(x), IN_PLAIN, _p(x), None, None, 1, None, _p(w), _p(b),
                   _p(y), _p(mean), _p(rstd), rows, C, 0, 0, 0, eps, _s(x))
         ctx.save_for_backward(x, w, mean, rstd)
+        ctx.affine = (w, b)
         return y
 
     @staticmethod
@@ -84,11 +118,13 @@ class _LayerNorm(torch.autograd.Function):
         C = x.shape[-1]
         rows = x.numel() // C
         dx = torch.empty_like(x)
-        dw = torch.empty(C, device=x.device, dtype=torch.float32)
-        db = torch.empty_like(dw)
+        dw, db, acc, direct = _ln_grads(ctx, C, x.device)
         n, part = _ln_parts(rows, C, x.device)
         _lib.call("msu_layernorm_bwd", _dt(x), IN_PLAIN, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, C, 0, 0, 0, _s(x))
+                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, C, 0, 0, 0, acc, _s(x))
+        if direct:
+            _notify(*ctx.affine)
+            return dx, None, None, None
         return dx, dw, db, None
 
 
@@ -115,6 +151,7 @@ class _AddLayerNorm(torch.autograd.Function):
                   _p(b), _p(y), _p(mean), _p(rstd), rows, C, 0, 0, 0, eps, _s(a))
         ctx.save_for_backward(s, w, mean, rstd, scale)
         ctx.rps = rps
+        ctx.affine = (w, b)
         ctx.set_materialize_grads(False)
         return s, y
 
@@ -129,11 +166,14 @@ class _AddLayerNorm(torch.autograd.Function):
         ds = None if ds is None else _as(ds, s.dtype)
         da = torch.empty_like(s)
         dbr = torch.empty_like(s) if scale is not None else None
-        dw = torch.empty(C, device=s.device, dtype=torch.float32)
-        dbb = torch.empty_like(dw)
+        dw, dbb, acc, direct = _ln_grads(ctx, C, s.device)
         n, part = _ln_parts(rows, C, s.device)
         _lib.call("msu_layernorm_bwd", _dt(s), IN_ADD, _p(dy), _p(s), _p(ds), _p(w), _p(mean), _p(rstd),
-                  _p(da), _p(dbr), _p(scale), ctx.rps, _p(part), n, _p(dw), _p(dbb), rows, C, 0, 0, 0, _s(s))
+                  _p(da), _p(dbr), _p(scale), ctx.rps, _p(part), n, _p(dw), _p(dbb), rows, C, 0, 0, 0, acc,
+                  _s(s))
+        if direct:
+            _notify(*ctx.affine)
+            dw = dbb = None
         return da, (dbr if dbr is not None else da), None, dw, dbb, None
 
 
@@ -156,6 +196,7 @@ class _MergeLayerNorm(torch.autograd.Function):
         _lib.call("msu_layernorm_fwd", _dt(x), IN_MERGE, _p(x), None, None, 1, None, _p(w), _p(b),
                   _p(y), _p(mean), _p(rstd), rows, 4 * C, H, W, C, eps, _s(x))
         ctx.save_for_backward(x, w, mean, rstd)
+        ctx.affine = (w, b)
         return y
 
     @staticmethod
@@ -165,11 +206,13 @@ class _MergeLayerNorm(torch.autograd.Function):
         rows = B * (H // 2) * (W // 2)
         dy = _as(dy, x.dtype)
         dx = torch.empty_like(x)
-        dw = torch.empty(4 * C, device=x.device, dtype=torch.float32)
-        db = torch.empty_like(dw)
+        dw, db, acc, direct = _ln_grads(ctx, 4 * C, x.device)
         n, part = _ln_parts(rows, 4 * C, x.device)
         _lib.call("msu_layernorm_bwd", _dt(x), IN_MERGE, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, 4 * C, H, W, C, _s(x))
+                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, 4 * C, H, W, C, acc, _s(x))
+        if direct:
+            _notify(*ctx.affine)
+            return dx, None, None, None
         return dx, dw, db, None
 
 
@@ -192,6 +235,7 @@ class _D2SLayerNorm(torch.autograd.Function):
         _lib.call("msu_layernorm_fwd", _dt(x), IN_D2S2, _p(x), None, None, 1, None, _p(w), _p(b),
                   _p(y), _p(mean), _p(rstd), rows, c, H, W, 0, eps, _s(x))
         ctx.save_for_backward(x, w, mean, rstd)
+        ctx.affine = (w, b)
         return y
 
     @staticmethod
@@ -202,11 +246,13 @@ class _D2SLayerNorm(torch.autograd.Function):
         rows = B * 4 * H * W
         dy = _as(dy, x.dtype)
         dx = torch.empty_like(x)
-        dw = torch.empty(c, device=x.device, dtype=torch.float32)
-        db = torch.empty_like(dw)
+        dw, db, acc, direct = _ln_grads(ctx, c, x.device)
         n, part = _ln_parts(rows, c, x.device)
         _lib.call("msu_layernorm_bwd", _dt(x), IN_D2S2, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, c, H, W, 0, _s(x))
+                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, c, H, W, 0, acc, _s(x))
+        if direct:
+            _notify(*ctx.affine)
+            return dx, None, None, None
         return dx, dw, db, None
 
 
@@ -278,17 +324,19 @@ class _LinearParams(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, dt):
-        w = weight.to(dt)
-        b = None if bias is None else bias.to(dt)
+        w = _shadow(weight, dt)
+        b = None if bias is None else _shadow(bias, dt)
         with torch.autocast("cuda", enabled=False):
             y = torch.nn.functional.linear(x, w, b)
         ctx.save_for_backward(x, w)
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
+        weight, bias = ctx.params
         dy = _as(dy, x.dtype)
         N, K = w.shape
         M = dy.numel() // N
@@ -298,10 +346,24 @@ class _LinearParams(torch.autograd.Function):
                 dx = dy.matmul(w)
         L = _lib.lib()
         ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
+        if _direct(weight) and (bias is None or _direct(bias)):
+            _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(weight.grad),
+                      _p(None if bias is None else bias.grad), _p(ws), M, N, K, 1, _s(x))
+            _notify(weight, bias)
+            return dx, None, None, None
         dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
         db = torch.empty(N, device=x.device, dtype=torch.float32) if ctx.has_bias else None
         _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(dw), _p(db), _p(ws), M, N, K, 0, _s(x))
         return dx, dw, db, None
+
+
+def _shadow(param, dt):
+    """bf16 copy of an f32 master parameter: the trainer's per-step shadow buffer when it
+    keeps one (``_msu_shadow``), else a cast."""
+    sh = getattr(param, "_msu_shadow", None)
+    if sh is not None and sh.dtype == dt and getattr(param, "_msu_shadow_ver", -1) == param._version:
+        return sh
+    return param.to(dt)
 
 
 # ----------------------------------------------------------------------------- GELU
@@ -352,8 +414,7 @@ class _HeadNormOut(torch.autograd.Function):
         rows = B * H * W
         dlogit = _f32(dlogit)
         dz = torch.empty_like(z)
-        dg = torch.empty(C, device=z.device, dtype=torch.float32)
-        db, dw = torch.empty_like(dg), torch.empty_like(dg)
+        dg, db, dw = torch.empty(3, C, device=z.device, dtype=torch.float32)  # contiguous: one reduction
         n, part = _ln_parts(rows, C, z.device)
         _lib.call("msu_head_bwd", _dt(z), _p(dlogit), _p(z), _p(gamma), _p(beta), _p(w), _p(mean),
                   _p(rstd), _p(dz), _p(part), n, _p(dg), _p(db), _p(dw), rows, C, _s(z))

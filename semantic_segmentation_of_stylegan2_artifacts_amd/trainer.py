@@ -60,6 +60,9 @@ class FlatGroup:
         self.grad = torch.zeros(n, device=device, dtype=torch.float32)
         self.exp_avg = torch.zeros_like(self.data)
         self.exp_avg_sq = torch.zeros_like(self.data)
+        # bf16 shadow of the parameters, refreshed once per step: the Linear ops read it
+        # instead of casting every weight at every call
+        self.shadow = torch.empty(n, device=device, dtype=torch.bfloat16)
         self.offsets = []
         off = 0
         for p in self.params:
@@ -67,16 +70,35 @@ class FlatGroup:
             self.data[off:off + k].copy_(p.detach().reshape(-1))
             p.data = self.data[off:off + k].view_as(p)
             p.grad = self.grad[off:off + k].view_as(p)
+            p._msu_shadow = self.shadow[off:off + k].view_as(p)
+            p._msu_shadow_ver = -1  # not valid until the first refresh
+            p._msu_direct = True  # backward kernels accumulate straight into p.grad
             self.offsets.append(off)
             off += k
 
+    def refresh_shadow(self):
+        """Re-cast the bf16 shadow after the master weights changed (AdamW writes them through
+        a raw pointer).  Each parameter records its version: an in-place write made through
+        the parameter itself (load_state_dict, ``p.copy_``) bumps it and makes the Linear ops
+        cast that weight again until the next refresh."""
+        self.shadow.copy_(self.data)
+        for p in self.params:
+            p._msu_shadow_ver = p._version
+
 
 class GradBucketer:
-    """Bucketed, backward-overlapped gradient all-reduce over flat gradient buffers."""
+    """Bucketed, backward-overlapped gradient all-reduce over flat gradient buffers.
+
+    A bucket is all-reduced as soon as every accumulation into its parameters' gradients has
+    happened.  Parameters used more than once per step (MS-UNet shares concat_back_dim[2/3]
+    between the central and the main decoder, model_parts.py:792-824) receive several
+    accumulations, so the number expected per bucket is measured on the first step (the
+    graph is static), which all-reduces every bucket after backward; later steps overlap.
+    """
 
     def __init__(self, groups, bucket_bytes, process_group=None):
         self.pg = process_group
-        self.buckets = []       # (group, start, end, n_params)
+        self.buckets = []       # (group, start, end)
         self.param_bucket = {}  # id(param) -> bucket index
         for g in groups:
             start = 0
@@ -86,33 +108,41 @@ class GradBucketer:
                 self.param_bucket[id(p)] = len(self.buckets)
                 count += 1
                 if (end - start) * 4 >= bucket_bytes:
-                    self.buckets.append([g, start, end, count])
+                    self.buckets.append([g, start, end])
                     start, count = end, 0
             if count:
-                self.buckets.append([g, start, g.numel, count])
+                self.buckets.append([g, start, g.numel])
+        self.expected = None    # accumulations per bucket, learned on the first step
         self.pending = [0] * len(self.buckets)
+        self.launched = [False] * len(self.buckets)
         self.works = []
         self.handles = []
         for g in groups:
             for p in g.params:
                 self.handles.append(p.register_post_accumulate_grad_hook(self._hook))
 
+    def _launch(self, b):
+        g, s, e = self.buckets[b]
+        self.launched[b] = True
+        self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+
     def _hook(self, p):
         b = self.param_bucket[id(p)]
         self.pending[b] += 1
-        if self.pending[b] == self.buckets[b][3]:
-            g, s, e, _ = self.buckets[b]
-            self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+        if self.expected is not None and self.pending[b] == self.expected[b]:
+            self._launch(b)
 
     def finish(self):
-        for b, (g, s, e, n) in enumerate(self.buckets):
-            if self.pending[b] != n:  # parameters that did not receive a gradient this step
-                self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg,
-                                                  async_op=True))
+        if self.expected is None:
+            self.expected = list(self.pending)
+        for b in range(len(self.buckets)):
+            if not self.launched[b]:
+                self._launch(b)
         for w in self.works:
             w.wait()
         self.works = []
         self.pending = [0] * len(self.buckets)
+        self.launched = [False] * len(self.buckets)
 
 
 class Trainer:
@@ -162,6 +192,10 @@ class Trainer:
     def step(self, images, labels):
         """One training step; returns the (device) loss of this rank's batch."""
         self.model.train()
+        ops.set_grad_ready_callback(self.reducer._hook if self.reducer is not None else None)
+        if self.amp_dtype == torch.bfloat16:
+            for g in self.groups:
+                g.refresh_shadow()
         loss = self.forward_loss(images, labels)
         loss.backward()
         if self.reducer is not None:
@@ -172,4 +206,6 @@ class Trainer:
             ops.adamw_(g.data, g.grad, g.exp_avg, g.exp_avg_sq, self.lr, self.betas[0], self.betas[1],
                        self.eps, g.weight_decay, self.step_count, inv_scale=inv)
             g.grad.zero_()
+            if self.amp_dtype == torch.bfloat16:
+                g.refresh_shadow()  # keeps evaluation between steps on the updated weights
         return loss.detach()

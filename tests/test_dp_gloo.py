@@ -23,9 +23,25 @@ def _free_port():
     return p
 
 
+class _Shared(nn.Module):
+    """A layer used twice per step, like MS-UNet's shared concat_back_dim[2/3]."""
+
+    def __init__(self):
+        super().__init__()
+        self.inp = nn.Linear(16, 32)
+        self.shared = nn.Linear(32, 32)
+        self.norm = nn.LayerNorm(32)
+        self.out = nn.Linear(32, 8)
+
+    def forward(self, x):
+        h = self.shared(torch.relu(self.inp(x)))
+        h = self.shared(torch.relu(self.norm(h)))
+        return self.out(h)
+
+
 def _model():
     torch.manual_seed(0)
-    return nn.Sequential(nn.Linear(16, 32), nn.LayerNorm(32), nn.GELU(), nn.Linear(32, 8))
+    return _Shared()
 
 
 def _data(rank, n=6):
@@ -42,7 +58,7 @@ def _worker(rank, world, port, bucket_bytes, out):
     nodecay = [(n, p) for n, p in named if is_no_decay(n, p)][::-1]
     groups = [FlatGroup(decay, 0.01, "cpu"), FlatGroup(nodecay, 0.0, "cpu")]
     red = GradBucketer(groups, bucket_bytes)
-    for step in range(2):
+    for step in range(3):  # step 0 learns the accumulation counts, later steps overlap
         x, y = _data(rank + 10 * step)
         loss = ((m(x) - y) ** 2).mean() / world  # each rank's share of the global mean
         loss.backward()
@@ -60,7 +76,7 @@ def test_bucketed_allreduce_equals_global_batch(bucket_bytes):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), bucket_bytes, out), nprocs=world, join=True)
-    for step in range(2):
+    for step in range(3):
         m = _model()
         named = list(m.named_parameters())
         xs, ys = zip(*[_data(r + 10 * step) for r in range(world)])

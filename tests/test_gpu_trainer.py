@@ -1,0 +1,90 @@
+"""GPU: the trainer's fast paths change nothing numerically.
+
+trainer.FlatGroup re-homes parameters into flat buffers, marks them for direct gradient
+accumulation (the backward kernels add into the preallocated .grad views instead of
+returning a gradient for AccumulateGrad) and keeps a per-step bf16 shadow that the Linear
+ops read instead of casting.  A bf16 forward+backward through the Trainer must give the
+same parameter gradients as the plain autograd path on an identical model, and one
+Trainer.step must equal torch.optim.AdamW (the reference's optimizer, trainer.py:130-152)
+applied to those gradients."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import cases  # noqa: E402
+from oracle.msunet import make_cfg  # noqa: E402
+
+DEV = "cuda"
+
+
+def _setup():
+    from semantic_segmentation_of_stylegan2_artifacts_amd import load_config
+    from semantic_segmentation_of_stylegan2_artifacts_amd.network.model_parts import MSUNetSys
+    spec = cases.model_cases()["swinT224"]
+    cfg = make_cfg(**spec["cfg"])
+    model = MSUNetSys(img_size=cfg["img_size"], patch_size=cfg["patch_size"], in_chans=cfg["in_chans"],
+                      num_classes=cfg["num_classes"], embed_dim=cfg["embed_dim"], depths=cfg["depths"],
+                      num_heads=cfg["num_heads"], window_size=cfg["window_size"], mlp_ratio=cfg["mlp_ratio"],
+                      drop_rate=0.0, attn_drop_rate=0.0, drop_path_rate=0.0)
+    model.load_state_dict(cases.model_params(cfg, spec["seed"]), strict=True)
+    x, target = cases.model_inputs(cfg, 2, spec["seed"])
+    conf = load_config(None, "swin_t", **{"TRAIN.BASE_LR": 1e-3})
+    return model.to(DEV).train(), x.to(DEV), target.to(DEV), conf
+
+
+def test_direct_grads_and_shadow_match_autograd():
+    from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import Trainer
+    model, x, target, conf = _setup()
+    ref = copy.deepcopy(model)
+    tr = Trainer(model, conf, DEV)
+    for g in tr.groups:
+        g.refresh_shadow()
+    loss = tr.forward_loss(x, target)
+    loss.backward()
+    loss_ref = tr.loss_fn
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        lr = loss_ref(ref(x), target)
+    lr.backward()
+    assert torch.equal(loss.detach(), lr.detach())
+    rp = dict(ref.named_parameters())
+    n_checked = 0
+    for g in tr.groups:
+        for name, p in zip(g.names, g.params):
+            gr = rp[name].grad
+            assert gr is not None, name
+            torch.testing.assert_close(p.grad, gr, rtol=1e-6, atol=1e-7, msg=name)
+            n_checked += 1
+    assert n_checked == sum(len(g.params) for g in tr.groups)
+
+
+def test_trainer_step_equals_torch_adamw():
+    from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import Trainer, is_no_decay
+    model, x, target, conf = _setup()
+    ref = copy.deepcopy(model)
+    tr = Trainer(model, conf, DEV)
+    tr.step(x, target)
+    # reference: same gradients through plain autograd, then torch AdamW with the two groups
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = tr.loss_fn(ref(x), target)
+    loss.backward()
+    live = {n for g in tr.groups for n in g.names}
+    decay = [p for n, p in ref.named_parameters() if n in live and not is_no_decay(n, p)]
+    nodecay = [p for n, p in ref.named_parameters() if n in live and is_no_decay(n, p)]
+    opt = torch.optim.AdamW([{"params": decay, "weight_decay": conf.TRAIN.WEIGHT_DECAY},
+                             {"params": nodecay, "weight_decay": 0.0}], lr=tr.lr,
+                            betas=tuple(conf.TRAIN.OPTIMIZER.BETAS), eps=conf.TRAIN.OPTIMIZER.EPS)
+    opt.step()
+    rp = dict(ref.named_parameters())
+    for g in tr.groups:
+        for name, p in zip(g.names, g.params):
+            torch.testing.assert_close(p.detach(), rp[name].detach(), rtol=1e-5, atol=1e-6, msg=name)
+    # the shadow follows the update; a write through the parameter invalidates it
+    p0 = tr.groups[0].params[0]
+    assert torch.equal(p0._msu_shadow, p0.detach().to(torch.bfloat16))
+    with torch.no_grad():
+        p0.mul_(2.0)
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    assert ops._shadow(p0, torch.bfloat16) is not p0._msu_shadow
