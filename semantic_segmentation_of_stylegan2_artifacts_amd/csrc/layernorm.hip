@@ -214,29 +214,30 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
       }
     }
   }
-  // block reduction of the per-lane parameter-gradient partials: groups share columns
-  __shared__ float red[2][2048 / 4][4];
-  // reduce in two passes over groups to bound LDS: accumulate group-by-group
-  for (int gsel = 0; gsel < GPB; ++gsel) {
-    if (grp == gsel) {
+  // block reduction of the per-lane parameter-gradient partials: every group writes its
+  // row of [GPB][C], one barrier, then each column is summed over the groups in fixed order
+  __shared__ float red[2][1024 * KMAX];  // GPB * C <= (256 / TPR) * TPR * KMAX * 4
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        const int ch = lane + k * TPR;
-        if (ch < nchunk) {
+  for (int k = 0; k < KMAX; ++k) {
+    const int ch = lane + k * TPR;
+    if (ch < nchunk) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (gsel == 0) { red[0][ch][e] = accg[k][e]; red[1][ch][e] = accb[k][e]; }
-            else { red[0][ch][e] += accg[k][e]; red[1][ch][e] += accb[k][e]; }
-          }
-        }
+      for (int e = 0; e < 4; ++e) {
+        red[0][grp * a.C + ch * 4 + e] = accg[k][e];
+        red[1][grp * a.C + ch * 4 + e] = accb[k][e];
       }
     }
-    __syncthreads();
   }
+  __syncthreads();
   float* P = a.part + (long)blockIdx.x * 2 * a.C;
   for (int i = threadIdx.x; i < a.C; i += 256) {
-    P[i] = red[0][i >> 2][i & 3];
-    P[a.C + i] = red[1][i >> 2][i & 3];
+    float sg = 0.f, sb = 0.f;
+    for (int g = 0; g < GPB; ++g) {
+      sg += red[0][g * a.C + i];
+      sb += red[1][g * a.C + i];
+    }
+    P[i] = sg;
+    P[a.C + i] = sb;
   }
 }
 
@@ -620,7 +621,7 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
 
 int msu_ln_part_blocks(long rows, int C) {
   (void)C;
-  long nb = (rows + 31) / 32;
+  long nb = (rows + 127) / 128;  // >= 128 rows per block: the per-block reduction amortises
   if (nb > 1024) nb = 1024;
   return nb < 1 ? 1 : (int)nb;
 }
