@@ -110,6 +110,21 @@ long msu_wgrad_workspace(long M, int N, int K);
 int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float* db, float* workspace,
                      long M, int N, int K, int accumulate, void* stream);
 
+/* ---------------------------------------------------------------- Linear forward / input gradient
+ * Token GEMM (bf16 in/out, f32 accumulate) for the same Linears as msu_linear_wgrad:
+ * Y[M][N] = epi(A[M][K] . W[N][K]^T + bias[N]); input gradients pass W^T ([K][N]).
+ *   epi 0  plain, optional bias; A2 != null: A's columns [K1, K) come from A2 ([M][K-K1]) --
+ *          the skip-fusion torch.cat([x, skip], -1) -> concat_back_dim (model_parts.py:792-794,
+ *          :804-806, :823-824) without the concatenated copy (needs bias);
+ *   epi 1  torchvision MLP mlp.0 + mlp.1 (Linear -> GELU): Y = H = A.W^T + b, Y2 = GELU(H);
+ *   epi 2  input gradient of mlp.3 through mlp.1: Y = (A.W^T) * GELU'(H) (no bias).
+ * msu_tok_gemm_supported() says whether a shape is covered (N % 32 == 0, K % 48 or 128 == 0
+ * and an LDS plan exists); uncovered shapes are the caller's to route to a library GEMM. */
+int msu_tok_gemm_supported(long M, int N, int K);
+int msu_tok_gemm(const void* A, const void* A2, int K1, const void* W, const float* bias, void* Y,
+                 void* Y2, const void* H, long M, int N, int K, int epi, void* stream);
+int msu_tok_gemm_plan(long M, int N, int K, long* out6);
+
 /* ---------------------------------------------------------------- streaming ops
  * nn.GELU() (exact erf): torchvision MLP activation, FinalPatchExpand_X4_V2.act. */
 int msu_gelu_fwd(int dtype, const void* x, void* y, long n, void* stream);

@@ -1,0 +1,8 @@
+// Token GEMM instantiations for a 128-deep K stage (see gemm_tok.h).
+#include "gemm_tok.h"
+
+namespace msu_tok {
+int dispatch_k128(const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st) {
+  return dispatch_nc<128, true>(p, a, epi, bias, concat, st);
+}
+}  // namespace msu_tok

@@ -140,12 +140,17 @@ class SwinTransformerBlock(nn.Module):
         sc1 = _drop_path_scale(self.stochastic_depth_prob, self.training, B, x.device)
         x1, xn2 = ops.add_layer_norm(x, a, sc1, self.norm2.weight, self.norm2.bias, self.norm2.eps)
         fc1, fc2 = self.mlp[0], self.mlp[3]
-        h = ops.gelu(ops.linear(xn2, fc1.weight, fc1.bias))
-        if self.dropout > 0 and self.training:
-            h = F.dropout(h, self.dropout, True)
-        m = ops.linear(h, fc2.weight, fc2.bias)
-        if self.dropout > 0 and self.training:
-            m = F.dropout(m, self.dropout, True)
+        drop = self.dropout > 0 and self.training
+        if not drop and fc1.bias is not None and fc2.bias is not None and \
+                ops.mlp_fusable(xn2, fc1.weight, fc2.weight):
+            m = ops.mlp(xn2, fc1.weight, fc1.bias, fc2.weight, fc2.bias)
+        else:
+            h = ops.gelu(ops.linear(xn2, fc1.weight, fc1.bias))
+            if drop:
+                h = F.dropout(h, self.dropout, True)
+            m = ops.linear(h, fc2.weight, fc2.bias)
+            if drop:
+                m = F.dropout(m, self.dropout, True)
         sc2 = _drop_path_scale(self.stochastic_depth_prob, self.training, B, x.device)
         return (x1, m, sc2)
 

@@ -306,9 +306,66 @@ def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0)
                                   int(shift), float(p_drop), int(seed) & ((1 << 63) - 1))
 
 
+# ----------------------------------------------------------------------------- token GEMM
+TOK_PLAIN, TOK_GELU_DUAL, TOK_GELU_GRAD = 0, 1, 2
+_tok_cache = {}
+
+
+def tok_supported(M, N, K):
+    """Whether the HIP token GEMM (csrc/gemm_tok.h) covers this bf16 Linear shape."""
+    key = (int(M), int(N), int(K))
+    r = _tok_cache.get(key)
+    if r is None:
+        r = _tok_cache[key] = bool(_lib.lib().msu_tok_gemm_supported(*key))
+    return r
+
+
+def tok_preferred(M, N, K):
+    """Token GEMM where it beats hipBLASLt (measured, tools/kbench.py tok): the HBM-bound
+    stage-0 shapes (M >= 256k tokens) and small weights (N*K <= 576*192); wider weights at
+    smaller M are MFMA-heavier and stay on the library GEMM."""
+    return tok_supported(M, N, K) and (M >= 262144 or N * K <= 576 * 192)
+
+
+def tok_gemm(a, w, bias=None, epi=TOK_PLAIN, h=None, a2=None):
+    """bf16 Y = epi(A . W^T + bias) on the token GEMM kernel.  a: [..., K1] (+ a2: [..., K-K1]),
+    w: [N, K] bf16, bias: [N] f32.  Returns Y (and GELU(Y) for TOK_GELU_DUAL)."""
+    N, K = w.shape
+    K1 = a.shape[-1]
+    M = a.numel() // K1
+    a = a.contiguous()
+    y = torch.empty(*a.shape[:-1], N, device=a.device, dtype=torch.bfloat16)
+    y2 = torch.empty_like(y) if epi == TOK_GELU_DUAL else None
+    _lib.call("msu_tok_gemm", _p(a), _p(None if a2 is None else a2.contiguous()), K1 if a2 is not None else 0,
+              _p(w), _p(bias), _p(y), _p(y2), _p(h), M, N, K, epi, _s(a))
+    return (y, y2) if epi == TOK_GELU_DUAL else y
+
+
+def _wt(w):
+    """[N, K] bf16 weight -> contiguous W^T [K, N] for the input-gradient GEMM."""
+    return w.t().contiguous()
+
+
+def _wgrad(dy, x, weight, bias, M, N, K):
+    """Linear weight/bias gradients on msu_linear_wgrad; (None, None) when accumulated
+    straight into the trainer's flat .grad views."""
+    L = _lib.lib()
+    ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
+    if _direct(weight) and (bias is None or _direct(bias)):
+        _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(weight.grad),
+                  _p(None if bias is None else bias.grad), _p(ws), M, N, K, 1, _s(x))
+        _notify(weight, bias)
+        return None, None
+    dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
+    db = torch.empty(N, device=x.device, dtype=torch.float32) if bias is not None else None
+    _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(dw), _p(db), _p(ws), M, N, K, 0, _s(x))
+    return dw, db
+
+
 # ----------------------------------------------------------------------------- Linear
 def linear(x, weight, bias=None):
-    """nn.functional.linear with the HIP weight-gradient kernel (activation dtype per autocast)."""
+    """nn.functional.linear with the HIP weight-gradient kernel (activation dtype per autocast);
+    bf16 forward / input-gradient GEMMs on the token GEMM where it covers the shape."""
     _need_cuda(x)
     dt = act_dtype()
     x = _as(x, dt)
@@ -325,9 +382,14 @@ class _LinearParams(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, dt):
         w = _shadow(weight, dt)
-        b = None if bias is None else _shadow(bias, dt)
-        with torch.autocast("cuda", enabled=False):
-            y = torch.nn.functional.linear(x, w, b)
+        N, K = w.shape
+        M = x.numel() // K
+        if dt == torch.bfloat16 and tok_preferred(M, N, K):
+            y = tok_gemm(x, w, None if bias is None else _f32(bias))
+        else:
+            b = None if bias is None else _shadow(bias, dt)
+            with torch.autocast("cuda", enabled=False):
+                y = torch.nn.functional.linear(x, w, b)
         ctx.save_for_backward(x, w)
         ctx.has_bias = bias is not None
         ctx.params = (weight, bias)
@@ -342,19 +404,57 @@ class _LinearParams(torch.autograd.Function):
         M = dy.numel() // N
         dx = None
         if ctx.needs_input_grad[0]:
-            with torch.autocast("cuda", enabled=False):
-                dx = dy.matmul(w)
-        L = _lib.lib()
-        ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
-        if _direct(weight) and (bias is None or _direct(bias)):
-            _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(weight.grad),
-                      _p(None if bias is None else bias.grad), _p(ws), M, N, K, 1, _s(x))
-            _notify(weight, bias)
-            return dx, None, None, None
-        dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
-        db = torch.empty(N, device=x.device, dtype=torch.float32) if ctx.has_bias else None
-        _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(dw), _p(db), _p(ws), M, N, K, 0, _s(x))
+            if x.dtype == torch.bfloat16 and tok_preferred(M, K, N):
+                dx = tok_gemm(dy, _wt(w))
+            else:
+                with torch.autocast("cuda", enabled=False):
+                    dx = dy.matmul(w)
+        dw, db = _wgrad(dy, x, weight, bias if ctx.has_bias else None, M, N, K)
         return dx, dw, db, None
+
+
+# ----------------------------------------------------------------------------- fused MLP
+def mlp_fusable(x, fc1_weight, fc2_weight):
+    """torchvision MLP (mlp.0 -> GELU -> mlp.3) fusable on the token GEMM in bf16?"""
+    if act_dtype() != torch.bfloat16:
+        return False
+    Hd, C = fc1_weight.shape
+    M = x.numel() // C
+    return (tok_preferred(M, Hd, C) and tok_preferred(M, C, Hd) and fc2_weight.shape == (C, Hd))
+
+
+class _Mlp(torch.autograd.Function):
+    """y = mlp.3(GELU(mlp.0(x))) (torchvision ops.misc.MLP without dropout): mlp.0's epilogue
+    stores H and GELU(H); mlp.3's input gradient applies GELU'(H) in its epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        W1 = _shadow(w1, torch.bfloat16)
+        W2 = _shadow(w2, torch.bfloat16)
+        h, g = tok_gemm(x, W1, _f32(b1), TOK_GELU_DUAL)
+        y = tok_gemm(g, W2, _f32(b2))
+        ctx.save_for_backward(x, h, g, W1, W2)
+        ctx.params = (w1, b1, w2, b2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, h, g, W1, W2 = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.params
+        dy = _as(dy, torch.bfloat16)
+        Hd, C = W1.shape
+        M = x.numel() // C
+        dw2, db2 = _wgrad(dy, g, w2, b2, M, C, Hd)
+        dh = tok_gemm(dy, _wt(W2), None, TOK_GELU_GRAD, h=h)
+        dw1, db1 = _wgrad(dh, x, w1, b1, M, Hd, C)
+        dx = tok_gemm(dh, _wt(W1)) if ctx.needs_input_grad[0] else None
+        return dx, dw1, db1, dw2, db2
+
+
+def mlp(x, fc1_weight, fc1_bias, fc2_weight, fc2_bias):
+    """Fused torchvision MLP forward/backward (bf16; see ``mlp_fusable``)."""
+    _need_cuda(x)
+    return _Mlp.apply(_as(x, torch.bfloat16), fc1_weight, fc1_bias, fc2_weight, fc2_bias)
 
 
 def _shadow(param, dt):

@@ -1,0 +1,151 @@
+"""GPU: the token GEMM (csrc/gemm_tok.h) and the fused MLP against plain fp32 PyTorch.
+
+Reference: fp32 matmul of the same bf16-rounded operands, then the epilogue in fp32.
+Tolerance: the kernel rounds its f32 accumulator to bf16 once (<= 2^-8 relative) and sums in a
+different order, so |y - ref| <= 1e-2 * |ref| + 4e-3 * max|ref| (bf16 storage, 8 significant
+bits); GELU uses the A&S 7.1.26 erf (|err| <= 1.5e-7, below bf16 rounding).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    return ops
+
+
+def _check(y, ref, what):
+    y = y.float()
+    scale = ref.abs().max().item()
+    err = (y - ref).abs() - 1e-2 * ref.abs()
+    assert err.max().item() <= 4e-3 * scale, f"{what}: excess err {err.max().item():.3e} vs scale {scale:.3e}"
+
+
+def _inputs(M, N, K, seed):
+    g = torch.Generator().manual_seed(seed)
+    a = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV)
+    return a, w, b
+
+
+# (M, N, K): Swin-T stage shapes at small M plus ragged M, multi-chunk N and multi-stage K
+SHAPES = [(1000, 288, 96), (4096, 384, 96), (4096, 96, 384), (2048, 192, 768), (777, 96, 48),
+          (4096, 576, 192), (1024, 1152, 384), (300, 128, 128), (512, 512, 128), (33, 96, 96),
+          (2048, 1536, 96), (64, 768, 3072)]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("bias", [False, True])
+def test_tok_gemm_plain(M, N, K, bias):
+    ops = _ops()
+    if not ops.tok_supported(M, N, K):
+        pytest.skip("shape not covered by the token GEMM plan")
+    a, w, b = _inputs(M, N, K, M + N + K)
+    y = ops.tok_gemm(a, w, b if bias else None)
+    ref = a.float() @ w.float().t() + (b if bias else 0)
+    _check(y, ref, f"plain {M}x{N}x{K}")
+
+
+def test_tok_gemm_plan_covers_stage0():
+    """Every stage-0 (the HBM-bound bulk) Swin-T 1024^2 bs8 Linear, forward and input
+    gradient, has a plan; wider-K shapes of deeper stages may go to the library GEMM."""
+    ops = _ops()
+    T, C = 8 * 256 ** 2, 96
+    need = [(T, 3 * C, C), (T, C, C), (T, 4 * C, C), (T, C, 4 * C), (T, C, 3 * C),
+            (T // 4, 2 * C, 4 * C), (T // 4, 4 * C, 2 * C), (T, C, 2 * C), (T, 2 * C, C),
+            (T, 96, 48), (T, 1536, 96)]
+    missing = [s for s in need if not ops.tok_supported(*s)]
+    assert not missing, missing
+
+
+@pytest.mark.parametrize("M,C,K1", [(1000, 96, 96), (2048, 192, 192), (333, 128, 128)])
+def test_tok_gemm_concat(M, C, K1):
+    """torch.cat([x, skip], -1) -> Linear(2C, C) without the cat (model_parts.py:792-794)."""
+    ops = _ops()
+    if not ops.tok_supported(M, C, 2 * K1):
+        pytest.skip("shape not covered by the token GEMM plan")
+    a, w, b = _inputs(M, C, 2 * K1, 7)
+    x, skip = a[:, :K1].contiguous(), a[:, K1:].contiguous()
+    y = ops.tok_gemm(x, w, b, a2=skip)
+    ref = a.float() @ w.float().t() + b
+    _check(y, ref, "concat")
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 384, 96), (4096, 768, 192), (555, 1536, 384)])
+def test_tok_gemm_gelu_dual_and_grad(M, N, K):
+    ops = _ops()
+    if not ops.tok_supported(M, N, K):
+        pytest.skip("shape not covered by the token GEMM plan")
+    a, w, b = _inputs(M, N, K, 11)
+    h, g = ops.tok_gemm(a, w, b, ops.TOK_GELU_DUAL)
+    ref_h = a.float() @ w.float().t() + b
+    _check(h, ref_h, "H")
+    _check(g, F.gelu(h.float()), "GELU(H)")
+    # epi 2: (dY . W2) * GELU'(H) with dY [M, K'] and W2^T [N, K']
+    g2 = torch.Generator().manual_seed(5)
+    dy = torch.randn(M, K, generator=g2).to(DEV, torch.bfloat16)
+    w2t = (torch.randn(N, K, generator=g2) / K ** 0.5).to(DEV, torch.bfloat16)
+    dh = ops.tok_gemm(dy, w2t, None, ops.TOK_GELU_GRAD, h=h)
+    hf = h.float().requires_grad_(True)
+    F.gelu(hf).backward(torch.ones_like(hf))
+    ref = (dy.float() @ w2t.float().t()) * hf.grad
+    _check(dh, ref, "dH")
+
+
+@pytest.mark.parametrize("M,C", [(4096, 96), (1000, 96), (512, 128)])
+def test_fused_mlp_matches_fp32(M, C):
+    """ops.mlp (mlp.0 -> GELU -> mlp.3) forward and all gradients vs fp32 autograd."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(M + C)
+    x = torch.randn(M, C, generator=g)
+    w1 = torch.randn(4 * C, C, generator=g) / C ** 0.5
+    b1 = 0.1 * torch.randn(4 * C, generator=g)
+    w2 = torch.randn(C, 4 * C, generator=g) / (4 * C) ** 0.5
+    b2 = 0.1 * torch.randn(C, generator=g)
+    dy = torch.randn(M, C, generator=g)
+    # fp32 reference on the bf16-rounded input
+    xr = x.bfloat16().float().requires_grad_(True)
+    pr = [t.clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
+    yr = F.linear(F.gelu(F.linear(xr, pr[0], pr[1])), pr[2], pr[3])
+    yr.backward(dy.bfloat16().float())
+    xg = x.to(DEV, torch.bfloat16).requires_grad_(True)
+    pg = [t.to(DEV).requires_grad_(True) for t in (w1, b1, w2, b2)]
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        assert ops.mlp_fusable(xg, pg[0], pg[2])
+        y = ops.mlp(xg, *pg)
+    y.backward(dy.to(DEV, torch.bfloat16))
+    _check(y, yr.to(DEV), "y")
+    # gradients: bf16 intermediates (H, G, dH) -> 3e-2 of the largest entry
+    for name, a, r in [("dx", xg.grad, xr.grad), ("dw1", pg[0].grad, pr[0].grad), ("db1", pg[1].grad, pr[1].grad),
+                       ("dw2", pg[2].grad, pr[2].grad), ("db2", pg[3].grad, pr[3].grad)]:
+        err = (a.float().cpu() - r).abs().max().item()
+        assert err <= 3e-2 * r.abs().max().item(), f"{name}: {err:.3e} vs {r.abs().max().item():.3e}"
+
+
+def test_linear_uses_tok_gemm_and_matches():
+    """ops.linear in bf16 routes through the token GEMM for covered shapes (fwd + dgrad)."""
+    ops = _ops()
+    M, N, K = 2048, 288, 96
+    assert ops.tok_supported(M, N, K) and ops.tok_supported(M, K, N)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    dy = torch.randn(M, N, generator=g)
+    xr = x.bfloat16().float().requires_grad_(True)
+    yr = F.linear(xr, w.bfloat16().float(), b)
+    yr.backward(dy.bfloat16().float())
+    xg = x.to(DEV, torch.bfloat16).requires_grad_(True)
+    wg = w.to(DEV).requires_grad_(True)
+    bg = b.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.linear(xg, wg, bg)
+    y.backward(dy.to(DEV, torch.bfloat16))
+    _check(y, yr.to(DEV), "y")
+    _check(xg.grad, xr.grad.to(DEV), "dx")

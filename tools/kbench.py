@@ -112,8 +112,37 @@ def ln():
               f"bwd {msb*1e3:.1f} us ({3*rows*C*2/msb/1e6:.0f} GB/s)")
 
 
+def tok():
+    """Token GEMM vs hipBLASLt (F.linear) at the Swin-T 1024^2 bs8 shapes."""
+    shapes = [(B * 65536, 288, 96), (B * 65536, 96, 96), (B * 65536, 384, 96), (B * 65536, 96, 384),
+              (B * 65536, 96, 192), (B * 65536, 1536, 96), (B * 65536, 96, 48), (B * 16384, 192, 384),
+              (B * 16384, 576, 192), (B * 16384, 192, 192), (B * 16384, 768, 192), (B * 16384, 192, 576),
+              (B * 4096, 1152, 384), (B * 4096, 384, 384), (B * 4096, 1536, 384), (B * 4096, 384, 1152),
+              (B * 1024, 2304, 768)]
+    for M, N, K in shapes:
+        a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+        w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+        bias = torch.randn(N, device=DEV)
+        bb = bias.bfloat16()
+        byts = M * (N + K) * 2
+        fl = 2.0 * M * N * K
+        mt = timeit(lambda: torch.nn.functional.linear(a, w, bb))
+        line = f"tok M={M:7d} N={N:5d} K={K:5d}: hipBLASLt {mt*1e3:7.1f} us ({byts/mt/1e6:5.0f} GB/s)"
+        if ops.tok_supported(M, N, K):
+            ms = timeit(lambda: ops.tok_gemm(a, w, bias))
+            line += f"  tok {ms*1e3:7.1f} us ({byts/ms/1e6:5.0f} GB/s, {fl/ms/1e9:6.1f} TF/s)"
+            if K * 4 == N:
+                md = timeit(lambda: ops.tok_gemm(a, w, bias, ops.TOK_GELU_DUAL))
+                h = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+                dy = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+                wt = w.contiguous()
+                mg = timeit(lambda: ops.tok_gemm(dy, wt, None, ops.TOK_GELU_GRAD, h=h))
+                line += f" dual {md*1e3:6.1f} us ({(byts + M*N*2)/md/1e6:5.0f} GB/s) ggrad {mg*1e3:6.1f} us ({(byts + M*N*2)/mg/1e6:5.0f} GB/s)"
+        print(line, flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
-    for name, fn in (("attn", attn), ("wgrad", wgrad), ("conv", conv), ("ln", ln)):
+    for name, fn in (("attn", attn), ("wgrad", wgrad), ("conv", conv), ("ln", ln), ("tok", tok)):
         if what in (name, "all"):
             fn()
