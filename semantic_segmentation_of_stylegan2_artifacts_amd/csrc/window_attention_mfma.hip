@@ -82,10 +82,11 @@ MSU_DEV int region(int p, int P, int s) { return s == 0 ? 0 : (p < P - WS ? 0 : 
 
 // Token table of the window: sTok = source token, TOK_PAD (padded) or TOK_ZERO (t >= 49);
 // sReg = mask region.  Returns whether the mask is non-trivial for this window.
-MSU_DEV bool window_tokens(const Geom& g, long win, int* sTok, int* sReg, int lane) {
+MSU_DEV bool window_tokens(const Geom& g, long win_l, int* sTok, int* sReg, int lane) {
+  const int win = (int)win_l;  // < 2^31 windows (checked on the host)
   const int nw = g.nWy * g.nWx;
-  const int b = (int)(win / nw);
-  const int wr = (int)(win - (long)b * nw);
+  const int b = win / nw;
+  const int wr = win - b * nw;
   const int wy = wr / g.nWx, wx = wr - (wr / g.nWx) * g.nWx;
   int tok = TOK_ZERO, reg = 0;
   if (lane < NT) {
@@ -149,16 +150,20 @@ MSU_DEV void lds_sync() {
 
 // S^T tiles (jt, it): bias image init + K Q^T from fragments ka[jt][ks], qb[it][ks];
 // mask; softmax over j with exp(scale * (s - max)) -> P^T
+// bimg: the head's bias image, lane-major ([tile][lane][16], global) or, LANE_INNER,
+// [tile][q][lane][4] (an LDS copy: consecutive lanes read consecutive 16 B, conflict-free)
+template <bool LANE_INNER = false>
 MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (&qb)[2][2],
                      const float* bimg, const int* sReg, bool boundary, float scale, int lane) {
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
-      const float4* bp = reinterpret_cast<const float4*>(bimg + ((jt * 2 + it) * 64 + lane) * 16);
+      const float4* bp = LANE_INNER ? reinterpret_cast<const float4*>(bimg) + (jt * 2 + it) * 256 + lane
+                                    : reinterpret_cast<const float4*>(bimg + ((jt * 2 + it) * 64 + lane) * 16);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 v = bp[q];
+        const float4 v = bp[LANE_INNER ? 64 * q : q];
         P[jt][it][4 * q] = v.x; P[jt][it][4 * q + 1] = v.y; P[jt][it][4 * q + 2] = v.z; P[jt][it][4 * q + 3] = v.w;
       }
     }
@@ -211,51 +216,91 @@ MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (
 struct Aux {
   const float* bimg;      // [nh][4096] bias image / scale
   const bf16_t* biasrow;  // [3C] bf16 qkv bias (padded tokens' q|k|v)
-  const bf16_t* zrow;     // [64] zeros
+  const bf16_t* zrow;     // [3C] zeros (row of a TOK_ZERO token, any column offset)
 };
 
 struct FwdLds {
   bf16_t v[64 * LD];
-  int tok[64], reg[64];
+  int tok[2][64], reg[2][64];  // double-buffered token tables (current / prefetched item)
 };
 
+// Operands of one (window, head) item, loaded into registers one item ahead.
+struct FwdItem {
+  bf16x8 ka[2][2], qb[2][2];
+  uint4 vr[4];
+  bool boundary;
+};
+
+// Persistent, head-stationary: grid (nblk, nh); a workgroup keeps its head's bias image in
+// LDS (read there instead of from L2 for every item) and its waves walk windows win,
+// win + stride, ...; the HBM loads of window i+1 (token table, K / Q fragments, V rows) are
+// issued before window i is computed, so their latency hides under window i's MFMAs and
+// softmax instead of being paid per item.
 template <int WAVES>
 __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __restrict__ qkv, Aux aux,
                                                                bf16_t* __restrict__ out, Geom g, float scale,
                                                                float p_drop, uint64_t seed) {
+  __shared__ __attribute__((aligned(16))) float4 sBimg[4 * 4 * 64];
   __shared__ __attribute__((aligned(16))) FwdLds lds_all[WAVES];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   FwdLds& L = lds_all[wave];
-  const long nitems = g.nwin * g.nh;
+  const int h = blockIdx.y;
+  {
+    // bias image [tile][lane][16] (global) -> [tile][q][lane] float4 (LDS)
+    const float4* src = reinterpret_cast<const float4*>(aux.bimg + (long)h * 4096);
+    for (int e = threadIdx.x; e < 1024; e += 64 * WAVES) {
+      const int t = e >> 8, q = (e >> 6) & 3, ln = e & 63;
+      sBimg[e] = src[(t * 64 + ln) * 4 + q];
+    }
+  }
+  __syncthreads();
+  const long nitems = g.nwin;  // windows of this head
   const long C3 = 3L * g.C;
-  const long nblk = gridDim.x;
-  const long b0 = xcd_remap(blockIdx.x, gridDim.x);
+  const long stride = (long)gridDim.x * WAVES;
   const int hh = lane >> 5;
-  for (long it0 = b0 * WAVES; it0 < nitems; it0 += nblk * WAVES) {
-    const long item = it0 + wave;
-    if (item >= nitems) break;  // no block-wide barriers: waves are independent
-    const long win = item / g.nh;
-    const int h = (int)(item - win * g.nh);
-    const bool boundary = window_tokens(g, win, L.tok, L.reg, lane);
+  long item = (long)xcd_remap(blockIdx.x, gridDim.x) * WAVES + wave;
+  if (item >= nitems) return;  // no block-wide barriers after this point: waves are independent
+
+  // row base of a window token: its qkv row, the qkv-bias row (padded token) or zeros
+  auto rowbase = [&](int tok) -> const bf16_t* {
+    return tok >= 0 ? qkv + (size_t)((unsigned)tok * (unsigned)C3) : (tok == TOK_PAD ? aux.biasrow : aux.zrow);
+  };
+  auto prep = [&](long it, int buf, FwdItem& f) __attribute__((always_inline)) {
+    const int win = (int)it;
+    f.boundary = window_tokens(g, win, L.tok[buf], L.reg[buf], lane);
     lds_sync();
-    const int cq = h * HD, ck = g.C + h * HD, cv = 2 * g.C + h * HD;
-    bf16x8 ka[2][2], qb[2][2];
+    const int cq = h * HD + 8 * (lane >> 5), ck = g.C + cq;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < 2; ++t) {
+      const bf16_t* rb = rowbase(L.tok[buf][32 * t + (lane & 31)]);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        ka[t][ks] = frag_global(L.tok, 32 * t, qkv + ck, C3, aux.biasrow + ck, aux.zrow, 16 * ks, lane);
-        qb[t][ks] = frag_global(L.tok, 32 * t, qkv + cq, C3, aux.biasrow + cq, aux.zrow, 16 * ks, lane);
+        f.ka[t][ks] = *reinterpret_cast<const bf16x8*>(rb + ck + 16 * ks);
+        f.qb[t][ks] = *reinterpret_cast<const bf16x8*>(rb + cq + 16 * ks);
       }
-    {
-      const bf16_t* const base[1] = {qkv + cv};
-      const long strd[1] = {C3};
-      const bf16_t* const pad[1] = {aux.biasrow + cv};
-      bf16_t* const dst[1] = {L.v};
-      stage_rows<1>(L.tok, base, strd, pad, aux.zrow, dst, lane);
     }
+    const int cv = 2 * g.C + h * HD + 8 * (lane & 3);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      f.vr[c] = *reinterpret_cast<const uint4*>(rowbase(L.tok[buf][(lane >> 2) + 16 * c]) + cv);
+  };
+
+  FwdItem cur;
+  prep(item, 0, cur);
+  int buf = 0;
+  for (;;) {
+    const int win = (int)item;
+    // V rows of this item -> LDS (the previous item's PV reads are complete: lds_sync below)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      *reinterpret_cast<uint4*>(L.v + ((lane >> 2) + 16 * c) * LD + (lane & 3) * 8) = cur.vr[c];
+    }
+    const long nxt = item + stride;
+    FwdItem nx;
+    if (nxt < nitems) prep(nxt, buf ^ 1, nx);
+    lds_sync();
     f32x16 P[2][2];
-    probs_T(P, ka, qb, aux.bimg + (long)h * 4096, L.reg, boundary, scale, lane);
+    probs_T<true>(P, cur.ka, cur.qb, reinterpret_cast<const float*>(sBimg), L.reg[buf], cur.boundary, scale, lane);
     if (p_drop > 0.f) {
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
@@ -265,7 +310,6 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
           for (int r = 0; r < 16; ++r)
             P[jt][it][r] *= drop_keep(seed, win, h, g.nh, it * 32 + (lane & 31), jt * 32 + crow(r, hh), p_drop);
     }
-    lds_sync();
     // O^T[d][i] = sum_j V[j][d] P^T[j][i]
     f32x16 O[2];
     O[0] = f32x16{0}; O[1] = f32x16{0};
@@ -281,9 +325,9 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int i = it * 32 + (lane & 31);
-      const int tok = L.tok[i];
+      const int tok = L.tok[buf][i];
       if (tok >= 0) {
-        bf16_t* dst = out + (long)tok * g.C + h * HD;
+        bf16_t* dst = out + (size_t)((unsigned)tok * (unsigned)g.C) + h * HD;
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
           uint2 w;
@@ -293,7 +337,11 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();
+    lds_sync();  // PV reads and token-table reads of this item done before they are overwritten
+    if (nxt >= nitems) break;
+    item = nxt;
+    buf ^= 1;
+    cur = nx;
   }
 }
 
@@ -465,7 +513,7 @@ __global__ void __launch_bounds__(256) aux_kernel(const float* table, const floa
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < C3; c += 256) biasrow[c] = from_f32<bf16_t>(qkv_bias[c]);
-    if (threadIdx.x < 64) zrow[threadIdx.x] = 0;
+    for (int c = threadIdx.x; c < C3; c += 256) zrow[c] = 0;
   }
   if (e >= nh * 4096) return;
   const int h = e / 4096, rem = e % 4096;
@@ -517,7 +565,7 @@ Geom make_geom(int B, int H, int W, int C, int nh, int shift) {
 constexpr int FWD_WAVES = 4, BWD_WAVES = 2;
 
 // aux workspace (f32 units): bias image nh*4096, bf16 bias row (3C bf16), zero row (64 bf16)
-long aux_floats(int C, int nh) { return (long)nh * 4096 + (3L * C + 64 + 1) / 2 + 4; }
+long aux_floats(int C, int nh) { return (long)nh * 4096 + (6L * C + 1) / 2 + 4; }
 
 Aux carve_aux(float* ws, int C, int nh, float** img_out, bf16_t** brow, bf16_t** zrow) {
   Aux a;
@@ -559,9 +607,11 @@ int msu_attn_mfma_fwd(const void* qkv, const float* qkv_bias, const float* table
   const Aux aux = carve_aux(ws, C, nh, &img, &brow, &zrow);
   hipLaunchKernelGGL(aux_kernel, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
                      1.0f / scale, img, brow, zrow);
-  long nb = (items + FWD_WAVES - 1) / FWD_WAVES;
-  if (nb > 65536) nb = 65536;
-  hipLaunchKernelGGL(attn_fwd_mfma<FWD_WAVES>, dim3((unsigned)nb), dim3(64 * FWD_WAVES), 0, st,
+  // persistent: about two 4-wave workgroups per CU, split over the heads
+  long nb = (g.nwin + FWD_WAVES - 1) / FWD_WAVES;
+  const long cap = 512 / nh > 0 ? 512 / nh : 1;
+  if (nb > cap) nb = cap;
+  hipLaunchKernelGGL(attn_fwd_mfma<FWD_WAVES>, dim3((unsigned)nb, (unsigned)nh), dim3(64 * FWD_WAVES), 0, st,
                      (const bf16_t*)qkv, aux, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed);
   return MSU_CHECK_LAUNCH();
 }
