@@ -112,6 +112,45 @@ def cpu_baseline(seconds_budget=25.0):
                       f"{len(steady)} steady steps of {len(times)}, {sps:.2f} s/step"}
 
 
+def dice_vs_reference(device):
+    """'Dice vs ref' of the metric: identical Swin-T weights and a 4 x 256^2 synthetic batch
+    (BASELINE config 1) through the CPU oracle (the reference path restated, fp32) and
+    through the HIP path (fp32 parity mode and bf16 training mode); soft Dice of both over
+    the fake images (validation_functions.py:300-301), the GPU side by the msu_seg_metrics
+    kernel.  Part of the cpu_baseline leg (the only bench leg that runs the oracle)."""
+    from oracle.msunet import make_cfg, init_params, msunet_forward
+    from oracle import metrics as om
+    from semantic_segmentation_of_stylegan2_artifacts_amd.network.model_parts import MSUNetSys
+    from semantic_segmentation_of_stylegan2_artifacts_amd.data import synthetic_batch
+    from semantic_segmentation_of_stylegan2_artifacts_amd import validation
+    cfg = make_cfg(img_size=256, embed_dim=96, depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24], drop_path_rate=0.0)
+    params = init_params(cfg, seed=0)
+    x, y = synthetic_batch(4, 256, "cpu", 120)
+    with torch.no_grad():
+        ref = msunet_forward(params, cfg, x)
+    ref_per = [om.image_metrics(ref[b], y[b]) for b in range(4)]
+    fake = [b for b in range(4) if y[b].sum() > 0]
+    ref_dice = sum(ref_per[b]["soft_dice"] for b in fake) / len(fake)
+    model = MSUNetSys(img_size=256, embed_dim=96, depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24],
+                      drop_path_rate=0.0)
+    model.load_state_dict(params, strict=True)
+    model = model.to(device).eval()
+    out = {"sample": "Swin-T 4x256^2 synthetic, oracle fp32 CPU vs HIP", "soft_dice_ref": round(ref_dice, 6)}
+    with torch.no_grad():
+        for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+            with torch.autocast("cuda", dtype=dt, enabled=dt != torch.float32):
+                logits = model(x.to(device))
+            per = validation.batch_metrics(logits, y.to(device))
+            d = sum(per[b]["soft_dice"] for b in fake) / len(fake)
+            out[f"soft_dice_hip_{name}"] = round(d, 6)
+            out[f"abs_diff_{name}"] = float(f"{abs(d - ref_dice):.3g}")
+            if dt == torch.float32:
+                err = (logits.float().cpu() - ref).abs().max().item() / ref.abs().max().item()
+                out["logits_max_rel_err_fp32"] = float(f"{err:.3g}")
+    out["within_1e-3"] = out["abs_diff_fp32"] <= 1e-3
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -181,6 +220,7 @@ def main():
             res["roofline"] = conv_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline()
+            res["dice_vs_ref"] = dice_vs_reference(device)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -147,6 +147,16 @@ int msu_dynloss_bwd(int dtype, const void* logits, const float* target, const fl
                     const float* loss, const float* gout, int B, long N, float alpha, float beta,
                     float mix, float* dlogits, void* stream);
 
+/* Validation metrics (scripts/validation_functions.py:37-309): per image, p = sigmoid(logit),
+ * pred_bin = p > threshold (:106-107), gt = label > 0 (:108).  out [B][12] f64 = sum(p g),
+ * sum(p^2), sum(g), sum(p), soft fp / fn / tn (:219-222, :291-294), binary tp / fp / fn / tn
+ * (:219-222, :267-270), 0 -- the host forms soft / binary Dice, IoU, recall, precision,
+ * accuracy, FPR and Score (calculate_metrics_fake :247-309, calculate_metrics_real :214-244,
+ * :180).  part [B * nblk * 12] f32 scratch, nblk from msu_metrics_nblk. */
+int msu_metrics_nblk(long N);
+int msu_seg_metrics(int dtype, const void* logits, const float* label, int B, long N, float threshold,
+                    float* part, int nblk, double* out, void* stream);
+
 /* AdamW step (trainer.py:143-152; torch.optim.AdamW, amsgrad=False) over a flat f32
  * parameter range; optional grad unscale (inv_scale) and skip-on-found_inf (GradScaler). */
 int msu_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,

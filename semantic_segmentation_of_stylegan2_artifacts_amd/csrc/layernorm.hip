@@ -621,7 +621,9 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
 
 int msu_ln_part_blocks(long rows, int C) {
   (void)C;
-  long nb = (rows + 127) / 128;  // >= 128 rows per block: the per-block reduction amortises
+  // >= 16 rows per block (the per-block parameter-gradient reduction amortises) and enough
+  // blocks to fill the CUs at the deep stages (8192 rows x 768: 512 blocks, not 64)
+  long nb = (rows + 15) / 16;
   if (nb > 1024) nb = 1024;
   return nb < 1 ? 1 : (int)nb;
 }
