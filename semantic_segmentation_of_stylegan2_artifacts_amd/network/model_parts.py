@@ -366,8 +366,7 @@ class BasicLayer_up(nn.Module):
 def _skip_fuse(lin, x, skip):
     """``torch.cat([x, skip], -1)`` -> ``concat_back_dim[k]`` (model_parts.py:792-793 etc.)."""
     B = x.shape[0]
-    x = torch.cat([x.reshape(B, -1, x.shape[-1]), skip.reshape(B, -1, skip.shape[-1]).to(x.dtype)], -1)
-    return ops.linear(x, lin.weight, lin.bias)
+    return ops.linear_cat(x.reshape(B, -1, x.shape[-1]), skip.reshape(B, -1, skip.shape[-1]), lin.weight, lin.bias)
 
 
 # ============================================================================ MSUNetSys

@@ -413,6 +413,71 @@ class _LinearParams(torch.autograd.Function):
         return dx, dw, db, None
 
 
+# ----------------------------------------------------------------------------- skip fusion
+class _LinearCat(torch.autograd.Function):
+    """Linear(cat([x, skip], -1)) with the concatenation folded into the token GEMM's A
+    loads (forward) and split back out of the input gradient (two GEMMs over W's halves)."""
+
+    @staticmethod
+    def forward(ctx, x, skip, weight, bias):
+        W = _shadow(weight, torch.bfloat16)
+        y = tok_gemm(x, W, _f32(bias), a2=skip)
+        ctx.save_for_backward(x, skip, W)
+        ctx.params = (weight, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, skip, W = ctx.saved_tensors
+        weight, bias = ctx.params
+        dy = _as(dy, torch.bfloat16)
+        N = W.shape[0]
+        C1, C2 = x.shape[-1], skip.shape[-1]
+        M = dy.numel() // N
+        outs = []
+        for part, (lo, hi) in ((x, (0, C1)), (skip, (C1, C1 + C2))):
+            wt = W[:, lo:hi].t().contiguous()
+            if tok_preferred(M, hi - lo, N):
+                outs.append(tok_gemm(dy, wt))
+            else:
+                with torch.autocast("cuda", enabled=False):
+                    outs.append(dy.matmul(wt.t()))
+        # weight gradient per half into temporaries ([N, C1], [N, C2]), bias with the first
+        dw1, db = _wgrad_tmp(dy, x, N, C1, M, with_bias=True)
+        dw2, _ = _wgrad_tmp(dy, skip, N, C2, M, with_bias=False)
+        if _direct(weight, bias):
+            weight.grad[:, :C1] += dw1
+            weight.grad[:, C1:] += dw2
+            bias.grad += db
+            _notify(weight, bias)
+            return outs[0], outs[1], None, None
+        return outs[0], outs[1], torch.cat([dw1, dw2], 1), db
+
+
+def _wgrad_tmp(dy, x, N, K, M, with_bias):
+    L = _lib.lib()
+    ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
+    dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
+    db = torch.empty(N, device=x.device, dtype=torch.float32) if with_bias else None
+    _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(dw), _p(db), _p(ws), M, N, K, 0, _s(x))
+    return dw, db
+
+
+def linear_cat(x, skip, weight, bias):
+    """``F.linear(torch.cat([x, skip], -1), weight, bias)`` (skip fusion, model_parts.py:792-794,
+    :804-806, :823-824); x / skip: [..., C1] / [..., C2] with equal leading dims."""
+    _need_cuda(x)
+    dt = act_dtype()
+    x, skip = _as(x, dt), _as(skip, dt)
+    N, K = weight.shape
+    C1, C2 = x.shape[-1], skip.shape[-1]
+    M = x.numel() // C1
+    if (dt == torch.bfloat16 and bias is not None and C1 + C2 == K and C1 % 8 == 0 and
+            tok_preferred(M, N, K)):
+        return _LinearCat.apply(x, skip, weight, bias)
+    return linear(torch.cat([x, skip], -1), weight, bias)
+
+
 # ----------------------------------------------------------------------------- fused MLP
 def mlp_fusable(x, fc1_weight, fc2_weight):
     """torchvision MLP (mlp.0 -> GELU -> mlp.3) fusable on the token GEMM in bf16?"""

@@ -149,3 +149,32 @@ def test_linear_uses_tok_gemm_and_matches():
     y.backward(dy.to(DEV, torch.bfloat16))
     _check(y, yr.to(DEV), "y")
     _check(xg.grad, xr.grad.to(DEV), "dx")
+
+
+@pytest.mark.parametrize("M,C", [(4096, 96), (1000, 192)])
+def test_linear_cat_matches_cat_then_linear(M, C):
+    """ops.linear_cat (skip fusion without the concatenated copy) == Linear(cat([x, skip])):
+    forward and all gradients, bf16 (model_parts.py:792-794)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(M + C)
+    x = torch.randn(M, C, generator=g)
+    sk = torch.randn(M, C, generator=g)
+    w = torch.randn(C, 2 * C, generator=g) / (2 * C) ** 0.5
+    b = torch.randn(C, generator=g)
+    dy = torch.randn(M, C, generator=g)
+    xr, sr = x.bfloat16().float().requires_grad_(True), sk.bfloat16().float().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = F.linear(torch.cat([xr, sr], -1), wr.bfloat16().float(), br)
+    yr.backward(dy.bfloat16().float())
+    xg = x.to(DEV, torch.bfloat16).requires_grad_(True)
+    sg = sk.to(DEV, torch.bfloat16).requires_grad_(True)
+    wg, bg = w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.linear_cat(xg, sg, wg, bg)
+    y.backward(dy.to(DEV, torch.bfloat16))
+    _check(y, yr.to(DEV), "y")
+    _check(xg.grad, xr.grad.to(DEV), "dx")
+    _check(sg.grad, sr.grad.to(DEV), "dskip")
+    for name, a, r in [("dw", wg.grad, wr.grad), ("db", bg.grad, br.grad)]:
+        err = (a.float().cpu() - r).abs().max().item()
+        assert err <= 2e-2 * r.abs().max().item(), f"{name}: {err:.3e}"
