@@ -20,10 +20,17 @@
 // Pd and dS once as [i][j] LDS images (8-byte stores) and runs dV = Pd^T dO,
 // dQ = dS K, dK = dS^T Q with tr-read operands; relative-bias gradients accumulate in
 // registers in the bias-image layout; padded tokens' dq/dk/dv go to the qkv-bias partial.
+#include <utility>
+
 #include "common.h"
 #include "reduce.h"
 
 namespace {
+
+template <typename F, int... Is>
+MSU_DEV void static_for(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
 
 constexpr int WS = 7, NT = 49, HD = 32;
 constexpr int LD = 40;   // staged [64 x 32] rows: 32 + 8 pad (80 B)
@@ -220,16 +227,13 @@ struct Aux {
 };
 
 struct FwdLds {
-  bf16_t v[64 * LD];
+  bf16_t k[64 * LD], q[64 * LD], v[64 * LD];  // q doubles as the output staging image
   int tok[2][64], reg[2][64];  // double-buffered token tables (current / prefetched item)
 };
 
-// Operands of one (window, head) item, loaded into registers one item ahead.
-struct FwdItem {
-  bf16x8 ka[2][2], qb[2][2];
-  uint4 vr[4];
-  bool boundary;
-};
+// Every token's 64-B head slice of q / k / v is fetched by 4 consecutive lanes (16 B each),
+// so a load instruction moves 16 whole 64-B pieces -- not 32 tokens x 32 B as MFMA-layout
+// fragment loads would (L2 request count, not bytes, bounds this kernel).
 
 // Persistent, head-stationary: grid (nblk, nh); a workgroup keeps its head's bias image in
 // LDS (read there instead of from L2 for every item) and its waves walk windows win,
@@ -265,42 +269,51 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
   auto rowbase = [&](int tok) -> const bf16_t* {
     return tok >= 0 ? qkv + (size_t)((unsigned)tok * (unsigned)C3) : (tok == TOK_PAD ? aux.biasrow : aux.zrow);
   };
-  auto prep = [&](long it, int buf, FwdItem& f) __attribute__((always_inline)) {
+  // operands of the current / next item, ping-ponged by a compile-time index so that they
+  // stay in registers (a struct passed by reference ended up in scratch)
+  u32x4 kr[2][4], qr[2][4], vr[2][4];
+  bool bnd[2] = {false, false};
+  auto prep = [&](long it, auto BUF) __attribute__((always_inline)) {
+    constexpr int buf = decltype(BUF)::value;
     const int win = (int)it;
-    f.boundary = window_tokens(g, win, L.tok[buf], L.reg[buf], lane);
+    bnd[buf] = window_tokens(g, win, L.tok[buf], L.reg[buf], lane);
     lds_sync();
-    const int cq = h * HD + 8 * (lane >> 5), ck = g.C + cq;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const bf16_t* rb = rowbase(L.tok[buf][32 * t + (lane & 31)]);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        f.ka[t][ks] = *reinterpret_cast<const bf16x8*>(rb + ck + 16 * ks);
-        f.qb[t][ks] = *reinterpret_cast<const bf16x8*>(rb + cq + 16 * ks);
-      }
-    }
-    const int cv = 2 * g.C + h * HD + 8 * (lane & 3);
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      f.vr[c] = *reinterpret_cast<const uint4*>(rowbase(L.tok[buf][(lane >> 2) + 16 * c]) + cv);
+    const int cq = h * HD + 8 * (lane & 3), ck = g.C + cq, cv = 2 * g.C + cq;
+    static_for([&](auto CI) {
+      constexpr int c = decltype(CI)::value;
+      const bf16_t* rb = rowbase(L.tok[buf][(lane >> 2) + 16 * c]);
+      kr[buf][c] = *reinterpret_cast<const u32x4*>(rb + ck);
+      qr[buf][c] = *reinterpret_cast<const u32x4*>(rb + cq);
+      vr[buf][c] = *reinterpret_cast<const u32x4*>(rb + cv);
+    }, std::make_integer_sequence<int, 4>{});
   };
 
-  FwdItem cur;
-  prep(item, 0, cur);
-  int buf = 0;
-  for (;;) {
-    const int win = (int)item;
-    // V rows of this item -> LDS (the previous item's PV reads are complete: lds_sync below)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      *reinterpret_cast<uint4*>(L.v + ((lane >> 2) + 16 * c) * LD + (lane & 3) * 8) = cur.vr[c];
-    }
-    const long nxt = item + stride;
-    FwdItem nx;
-    if (nxt < nitems) prep(nxt, buf ^ 1, nx);
+  // one item: operands in `cur` (loaded during the previous item), next item's into `nx`
+  auto step = [&](auto BUF, long it_cur) __attribute__((always_inline)) -> bool {
+    constexpr int buf = decltype(BUF)::value;
+    const int win = (int)it_cur;
+    // K / Q / V rows of this item -> LDS (the previous item's reads are complete: lds_sync below)
+    static_for([&](auto CI) {
+      constexpr int c = decltype(CI)::value;
+      const int o = ((lane >> 2) + 16 * c) * LD + (lane & 3) * 8;
+      *reinterpret_cast<u32x4*>(L.k + o) = kr[buf][c];
+      *reinterpret_cast<u32x4*>(L.q + o) = qr[buf][c];
+      *reinterpret_cast<u32x4*>(L.v + o) = vr[buf][c];
+    }, std::make_integer_sequence<int, 4>{});
+    const long nxt = it_cur + stride;
+    const bool more = nxt < nitems;
+    if (more) prep(nxt, std::integral_constant<int, buf ^ 1>{});
     lds_sync();
+    bf16x8 ka[2][2], qb[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        ka[t][ks] = frag_rows(L.k, LD, 32 * t, 16 * ks, lane);
+        qb[t][ks] = frag_rows(L.q, LD, 32 * t, 16 * ks, lane);
+      }
     f32x16 P[2][2];
-    probs_T<true>(P, cur.ka, cur.qb, reinterpret_cast<const float*>(sBimg), L.reg[buf], cur.boundary, scale, lane);
+    probs_T<true>(P, ka, qb, reinterpret_cast<const float*>(sBimg), L.reg[buf], bnd[buf], scale, lane);
     if (p_drop > 0.f) {
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
@@ -321,27 +334,42 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
 #pragma unroll
         for (int it = 0; it < 2; ++it) O[it] = mfma32(a, pack8(P[jt][it], s), O[it]);
       }
-    // store: lane -> query i, registers 4gq..4gq+3 -> d = 8gq + 4hh .. +3 (8-byte stores)
+    // output through the q image (its fragments are consumed): lane -> query i, registers
+    // 4gq..4gq+3 -> d = 8gq + 4hh .. +3; then 4 lanes per token store its 64-B slice
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int i = it * 32 + (lane & 31);
-      const int tok = L.tok[buf][i];
-      if (tok >= 0) {
-        bf16_t* dst = out + (size_t)((unsigned)tok * (unsigned)g.C) + h * HD;
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          uint2 w;
-          w.x = (uint32_t)from_f32<bf16_t>(O[it][4 * gq]) | ((uint32_t)from_f32<bf16_t>(O[it][4 * gq + 1]) << 16);
-          w.y = (uint32_t)from_f32<bf16_t>(O[it][4 * gq + 2]) | ((uint32_t)from_f32<bf16_t>(O[it][4 * gq + 3]) << 16);
-          *reinterpret_cast<uint2*>(dst + 8 * gq + 4 * hh) = w;
-        }
+      for (int gq = 0; gq < 4; ++gq) {
+        uint2 w;
+        w.x = (uint32_t)from_f32<bf16_t>(O[it][4 * gq]) | ((uint32_t)from_f32<bf16_t>(O[it][4 * gq + 1]) << 16);
+        w.y = (uint32_t)from_f32<bf16_t>(O[it][4 * gq + 2]) | ((uint32_t)from_f32<bf16_t>(O[it][4 * gq + 3]) << 16);
+        *reinterpret_cast<uint2*>(L.q + i * LD + 8 * gq + 4 * hh) = w;
       }
     }
-    lds_sync();  // PV reads and token-table reads of this item done before they are overwritten
-    if (nxt >= nitems) break;
-    item = nxt;
-    buf ^= 1;
-    cur = nx;
+    lds_sync();
+    u32x4 ov[4];
+    int otok[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int t = (lane >> 2) + 16 * c;
+      otok[c] = L.tok[buf][t];
+      ov[c] = *reinterpret_cast<const u32x4*>(L.q + t * LD + 8 * (lane & 3));
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (otok[c] >= 0)
+        *reinterpret_cast<u32x4*>(out + (size_t)((unsigned)otok[c] * (unsigned)g.C) + h * HD + 8 * (lane & 3)) = ov[c];
+    lds_sync();  // LDS reads of this item done before they are overwritten
+    return more;
+  };
+
+  prep(item, std::integral_constant<int, 0>{});
+  for (;;) {
+    if (!step(std::integral_constant<int, 0>{}, item)) break;
+    item += stride;
+    if (!step(std::integral_constant<int, 1>{}, item)) break;
+    item += stride;
   }
 }
 
