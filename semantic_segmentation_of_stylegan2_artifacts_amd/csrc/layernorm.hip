@@ -15,6 +15,41 @@ namespace {
 
 enum InMode { IN_PLAIN = 0, IN_ADD = 1, IN_MERGE = 2, IN_D2S2 = 3 };
 
+// 16-byte row chunks: 4 f32 or 8 bf16 elements per lane access
+template <typename T> struct VecW;
+template <> struct VecW<float> {
+  static constexpr int W = 4;
+  static MSU_DEV void load(const float* p, float (&v)[4]) { Vec4<float>::load(p, v); }
+  static MSU_DEV void store(float* p, const float (&v)[4]) { Vec4<float>::store(p, v); }
+};
+template <> struct VecW<bf16_t> {
+  static constexpr int W = 8;
+  static MSU_DEV void load(const bf16_t* p, float (&v)[8]) {
+    const uint4 q = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  static MSU_DEV void store(bf16_t* p, const float (&v)[8]) {
+    uint4 q;
+    q.x = (uint32_t)from_f32<bf16_t>(v[0]) | ((uint32_t)from_f32<bf16_t>(v[1]) << 16);
+    q.y = (uint32_t)from_f32<bf16_t>(v[2]) | ((uint32_t)from_f32<bf16_t>(v[3]) << 16);
+    q.z = (uint32_t)from_f32<bf16_t>(v[4]) | ((uint32_t)from_f32<bf16_t>(v[5]) << 16);
+    q.w = (uint32_t)from_f32<bf16_t>(v[6]) | ((uint32_t)from_f32<bf16_t>(v[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = q;
+  }
+};
+template <int VW> MSU_DEV void load_f32(const float* p, float (&v)[VW]) {
+#pragma unroll
+  for (int i = 0; i < VW; i += 4) {
+    const float4 q = *reinterpret_cast<const float4*>(p + i);
+    v[i] = q.x; v[i + 1] = q.y; v[i + 2] = q.z; v[i + 3] = q.w;
+  }
+}
+
 struct LnArgs {
   const void* x;      // IN_PLAIN/MERGE/D2S2: source; IN_ADD: residual stream a
   const void* b;      // IN_ADD: branch output (may be null)
@@ -58,14 +93,15 @@ MSU_DEV long src_off(const LnArgs& a, long r, int col) {
 
 template <typename T, int MODE, int TPR, int KMAX>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs a) {
+  constexpr int VW = VecW<T>::W;  // elements per 16-B chunk
   const int lane = threadIdx.x % TPR;
   const int grp = threadIdx.x / TPR;
   constexpr int GPB = 256 / TPR;
-  const int nchunk = a.C >> 2;
+  const int nchunk = a.C / VW;
   const T* X = reinterpret_cast<const T*>(a.x);
   const T* Bv = reinterpret_cast<const T*>(a.b);
   for (long r = (long)blockIdx.x * GPB + grp; r < a.rows; r += (long)gridDim.x * GPB) {
-    float v[KMAX][4];
+    float v[KMAX][VW];
     float sum = 0.f;
     float sc = 1.f;
     if constexpr (MODE == IN_ADD) {
@@ -75,23 +111,23 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs a) {
     for (int k = 0; k < KMAX; ++k) {
       const int ch = lane + k * TPR;
       if (ch < nchunk) {
-        const long off = src_off<MODE>(a, r, ch * 4);
-        Vec4<T>::load(X + off, v[k]);
+        const long off = src_off<MODE>(a, r, ch * VW);
+        VecW<T>::load(X + off, v[k]);
         if constexpr (MODE == IN_ADD) {
           if (Bv) {
-            float w[4];
-            Vec4<T>::load(Bv + off, w);
+            float w[VW];
+            VecW<T>::load(Bv + off, w);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[k][e] += sc * w[e];
+            for (int e = 0; e < VW; ++e) v[k][e] += sc * w[e];
           }
           // round the residual stream to storage precision first: the stored value is
           // what later layers (and backward) see, so normalise exactly that value
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[k][e] = to_f32(from_f32<T>(v[k][e]));
-          if (a.s_out) Vec4<T>::store(reinterpret_cast<T*>(a.s_out) + off, v[k]);
+          for (int e = 0; e < VW; ++e) v[k][e] = to_f32(from_f32<T>(v[k][e]));
+          if (a.s_out) VecW<T>::store(reinterpret_cast<T*>(a.s_out) + off, v[k]);
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) sum += v[k][e];
+        for (int e = 0; e < VW; ++e) sum += v[k][e];
       }
     }
     sum = group_sum<TPR>(sum);
@@ -102,7 +138,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs a) {
       const int ch = lane + k * TPR;
       if (ch < nchunk) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { const float d = v[k][e] - mu; var += d * d; }
+        for (int e = 0; e < VW; ++e) { const float d = v[k][e] - mu; var += d * d; }
       }
     }
     var = group_sum<TPR>(var);
@@ -112,14 +148,12 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs a) {
     for (int k = 0; k < KMAX; ++k) {
       const int ch = lane + k * TPR;
       if (ch < nchunk) {
-        float o[4];
-        const float4 g = *reinterpret_cast<const float4*>(a.gamma + ch * 4);
-        const float4 bt = *reinterpret_cast<const float4*>(a.beta + ch * 4);
-        o[0] = (v[k][0] - mu) * rs * g.x + bt.x;
-        o[1] = (v[k][1] - mu) * rs * g.y + bt.y;
-        o[2] = (v[k][2] - mu) * rs * g.z + bt.z;
-        o[3] = (v[k][3] - mu) * rs * g.w + bt.w;
-        Vec4<T>::store(Y + r * (long)a.C + ch * 4, o);
+        float o[VW], g[VW], bt[VW];
+        load_f32<VW>(a.gamma + ch * VW, g);
+        load_f32<VW>(a.beta + ch * VW, bt);
+#pragma unroll
+        for (int e = 0; e < VW; ++e) o[e] = (v[k][e] - mu) * rs * g[e] + bt[e];
+        VecW<T>::store(Y + r * (long)a.C + ch * VW, o);
       }
     }
     if (lane == 0) { a.mean[r] = mu; a.rstd[r] = rs; }
@@ -144,34 +178,34 @@ struct LnBwdArgs {
 
 template <typename T, int MODE, int TPR, int KMAX>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
+  constexpr int VW = VecW<T>::W;  // elements per 16-B chunk
   const int lane = threadIdx.x % TPR;
   const int grp = threadIdx.x / TPR;
   constexpr int GPB = 256 / TPR;
-  const int nchunk = a.C >> 2;
+  const int nchunk = a.C / VW;
   const T* X = reinterpret_cast<const T*>(a.x);
   const T* DY = reinterpret_cast<const T*>(a.dy);
-  float accg[KMAX][4], accb[KMAX][4];
+  float accg[KMAX][VW], accb[KMAX][VW];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { accg[k][e] = 0.f; accb[k][e] = 0.f; }
+    for (int e = 0; e < VW; ++e) { accg[k][e] = 0.f; accb[k][e] = 0.f; }
   LnArgs fa;
   fa.C = a.C; fa.H = a.H; fa.W = a.W; fa.Cin = a.Cin;
   for (long r = (long)blockIdx.x * GPB + grp; r < a.rows; r += (long)gridDim.x * GPB) {
     const float mu = a.mean[r], rs = a.rstd[r];
-    float xh[KMAX][4], g[KMAX][4];
+    float xh[KMAX][VW], g[KMAX][VW];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       const int ch = lane + k * TPR;
       if (ch < nchunk) {
-        float xv[4], dv[4];
-        Vec4<T>::load(X + src_off<MODE>(fa, r, ch * 4), xv);
-        Vec4<T>::load(DY + r * (long)a.C + ch * 4, dv);
-        const float4 gm = *reinterpret_cast<const float4*>(a.gamma + ch * 4);
-        const float gg[4] = {gm.x, gm.y, gm.z, gm.w};
+        float xv[VW], dv[VW], gg[VW];
+        VecW<T>::load(X + src_off<MODE>(fa, r, ch * VW), xv);
+        VecW<T>::load(DY + r * (long)a.C + ch * VW, dv);
+        load_f32<VW>(a.gamma + ch * VW, gg);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < VW; ++e) {
           xh[k][e] = (xv[e] - mu) * rs;
           g[k][e] = dv[e] * gg[e];
           s1 += g[k][e];
@@ -191,60 +225,67 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
     for (int k = 0; k < KMAX; ++k) {
       const int ch = lane + k * TPR;
       if (ch < nchunk) {
-        float o[4];
+        float o[VW];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = rs * (g[k][e] - s1 - xh[k][e] * s2);
-        const long off = src_off<MODE>(fa, r, ch * 4);
+        for (int e = 0; e < VW; ++e) o[e] = rs * (g[k][e] - s1 - xh[k][e] * s2);
+        const long off = src_off<MODE>(fa, r, ch * VW);
         if constexpr (MODE == IN_ADD || MODE == IN_PLAIN) {
           if (a.dres) {
-            float dr[4];
-            Vec4<T>::load(reinterpret_cast<const T*>(a.dres) + off, dr);
+            float dr[VW];
+            VecW<T>::load(reinterpret_cast<const T*>(a.dres) + off, dr);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] += dr[e];
+            for (int e = 0; e < VW; ++e) o[e] += dr[e];
           }
         }
-        Vec4<T>::store(reinterpret_cast<T*>(a.dx) + off, o);
+        VecW<T>::store(reinterpret_cast<T*>(a.dx) + off, o);
         if constexpr (MODE == IN_ADD) {
           if (a.db) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] *= sc;
-            Vec4<T>::store(reinterpret_cast<T*>(a.db) + off, o);
+            for (int e = 0; e < VW; ++e) o[e] *= sc;
+            VecW<T>::store(reinterpret_cast<T*>(a.db) + off, o);
           }
         }
       }
     }
   }
-  // block reduction of the per-lane parameter-gradient partials: every group writes its
-  // row of [GPB][C], one barrier, then each column is summed over the groups in fixed order
-  __shared__ float red[2][1024 * KMAX];  // GPB * C <= (256 / TPR) * TPR * KMAX * 4
+  // parameter-gradient partials: the row groups of a wave hold the same columns in the
+  // same lanes -> fixed xor-shuffle tree over the groups, then the 4 waves' rows are summed
+  // through LDS in a fixed order (deterministic)
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    const int ch = lane + k * TPR;
-    if (ch < nchunk) {
+  for (int k = 0; k < KMAX; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        red[0][grp * a.C + ch * 4 + e] = accg[k][e];
-        red[1][grp * a.C + ch * 4 + e] = accb[k][e];
+    for (int e = 0; e < VW; ++e)
+#pragma unroll
+      for (int o = TPR; o < 64; o <<= 1) {
+        accg[k][e] += __shfl_xor(accg[k][e], o, 64);
+        accb[k][e] += __shfl_xor(accb[k][e], o, 64);
+      }
+  __shared__ float red[2][4][TPR * KMAX * VW];  // [g/b][wave][column]
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < TPR) {
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+#pragma unroll
+        for (int e = 0; e < VW; ++e) {
+          red[0][wave][ch * VW + e] = accg[k][e];
+          red[1][wave][ch * VW + e] = accb[k][e];
+        }
       }
     }
   }
   __syncthreads();
   float* P = a.part + (long)blockIdx.x * 2 * a.C;
   for (int i = threadIdx.x; i < a.C; i += 256) {
-    float sg = 0.f, sb = 0.f;
-    for (int g = 0; g < GPB; ++g) {
-      sg += red[0][g * a.C + i];
-      sb += red[1][g * a.C + i];
-    }
-    P[i] = sg;
-    P[a.C + i] = sb;
+    P[i] = ((red[0][0][i] + red[0][1][i]) + red[0][2][i]) + red[0][3][i];
+    P[a.C + i] = ((red[1][0][i] + red[1][1][i]) + red[1][2][i]) + red[1][3][i];
   }
 }
 
-
 template <typename T, int MODE>
 int launch_fwd(const LnArgs& a, hipStream_t st, int max_blocks) {
-  const int nchunk = a.C / 4;
+  const int nchunk = a.C / VecW<T>::W;
   auto go = [&](auto kern, int tpr) {
     const long gpb = 256 / tpr;
     long nb = (a.rows + gpb - 1) / gpb;
@@ -253,6 +294,7 @@ int launch_fwd(const LnArgs& a, hipStream_t st, int max_blocks) {
     hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, st, a);
     return MSU_CHECK_LAUNCH();
   };
+  if (nchunk <= 4 * 4) return go(ln_fwd_kernel<T, MODE, 4, 4>, 4);
   if (nchunk <= 8 * 4) return go(ln_fwd_kernel<T, MODE, 8, 4>, 8);
   if (nchunk <= 16 * 4) return go(ln_fwd_kernel<T, MODE, 16, 4>, 16);
   if (nchunk <= 32 * 4) return go(ln_fwd_kernel<T, MODE, 32, 4>, 32);
@@ -263,11 +305,12 @@ int launch_fwd(const LnArgs& a, hipStream_t st, int max_blocks) {
 
 template <typename T, int MODE>
 int launch_bwd(const LnBwdArgs& a, hipStream_t st, int nblocks) {
-  const int nchunk = a.C / 4;
+  const int nchunk = a.C / VecW<T>::W;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(256), 0, st, a);
     return MSU_CHECK_LAUNCH();
   };
+  if (nchunk <= 4 * 4) return go(ln_bwd_kernel<T, MODE, 4, 4>);
   if (nchunk <= 8 * 4) return go(ln_bwd_kernel<T, MODE, 8, 4>);
   if (nchunk <= 16 * 4) return go(ln_bwd_kernel<T, MODE, 16, 4>);
   if (nchunk <= 32 * 4) return go(ln_bwd_kernel<T, MODE, 32, 4>);
@@ -278,7 +321,7 @@ int launch_bwd(const LnBwdArgs& a, hipStream_t st, int nblocks) {
 
 template <int MODE>
 int fwd_dispatch(int dtype, const LnArgs& a, hipStream_t st) {
-  if (a.C % 4 != 0 || a.C > 2048) return -2;
+  if (a.C % (dtype == MSU_BF16 ? 8 : 4) != 0 || a.C > 2048) return -2;
   if (a.rows == 0) return 0;
   return dtype == MSU_BF16 ? launch_fwd<bf16_t, MODE>(a, st, 4096) : launch_fwd<float, MODE>(a, st, 4096);
 }
@@ -286,7 +329,7 @@ int fwd_dispatch(int dtype, const LnArgs& a, hipStream_t st) {
 template <int MODE>
 int bwd_dispatch(int dtype, const LnBwdArgs& a, float* dgamma, float* dbeta, int nparts, int accumulate,
                  hipStream_t st) {
-  if (a.C % 4 != 0 || a.C > 2048) return -2;
+  if (a.C % (dtype == MSU_BF16 ? 8 : 4) != 0 || a.C > 2048) return -2;
   if (a.rows == 0) return 0;
   int rc = dtype == MSU_BF16 ? launch_bwd<bf16_t, MODE>(a, st, nparts) : launch_bwd<float, MODE>(a, st, nparts);
   if (rc) return rc;
