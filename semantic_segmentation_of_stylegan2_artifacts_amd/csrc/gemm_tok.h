@@ -37,7 +37,8 @@
 namespace msu_tok {
 
 constexpr int RT = 32;  // token rows per tile (one 32x32 MFMA B operand)
-constexpr int WPB = 4;  // waves per workgroup
+// waves per workgroup: a template parameter NW (4, or 8 when the W image leaves room for
+// eight 2-deep rings: two waves per SIMD overlap one's epilogue with the other's MFMAs)
 
 enum { EPI_PLAIN = 0, EPI_GELU_DUAL = 1, EPI_GELU_GRAD = 2 };
 
@@ -100,8 +101,9 @@ constexpr int stage_cols() {
        : (NC % 64 == 0 && 32 * (64 * 2 + 16) <= bytes)   ? 64 : 32;
 }
 
-template <int KC, int NC, int NST, int EPI, bool BIAS, bool CONCAT>
-__global__ void __launch_bounds__(64 * WPB) tokgemm_kernel(TokArgs a) {
+template <int KC, int NC, int NST, int NW, int EPI, bool BIAS, bool CONCAT>
+__global__ void __launch_bounds__(64 * NW) tokgemm_kernel(TokArgs a) {
+  constexpr int WPB = NW;
   using G = StageGeom<KC>;
   constexpr int NT = NC / 32;                 // 32-column MFMA tiles per chunk
   constexpr int NPAIR = NC / 16;              // 16-column store pairs
@@ -345,7 +347,7 @@ __global__ void __launch_bounds__(64 * WPB) tokgemm_kernel(TokArgs a) {
 
 // ------------------------------------------------------------------ host side
 struct TokPlan {
-  int kc = 0, nc = 0, nst = 0;
+  int kc = 0, nc = 0, nst = 0, nw = 4;
   size_t lds = 0;
   int nchunk = 0, grid = 0;
 };
@@ -354,14 +356,14 @@ constexpr size_t LDS_MAX = 160 * 1024;
 
 
 
-inline size_t plan_lds(int kc, int nc, int nst, int K) {
+inline size_t plan_lds(int kc, int nc, int nst, int K, int nw = 4) {
   const size_t stage = (size_t)((RT * (kc / 8 + 1) + 63) / 64) * 1024;
-  return (size_t)nc * (K + 16 + 8) * 2 + (size_t)WPB * nst * stage;  // W image incl. bias block
+  return (size_t)nc * (K + 16 + 8) * 2 + (size_t)nw * nst * stage;  // W image incl. bias block
 }
 
-template <int KC, int NC, int NST, int EPI, bool BIAS, bool CONCAT>
+template <int KC, int NC, int NST, int NW, int EPI, bool BIAS, bool CONCAT>
 int launch_tok(const TokPlan& p, TokArgs a, hipStream_t st) {
-  auto kern = tokgemm_kernel<KC, NC, NST, EPI, BIAS, CONCAT>;
+  auto kern = tokgemm_kernel<KC, NC, NST, NW, EPI, BIAS, CONCAT>;
   static size_t attr = 0;
   if (attr < p.lds) {
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess)
@@ -370,15 +372,15 @@ int launch_tok(const TokPlan& p, TokArgs a, hipStream_t st) {
   }
   a.nchunk = p.nchunk;
   a.rgroups = p.grid / p.nchunk;
-  hipLaunchKernelGGL(kern, dim3(p.grid), dim3(64 * WPB), p.lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(p.grid), dim3(64 * NW), p.lds, st, a);
   return 0;
 }
 
 // epilogue variants instantiated per (KC, NC, NST); FULL = all five, else plain (+bias) only
-template <int KC, int NC, int NST, bool FULL>
+template <int KC, int NC, int NST, int NW, bool FULL>
 int dispatch_epi(const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st) {
 #define MSU_TOK(E, B, C) \
-  if (epi == E && bias == B && concat == C) return launch_tok<KC, NC, NST, E, B, C>(p, a, st);
+  if (epi == E && bias == B && concat == C) return launch_tok<KC, NC, NST, NW, E, B, C>(p, a, st);
   MSU_TOK(EPI_PLAIN, true, false)
   MSU_TOK(EPI_PLAIN, false, false)
   if constexpr (FULL) {
@@ -392,10 +394,11 @@ int dispatch_epi(const TokPlan& p, const TokArgs& a, int epi, bool bias, bool co
 
 template <int KC, bool FULL>
 int dispatch_nc(const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st) {
-#define MSU_NC(NC)                                                                       \
-  if (p.nc == NC) {                                                                      \
-    if (p.nst == 3) return dispatch_epi<KC, NC, 3, FULL>(p, a, epi, bias, concat, st);   \
-    if (p.nst == 2) return dispatch_epi<KC, NC, 2, FULL>(p, a, epi, bias, concat, st);   \
+#define MSU_NC(NC)                                                                                   \
+  if (p.nc == NC) {                                                                                  \
+    if (p.nst == 3) return dispatch_epi<KC, NC, 3, 4, FULL>(p, a, epi, bias, concat, st);           \
+    if (p.nst == 2 && p.nw == 8) return dispatch_epi<KC, NC, 2, 8, FULL>(p, a, epi, bias, concat, st); \
+    if (p.nst == 2) return dispatch_epi<KC, NC, 2, 4, FULL>(p, a, epi, bias, concat, st);           \
   }
   MSU_NC(384) MSU_NC(288) MSU_NC(256) MSU_NC(192) MSU_NC(128) MSU_NC(96) MSU_NC(64)
 #undef MSU_NC

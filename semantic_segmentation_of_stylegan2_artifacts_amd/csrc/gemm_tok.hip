@@ -37,12 +37,19 @@ TokPlan tok_plan(long M, int N, int K, int epi = EPI_PLAIN) {
   if (!p.nc) return p;
   p.nst = nst;
   p.lds = plan_lds(p.kc, p.nc, nst, K);
+  // eight waves with 2-deep rings when the W chunk leaves room (A/B switch: MSU_TOK_NW=4)
+  static const int force_nw = getenv("MSU_TOK_NW") ? atoi(getenv("MSU_TOK_NW")) : 0;
+  if (force_nw != 4 && plan_lds(p.kc, p.nc, 2, K, 8) <= LDS_MAX) {
+    p.nst = 2;
+    p.nw = 8;
+    p.lds = plan_lds(p.kc, p.nc, 2, K, 8);
+  }
   p.nchunk = N / p.nc;
-  const int per_cu = 2 * p.lds <= LDS_MAX ? 2 : 1;
+  const int per_cu = (p.nw == 4 && 2 * p.lds <= LDS_MAX) ? 2 : 1;
   int groups = (256 * per_cu) / (8 * p.nchunk);
   if (groups < 1) groups = 1;
   const long ntiles = (M + RT - 1) / RT;
-  const long max_groups = (ntiles + 8L * WPB - 1) / (8L * WPB);  // every wave gets a tile
+  const long max_groups = (ntiles + 8L * p.nw - 1) / (8L * p.nw);  // every wave gets a tile
   if (groups > max_groups) groups = (int)(max_groups < 1 ? 1 : max_groups);
   p.grid = 8 * p.nchunk * groups;
   return p;
@@ -104,7 +111,8 @@ int msu_tok_gemm(const void* A, const void* A2, int K1, const void* W, const flo
 // Plan introspection for tests / benchmarks: out6 = {kc, nc, nst, nchunk, grid, lds bytes}.
 int msu_tok_gemm_plan(long M, int N, int K, long* out6) {
   const TokPlan p = tok_plan(M, N, K);
-  out6[0] = p.kc; out6[1] = p.nc; out6[2] = p.nst; out6[3] = p.nchunk; out6[4] = p.grid; out6[5] = (long)p.lds;
+  out6[0] = p.kc; out6[1] = p.nc; out6[2] = p.nst * 100 + p.nw; out6[3] = p.nchunk; out6[4] = p.grid;
+  out6[5] = (long)p.lds;
   return p.nc ? 0 : -3;
 }
 
