@@ -374,9 +374,9 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
 }
 
 struct BwdLds {
-  bf16_t q[64 * LD], k[64 * LD], dO[64 * LD];
+  bf16_t q[64 * LD], k[64 * LD], v[64 * LD], dO[64 * LD];
   bf16_t P[64 * LDP], dS[64 * LDP];  // [i][j] images
-  int tok[64], reg[64];
+  int tok[2][64], reg[2][64];          // current / prefetched window
 };
 
 template <int WAVES>
@@ -400,23 +400,51 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
     for (int b = 0; b < 2; ++b) dB[a][b] = f32x16{0};
   float padacc[3] = {0.f, 0.f, 0.f};  // column d = lane&31 of padded tokens' dq, dk, dv (per half)
   const long stride = (long)nblk * WAVES;
-  for (long win = (long)blockIdx.x * WAVES + wave; win < g.nwin; win += stride) {
-    const bool boundary = window_tokens(g, win, L.tok, L.reg, lane);
+  // The window's q / k / v / dO head slices (4 lanes per 64-B slice) are loaded into
+  // registers one window ahead: window i+1's HBM latency hides under window i's math.
+  u32x4 rq[2][4], rk[2][4], rv[2][4], rd[2][4];
+  bool bnd[2] = {false, false};
+  auto rowbase = [&](int tok) -> const bf16_t* {
+    return tok >= 0 ? qkv + (size_t)((unsigned)tok * (unsigned)C3) : (tok == TOK_PAD ? aux.biasrow : aux.zrow);
+  };
+  auto prep = [&](long w, auto BUF) __attribute__((always_inline)) {
+    constexpr int buf = decltype(BUF)::value;
+    bnd[buf] = window_tokens(g, w, L.tok[buf], L.reg[buf], lane);
+    lds_sync();
+    const int o = 8 * (lane & 3);
+    static_for([&](auto CI) {
+      constexpr int c = decltype(CI)::value;
+      const int tok = L.tok[buf][(lane >> 2) + 16 * c];
+      const bf16_t* rb = rowbase(tok);
+      rq[buf][c] = *reinterpret_cast<const u32x4*>(rb + cq + o);
+      rk[buf][c] = *reinterpret_cast<const u32x4*>(rb + ck + o);
+      rv[buf][c] = *reinterpret_cast<const u32x4*>(rb + cv + o);
+      const bf16_t* db = tok >= 0 ? dout + (size_t)((unsigned)tok * (unsigned)g.C) + h * HD : aux.zrow;
+      rd[buf][c] = *reinterpret_cast<const u32x4*>(db + o);
+    }, std::make_integer_sequence<int, 4>{});
+  };
+  auto step = [&](auto BUF, long win) __attribute__((always_inline)) -> bool {
+    constexpr int buf = decltype(BUF)::value;
+    static_for([&](auto CI) {
+      constexpr int c = decltype(CI)::value;
+      const int off = ((lane >> 2) + 16 * c) * LD + 8 * (lane & 3);
+      *reinterpret_cast<u32x4*>(L.q + off) = rq[buf][c];
+      *reinterpret_cast<u32x4*>(L.k + off) = rk[buf][c];
+      *reinterpret_cast<u32x4*>(L.v + off) = rv[buf][c];
+      *reinterpret_cast<u32x4*>(L.dO + off) = rd[buf][c];
+    }, std::make_integer_sequence<int, 4>{});
+    const long nxt = win + stride;
+    const bool more = nxt < g.nwin;
+    if (more) prep(nxt, std::integral_constant<int, buf ^ 1>{});
+    const bool boundary = bnd[buf];
+    const int* sTok = L.tok[buf];
+    const int* sReg = L.reg[buf];
     lds_sync();
     bf16x8 va[2][2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        va[t][ks] = frag_global(L.tok, 32 * t, qkv + cv, C3, aux.biasrow + cv, aux.zrow, 16 * ks, lane);
-    {
-      const bf16_t* const base[3] = {qkv + cq, qkv + ck, dout + h * HD};
-      const long strd[3] = {C3, C3, (long)g.C};
-      const bf16_t* const pad[3] = {aux.biasrow + cq, aux.biasrow + ck, aux.zrow};
-      bf16_t* const dst[3] = {L.q, L.k, L.dO};
-      stage_rows<3>(L.tok, base, strd, pad, aux.zrow, dst, lane);
-    }
-    lds_sync();
+      for (int ks = 0; ks < 2; ++ks) va[t][ks] = frag_rows(L.v, LD, 32 * t, 16 * ks, lane);
     bf16x8 ka[2][2], qb[2][2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -426,7 +454,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
         qb[t][ks] = frag_rows(L.q, LD, 32 * t, 16 * ks, lane);
       }
     f32x16 P[2][2];
-    probs_T(P, ka, qb, bimg, L.reg, boundary, scale, lane);
+    probs_T(P, ka, qb, bimg, sReg, boundary, scale, lane);
     // dPd^T[j][i] = sum_d V[j][d] dO[i][d]
     f32x16 D[2][2];
 #pragma unroll
@@ -500,7 +528,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int t = mt * 32 + crow(r, hh);
-        const int tok = L.tok[t];
+        const int tok = sTok[t];
         if (tok >= 0) {
           bf16_t* row = dqkv + (long)tok * C3 + h * HD + d;
           row[0] = from_f32<bf16_t>(aq[r] * scale);
@@ -513,8 +541,21 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();
+    lds_sync();  // this window's LDS reads are done before the next window's rows land
+    return more;
+  };
+
+  long win = (long)blockIdx.x * WAVES + wave;
+  if (win < g.nwin) {
+    prep(win, std::integral_constant<int, 0>{});
+    for (;;) {
+      if (!step(std::integral_constant<int, 0>{}, win)) break;
+      win += stride;
+      if (!step(std::integral_constant<int, 1>{}, win)) break;
+      win += stride;
+    }
   }
+
   const long part = (long)blockIdx.x * WAVES + wave;
   float* db = dB_part + (part * g.nh + h) * 4096;
 #pragma unroll
