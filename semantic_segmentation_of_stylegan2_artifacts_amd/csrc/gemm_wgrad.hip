@@ -222,19 +222,29 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
     wait_vmcnt<PER_WAVE * (NST - 2)>();
     __builtin_amdgcn_s_barrier();
     issue(st + NST - 1);  // into the buffer computed in the previous iteration
+    // fragments by untracked reads (a visible ds_read would wait for the whole ring);
+    // A fragment i+1 is read while the MFMAs of fragment i run
     const bf16_t* buf = lds + (st % NST) * STG;
-    const bf16_t* pa = buf + laneA;
-    const bf16_t* pb = buf + laneB;
-    bf16x8 bf[NTW];
+    const uint32_t pa = lds_u32(buf + laneA), pb = lds_u32(buf + laneB);
+    bf16x8 bf[NTW], af[2];
+    unroll_for<NTW>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      bf[j] = tr8_untracked<32 * j, 32 * j + 8 * LB>(pb);
+    });
+    af[0] = tr8_untracked<0, 8 * LA>(pa);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) bf[j] = tr8(pb + 16 * j, 4 * LB);
+    for (int j = 0; j < NTW; ++j) asm volatile("" : "+v"(bf[j]));
+    asm volatile("" : "+v"(af[0]));
+    unroll_for<NTW>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if constexpr (i + 1 < NTW) af[(i + 1) & 1] = tr8_untracked<32 * (i + 1), 32 * (i + 1) + 8 * LA>(pa);
 #pragma unroll
-    for (int i = 0; i < NTW; ++i) {
-      const bf16x8 af = tr8(pa + 16 * i, 4 * LA);
-#pragma unroll
-      for (int j = 0; j < NTW; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
-      accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, ones, accb[i], 0, 0, 0);  // unconditional: no branch
-    }
+      for (int j = 0; j < NTW; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i & 1], bf[j], acc[i][j], 0, 0, 0);
+      accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i & 1], ones, accb[i], 0, 0, 0);  // unconditional
+      if constexpr (i + 1 < NTW) lds_wait_tie<0>(af[(i + 1) & 1]);
+    });
   }
   wait_vmcnt<0>();  // every DMA has landed: the ring may be reused
   // row-waves of the same output tile are summed in LDS first: one slab per split

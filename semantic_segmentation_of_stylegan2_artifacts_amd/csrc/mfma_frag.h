@@ -7,6 +7,8 @@
 // Every lane supplies its own row address, so row maps may be arbitrary (tap shifts,
 // gathered rows); addresses must be 8-byte aligned and EXEC all ones.
 #pragma once
+#include <utility>
+
 #include "common.h"
 
 namespace {
@@ -33,6 +35,49 @@ template <> struct TR<bf16_t> {
                                                   acc, 0, 0, 0);
   }
 };
+// Untracked fragment reads for LDS images filled by LDS-DMA (global_load_lds): the compiler
+// treats every pending LDS-DMA as a possible alias of a visible ds_read and puts an
+// s_waitcnt vmcnt(0) in front of it, draining the whole prefetch ring every stage.  These
+// reads are inline asm (byte offsets folded into the instruction); the caller makes the
+// data visible with lds_wait_tie() before the MFMAs that consume it.
+template <int OFF>
+MSU_DEV msu_v4s ds_tr_b64_untracked(uint32_t addr) {
+  msu_v4s v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+template <int OFF0, int OFF1>
+MSU_DEV bf16x8 tr8_untracked(uint32_t addr) {
+  const msu_v4s lo = ds_tr_b64_untracked<OFF0>(addr);
+  const msu_v4s hi = ds_tr_b64_untracked<OFF1>(addr);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+// s_waitcnt lgkmcnt(N), then pin the fragments after it (an empty asm rewriting each one, so
+// no consumer can be scheduled above the wait)
+template <typename T>
+MSU_DEV void vreg_pin(T& v) {
+  asm volatile("" : "+v"(v));
+}
+template <int N, typename... Fr>
+MSU_DEV void lds_wait_tie(Fr&... fr) {
+  static_assert(N >= 0 && N < 16, "lgkmcnt range");
+  asm volatile("s_waitcnt lgkmcnt(%0)" : : "i"(N) : "memory");
+  (vreg_pin(fr), ...);
+}
+template <typename F, int... Is>
+MSU_DEV void unroll_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>): indices usable as template
+// arguments (instruction offsets) and as constant register-array indices
+template <int N, typename F>
+MSU_DEV void unroll_for(F&& f) {
+  unroll_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+MSU_DEV uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)(p);
+}
+
 template <> struct TR<float> {
   template <typename RA, typename RB>
   static MSU_DEV void mma(f32x4& acc, RA ra, int colA, RB rb, int colB, int kbase, int lane) {

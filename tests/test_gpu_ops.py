@@ -348,7 +348,7 @@ def test_adamw_matches_torch():
 
 
 @pytest.mark.parametrize("M,N,K", [(100, 96, 288), (4096, 288, 96), (777, 32, 48), (65536, 384, 96),
-                                   (3000, 1536, 96), (512, 192, 768)])
+                                   (3000, 1536, 96), (512, 192, 768), (8192, 1152, 384), (2000, 384, 384)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_linear(M, N, K, dtype):
     """ops.linear: hipBLASLt fwd/dgrad + HIP split-M weight/bias gradient vs fp32 torch."""

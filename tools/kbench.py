@@ -61,7 +61,12 @@ def wgrad():
     from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
     shapes = [(B * 65536, 288, 96), (B * 65536, 96, 96), (B * 65536, 384, 96), (B * 65536, 96, 384),
               (B * 65536, 1536, 96), (B * 16384, 576, 192), (B * 16384, 768, 192), (B * 16384, 192, 768),
-              (B * 4096, 1152, 384), (B * 4096, 1536, 384), (B * 1024, 3072, 768)]
+              (B * 16384, 192, 192), (B * 4096, 1152, 384), (B * 4096, 384, 384), (B * 4096, 1536, 384),
+              (B * 4096, 384, 1536), (B * 1024, 2304, 768), (B * 1024, 768, 768), (B * 1024, 3072, 768),
+              (B * 1024, 768, 3072)]
+    only = os.environ.get("KB_STAGE")
+    if only:
+        shapes = [s for s in shapes if s[0] == B * {"0": 65536, "1": 16384, "2": 4096, "3": 1024}[only]]
     for M, N, K in shapes:
         dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
         x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
