@@ -691,42 +691,52 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
     if (next < ntiles) stage(next, cur ^ 1);
     const bf16_t* sX = lds + cur * BUF;
     const bf16_t* sD = sX + HPIX * PS;
+    // All LDS reads of the tile are untracked (inline asm): a compiler-visible ds_read would
+    // be preceded by vmcnt(0) for the next tile's pending LDS-DMA and serialise the two.
     // bias gradient: 16 groups x 48 channel pairs, 8 pixels each
+    {
+      const uint32_t ba = lds_u32(sD + dbg * PS + dbc);
+      uint32_t v[DPIX / 16];
+      unroll_for<DPIX / 16>([&](auto P) {
+        v[decltype(P)::value] = ds_b32_untracked<2 * 16 * PS * decltype(P)::value>(ba);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int p = 0; p < DPIX / 16; ++p) {
-      const uint32_t v = *reinterpret_cast<const uint32_t*>(sD + (dbg + 16 * p) * PS + dbc);
-      dbacc[0] += __uint_as_float(v << 16);
-      dbacc[1] += __uint_as_float(v & 0xffff0000u);
-    }
-    // lane part of a k-strided fragment read: rows 8(lane>>4) + (lane&15)>>2 (+4 for the
-    // second half), columns 4(lane&3); everything else is an immediate offset
-    const int laneoff = opaque((8 * (lane >> 4) + ((lane & 15) >> 2)) * PS + 4 * (lane & 3));
-    const bf16_t* xl = sX + laneoff + dy * HWD * PS;
-    const bf16_t* dl = sD + laneoff;
-    auto tr8 = [](const bf16_t* p) {
-      typedef __attribute__((address_space(3))) msu_v4s lds_v4s;
-      const msu_v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
-      const msu_v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p + 4 * PS));
-      msu_v4s both[2] = {lo, hi};
-      return *reinterpret_cast<bf16x8*>(both);
-    };
-#pragma unroll
-    for (int r = 0; r < TH; ++r) {
-#pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        bf16x8 bf[3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) bf[j] = tr8(xl + (r * HWD + d) * PS + 48 * cih + 16 * j);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const bf16x8 af = tr8(dl + r * TWV * PS + 48 * coh + 16 * i);
-#pragma unroll
-          for (int j = 0; j < 3; ++j)
-            acc[d][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[d][i][j], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+      for (int p = 0; p < DPIX / 16; ++p) {
+        vreg_pin(v[p]);
+        dbacc[0] += __uint_as_float(v[p] << 16);
+        dbacc[1] += __uint_as_float(v[p] & 0xffff0000u);
       }
     }
+    // lane part of a k-strided fragment read: pixels 2(4g + q) + half (+16 for the second
+    // half of the fragment), g = lane group within the 32-lane half, q = (lane&15)>>2,
+    // columns 4(lane&3); everything else is an immediate offset.  Same pixel order for both
+    // operands; pixels of one parity sit 104 * 2j B apart: distinct 32-B bank spans, so each
+    // half's 32 lanes hit all 64 banks once (pixels 8(lane>>4) + q: 2-way conflicts).
+    const int laneoff = opaque((2 * (4 * ((lane >> 4) & 1) + ((lane & 15) >> 2)) + (lane >> 5)) * PS + 4 * (lane & 3));
+    const uint32_t xa = lds_u32(sX + laneoff + dy * HWD * PS + 48 * cih);
+    const uint32_t da = lds_u32(sD + laneoff + 48 * coh);
+    unroll_for<TH>([&](auto R) {
+      unroll_for<3>([&](auto D) {
+        constexpr int r = decltype(R)::value, d = decltype(D)::value;
+        bf16x8 bf[3], af[3];
+        unroll_for<3>([&](auto J) {
+          constexpr int o = 2 * ((r * HWD + d) * PS + 16 * decltype(J)::value);
+          bf[decltype(J)::value] = tr8_untracked<o, o + 32 * PS>(xa);
+        });
+        unroll_for<3>([&](auto I) {
+          constexpr int o = 2 * (r * TWV * PS + 16 * decltype(I)::value);
+          af[decltype(I)::value] = tr8_untracked<o, o + 32 * PS>(da);
+        });
+        lds_wait_tie<0>(bf[0], bf[1], bf[2], af[0], af[1], af[2]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            acc[d][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[d][i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
     if (next < ntiles) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       gelu_own(cur ^ 1);

@@ -204,9 +204,13 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
   bf16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
-  // lane part of a k-strided fragment read (ds_read_b64_tr_b16): rows 8(lane>>4) + q,
-  // columns 4p; the second half of the fragment is 4 rows further
-  const int q = (lane & 15) >> 2, p4 = 4 * (lane & 3), r0 = wmi * 32 + 8 * (lane >> 4) + q;
+  // lane part of a k-strided fragment read (ds_read_b64_tr_b16), columns 4p.  The k order
+  // is free (both operands use the same one): each 32-lane half reads 8 rows of one parity,
+  // 2(4g + q) + half (g = lane group within the half), and the second half of the fragment
+  // 16 rows further.  Rows 2j apart sit 2j * stride dwords apart, distinct multiples of 8
+  // mod 64 for both row strides (52 and 196 dwords): the 32 lanes cover all 64 banks
+  // exactly once (rows 8(lane>>4) + q put two rows on each bank span: 2-way conflicts).
+  const int q = (lane & 15) >> 2, p4 = 4 * (lane & 3), r0 = wmi * 32 + 2 * (4 * ((lane >> 4) & 1) + q) + (lane >> 5);
   const int laneA = r0 * LA + wni * WT + p4, laneB = RS * LA + r0 * LB + p4;
   auto tr8 = [](const bf16_t* p, int second) {
     typedef __attribute__((address_space(3))) msu_v4s lds_v4s;
@@ -229,16 +233,16 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
     bf16x8 bf[NTW], af[2];
     unroll_for<NTW>([&](auto J) {
       constexpr int j = decltype(J)::value;
-      bf[j] = tr8_untracked<32 * j, 32 * j + 8 * LB>(pb);
+      bf[j] = tr8_untracked<32 * j, 32 * j + 32 * LB>(pb);
     });
-    af[0] = tr8_untracked<0, 8 * LA>(pa);
+    af[0] = tr8_untracked<0, 32 * LA>(pa);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int j = 0; j < NTW; ++j) asm volatile("" : "+v"(bf[j]));
     asm volatile("" : "+v"(af[0]));
     unroll_for<NTW>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      if constexpr (i + 1 < NTW) af[(i + 1) & 1] = tr8_untracked<32 * (i + 1), 32 * (i + 1) + 8 * LA>(pa);
+      if constexpr (i + 1 < NTW) af[(i + 1) & 1] = tr8_untracked<32 * (i + 1), 32 * (i + 1) + 32 * LA>(pa);
 #pragma unroll
       for (int j = 0; j < NTW; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i & 1], bf[j], acc[i][j], 0, 0, 0);

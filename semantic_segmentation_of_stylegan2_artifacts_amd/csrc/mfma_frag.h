@@ -46,6 +46,12 @@ MSU_DEV msu_v4s ds_tr_b64_untracked(uint32_t addr) {
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
   return v;
 }
+template <int OFF>
+MSU_DEV uint32_t ds_b32_untracked(uint32_t addr) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
 template <int OFF0, int OFF1>
 MSU_DEV bf16x8 tr8_untracked(uint32_t addr) {
   const msu_v4s lo = ds_tr_b64_untracked<OFF0>(addr);

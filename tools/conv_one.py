@@ -1,5 +1,5 @@
 """Run one refine-conv forward shape repeatedly (for rocprofv3 counter passes).
-    python tools/conv_one.py [d2s 0|1] [reps]"""
+    python tools/conv_one.py [d2s 0|1] [reps] [bwd]"""
 import os
 import sys
 
@@ -14,8 +14,16 @@ B, C, H = 8, 96, 1024
 x = torch.randn((B, H // 4, H // 4, 16 * C) if d2s else (B, H, H, C), device="cuda", dtype=torch.bfloat16)
 w = torch.randn(C, C, 3, 3, device="cuda") * 0.03
 b = torch.randn(C, device="cuda")
+bwd = len(sys.argv) > 3 and sys.argv[3] == "bwd"
 with torch.autocast("cuda", dtype=torch.bfloat16):
+    if bwd:
+        xq, wq = x.requires_grad_(True), w.requires_grad_(True)
+        z = ops.refine_conv(xq, wq, b, d2s, (H, H))
+        dz = torch.randn_like(z)
     for _ in range(reps):
-        ops.refine_conv(x, w, b, d2s, (H, H))
+        if bwd:
+            torch.autograd.grad(z, (xq, wq), dz, retain_graph=True)
+        else:
+            ops.refine_conv(x, w, b, d2s, (H, H))
 torch.cuda.synchronize()
 print("ok")

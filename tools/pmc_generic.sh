@@ -7,7 +7,8 @@ mkdir -p $O
 i=0
 for ctrs in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES" \
             "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS" \
-            "GRBM_GUI_ACTIVE TCC_HIT TCC_MISS TCC_BUSY TA_BUSY"; do
+            "GRBM_GUI_ACTIVE TCC_HIT TCC_MISS TCC_BUSY TA_BUSY" \
+            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_INSTS_VALU_MFMA_MOPS_BF16"; do
   i=$((i+1))
   timeout -s KILL 60 rocprofv3 --pmc $ctrs -d $O -o p$i --output-format csv -- "$@" > $O/p$i.log 2>&1 || { tail -5 $O/p$i.log; exit 1; }
 done
