@@ -89,6 +89,11 @@ int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const fl
  * (model_parts.py:464-465).  Wt: [9][Cout][roundup(Cin,32)] in the activation dtype. */
 int msu_conv3x3_fwd(int dtype, int in_mode, const void* X, const void* Wt, const float* bias,
                     void* Y, int B, int H, int W, int Cin, int Cout, void* stream);
+/* As msu_conv3x3_fwd; Y2 (may be null; only with in_mode bit0 clear) receives GELU(Y) from
+ * the same epilogue, so the next refine conv loads its activation instead of converting its
+ * halo (model_parts.py:469: refine2(act(refine1(.)))). */
+int msu_conv3x3_fwd2(int dtype, int in_mode, const void* X, const void* Wt, const float* bias,
+                     void* Y, void* Y2, int B, int H, int W, int Cin, int Cout, void* stream);
 /* dX = conv(dY, Wflip) * GELU'(S) through the same input map (out_mode as in_mode);
  * Wflip [9][Cin][roundup(Cout,32)], Wflip[t][ci][co] = W[co][ci][8-t]. */
 int msu_conv3x3_dgrad(int dtype, int out_mode, const void* dY, const void* Wflip, const void* S,

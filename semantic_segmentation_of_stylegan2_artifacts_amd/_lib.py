@@ -6,7 +6,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmsunet_hip.so")
+# MSU_LIB_OVERRIDE: an alternative build of the same library (kernel ablation builds made by
+# tools/build_exp.sh); the product path never sets it
+LIB_PATH = os.environ.get("MSU_LIB_OVERRIDE") or os.path.join(_HERE, "libmsunet_hip.so")
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -37,6 +39,7 @@ SIGNATURES = {
     "msu_nonfinite": (I, [P, L, P, P]),
     "msu_cast": (I, [I, P, P, L, P]),
     "msu_conv3x3_fwd": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),
+    "msu_conv3x3_fwd2": (I, [I, I, P, P, P, P, P, I, I, I, I, I, P]),
     "msu_conv3x3_dgrad": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),
     "msu_conv3x3_wgrad_workspace": (L, [I, I, I, I, I]),
     "msu_conv3x3_wgrad": (I, [I, I, P, P, P, P, P, P, I, I, I, I, I, I, P]),

@@ -1,965 +1,42 @@
-// 3x3 / stride 1 / pad 1 convolution of the full-resolution decoder head, NHWC, as an
-// implicit GEMM on MFMA with an LDS halo tile.  Replaces FinalPatchExpand_X4_V2's
-// refine1 / refine2 (network/model_parts.py:447-448, :468-471) together with the ops
-// around them:
-//   * depth-to-space 4x4 of the expand output (model_parts.py:464-465) is folded into the
-//     input addressing (IN_D2S) -- the d2s tensor and the NHWC->NCHW permute never exist;
-//   * GELU of the conv input (model_parts.py:460, :469) is applied on load (IN_GELU), so
-//     only pre-activations are stored;
-//   * bias add in the epilogue; backward-data multiplies by GELU'(pre-activation) in the
-//     epilogue and scatters through the same d2s map (OUT_D2S / OUT_GGRAD).
-// fwd and dgrad share one kernel (dgrad = conv with spatially flipped, ci<->co swapped
-// weights).  wgrad reads both operands k-strided from natural [pixel][channel] LDS images
-// with ds_read_b64_tr_b16 (bf16) and writes deterministic per-block partials.
-#include <utility>
-
-#include "common.h"
-#include "mfma_frag.h"
-
-namespace {
-
-constexpr int TW = 16;  // output tile width (pixels) = one MFMA M tile
-
-struct ConvGeom {
-  int B, H, W;
-  int Cin, CinP;   // GEMM input channels, padded to a multiple of 32
-  int Cout;        // GEMM output channels (multiple of 16)
-  int PS;          // LDS pixel stride (elements) of the input image
-  int PSW;         // LDS row stride of the weight tile (fwd/dgrad)
-  int PSD;         // LDS pixel stride of the dY tile (wgrad)
-};
-
-// element offset of channel 0 of pixel (b, y, x) of the logical [B,H,W,C] image
-template <bool D2S>
-MSU_DEV long pix_off(int b, int y, int x, int H, int W, int C) {
-  if constexpr (D2S) {
-    const int h4 = H >> 2, w4 = W >> 2;
-    return (((long)b * h4 + (y >> 2)) * w4 + (x >> 2)) * (16L * C) + (long)(((y & 3) * 4 + (x & 3)) * C);
-  } else {
-    return (((long)b * H + y) * W + x) * (long)C;
-  }
-}
-
-// 32-bit variant (tensors below 2^31 elements; checked on the host)
-template <bool D2S>
-MSU_DEV int pix_off32(int b, int y, int x, int H, int W, int C) {
-  if constexpr (D2S) {
-    const int h4 = H >> 2, w4 = W >> 2;
-    return ((b * h4 + (y >> 2)) * w4 + (x >> 2)) * (16 * C) + ((y & 3) * 4 + (x & 3)) * C;
-  } else {
-    return ((b * H + y) * W + x) * C;
-  }
-}
-
-// opaque copy of a value: stops the compiler from hoisting per-chunk index math out of the
-// persistent tile loop (it would keep ~5 registers per chunk live across the whole loop)
-MSU_DEV int opaque(int v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-
-// Stage rows [y_first, y_first + nrows) x cols [x0 - 1, x0 + TW + 1) of the transformed
-// input image (GELU optional) into LDS sX[(row * (TW+2) + col) * PS + c]; zero outside.
-template <typename T, bool D2S, bool GELU>
-MSU_DEV void stage_halo(const T* X, T* sX, int b, int y_first, int nrows, int x0, const ConvGeom& g,
-                        int tid, int nthreads) {
-  const int cpp = g.CinP / 8;  // 8-element chunks per pixel
-  const int total = nrows * (TW + 2) * cpp;
-  for (int i = tid; i < total; i += nthreads) {
-    const int pix = i / cpp, ch = i - pix * cpp;
-    const int row = pix / (TW + 2), col = pix - row * (TW + 2);
-    const int y = y_first + row, x = x0 - 1 + col;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = 0.f;
-    if (y >= 0 && y < g.H && x >= 0 && x < g.W && ch * 8 < g.Cin) {
-      const T* p = X + pix_off<D2S>(b, y, x, g.H, g.W, g.Cin) + ch * 8;
-      float a[4], c[4];
-      Vec4<T>::load(p, a);
-      Vec4<T>::load(p + 4, c);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = c[e]; }
-      if constexpr (GELU) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
-      }
-    }
-    T* d = sX + pix * g.PS + ch * 8;
-    float lo[4] = {v[0], v[1], v[2], v[3]}, hi[4] = {v[4], v[5], v[6], v[7]};
-    Vec4<T>::store(d, lo);
-    Vec4<T>::store(d + 4, hi);
-  }
-}
-
-// acc += A(16 x 32) B(32 x 16) with both operands k-contiguous in LDS.
-template <typename T> struct KC;
-template <> struct KC<bf16_t> {
-  static MSU_DEV void mma(f32x4& acc, const bf16_t* A, int lda, const bf16_t* B, int ldb, int lane) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + (lane & 15) * lda + 8 * (lane >> 4));
-    const bf16x8 b = *reinterpret_cast<const bf16x8*>(B + (lane & 15) * ldb + 8 * (lane >> 4));
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-  }
-  static MSU_DEV bf16x8 fragA(const bf16_t* A, int lda, int lane) {
-    return *reinterpret_cast<const bf16x8*>(A + (lane & 15) * lda + 8 * (lane >> 4));
-  }
-};
-template <> struct KC<float> {
-  static MSU_DEV void mma(f32x4& acc, const float* A, int lda, const float* B, int ldb, int lane) {
-    const float* pa = A + (lane & 15) * lda + (lane >> 4);
-    const float* pb = B + (lane & 15) * ldb + (lane >> 4);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[4 * s], pb[4 * s], acc, 0, 0, 0);
-  }
-};
-
-// ------------------------------------------------------------------ fwd / dgrad kernel
-// Y[pixel][co] = sum_{tap, ci} Xt[pixel + off(tap)][ci] * Wt[tap][co][ci] (+ bias[co])
-//               (* GELU'(S[pixel][co]) when OUT_GGRAD), Xt = GELU?(map(X)).
-// Block = NWAVES waves = TH x 16 output pixels x all Cout; wave w owns MT image rows.
-template <typename T, int NT, int TH, int MT, bool DB, bool IN_D2S, bool IN_GELU, bool OUT_D2S,
-          bool OUT_GGRAD, bool BIAS>
-__global__ void __launch_bounds__(64 * (TH / MT)) conv3x3_kernel(const T* __restrict__ X,
-                                                                 const T* __restrict__ Wt,
-                                                                 const float* __restrict__ bias,
-                                                                 const T* __restrict__ S,
-                                                                 T* __restrict__ Y, ConvGeom g) {
-  constexpr int NWAVES = TH / MT;
-  constexpr int NTHR = 64 * NWAVES;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  T* sX = reinterpret_cast<T*>(smem_raw);
-  T* sW0 = sX + (TH + 2) * (TW + 2) * g.PS;
-  T* sW1 = sW0 + g.Cout * g.PSW;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tiles_x = (g.W + TW - 1) / TW, tiles_y = (g.H + TH - 1) / TH;
-  const long ntiles = (long)g.B * tiles_x * tiles_y;
-  const long tile = xcd_remap(blockIdx.x, gridDim.x);
-  if (tile >= ntiles) return;
-  const int b = (int)(tile / ((long)tiles_x * tiles_y));
-  const int trem = (int)(tile - (long)b * tiles_x * tiles_y);
-  const int y0 = (trem / tiles_x) * TH, x0 = (trem % tiles_x) * TW;
-
-  stage_halo<T, IN_D2S, IN_GELU>(X, sX, b, y0 - 1, TH + 2, x0, g, tid, NTHR);
-  // weight tile of tap t: Wt[t] is [Cout][CinP] contiguous -> sW[co * PSW + ci]
-  const int wchunks = g.Cout * (g.CinP / 8);
-  auto load_w = [&](int t, T* dst) {
-    const T* src = Wt + (long)t * g.Cout * g.CinP;
-    for (int i = tid; i < wchunks; i += NTHR) {
-      const int co = i / (g.CinP / 8), ch = i - co * (g.CinP / 8);
-      *reinterpret_cast<uint4*>(dst + co * g.PSW + ch * 8) =
-          *reinterpret_cast<const uint4*>(src + (long)co * g.CinP + ch * 8);
-    }
-  };
-  static_assert(sizeof(T) == 2 || !DB, "double-buffered weights only for bf16");
-  if constexpr (sizeof(T) == 2) {
-    load_w(0, sW0);
-  } else {
-    // f32: 8-element chunks are 32 bytes
-    const float* src = reinterpret_cast<const float*>(Wt);
-    for (int i = tid; i < g.Cout * g.CinP; i += NTHR) {
-      const int co = i / g.CinP, ci = i - co * g.CinP;
-      reinterpret_cast<float*>(sW0)[co * g.PSW + ci] = src[i];
-    }
-  }
-  __syncthreads();
-
-  f32x4 acc[MT][NT];
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nks = g.CinP / 32;
-  for (int tap = 0; tap < 9; ++tap) {
-    const int dy = tap / 3, dx = tap - (tap / 3) * 3;
-    T* sW = (DB && (tap & 1)) ? sW1 : sW0;
-    if constexpr (DB) {
-      if (tap + 1 < 9) load_w(tap + 1, (tap & 1) ? sW0 : sW1);
-    }
-    for (int ks = 0; ks < nks; ++ks) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int hrow = wave * MT + m + dy;  // halo row
-        const T* A = sX + (hrow * (TW + 2) + dx) * g.PS + ks * 32;
-#pragma unroll
-        for (int n = 0; n < NT; ++n)
-          KC<T>::mma(acc[m][n], A, g.PS, sW + n * 16 * g.PSW + ks * 32, g.PSW, lane);
-      }
-    }
-    __syncthreads();
-    if constexpr (!DB) {
-      if (tap + 1 < 9) {
-        if constexpr (sizeof(T) == 2) {
-          load_w(tap + 1, sW0);
-        } else {
-          const float* src = reinterpret_cast<const float*>(Wt) + (long)(tap + 1) * g.Cout * g.CinP;
-          for (int i = tid; i < g.Cout * g.CinP; i += NTHR) {
-            const int co = i / g.CinP, ci = i - co * g.CinP;
-            reinterpret_cast<float*>(sW0)[co * g.PSW + ci] = src[i];
-          }
-        }
-        __syncthreads();
-      }
-    }
-  }
-
-  // epilogue: lane holds pixel x0 + (lane>>4)*4 + r of row y0 + wave*MT + m, channel n*16 + (lane&15)
-#pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const int y = y0 + wave * MT + m;
-    if (y >= g.H) continue;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int x = x0 + (lane >> 4) * 4 + r;
-      if (x >= g.W) continue;
-      const long base = pix_off<OUT_D2S>(b, y, x, g.H, g.W, g.Cout);
-#pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        const int co = n * 16 + (lane & 15);
-        float v = acc[m][n][r];
-        if constexpr (BIAS) v += bias[co];
-        if constexpr (OUT_GGRAD) v *= gelu_grad_f(to_f32(S[base + co]));
-        Y[base + co] = from_f32<T>(v);
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------ bf16 fwd / dgrad, v2
-// Persistent implicit GEMM on v_mfma_f32_32x32x16_bf16 (Cout = 32*NCT, CinP = 16*KS).  One
-// workgroup of NW waves per CU loops over output tiles of NW*MT rows x 32 pixels x all
-// Cout; wave w owns MT image rows.  D[co][pixel] = W_tap[co][ci] * X[ci][pixel]: the weight
-// fragment is the A operand, so each lane ends with 4 consecutive output channels of one
-// pixel (8-B stores).  Everything is register staged:
-//   * weights: a ring of three register sets; W(tap+1) is written to the other LDS buffer
-//     while tap runs (WDB: one barrier per tap; else between two barriers after the tap),
-//     its global load issued three taps earlier;
-//   * halo of the next tile: loaded after tap 0, GELU-converted in registers a third per
-//     tap (waves of the lower half at taps 2-4, the upper half at 5-7: on each SIMD one wave
-//     converts while its partner issues MFMAs), stored to LDS after tap 8;
-//   * dgrad: the pre-activation S of the tile's outputs is prefetched at tap 5 for the
-//     GELU' epilogue.
-// Index math of the halo chunks goes through opaque() so it is recomputed per tile instead
-// of pinning registers for the whole persistent loop.
-MSU_DEV void unpack8(const u32x4& q, float (&v)[8]) {
-  const uint32_t w[4] = {q[0], q[1], q[2], q[3]};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-MSU_DEV uint32_t pack2(float a, float b) {
-  return (uint32_t)from_f32<bf16_t>(a) | ((uint32_t)from_f32<bf16_t>(b) << 16);
-}
-MSU_DEV u32x4 gelu8(const u32x4& q) {
-  float v[8];
-  unpack8(q, v);
-  return u32x4{pack2(gelu_fast(v[0]), gelu_fast(v[1])), pack2(gelu_fast(v[2]), gelu_fast(v[3])),
-               pack2(gelu_fast(v[4]), gelu_fast(v[5])), pack2(gelu_fast(v[6]), gelu_fast(v[7]))};
-}
-
-template <int I> using IC = std::integral_constant<int, I>;
-template <typename F, int... Is>
-MSU_DEV void static_for(F&& f, std::integer_sequence<int, Is...>) {
-  (f(IC<Is>{}), ...);
-}
-
-template <int NCT, int KS, int NW, int MT, bool WDB, bool IN_D2S, bool IN_GELU, bool OUT_D2S, bool OUT_GGRAD,
-          bool BIAS>
-__global__ void __launch_bounds__(64 * NW) conv3x3_v2_kernel(const bf16_t* __restrict__ X,
-                                                         const bf16_t* __restrict__ Wt,
-                                                         const float* __restrict__ bias,
-                                                         const bf16_t* __restrict__ S,
-                                                         bf16_t* __restrict__ Y, ConvGeom g, int ntiles) {
-  constexpr int TH = NW * MT, TWV = 32;
-  constexpr int CinP = KS * 16, Cout = NCT * 32;
-  constexpr int PS = CinP + 8;           // LDS pixel / weight-row stride: conflict-free b128 reads
-  constexpr int CPP = CinP / 8;          // 16-B chunks per pixel
-  constexpr int HWD = TWV + 2;           // halo width
-  constexpr int HPIX = (TH + 2) * HWD;
-  constexpr int HCH = HPIX * CPP;
-  constexpr int NTHR = 64 * NW;
-  constexpr int NHC = (HCH + NTHR - 1) / NTHR;
-  constexpr int WCH = Cout * CPP;
-  constexpr int NWC = (WCH + NTHR - 1) / NTHR;
-  constexpr int WIMG = Cout * PS;        // elements of one LDS weight image
-
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  bf16_t* sX = reinterpret_cast<bf16_t*>(smem_raw);
-  bf16_t* sW = sX + HPIX * PS;           // [WDB ? 2 : 1][Cout][PS]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tiles_x = (g.W + TWV - 1) / TWV, tiles_y = (g.H + TH - 1) / TH;
-  const int per_img = tiles_x * tiles_y;
-
-  u32x4 hr[NHC];
-  u32x4 w0[NWC], w1[NWC], w2[NWC];       // weight register ring (sets picked at compile time)
-  u32x2 sp[OUT_GGRAD ? MT : 1][OUT_GGRAD ? NCT : 1][4];
-
-  auto coords = [&](int tile, int& b, int& y0, int& x0) {
-    b = tile / per_img;
-    const int r = tile - b * per_img;
-    y0 = (r / tiles_x) * TH;
-    x0 = (r - (r / tiles_x) * tiles_x) * TWV;
-  };
-  // branch-free halo load: out-of-image / padding chunks load a clamped in-image address and
-  // are zeroed by a select
-  auto load_halo = [&](int tile) {
-    int b, y0, x0;
-    coords(tile, b, y0, x0);
-    const int t = opaque(tid);
-#pragma unroll
-    for (int c = 0; c < NHC; ++c) {
-      const int i = t + NTHR * c;
-      const int pix = i / CPP, ch = i - (i / CPP) * CPP;
-      const int row = pix / HWD, col = pix - (pix / HWD) * HWD;
-      const int y = y0 - 1 + row, x = x0 - 1 + col;
-      const bool ok = i < HCH && y >= 0 && y < g.H && x >= 0 && x < g.W && ch * 8 < g.Cin;
-      const int yc = min(max(y, 0), g.H - 1), xc = min(max(x, 0), g.W - 1);
-      const int chc = ch * 8 < g.Cin ? ch : 0;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(X + pix_off32<IN_D2S>(b, yc, xc, g.H, g.W, g.Cin) + chc * 8);
-      hr[c] = ok ? v : u32x4{0u, 0u, 0u, 0u};
-    }
-  };
-  auto store_halo = [&]() {
-    const int t = opaque(tid);
-#pragma unroll
-    for (int c = 0; c < NHC; ++c) {
-      const int i = t + NTHR * c;
-      if (HCH % NTHR == 0 || c + 1 < NHC || i < HCH) {
-        const int pix = i / CPP, ch = i - (i / CPP) * CPP;
-        *reinterpret_cast<u32x4*>(sX + pix * PS + ch * 8) = hr[c];
-      }
-    }
-  };
-  auto load_w = [&](int tap, u32x4 (&dst)[NWC]) {
-    const bf16_t* src = Wt + (long)tap * Cout * CinP;
-#pragma unroll
-    for (int c = 0; c < NWC; ++c) {
-      const int i = min(tid + NTHR * c, WCH - 1);
-      dst[c] = *reinterpret_cast<const u32x4*>(src + (long)i * 8);
-    }
-  };
-  auto store_w = [&](const u32x4 (&srcr)[NWC], bf16_t* dst) {
-#pragma unroll
-    for (int c = 0; c < NWC; ++c) {
-      const int i = tid + NTHR * c;
-      if (WCH % NTHR == 0 || c + 1 < NWC || i < WCH) {
-        const int co = i / CPP, ch = i - (i / CPP) * CPP;
-        *reinterpret_cast<u32x4*>(dst + co * PS + ch * 8) = srcr[c];
-      }
-    }
-  };
-  // ring step: write set K to LDS, refill it with W(tap); sets are named, never selected
-  // through a reference, so they stay in registers
-  auto ring = [&](auto K, bf16_t* dst, int tap) {
-    if constexpr (decltype(K)::value == 0) { store_w(w0, dst); load_w(tap, w0); }
-    else if constexpr (decltype(K)::value == 1) { store_w(w1, dst); load_w(tap, w1); }
-    else { store_w(w2, dst); load_w(tap, w2); }
-  };
-  auto out_off = [&](int b, int y, int x, int co) -> int { return pix_off32<OUT_D2S>(b, y, x, g.H, g.W, Cout) + co; };
-
-  int tile = blockIdx.x;
-  if (tile >= ntiles) return;
-  // prologue: halo of the first tile, W(0) in LDS buffer 0, W(1..3) in flight in sets 1, 2, 0
-  load_halo(tile);
-  if constexpr (IN_GELU) {
-#pragma unroll
-    for (int c = 0; c < NHC; ++c) hr[c] = gelu8(hr[c]);
-  }
-  store_halo();
-  load_w(0, w0);
-  store_w(w0, sW);
-  load_w(1, w1);
-  load_w(2, w2);
-  load_w(3, w0);
-  __syncthreads();
-
-  const int xl = lane & 31, kh = 8 * (lane >> 5);
-  int wbuf = 0;
-  for (; tile < ntiles; tile += gridDim.x) {
-    const int next = tile + gridDim.x;
-    int b, y0, x0;
-    coords(tile, b, y0, x0);
-    const int xo = x0 + xl;
-    f32x16 acc[MT][NCT];
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int n = 0; n < NCT; ++n)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
-
-    static_for([&](auto TAP) {
-      constexpr int tap = decltype(TAP)::value;
-      constexpr int dy = tap / 3, dx = tap % 3;
-      const bf16_t* wcur = sW + (WDB ? wbuf * WIMG : 0);
-      if constexpr (WDB) {
-        // W(tap+1) into the other buffer (read during tap-1, released by its barrier)
-        ring(IC<(tap + 1) % 3>{}, sW + (wbuf ^ 1) * WIMG, (tap + 4) % 9);
-      }
-      if constexpr (tap == 0) {
-        if (next < ntiles) load_halo(next);
-      }
-      if constexpr (IN_GELU && tap >= 2 && tap <= 7) {
-        // GELU of the prefetched halo, a third per tap: waves 0..NW/2-1 at taps 2-4, the
-        // others at taps 5-7, so on every SIMD one wave converts while its partner runs MFMAs
-        constexpr int part = (tap - 2) % 3;
-        constexpr int c0 = part * ((NHC + 2) / 3);
-        constexpr int c1 = (c0 + (NHC + 2) / 3) < NHC ? (c0 + (NHC + 2) / 3) : NHC;
-        if ((wave < NW / 2) == (tap <= 4)) {
-#pragma unroll
-          for (int c = c0; c < c1; ++c) hr[c] = gelu8(hr[c]);
-        }
-      }
-      if constexpr (OUT_GGRAD && tap == 5) {
-        if (xo < g.W) {
-#pragma unroll
-          for (int m = 0; m < MT; ++m) {
-            const int y = min(y0 + wave * MT + m, g.H - 1);
-#pragma unroll
-            for (int n = 0; n < NCT; ++n)
-#pragma unroll
-              for (int q = 0; q < 4; ++q)
-                sp[m][n][q] = *reinterpret_cast<const u32x2*>(S + out_off(b, y, xo, 32 * n + 8 * q + 4 * (lane >> 5)));
-          }
-        }
-      }
-      // fragments double buffered in registers: the reads of k-step ks+1 are issued before
-      // the MFMAs of ks; a scheduling fence per k-step keeps the compiler from hoisting more
-      const bf16_t* xb = sX + ((wave * MT + dy) * HWD + dx + xl) * PS + kh;
-      const bf16_t* wb = wcur + xl * PS + kh;
-      bf16x8 xa[2][MT], wf[2][NCT];
-      auto read_frags = [&](int ks, int set) {
-#pragma unroll
-        for (int m = 0; m < MT; ++m) xa[set][m] = *reinterpret_cast<const bf16x8*>(xb + m * HWD * PS + ks * 16);
-#pragma unroll
-        for (int n = 0; n < NCT; ++n) wf[set][n] = *reinterpret_cast<const bf16x8*>(wb + n * 32 * PS + ks * 16);
-      };
-      read_frags(0, 0);
-      static_for([&](auto KSI) {
-        constexpr int ks = decltype(KSI)::value;
-        constexpr int cur = ks & 1;
-        if constexpr (ks + 1 < KS) read_frags(ks + 1, cur ^ 1);
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int n = 0; n < NCT; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[cur][n], xa[cur][m], acc[m][n], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }, std::make_integer_sequence<int, KS>{});
-      __syncthreads();
-      if constexpr (!WDB) {
-        ring(IC<(tap + 1) % 3>{}, sW, (tap + 4) % 9);
-      }
-      if constexpr (tap == 8) {
-        if (next < ntiles) store_halo();
-      }
-      if constexpr (!WDB || tap == 8) __syncthreads();
-      if constexpr (WDB) wbuf ^= 1;
-    }, std::make_integer_sequence<int, 9>{});
-
-    // epilogue: lane holds pixel xo, channels 32n + 8q + 4(lane>>5) + e of its two rows
-    if (xo < g.W) {
-#pragma unroll
-      for (int n = 0; n < NCT; ++n)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int co = 32 * n + 8 * q + 4 * (lane >> 5);
-          float bv[4] = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (BIAS) {
-            const float4 t = *reinterpret_cast<const float4*>(bias + co);
-            bv[0] = t.x; bv[1] = t.y; bv[2] = t.z; bv[3] = t.w;
-          }
-#pragma unroll
-          for (int m = 0; m < MT; ++m) {
-            const int y = y0 + wave * MT + m;
-            if (y >= g.H) continue;
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = acc[m][n][4 * q + e] + bv[e];
-            if constexpr (OUT_GGRAD) {
-              const u32x2 t = sp[m][n][q];
-              const float s[4] = {__uint_as_float(t[0] << 16), __uint_as_float(t[0] & 0xffff0000u),
-                                  __uint_as_float(t[1] << 16), __uint_as_float(t[1] & 0xffff0000u)};
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] *= gelu_grad_fast(s[e]);
-            }
-            *reinterpret_cast<u32x2*>(Y + out_off(b, y, xo, co)) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
-          }
-        }
-    }
-  }
-}
-
-// ------------------------------------------------------------------ wgrad kernel
-// dW[dy][co][dx][ci] partial per block: sum over the block's pixel tiles of
-//   DY[pixel][co] * Xt[pixel + (dy-1, dx-1)][ci];  one block = one dy, NT waves (one per
-//   co tile), each wave 3 * CinP/16 n-tiles.  dbias partial from the dy == 0 blocks.
-
-template <typename T, int NT, int NTI, int TH, bool IN_D2S, bool IN_GELU>
-__global__ void __launch_bounds__(64 * NT) conv3x3_wgrad_kernel(const T* __restrict__ X,
-                                                                const T* __restrict__ DY,
-                                                                float* __restrict__ part,
-                                                                float* __restrict__ dbpart,
-                                                                ConvGeom g, int nchunk) {
-  // NT = Cout/16 (waves), NTI = CinP/16 (ci tiles per dx)
-  constexpr int NTHR = 64 * NT;
-  constexpr int NPIX = TH * TW;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  T* sX = reinterpret_cast<T*>(smem_raw);         // [TH][TW+2][PS]
-  T* sD = sX + TH * (TW + 2) * g.PS;              // [NPIX][PSD]   (PSD = Cout + pad)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int w = xcd_remap(blockIdx.x, gridDim.x);
-  const int dy = w % 3, chunk = w / 3;
-  const int tiles_x = (g.W + TW - 1) / TW, tiles_y = (g.H + TH - 1) / TH;
-  const long ntiles = (long)g.B * tiles_x * tiles_y;
-
-  f32x4 acc[3][NTI];
-#pragma unroll
-  for (int d = 0; d < 3; ++d)
-#pragma unroll
-    for (int n = 0; n < NTI; ++n) acc[d][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float dbacc = 0.f;
-
-  for (long tile = chunk; tile < ntiles; tile += nchunk) {
-    const int b = (int)(tile / ((long)tiles_x * tiles_y));
-    const int trem = (int)(tile - (long)b * tiles_x * tiles_y);
-    const int y0 = (trem / tiles_x) * TH, x0 = (trem % tiles_x) * TW;
-    __syncthreads();
-    stage_halo<T, IN_D2S, IN_GELU>(X, sX, b, y0 + dy - 1, TH, x0, g, tid, NTHR);
-    // dY tile [NPIX][Cout]: rows outside the image are zero
-    {
-      const int cpp = g.Cout / 8;
-      for (int i = tid; i < NPIX * cpp; i += NTHR) {
-        const int pix = i / cpp, ch = i - pix * cpp;
-        const int y = y0 + pix / TW, x = x0 + pix % TW;
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = 0.f;
-        if (y < g.H && x < g.W) {
-          const T* p = DY + (((long)b * g.H + y) * g.W + x) * g.Cout + ch * 8;
-          float a[4], c[4];
-          Vec4<T>::load(p, a);
-          Vec4<T>::load(p + 4, c);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[4 + e] = c[e]; }
-        }
-        float lo[4] = {v[0], v[1], v[2], v[3]}, hi[4] = {v[4], v[5], v[6], v[7]};
-        Vec4<T>::store(sD + pix * g.PSD + ch * 8, lo);
-        Vec4<T>::store(sD + pix * g.PSD + ch * 8 + 4, hi);
-      }
-    }
-    __syncthreads();
-    if (dy == 0 && tid < g.Cout) {
-      for (int p = 0; p < NPIX; ++p) dbacc += to_f32(sD[p * g.PSD + tid]);
-    }
-    auto rowA = [&](int k) { return sD + k * g.PSD; };
-#pragma unroll
-    for (int ks = 0; ks < NPIX / 32; ++ks) {
-#pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        auto rowB = [&](int k) { return sX + ((k / TW) * (TW + 2) + (k % TW) + d) * g.PS; };
-#pragma unroll
-        for (int n = 0; n < NTI; ++n)
-          TR<T>::mma(acc[d][n], rowA, wave * 16, rowB, n * 16, ks * 32, lane);
-      }
-    }
-  }
-  // partial [blk][dy][co][dx][ci]   (co = wave*16 + row, ci = n*16 + (lane&15))
-  float* out = part + ((long)chunk * 3 + dy) * (long)g.Cout * 3 * g.CinP;
-#pragma unroll
-  for (int d = 0; d < 3; ++d)
-#pragma unroll
-    for (int n = 0; n < NTI; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = wave * 16 + (lane >> 4) * 4 + r;
-        const int ci = n * 16 + (lane & 15);
-        out[((long)co * 3 + d) * g.CinP + ci] = acc[d][n][r];
-      }
-  if (dy == 0 && tid < g.Cout) dbpart[(long)chunk * g.Cout + tid] = dbacc;
-}
-
-// ------------------------------------------------------------------ bf16 wgrad, v2
-// Persistent weight gradient for CinP = Cout = 96 on v_mfma_f32_16x16x32_bf16.  One
-// 12-wave workgroup per CU (3 waves per SIMD) owns all 9 x 96 x 96 accumulators for its
-// share of the pixels: wave w = (dy = w/4, co half, ci half) holds 3 dx x 3 co-tiles x
-// 3 ci-tiles = 27 16x16 tiles (108 registers).  Per pixel tile (4 rows x 32 pixels) the
-// input halo [(4+2) x 34][ci] and the dY tile [128][co] sit in LDS (pixel stride 104
-// elements); both operands are read k-strided (k = pixels) with ds_read_b64_tr_b16.
-// Staging is LDS-DMA (global_load_lds_dwordx4) into the other of two LDS buffers while the
-// current tile is multiplied: the image is 13 16-B slots per pixel (12 data + 1 pad) filled
-// lane-linearly; pad slots and out-of-image pixels read a 16-B zero block.  After its own
-// DMAs land (vmcnt), each wave GELU-converts the halo slots it wrote, in place, so no
-// registers are held across the tile and no extra barrier is needed.
-// Partials: [block][dy][co][dx][ci] + db [block][co], the layout wgrad_reduce_kernel sums.
-template <bool IN_D2S, bool IN_GELU>
-__global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __restrict__ X,
-                                                               const bf16_t* __restrict__ DY,
-                                                               float* __restrict__ part,
-                                                               float* __restrict__ dbpart, ConvGeom g,
-                                                               int ntiles) {
-  constexpr int C = 96, TH = 4, TWV = 32, NW = 12;
-  constexpr int PS = C + 8;                  // LDS pixel stride (both images), 13 slots
-  constexpr int SLOTS = PS / 8;
-  constexpr int HWD = TWV + 2;
-  constexpr int HPIX = (TH + 2) * HWD;       // 204 halo pixels
-  constexpr int DPIX = TH * TWV;             // 128 dY pixels
-  constexpr int NSLOT = (HPIX + DPIX) * SLOTS;
-  constexpr int NINS = (NSLOT + 63) / 64;    // DMA wave-instructions per tile
-  constexpr int PER_WAVE = (NINS + NW - 1) / NW;
-  constexpr int BUF = NINS * 64 * 8;         // elements per LDS buffer (covers the overrun)
-  typedef __attribute__((address_space(3))) void lds_void;
-  typedef __attribute__((address_space(1))) void glb_void;
-
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  bf16_t* lds = reinterpret_cast<bf16_t*>(smem_raw);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int dy = wave >> 2, coh = (wave >> 1) & 1, cih = wave & 1;
-  const int tiles_x = (g.W + TWV - 1) / TWV, tiles_y = (g.H + TH - 1) / TH;
-  const int per_img = tiles_x * tiles_y;
-
-  auto coords = [&](int tile, int& b, int& y0, int& x0) {
-    b = tile / per_img;
-    const int r = tile - b * per_img;
-    y0 = (r / tiles_x) * TH;
-    x0 = (r - (r / tiles_x) * tiles_x) * TWV;
-  };
-  // issue this wave's DMAs of tile `tile` into buffer `buf`
-  auto stage = [&](int tile, int buf) __attribute__((always_inline)) {
-    int b, y0, x0;
-    coords(tile, b, y0, x0);
-    const int ln = opaque(lane);
-#pragma unroll
-    for (int r = 0; r < PER_WAVE; ++r) {
-      const int k = wave + NW * r;
-      if (k < NINS) {
-        const int s = 64 * k + ln;
-        const int pix = s / SLOTS, ch0 = s - (s / SLOTS) * SLOTS;
-        const int ch = ch0 < SLOTS - 1 ? ch0 : 0;  // pad slot: re-read chunk 0 of the pixel
-        const void* src = zero_src(s);
-        if (pix < HPIX) {
-          const int row = pix / HWD, col = pix - (pix / HWD) * HWD;
-          const int y = y0 - 1 + row, x = x0 - 1 + col;
-          if (y >= 0 && y < g.H && x >= 0 && x < g.W) src = X + pix_off32<IN_D2S>(b, y, x, g.H, g.W, C) + ch * 8;
-        } else if (pix < HPIX + DPIX) {
-          const int dp = pix - HPIX;
-          const int y = y0 + dp / TWV, x = x0 + dp % TWV;
-          if (y < g.H && x < g.W) src = DY + pix_off32<false>(b, y, x, g.H, g.W, C) + ch * 8;
-        }
-        __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(lds + buf * BUF + 64 * 8 * k), 16, 0, 0);
-      }
-    }
-  };
-  // after this wave's DMAs landed: GELU the halo slots it wrote, in place
-  auto gelu_own = [&](int buf) __attribute__((always_inline)) {
-    if constexpr (IN_GELU) {
-      const int ln = opaque(lane);
-#pragma unroll
-      for (int r = 0; r < PER_WAVE; ++r) {
-        const int k = wave + NW * r;
-        const int s = 64 * k + ln;
-        if (k < NINS && s / SLOTS < HPIX && s % SLOTS < SLOTS - 1) {
-          u32x4* p = reinterpret_cast<u32x4*>(lds + buf * BUF + 8 * s);
-          *p = gelu8(*p);
-        }
-      }
-    }
-  };
-
-  f32x4 acc[3][3][3];  // [dx][co tile][ci tile]
-#pragma unroll
-  for (int d = 0; d < 3; ++d)
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) acc[d][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float dbacc[2] = {0.f, 0.f};
-  const int dbc = 2 * (tid % 48), dbg = tid / 48;  // channel pair, pixel group (16 groups)
-
-  int tile = blockIdx.x;
-  int cur = 0;
-  if (tile < ntiles) {
-    stage(tile, 0);
-    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) & lgkmcnt(0)
-    gelu_own(0);
-  }
-  __syncthreads();
-  for (; tile < ntiles; tile += gridDim.x) {
-    const int next = tile + gridDim.x;
-    if (next < ntiles) stage(next, cur ^ 1);
-    const bf16_t* sX = lds + cur * BUF;
-    const bf16_t* sD = sX + HPIX * PS;
-    // All LDS reads of the tile are untracked (inline asm): a compiler-visible ds_read would
-    // be preceded by vmcnt(0) for the next tile's pending LDS-DMA and serialise the two.
-    // bias gradient: 16 groups x 48 channel pairs, 8 pixels each
-    {
-      const uint32_t ba = lds_u32(sD + dbg * PS + dbc);
-      uint32_t v[DPIX / 16];
-      unroll_for<DPIX / 16>([&](auto P) {
-        v[decltype(P)::value] = ds_b32_untracked<2 * 16 * PS * decltype(P)::value>(ba);
-      });
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int p = 0; p < DPIX / 16; ++p) {
-        vreg_pin(v[p]);
-        dbacc[0] += __uint_as_float(v[p] << 16);
-        dbacc[1] += __uint_as_float(v[p] & 0xffff0000u);
-      }
-    }
-    // lane part of a k-strided fragment read: pixels 2(4g + q) + half (+16 for the second
-    // half of the fragment), g = lane group within the 32-lane half, q = (lane&15)>>2,
-    // columns 4(lane&3); everything else is an immediate offset.  Same pixel order for both
-    // operands; pixels of one parity sit 104 * 2j B apart: distinct 32-B bank spans, so each
-    // half's 32 lanes hit all 64 banks once (pixels 8(lane>>4) + q: 2-way conflicts).
-    const int laneoff = opaque((2 * (4 * ((lane >> 4) & 1) + ((lane & 15) >> 2)) + (lane >> 5)) * PS + 4 * (lane & 3));
-    const uint32_t xa = lds_u32(sX + laneoff + dy * HWD * PS + 48 * cih);
-    const uint32_t da = lds_u32(sD + laneoff + 48 * coh);
-    unroll_for<TH>([&](auto R) {
-      unroll_for<3>([&](auto D) {
-        constexpr int r = decltype(R)::value, d = decltype(D)::value;
-        bf16x8 bf[3], af[3];
-        unroll_for<3>([&](auto J) {
-          constexpr int o = 2 * ((r * HWD + d) * PS + 16 * decltype(J)::value);
-          bf[decltype(J)::value] = tr8_untracked<o, o + 32 * PS>(xa);
-        });
-        unroll_for<3>([&](auto I) {
-          constexpr int o = 2 * (r * TWV * PS + 16 * decltype(I)::value);
-          af[decltype(I)::value] = tr8_untracked<o, o + 32 * PS>(da);
-        });
-        lds_wait_tie<0>(bf[0], bf[1], bf[2], af[0], af[1], af[2]);
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j)
-            acc[d][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[d][i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      });
-    });
-    if (next < ntiles) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      gelu_own(cur ^ 1);
-    }
-    __syncthreads();
-    cur ^= 1;
-  }
-  // partial [blk][dy][co][dx][ci]: lane holds co = co0 + 4(lane>>4) + r, ci = ci0 + (lane&15)
-  float* out = part + ((long)blockIdx.x * 3 + dy) * (long)C * 3 * C;
-#pragma unroll
-  for (int d = 0; d < 3; ++d)
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = 48 * coh + 16 * i + 4 * (lane >> 4) + r;
-          const int ci = 48 * cih + 16 * j + (lane & 15);
-          out[((long)co * 3 + d) * C + ci] = acc[d][i][j][r];
-        }
-  // bias partial: reduce the 16 pixel groups through LDS
-  float* red = reinterpret_cast<float*>(smem_raw);
-  __syncthreads();
-  red[dbg * C + dbc] = dbacc[0];
-  red[dbg * C + dbc + 1] = dbacc[1];
-  __syncthreads();
-  if (tid < C) {
-    float sum = 0.f;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) sum += red[q * C + tid];
-    dbpart[(long)blockIdx.x * C + tid] = sum;
-  }
-}
-
-// sum partials -> dW[co][ci][3][3] (torch Conv2d layout) and db[co]
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* part, const float* dbpart,
-                                                           int nchunk, int Cout, int Cin, int CinP,
-                                                           float* dW, float* db) {
-  const long n = (long)Cout * Cin * 9;
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) {
-    const int co = (int)(i / (Cin * 9));
-    const int rem = (int)(i - (long)co * Cin * 9);
-    const int ci = rem / 9, tap = rem % 9, dy = tap / 3, dx = tap % 3;
-    const long slab = (long)Cout * 3 * CinP;
-    float s = 0.f;
-    for (int c = 0; c < nchunk; ++c)
-      s += part[((long)c * 3 + dy) * slab + ((long)co * 3 + dx) * CinP + ci];
-    dW[i] = s;
-  }
-  if (db && i < Cout) {
-    float s = 0.f;
-    for (int c = 0; c < nchunk; ++c) s += dbpart[(long)c * Cout + i];
-    db[i] = s;
-  }
-}
-
-// ------------------------------------------------------------------ host dispatch
-ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int elem_bytes) {
-  ConvGeom g;
-  g.B = B; g.H = H; g.W = W; g.Cin = Cin; g.Cout = Cout;
-  g.CinP = (Cin + 31) / 32 * 32;
-  const int pad = elem_bytes == 2 ? 8 : 4;
-  g.PS = g.CinP + pad;
-  g.PSW = g.CinP + pad;
-  g.PSD = Cout + pad;
-  return g;
-}
-
-template <typename T, int NT, bool IN_D2S, bool IN_GELU, bool OUT_D2S, bool OUT_GGRAD, bool BIAS>
-int launch_conv(const ConvGeom& g, const T* X, const T* Wt, const float* bias, const T* S, T* Y,
-                hipStream_t st) {
-  constexpr bool BF = sizeof(T) == 2;
-  constexpr int TH = BF ? 16 : 4;
-  constexpr int MT = BF ? 2 : 1;
-  constexpr int NW = TH / MT;
-  const size_t lds = sizeof(T) * ((size_t)(TH + 2) * (TW + 2) * g.PS + (size_t)(BF ? 2 : 1) * g.Cout * g.PSW);
-  if (lds > 160 * 1024) return -4;
-  auto kern = conv3x3_kernel<T, NT, TH, MT, BF, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
-  const long ntiles = (long)g.B * ((g.W + TW - 1) / TW) * ((g.H + TH - 1) / TH);
-  if (ntiles == 0) return 0;
-  hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(64 * NW), lds, st, X, Wt, bias, S, Y, g);
-  return MSU_CHECK_LAUNCH();
-}
-
-int num_cus() {
-  static int n = 0;
-  if (n <= 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  }
-  return n;
-}
-
-template <int NCT, int KS, int NW, int MT, bool WDB, bool IN_D2S, bool IN_GELU, bool OUT_D2S, bool OUT_GGRAD,
-          bool BIAS>
-int launch_v2(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S,
-              bf16_t* Y, hipStream_t st) {
-  constexpr int PS = KS * 16 + 8, TH = NW * MT;
-  constexpr size_t lds = sizeof(bf16_t) * ((size_t)(TH + 2) * 34 * PS + (WDB ? 2 : 1) * (size_t)NCT * 32 * PS);
-  static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = conv3x3_v2_kernel<NCT, KS, NW, MT, WDB, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
-  const long ntiles = (long)g.B * ((g.W + 31) / 32) * ((g.H + TH - 1) / TH);
-  if (ntiles == 0) return 0;
-  // 32-bit element offsets inside the kernel
-  if ((long)g.B * g.H * g.W * (g.Cin > g.Cout ? g.Cin : g.Cout) >= (1L << 31)) return -2;
-  const int grid = (int)(ntiles < num_cus() ? ntiles : num_cus());
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), lds, st, X, Wt, bias, S, Y, g, (int)ntiles);
-  return MSU_CHECK_LAUNCH();
-}
-
-template <typename T, bool IN_D2S, bool IN_GELU, bool OUT_D2S, bool OUT_GGRAD, bool BIAS>
-int conv_nt(const ConvGeom& g, const void* X, const void* Wt, const float* bias, const void* S,
-            void* Y, hipStream_t st) {
-  const T* x = (const T*)X; const T* w = (const T*)Wt; const T* s = (const T*)S; T* y = (T*)Y;
-  if constexpr (sizeof(T) == 2) {
-    // the Swin-T/S decoder head width takes the persistent v2 kernel
-    if (g.Cout == 96 && g.CinP == 96)
-      return launch_v2<3, 6, 8, 1, true, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS>(g, x, w, bias, s, y, st);
-  }
-  switch (g.Cout / 16) {
-    case 1: return launch_conv<T, 1, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS>(g, x, w, bias, s, y, st);
-    case 2: return launch_conv<T, 2, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS>(g, x, w, bias, s, y, st);
-    case 4: return launch_conv<T, 4, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS>(g, x, w, bias, s, y, st);
-    case 6: return launch_conv<T, 6, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS>(g, x, w, bias, s, y, st);
-    case 8: return launch_conv<T, 8, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS>(g, x, w, bias, s, y, st);
-  }
-  return -2;
-}
-
-template <typename T, int NT, bool IN_D2S, bool IN_GELU>
-int launch_wgrad_nti(const ConvGeom& g, const T* X, const T* DY, float* part, float* dbpart,
-                     int nchunk, hipStream_t st) {
-  constexpr int TH = 8;
-  const size_t lds = sizeof(T) * ((size_t)TH * (TW + 2) * g.PS + (size_t)TH * TW * g.PSD);
-  if (lds > 160 * 1024) return -4;
-  auto go = [&](auto kern) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(nchunk * 3)), dim3(64 * NT), lds, st, X, DY, part, dbpart, g, nchunk);
-    return MSU_CHECK_LAUNCH();
-  };
-  switch (g.CinP / 16) {
-    case 2: return go(conv3x3_wgrad_kernel<T, NT, 2, TH, IN_D2S, IN_GELU>);
-    case 4: return go(conv3x3_wgrad_kernel<T, NT, 4, TH, IN_D2S, IN_GELU>);
-    case 6: return go(conv3x3_wgrad_kernel<T, NT, 6, TH, IN_D2S, IN_GELU>);
-    case 8: return go(conv3x3_wgrad_kernel<T, NT, 8, TH, IN_D2S, IN_GELU>);
-  }
-  return -2;
-}
-
-template <bool IN_D2S, bool IN_GELU>
-int launch_wgrad_v2(const ConvGeom& g, const bf16_t* X, const bf16_t* DY, float* part, float* dbpart,
-                    int nblocks, hipStream_t st) {
-  constexpr int nins = ((6 * 34 + 4 * 32) * 13 + 63) / 64;
-  constexpr size_t lds = 2 * sizeof(bf16_t) * (size_t)nins * 64 * 8;
-  static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = conv3x3_wgrad_v2_kernel<IN_D2S, IN_GELU>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
-  if ((long)g.B * g.H * g.W * 96 >= (1L << 31)) return -2;
-  const long ntiles = (long)g.B * ((g.W + 31) / 32) * ((g.H + 3) / 4);
-  // every block writes its partial slabs, even with no tile (zeros)
-  hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(768), lds, st, X, DY, part, dbpart, g, (int)ntiles);
-  return MSU_CHECK_LAUNCH();
-}
-
-template <typename T, bool IN_D2S, bool IN_GELU>
-int wgrad_nt(const ConvGeom& g, const void* X, const void* DY, float* part, float* dbpart,
-             int nchunk, hipStream_t st) {
-  const T* x = (const T*)X; const T* d = (const T*)DY;
-  switch (g.Cout / 16) {
-    case 1: return launch_wgrad_nti<T, 1, IN_D2S, IN_GELU>(g, x, d, part, dbpart, nchunk, st);
-    case 2: return launch_wgrad_nti<T, 2, IN_D2S, IN_GELU>(g, x, d, part, dbpart, nchunk, st);
-    case 4: return launch_wgrad_nti<T, 4, IN_D2S, IN_GELU>(g, x, d, part, dbpart, nchunk, st);
-    case 6: return launch_wgrad_nti<T, 6, IN_D2S, IN_GELU>(g, x, d, part, dbpart, nchunk, st);
-    case 8: return launch_wgrad_nti<T, 8, IN_D2S, IN_GELU>(g, x, d, part, dbpart, nchunk, st);
-  }
-  return -2;
-}
-
-}  // namespace
+// Refine-conv forward and backward-data entry points (kernels: conv3x3.h).
+#include "conv3x3.h"
 
 extern "C" {
 
 // in_mode bit 0: GELU on the loaded input, bit 1: input is the pre-d2s [B,H/4,W/4,16*Cin]
 // tensor.  Wt: [9][Cout][CinP] (CinP = roundup(Cin, 32), zero padded), dtype of X.
-int msu_conv3x3_fwd(int dtype, int in_mode, const void* X, const void* Wt, const float* bias,
-                    void* Y, int B, int H, int W, int Cin, int Cout, void* stream) {
+// Y2 (may be null, only without GELU on load): GELU(Y) written by the same epilogue.
+int msu_conv3x3_fwd2(int dtype, int in_mode, const void* X, const void* Wt, const float* bias,
+                     void* Y, void* Y2, int B, int H, int W, int Cin, int Cout, void* stream) {
   if (Cout % 16 || Cin % 8 || Cout > 128 || Cin > 128) return -2;
   if ((in_mode & 2) && (H % 4 || W % 4)) return -2;
+  if (Y2 && (in_mode & 1)) return -2;
   const ConvGeom g = make_geom(B, H, W, Cin, Cout, dtype == MSU_BF16 ? 2 : 4);
   hipStream_t st = (hipStream_t)stream;
   if (bias == nullptr) return -2;
-#define MSU_FWD(T, D2S, GL) return conv_nt<T, D2S, GL, false, false, true>(g, X, Wt, bias, nullptr, Y, st)
-  // instantiated modes: GELU on load (the refine convs' inputs are always GELU outputs)
-  if (dtype == MSU_BF16) {
-    switch (in_mode & 3) {
-      case 1: MSU_FWD(bf16_t, false, true);
-      case 3: MSU_FWD(bf16_t, true, true);
-    }
-  } else {
-    switch (in_mode & 3) {
-      case 1: MSU_FWD(float, false, true);
-      case 3: MSU_FWD(float, true, true);
-    }
+#define MSU_FWD(T, D2S, GL, DU) return conv_nt<T, D2S, GL, false, false, true, DU>(g, X, Wt, bias, nullptr, Y, Y2, st)
+#define MSU_FWD_ALL(T)                              \
+  switch ((in_mode & 3) | (Y2 ? 4 : 0)) {           \
+    case 0: MSU_FWD(T, false, false, false);        \
+    case 1: MSU_FWD(T, false, true, false);         \
+    case 2: MSU_FWD(T, true, false, false);         \
+    case 3: MSU_FWD(T, true, true, false);          \
+    case 4: MSU_FWD(T, false, false, true);         \
+    case 6: MSU_FWD(T, true, false, true);          \
   }
+  if (dtype == MSU_BF16) {
+    MSU_FWD_ALL(bf16_t)
+  } else {
+    MSU_FWD_ALL(float)
+  }
+#undef MSU_FWD_ALL
 #undef MSU_FWD
   return -3;
+}
+
+int msu_conv3x3_fwd(int dtype, int in_mode, const void* X, const void* Wt, const float* bias,
+                    void* Y, int B, int H, int W, int Cin, int Cout, void* stream) {
+  return msu_conv3x3_fwd2(dtype, in_mode, X, Wt, bias, Y, nullptr, B, H, W, Cin, Cout, stream);
 }
 
 // dX = (conv(dY, Wflip) * GELU'(S)) scattered through the input map.  Wflip: [9][Cin][CoutP]
@@ -972,7 +49,7 @@ int msu_conv3x3_dgrad(int dtype, int out_mode, const void* dY, const void* Wflip
   if ((out_mode & 2) && (H % 4 || W % 4)) return -2;
   const ConvGeom g = make_geom(B, H, W, Cout, Cin, dtype == MSU_BF16 ? 2 : 4);
   hipStream_t st = (hipStream_t)stream;
-#define MSU_DG(T, D2S, GG) return conv_nt<T, false, false, D2S, GG, false>(g, dY, Wflip, nullptr, S, dX, st)
+#define MSU_DG(T, D2S, GG) return conv_nt<T, false, false, D2S, GG, false>(g, dY, Wflip, nullptr, S, dX, nullptr, st)
   if (dtype == MSU_BF16) {
     switch (out_mode & 3) {
       case 1: MSU_DG(bf16_t, false, true);
@@ -986,47 +63,6 @@ int msu_conv3x3_dgrad(int dtype, int out_mode, const void* dY, const void* Wflip
   }
 #undef MSU_DG
   return -3;
-}
-
-long msu_conv3x3_wgrad_workspace(int nchunk, int Cin, int Cout, int dtype, int unused) {
-  (void)dtype; (void)unused;
-  const int CinP = (Cin + 31) / 32 * 32;
-  return (long)nchunk * 3 * Cout * 3 * CinP + (long)nchunk * Cout;
-}
-
-// dW [Cout][Cin][3][3] f32 and db [Cout] f32 (db may be null).  in_mode as in fwd.
-int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, float* dW, float* db,
-                      float* workspace, void* unused, int nchunk, int B, int H, int W, int Cin,
-                      int Cout, void* stream) {
-  (void)unused;
-  if (Cout % 16 || Cin % 8 || Cout > 128 || Cin > 128 || nchunk < 1) return -2;
-  const ConvGeom g = make_geom(B, H, W, Cin, Cout, dtype == MSU_BF16 ? 2 : 4);
-  hipStream_t st = (hipStream_t)stream;
-  float* part = workspace;
-  float* dbpart = workspace + (long)nchunk * 3 * Cout * 3 * g.CinP;
-  int rc = -3;
-#define MSU_WG(T, D2S, GL) rc = wgrad_nt<T, D2S, GL>(g, X, dY, part, dbpart, nchunk, st)
-  if (dtype == MSU_BF16 && Cin == 96 && Cout == 96) {
-    rc = (in_mode & 3) == 3 ? launch_wgrad_v2<true, true>(g, (const bf16_t*)X, (const bf16_t*)dY, part, dbpart, nchunk, st)
-       : (in_mode & 3) == 1 ? launch_wgrad_v2<false, true>(g, (const bf16_t*)X, (const bf16_t*)dY, part, dbpart, nchunk, st)
-                            : -3;
-  } else if (dtype == MSU_BF16) {
-    switch (in_mode & 3) {
-      case 1: MSU_WG(bf16_t, false, true); break;
-      case 3: MSU_WG(bf16_t, true, true); break;
-    }
-  } else {
-    switch (in_mode & 3) {
-      case 1: MSU_WG(float, false, true); break;
-      case 3: MSU_WG(float, true, true); break;
-    }
-  }
-#undef MSU_WG
-  if (rc) return rc;
-  const long n = (long)Cout * Cin * 9;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part,
-                     dbpart, nchunk, Cout, Cin, g.CinP, dW, db);
-  return MSU_CHECK_LAUNCH();
 }
 
 }  // extern "C"

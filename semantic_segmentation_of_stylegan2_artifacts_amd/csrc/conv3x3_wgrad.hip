@@ -1,0 +1,55 @@
+// Refine-conv weight-gradient entry points (kernels: conv3x3.h).
+#include "conv3x3.h"
+
+extern "C" {
+
+long msu_conv3x3_wgrad_workspace(int nchunk, int Cin, int Cout, int dtype, int unused) {
+  (void)dtype; (void)unused;
+  const int CinP = (Cin + 31) / 32 * 32;
+  return (long)nchunk * 3 * Cout * 3 * CinP + (long)nchunk * Cout;
+}
+
+// dW [Cout][Cin][3][3] f32 and db [Cout] f32 (db may be null).  in_mode as in fwd.
+int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, float* dW, float* db,
+                      float* workspace, void* unused, int nchunk, int B, int H, int W, int Cin,
+                      int Cout, void* stream) {
+  (void)unused;
+  if (Cout % 16 || Cin % 8 || Cout > 128 || Cin > 128 || nchunk < 1) return -2;
+  const ConvGeom g = make_geom(B, H, W, Cin, Cout, dtype == MSU_BF16 ? 2 : 4);
+  hipStream_t st = (hipStream_t)stream;
+  float* part = workspace;
+  float* dbpart = workspace + (long)nchunk * 3 * Cout * 3 * g.CinP;
+  int rc = -3;
+#define MSU_WG(T, D2S, GL) rc = wgrad_nt<T, D2S, GL>(g, X, dY, part, dbpart, nchunk, st)
+  if (dtype == MSU_BF16 && Cin == 96 && Cout == 96) {
+    const bf16_t* x = (const bf16_t*)X; const bf16_t* d = (const bf16_t*)dY;
+    switch (in_mode & 3) {
+      case 0: rc = launch_wgrad_v2<false, false>(g, x, d, part, dbpart, nchunk, st); break;
+      case 1: rc = launch_wgrad_v2<false, true>(g, x, d, part, dbpart, nchunk, st); break;
+      case 2: rc = launch_wgrad_v2<true, false>(g, x, d, part, dbpart, nchunk, st); break;
+      case 3: rc = launch_wgrad_v2<true, true>(g, x, d, part, dbpart, nchunk, st); break;
+    }
+  } else if (dtype == MSU_BF16) {
+    switch (in_mode & 3) {
+      case 0: MSU_WG(bf16_t, false, false); break;
+      case 1: MSU_WG(bf16_t, false, true); break;
+      case 2: MSU_WG(bf16_t, true, false); break;
+      case 3: MSU_WG(bf16_t, true, true); break;
+    }
+  } else {
+    switch (in_mode & 3) {
+      case 0: MSU_WG(float, false, false); break;
+      case 1: MSU_WG(float, false, true); break;
+      case 2: MSU_WG(float, true, false); break;
+      case 3: MSU_WG(float, true, true); break;
+    }
+  }
+#undef MSU_WG
+  if (rc) return rc;
+  const long n = (long)Cout * Cin * 9;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part,
+                     dbpart, nchunk, Cout, Cin, g.CinP, dW, db);
+  return MSU_CHECK_LAUNCH();
+}
+
+}  // extern "C"

@@ -294,7 +294,8 @@ class PatchExpand(nn.Module):
 
 class FinalPatchExpand_X4_V2(nn.Module):
     """``model_parts.py:437-476``: Linear(C, 16C) -> GELU -> d2s 4x4 -> conv3x3+b -> GELU ->
-    conv3x3+b -> LN(C).  d2s/GELU are fused into the conv loads (no NCHW permutes)."""
+    conv3x3+b -> LN(C).  d2s is folded into refine1's loads (no NCHW permutes); each GELU
+    output is stored by its producer's epilogue next to the pre-activation."""
 
     def __init__(self, input_resolution, dim, dim_scale=4, norm_layer=nn.LayerNorm):
         super().__init__()
@@ -315,9 +316,12 @@ class FinalPatchExpand_X4_V2(nn.Module):
         H, W = self.input_resolution
         B, L, C = x.shape
         assert L == H * W, "input feature has wrong size"
-        e = ops.linear(x, self.expand.weight).view(B, H, W, 16 * C)
-        z1 = ops.refine_conv(e, self.refine1.weight, self.refine1.bias, True, (4 * H, 4 * W))
-        return ops.refine_conv(z1, self.refine2.weight, self.refine2.bias, False, (4 * H, 4 * W))
+        # expand's epilogue also stores act(e) and refine1's also stores act(z1): each conv
+        # loads its activation, while the dgrad epilogues apply act' to e / z1
+        e, a0 = ops.linear_gelu(x, self.expand.weight)
+        e, a0 = e.view(B, H, W, 16 * C), a0.view(B, H, W, 16 * C)
+        z1, a1 = ops.refine_conv_act(e, a0, self.refine1.weight, self.refine1.bias, True, (4 * H, 4 * W), dual=True)
+        return ops.refine_conv_act(z1, a1, self.refine2.weight, self.refine2.bias, False, (4 * H, 4 * W))
 
     def forward(self, x):
         z2 = self.pre_norm(x)

@@ -656,6 +656,115 @@ def refine_conv(x, weight, bias, d2s, out_hw):
     return _RefineConv.apply(_as(x, act_dtype()), _f32(weight), _f32(bias), bool(d2s), tuple(out_hw))
 
 
+class _RefineConvAct(torch.autograd.Function):
+    """z = conv3x3(a, W) + b with a = GELU(map(x)) already materialised by the producer
+    (x: the differentiable pre-activation, a: its activation, non-differentiable).  The
+    conv loads a as is (no GELU on its halo); the input gradient still applies GELU'(x)
+    in the dgrad epilogue, the weight gradient reads a.  dual: also returns GELU(z) from
+    the same epilogue (the next refine conv's input)."""
+
+    @staticmethod
+    def forward(ctx, x, a, weight, bias, d2s, out_hw, dual):
+        _need_cuda(x, a)
+        a = a.contiguous()
+        Cout, Cin = weight.shape[0], weight.shape[1]
+        B = a.shape[0]
+        H, W = out_hw
+        dt = a.dtype
+        wt = _pad_to(weight.permute(2, 3, 0, 1).reshape(9, Cout, Cin), 2, 32).to(dt).contiguous()
+        z = torch.empty(B, H, W, Cout, device=a.device, dtype=dt)
+        z2 = torch.empty_like(z) if dual else None
+        _lib.call("msu_conv3x3_fwd2", _dt(a), 2 if d2s else 0, _p(a), _p(wt), _p(bias), _p(z), _p(z2),
+                  B, H, W, Cin, Cout, _s(a))
+        ctx.save_for_backward(x, a, weight)
+        ctx.cfg = (d2s, H, W)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for GELU(z)
+        if dual:
+            ctx.mark_non_differentiable(z2)
+            return z, z2
+        return z
+
+    @staticmethod
+    def backward(ctx, dz, *unused):
+        x, a, weight = ctx.saved_tensors
+        d2s, H, W = ctx.cfg
+        Cout, Cin = weight.shape[0], weight.shape[1]
+        B = a.shape[0]
+        dz = _as(dz, a.dtype)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wf = _pad_to(weight.flip(2, 3).permute(2, 3, 1, 0).reshape(9, Cin, Cout), 2, 32)
+            wf = wf.to(a.dtype).contiguous()
+            dx = torch.empty_like(x)
+            _lib.call("msu_conv3x3_dgrad", _dt(a), 1 | (2 if d2s else 0), _p(dz), _p(wf), _p(x), _p(dx),
+                      B, H, W, Cin, Cout, _s(a))
+        L = _lib.lib()
+        nchunk = 256
+        ws = torch.empty(L.msu_conv3x3_wgrad_workspace(nchunk, Cin, Cout, 0, 0), device=a.device,
+                         dtype=torch.float32)
+        dw = torch.empty(Cout, Cin, 3, 3, device=a.device, dtype=torch.float32)
+        db = torch.empty(Cout, device=a.device, dtype=torch.float32)
+        _lib.call("msu_conv3x3_wgrad", _dt(a), 2 if d2s else 0, _p(a), _p(dz), _p(dw), _p(db), _p(ws), None,
+                  nchunk, B, H, W, Cin, Cout, _s(a))
+        return dx, None, dw, db, None, None, None
+
+
+def refine_conv_act(x, a, weight, bias, d2s, out_hw, dual=False):
+    """``conv(GELU(map(x)))`` of FinalPatchExpand_X4_V2 with a = GELU(x) supplied by the
+    producer's epilogue; returns z (and GELU(z), non-differentiable, when dual)."""
+    dt = act_dtype()
+    return _RefineConvAct.apply(_as(x, dt), _as(a, dt), _f32(weight), _f32(bias), bool(d2s), tuple(out_hw),
+                                bool(dual))
+
+
+class _LinearGelu(torch.autograd.Function):
+    """y = x . W^T (no bias) returning y and the non-differentiable GELU(y) from the same
+    epilogue (FinalPatchExpand_X4_V2.expand -> act, model_parts.py:458-460); the activation
+    gradient is applied by the consumer (refine_conv_act's dgrad epilogue)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, dt):
+        w = _shadow(weight, dt)
+        N, K = w.shape
+        M = x.numel() // K
+        if dt == torch.bfloat16 and tok_supported(M, N, K):
+            y, g = tok_gemm(x, w, torch.zeros(N, device=x.device, dtype=torch.float32), TOK_GELU_DUAL)
+        else:
+            with torch.autocast("cuda", enabled=False):
+                y = torch.nn.functional.linear(x, w)
+            g = torch.empty_like(y)
+            _lib.call("msu_gelu_fwd", _dt(y), _p(y), _p(g), y.numel(), _s(y))
+        ctx.save_for_backward(x, w)
+        ctx.params = (weight,)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for GELU(y)
+        ctx.mark_non_differentiable(g)
+        return y, g
+
+    @staticmethod
+    def backward(ctx, dy, unused):
+        x, w = ctx.saved_tensors
+        (weight,) = ctx.params
+        dy = _as(dy, x.dtype)
+        N, K = w.shape
+        M = dy.numel() // N
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if x.dtype == torch.bfloat16 and tok_preferred(M, K, N):
+                dx = tok_gemm(dy, _wt(w))
+            else:
+                with torch.autocast("cuda", enabled=False):
+                    dx = dy.matmul(w)
+        dw, _ = _wgrad(dy, x, weight, None, M, N, K)
+        return dx, dw, None
+
+
+def linear_gelu(x, weight):
+    """(x . W^T, GELU(x . W^T)): the second output is not differentiable (see _LinearGelu)."""
+    _need_cuda(x)
+    dt = act_dtype()
+    return _LinearGelu.apply(_as(x, dt), weight, dt)
+
+
 # ----------------------------------------------------------------------------- patch embed
 def patchify(img, patch, dtype):
     """[B, Cin, H, W] f32 image -> [B*(H/p)*(W/p), Cin*p*p] im2col rows (no grad)."""

@@ -266,6 +266,62 @@ def test_refine_conv(B, H, W, C, d2s, dtype):
     _close(bg.grad, br.grad, tol, tol, "db")
 
 
+@pytest.mark.parametrize("B,H,W,C,d2s", CONV_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_refine_conv_act(B, H, W, C, d2s, dtype):
+    """refine_conv_act (activation supplied by the producer, conv loads it as is; dual
+    epilogue) against refine_conv (GELU on load) on the same pre-activation: same z, dz->dx,
+    dW, db; the dual output equals GELU(z) as the GELU op computes it."""
+    ops = _ops()
+    g = _g(H * W + C + 7)
+    xs = (B, H // 4, W // 4, 16 * C) if d2s else (B, H, W, C)
+    x = torch.randn(xs, generator=g).to(DEV, dtype)
+    w = (torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(DEV)
+    b = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    dz = torch.randn(B, H, W, C, generator=g).to(DEV, dtype)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        x1, w1, b1 = [t.clone().requires_grad_(True) for t in (x, w, b)]
+        z1 = ops.refine_conv(x1, w1, b1, d2s, (H, W))
+        z1.backward(dz)
+        x2, w2, b2 = [t.clone().requires_grad_(True) for t in (x, w, b)]
+        a = ops.gelu(x2.detach())
+        z2, g2 = ops.refine_conv_act(x2, a, w2, b2, d2s, (H, W), dual=True)
+        z2.backward(dz)
+        gz = ops.gelu(z2.detach())
+    # bf16: the conv's on-load GELU (fast erf) and the GELU op (erf) may round a few inputs
+    # one bf16 ulp apart
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    _close(z2, z1, tol, tol, "z")
+    _close(g2, gz, tol, tol, "GELU(z)")
+    _close(x2.grad, x1.grad, tol, tol, "dx")
+    _close(w2.grad, w1.grad, tol, tol, "dW")
+    _close(b2.grad, b1.grad, tol, tol, "db")
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 1536, 96), (1000, 256, 16)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_linear_gelu(M, N, K, dtype):
+    """linear_gelu: (x W^T, GELU(x W^T)) with gradients of the first output = ops.linear's."""
+    ops = _ops()
+    g = _g(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV, dtype)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
+    dy = torch.randn(M, N, generator=g).to(DEV, dtype)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        x1, w1 = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+        y1 = ops.linear(x1, w1)
+        y1.backward(dy)
+        g1 = ops.gelu(y1.detach())
+        x2, w2 = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+        y2, g2 = ops.linear_gelu(x2, w2)
+        y2.backward(dy)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    _close(y2, y1, tol, tol, "y")
+    _close(g2, g1, tol, tol, "GELU(y)")
+    _close(x2.grad, x1.grad, tol, tol, "dx")
+    _close(w2.grad, w1.grad, tol, tol, "dW")
+
+
 @pytest.mark.parametrize("dtype,C,W", [(torch.float32, 96, 12), (torch.bfloat16, 96, 13), (torch.bfloat16, 128, 7)])
 def test_head_norm_output(dtype, C, W):
     ops = _ops()
