@@ -425,8 +425,8 @@ int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float*
       float* dbpart = db ? workspace + (long)p.slabs() * N * K : nullptr;
       const int rc = run_wave(p, (const bf16_t*)dY, (const bf16_t*)X, part, dbpart, M, N, K, st);
       if (rc) return rc;
-      colsum(part, p.slabs(), (long)N * K, (long)N * K, dW, accumulate, st);
-      if (db) colsum(dbpart, p.slabs(), N, N, db, accumulate, st);
+      const ColSeg segs[2] = {{part, (long)N * K, (long)N * K, dW}, {dbpart, N, N, db}};
+      colsum_multi(segs, db ? 2 : 1, p.slabs(), accumulate, st);
       return MSU_CHECK_LAUNCH();
     }
   }
@@ -452,8 +452,8 @@ int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float*
       hipLaunchKernelGGL((wgrad_kernel<float, 4>), grid, dim3(256), 0, st, (const float*)dY,
                          (const float*)X, part, dbpart, M, N, K, mchunk);
   }
-  colsum(part, S, (long)N * K, (long)N * K, dW, accumulate, st);
-  if (db) colsum(dbpart, S, N, N, db, accumulate, st);
+  const ColSeg segs[2] = {{part, (long)N * K, (long)N * K, dW}, {dbpart, N, N, db}};
+  colsum_multi(segs, db ? 2 : 1, S, accumulate, st);
   return MSU_CHECK_LAUNCH();
 }
 

@@ -336,8 +336,8 @@ int bwd_dispatch(int dtype, const LnBwdArgs& a, float* dgamma, float* dbeta, int
   if (dbeta == dgamma + a.C) {  // contiguous [dgamma | dbeta]: one reduction launch
     colsum(a.part, nparts, 2L * a.C, 2L * a.C, dgamma, accumulate, st);
   } else {
-    colsum(a.part, nparts, a.C, (long)2 * a.C, dgamma, accumulate, st);
-    colsum(a.part + a.C, nparts, a.C, (long)2 * a.C, dbeta, accumulate, st);
+    const ColSeg segs[2] = {{a.part, a.C, 2L * a.C, dgamma}, {a.part + a.C, a.C, 2L * a.C, dbeta}};
+    colsum_multi(segs, 2, nparts, accumulate, st);
   }
   return MSU_CHECK_LAUNCH();
 }
@@ -655,9 +655,8 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
   if (dbeta == dgamma + C && dw == dgamma + 2 * C) {  // contiguous [dgamma | dbeta | dw]
     colsum(part, nparts, 3L * C, 3L * C, dgamma, 0, st);
   } else {
-    colsum(part, nparts, C, (long)3 * C, dgamma, 0, st);
-    colsum(part + C, nparts, C, (long)3 * C, dbeta, 0, st);
-    colsum(part + 2 * C, nparts, C, (long)3 * C, dw, 0, st);
+    const ColSeg segs[3] = {{part, C, 3L * C, dgamma}, {part + C, C, 3L * C, dbeta}, {part + 2 * C, C, 3L * C, dw}};
+    colsum_multi(segs, 3, nparts, 0, st);
   }
   return MSU_CHECK_LAUNCH();
 }

@@ -703,8 +703,8 @@ int msu_attn_mfma_bwd(const void* qkv, const float* qkv_bias, const float* table
   hipLaunchKernelGGL(attn_bwd_mfma<BWD_WAVES>, dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
                      (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
                      p_drop, (uint64_t)seed, nblk);
-  colsum(dB_part, (int)parts, (long)nh * 4096, (long)nh * 4096, dimg, 0, st);
+  const ColSeg segs[2] = {{dB_part, (long)nh * 4096, (long)nh * 4096, dimg}, {qb_part, 3L * C, 3L * C, dqkv_bias_pad}};
+  colsum_multi(segs, 2, (int)parts, 0, st);
   hipLaunchKernelGGL(bias_image_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, st, dimg, nh, dtable);
-  colsum(qb_part, (int)parts, 3L * C, 3L * C, dqkv_bias_pad, 0, st);
   return MSU_CHECK_LAUNCH();
 }

@@ -54,18 +54,24 @@ class FlatGroup:
         self.names = [n for n, _ in named_params]
         self.params = [p for _, p in named_params]
         self.weight_decay = weight_decay
-        n = sum(p.numel() for p in self.params)
+        # every parameter starts on a 64-B boundary (16-B vector kernels write gradients in
+        # place); the gaps stay zero in data, grad and both moments
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += (p.numel() + 15) // 16 * 16
+        n = off
         self.numel = n
-        self.data = torch.empty(n, device=device, dtype=torch.float32)
+        self.count = sum(p.numel() for p in self.params)
+        self.data = torch.zeros(n, device=device, dtype=torch.float32)
         self.grad = torch.zeros(n, device=device, dtype=torch.float32)
         self.exp_avg = torch.zeros_like(self.data)
         self.exp_avg_sq = torch.zeros_like(self.data)
         # bf16 shadow of the parameters, refreshed once per step: the Linear ops read it
         # instead of casting every weight at every call
         self.shadow = torch.empty(n, device=device, dtype=torch.bfloat16)
-        self.offsets = []
-        off = 0
-        for p in self.params:
+        for p, off in zip(self.params, self.offsets):
             k = p.numel()
             self.data[off:off + k].copy_(p.detach().reshape(-1))
             p.data = self.data[off:off + k].view_as(p)
@@ -73,8 +79,6 @@ class FlatGroup:
             p._msu_shadow = self.shadow[off:off + k].view_as(p)
             p._msu_shadow_ver = -1  # not valid until the first refresh
             p._msu_direct = True  # backward kernels accumulate straight into p.grad
-            self.offsets.append(off)
-            off += k
 
     def refresh_shadow(self):
         """Re-cast the bf16 shadow after the master weights changed (AdamW writes them through
@@ -177,7 +181,7 @@ class Trainer:
         self.reducer = GradBucketer(self.groups, bucket_mb << 20, process_group) if world_size > 1 else None
 
     def num_params(self):
-        return sum(g.numel for g in self.groups)
+        return sum(g.count for g in self.groups)
 
     def set_epoch(self, epoch, config):
         t = config.TRAIN

@@ -63,7 +63,12 @@ def _worker(rank, world, port, bucket_bytes, out):
         loss = ((m(x) - y) ** 2).mean() / world  # each rank's share of the global mean
         loss.backward()
         red.finish()
-        grads = torch.cat([g.grad.clone() for g in groups])
+        grads = torch.cat([p.grad.reshape(-1).clone() for g in groups for p in g.params])
+        for g in groups:  # alignment gaps of the flat buffers stay zero
+            used = torch.zeros(g.numel, dtype=torch.bool)
+            for p, off in zip(g.params, g.offsets):
+                used[off:off + p.numel()] = True
+            assert not g.grad[~used].any()
         out[(rank, step)] = grads
         for g in groups:
             g.grad.zero_()
