@@ -86,18 +86,23 @@ def wgrad():
 
 
 def conv():
+    """The MS-UNet head as the model runs it: refine_conv_act (activations precomputed by the
+    producers), conv1 from the pre-d2s expand output with the dual epilogue, conv2 plain."""
     C, H = 96, 1024
-    x = torch.randn(B, H // 4, H // 4, 16 * C, device=DEV, dtype=torch.bfloat16)
+    e = torch.randn(B, H // 4, H // 4, 16 * C, device=DEV, dtype=torch.bfloat16)
+    a0 = torch.nn.functional.gelu(e)
     z1 = torch.randn(B, H, H, C, device=DEV, dtype=torch.bfloat16)
+    a1 = torch.nn.functional.gelu(z1)
     w = torch.randn(C, C, 3, 3, device=DEV) * 0.03
     b = torch.randn(C, device=DEV)
     fl = 2.0 * B * H * H * C * C * 9
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        for name, inp, d2s in (("conv1(d2s)", x, True), ("conv2", z1, False)):
-            ms = timeit(lambda: ops.refine_conv(inp, w, b, d2s, (H, H)), 5)
-            q = inp.clone().requires_grad_(True)
+        for name, x, a, d2s in (("conv1(d2s,dual)", e, a0, True), ("conv2", z1, a1, False)):
+            ms = timeit(lambda: ops.refine_conv_act(x, a, w, b, d2s, (H, H), dual=d2s), 5)
+            q = x.clone().requires_grad_(True)
             wq = w.clone().requires_grad_(True)
-            z = ops.refine_conv(q, wq, b, d2s, (H, H))
+            z = ops.refine_conv_act(q, a, wq, b, d2s, (H, H), dual=d2s)
+            z = z[0] if d2s else z
             dz = torch.randn_like(z)
             msb = timeit(lambda: torch.autograd.grad(z, (q, wq), dz, retain_graph=True), 5)
             print(f"{name}: fwd {ms:.3f} ms ({fl/ms/1e9:.0f} TF/s)  bwd(dgrad+wgrad) {msb:.3f} ms ({2*fl/msb/1e9:.0f} TF/s)")
