@@ -14,7 +14,9 @@ B, C, H = 8, 96, 1024
 x = torch.randn((B, H // 4, H // 4, 16 * C) if d2s else (B, H, H, C), device="cuda", dtype=torch.bfloat16)
 w = torch.randn(C, C, 3, 3, device="cuda") * 0.03
 b = torch.randn(C, device="cuda")
+a = torch.nn.functional.gelu(x)
 bwd = len(sys.argv) > 3 and sys.argv[3] == "bwd"
+act = len(sys.argv) > 4 and sys.argv[4] == "act"  # the model's path: activation precomputed
 with torch.autocast("cuda", dtype=torch.bfloat16):
     if bwd:
         xq, wq = x.requires_grad_(True), w.requires_grad_(True)
@@ -23,6 +25,8 @@ with torch.autocast("cuda", dtype=torch.bfloat16):
     for _ in range(reps):
         if bwd:
             torch.autograd.grad(z, (xq, wq), dz, retain_graph=True)
+        elif act:
+            ops.refine_conv_act(x, a, w, b, d2s, (H, H))
         else:
             ops.refine_conv(x, w, b, d2s, (H, H))
 torch.cuda.synchronize()

@@ -18,9 +18,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o run --outp
     python3 $R/bench.py --steps 4 --warmup 2 --no-cpu-baseline > $O/prof_$TAG.log 2>&1 || { tail -30 $O/prof_$TAG.log; exit 1; }
 echo "== HBM counters (conv fwd)"
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_$TAG -o fetch --output-format csv -- \
-    python3 $R/tools/conv_one.py 0 3 > $O/pmc_$TAG.log 2>&1 || { tail -20 $O/pmc_$TAG.log; exit 1; }
+    python3 $R/tools/conv_one.py 0 3 fwd act > $O/pmc_$TAG.log 2>&1 || { tail -20 $O/pmc_$TAG.log; exit 1; }
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_$TAG -o write --output-format csv -- \
-    python3 $R/tools/conv_one.py 0 3 >> $O/pmc_$TAG.log 2>&1 || { tail -20 $O/pmc_$TAG.log; exit 1; }
+    python3 $R/tools/conv_one.py 0 3 fwd act >> $O/pmc_$TAG.log 2>&1 || { tail -20 $O/pmc_$TAG.log; exit 1; }
 python3 $R/tools/pmc_json.py conv3x3_v2_kernel $O/pmc_$TAG/fetch_counter_collection.csv \
     $O/pmc_$TAG/write_counter_collection.csv $O/conv3x3_fwd_pmc_$TAG.json
 python3 $R/tools_profsum.py $O/prof_$TAG/run_kernel_stats.csv 6 40
