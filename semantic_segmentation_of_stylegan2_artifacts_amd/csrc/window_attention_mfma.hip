@@ -25,6 +25,11 @@
 #include "common.h"
 #include "reduce.h"
 
+// MSU_EXP: ablation bits for timing experiments only (tools/build_exp.sh); 0 in every real build
+#ifndef MSU_EXP
+#define MSU_EXP 0
+#endif
+
 namespace {
 
 template <typename F, int... Is>
@@ -71,6 +76,19 @@ MSU_DEV bf16x8 frag_tr_perm(const bf16_t* img, int ld, int r0, int col0, int lan
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
   const int col = col0 + 16 * (g & 1) + 4 * p;
   v4s both[2] = {tr_read(img + (r0 + 4 * h + q) * ld + col), tr_read(img + (r0 + 8 + 4 * h + q) * ld + col)};
+  return *reinterpret_cast<bf16x8*>(both);
+}
+
+// k-strided fragment in the bank-spread k order: element e of lane half h -> row
+// r0 + 4(e&3) + 2h + (e>>2).  Each half-wave's tr read then covers rows 4 apart, whose
+// 64-B column runs start 16 dwords apart for row strides of 20 and 36 dwords (LD, LDP):
+// all 64 banks once (natural order: 4 consecutive rows, 2-way conflicts).  Only for
+// products whose other operand is read the same way.
+MSU_DEV bf16x8 frag_tr_q4(const bf16_t* img, int ld, int r0, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
+  const int col = col0 + 16 * (g & 1) + 4 * p;
+  const int row = r0 + 4 * q + 2 * h;
+  v4s both[2] = {tr_read(img + row * ld + col), tr_read(img + (row + 1) * ld + col)};
   return *reinterpret_cast<bf16x8*>(both);
 }
 
@@ -160,8 +178,7 @@ MSU_DEV void lds_sync() {
 // bimg: the head's bias image, lane-major ([tile][lane][16], global) or, LANE_INNER,
 // [tile][q][lane][4] (an LDS copy: consecutive lanes read consecutive 16 B, conflict-free)
 template <bool LANE_INNER = false>
-MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (&qb)[2][2],
-                     const float* bimg, const int* sReg, bool boundary, float scale, int lane) {
+MSU_DEV void bias_init(f32x16 (&P)[2][2], const float* bimg, int lane) {
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
@@ -174,6 +191,11 @@ MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (
         P[jt][it][4 * q] = v.x; P[jt][it][4 * q + 1] = v.y; P[jt][it][4 * q + 2] = v.z; P[jt][it][4 * q + 3] = v.w;
       }
     }
+}
+
+// P: the bias image (bias_init); + K Q^T, mask, softmax over j
+MSU_DEV void probs_T_from(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (&qb)[2][2],
+                          const int* sReg, bool boundary, float scale, int lane) {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -218,6 +240,13 @@ MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (
 #pragma unroll
       for (int r = 0; r < 16; ++r) P[jt][it][r] *= inv;
   }
+}
+
+template <bool LANE_INNER = false>
+MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (&qb)[2][2],
+                     const float* bimg, const int* sReg, bool boundary, float scale, int lane) {
+  bias_init<LANE_INNER>(P, bimg, lane);
+  probs_T_from(P, ka, qb, sReg, boundary, scale, lane);
 }
 
 struct Aux {
@@ -435,7 +464,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
     }, std::make_integer_sequence<int, 4>{});
     const long nxt = win + stride;
     const bool more = nxt < g.nwin;
-    if (more) prep(nxt, std::integral_constant<int, buf ^ 1>{});
+    if (more && !(MSU_EXP & 32)) prep(nxt, std::integral_constant<int, buf ^ 1>{});
     const bool boundary = bnd[buf];
     const int* sTok = L.tok[buf];
     const int* sReg = L.reg[buf];
@@ -454,7 +483,13 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
         qb[t][ks] = frag_rows(L.q, LD, 32 * t, 16 * ks, lane);
       }
     f32x16 P[2][2];
-    probs_T(P, ka, qb, bimg, sReg, boundary, scale, lane);
+    bias_init(P, bimg, lane);
+    if constexpr (MSU_EXP & 2) {
+      for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) P[a][b][0] += (float)ka[a][b][0] * (float)qb[b][a][1];
+    } else {
+      probs_T_from(P, ka, qb, sReg, boundary, scale, lane);
+    }
     // dPd^T[j][i] = sum_d V[j][d] dO[i][d]
     f32x16 D[2][2];
 #pragma unroll
@@ -469,7 +504,10 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-        for (int it = 0; it < 2; ++it) D[jt][it] = mfma32(va[jt][ks], b[it], D[jt][it]);
+        for (int it = 0; it < 2; ++it) {
+          if constexpr (MSU_EXP & 4) D[jt][it][ks] += (float)va[jt][ks][0] * (float)b[it][1];
+          else D[jt][it] = mfma32(va[jt][ks], b[it], D[jt][it]);
+        }
     }
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
@@ -505,8 +543,10 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
           wp.y = (uint32_t)from_f32<bf16_t>(pd[2]) | ((uint32_t)from_f32<bf16_t>(pd[3]) << 16);
           wd.x = (uint32_t)from_f32<bf16_t>(ds[0]) | ((uint32_t)from_f32<bf16_t>(ds[1]) << 16);
           wd.y = (uint32_t)from_f32<bf16_t>(ds[2]) | ((uint32_t)from_f32<bf16_t>(ds[3]) << 16);
-          *reinterpret_cast<uint2*>(L.P + i * LDP + j0) = wp;
-          *reinterpret_cast<uint2*>(L.dS + i * LDP + j0) = wd;
+          if (!(MSU_EXP & 16) || pd[0] == 1.2345e-30f) {
+            *reinterpret_cast<uint2*>(L.P + i * LDP + j0) = wp;
+            *reinterpret_cast<uint2*>(L.dS + i * LDP + j0) = wd;
+          }
         }
     }
     lds_sync();
@@ -517,19 +557,23 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
       f32x16 av = f32x16{0}, ak = f32x16{0}, aq = f32x16{0};
 #pragma unroll
       for (int ks = 0; ks < 64; ks += 16) {
-        const bf16x8 bdo = frag_tr(L.dO, LD, ks, 0, lane);
-        const bf16x8 bq = frag_tr(L.q, LD, ks, 0, lane);
+        const bf16x8 bdo = frag_tr_q4(L.dO, LD, ks, 0, lane);
+        const bf16x8 bq = frag_tr_q4(L.q, LD, ks, 0, lane);
         const bf16x8 bk = frag_tr(L.k, LD, ks, 0, lane);
-        av = mfma32(frag_tr(L.P, LDP, ks, mt * 32, lane), bdo, av);
-        ak = mfma32(frag_tr(L.dS, LDP, ks, mt * 32, lane), bq, ak);
-        aq = mfma32(frag_rows(L.dS, LDP, mt * 32, ks, lane), bk, aq);
+        if constexpr (MSU_EXP & 8) {
+          av[ks / 16] += (float)bdo[0] * (float)bq[1] * (float)bk[2];
+        } else {
+          av = mfma32(frag_tr_q4(L.P, LDP, ks, mt * 32, lane), bdo, av);
+          ak = mfma32(frag_tr_q4(L.dS, LDP, ks, mt * 32, lane), bq, ak);
+          aq = mfma32(frag_rows(L.dS, LDP, mt * 32, ks, lane), bk, aq);
+        }
       }
       const int d = lane & 31;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int t = mt * 32 + crow(r, hh);
         const int tok = sTok[t];
-        if (tok >= 0) {
+        if (tok >= 0 && (!(MSU_EXP & 1) || aq[r] == 1.2345e-30f)) {
           bf16_t* row = dqkv + (long)tok * C3 + h * HD + d;
           row[0] = from_f32<bf16_t>(aq[r] * scale);
           row[g.C] = from_f32<bf16_t>(ak[r] * scale);
