@@ -19,6 +19,11 @@
 #include "mfma_frag.h"
 #include "reduce.h"
 
+// MSU_EXP: ablation bits for timing experiments only (tools/build_exp.sh); 0 in every real build
+#ifndef MSU_EXP
+#define MSU_EXP 0
+#endif
+
 namespace {
 
 constexpr int BM = 64;
@@ -228,6 +233,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
     issue(st + NST - 1);  // into the buffer computed in the previous iteration
     // fragments by untracked reads (a visible ds_read would wait for the whole ring);
     // A fragment i+1 is read while the MFMAs of fragment i run
+    if constexpr (MSU_EXP & 2) continue;
     const bf16_t* buf = lds + (st % NST) * STG;
     const uint32_t pa = lds_u32(buf + laneA), pb = lds_u32(buf + laneB);
     bf16x8 bf[NTW], af[2];
@@ -244,9 +250,14 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
       constexpr int i = decltype(I)::value;
       if constexpr (i + 1 < NTW) af[(i + 1) & 1] = tr8_untracked<32 * (i + 1), 32 * (i + 1) + 32 * LA>(pa);
 #pragma unroll
-      for (int j = 0; j < NTW; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i & 1], bf[j], acc[i][j], 0, 0, 0);
-      accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i & 1], ones, accb[i], 0, 0, 0);  // unconditional
+      for (int j = 0; j < NTW; ++j) {
+        if constexpr (MSU_EXP & 1)
+          acc[i][j][0] += (float)af[i & 1][j] * (float)bf[j][i];
+        else
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i & 1], bf[j], acc[i][j], 0, 0, 0);
+      }
+      if constexpr (!(MSU_EXP & 1))
+        accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i & 1], ones, accb[i], 0, 0, 0);  // unconditional
       if constexpr (i + 1 < NTW) lds_wait_tie<0>(af[(i + 1) & 1]);
     });
   }
@@ -327,6 +338,8 @@ inline WavePlan wave_plan(long M, int N, int K) {
   const long stage_bytes = (long)ins * 64 * 16;
   p.nst = (int)((160L * 1024) / stage_bytes);
   if (p.nst > 6) p.nst = 6;
+  static const int nst_cap = getenv("MSU_WGRAD_NST") ? atoi(getenv("MSU_WGRAD_NST")) : 0;  // A/B switch
+  if (nst_cap >= 3 && p.nst > nst_cap) p.nst = nst_cap;
   if (p.nst < 3) {  // ring too shallow: generic kernel
     p.ntw = 0;
     return p;

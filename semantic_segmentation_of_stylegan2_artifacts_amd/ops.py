@@ -8,6 +8,8 @@ float32.
 """
 import math
 
+import os
+
 import torch
 
 from . import _lib
@@ -64,6 +66,36 @@ _grad_ready = None
 def set_grad_ready_callback(fn):
     global _grad_ready
     _grad_ready = fn
+
+
+# Linear weight gradients that accumulate straight into .grad run on a side stream: nothing
+# later in backward reads them, so they overlap the input-gradient chain (which is often
+# latency-bound at stages 1-3) instead of sitting on it.  The trainer joins the side stream
+# before the optimizer (join_side_streams) and the bucketed all-reduce is issued from it.
+_side_enabled = os.environ.get("MSU_WGRAD_SIDE", "1") != "0"
+_side_streams = {}
+
+
+def side_stream(device):
+    """The weight-gradient side stream of a device, or None when disabled / never used."""
+    device = torch.device(device)
+    if device.type != "cuda" or not _side_streams:
+        return None
+    return _side_streams.get(device.index if device.index is not None else torch.cuda.current_device())
+
+
+def _side_stream_for(device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _side_streams.get(idx)
+    if st is None:
+        st = _side_streams[idx] = torch.cuda.Stream(device=idx)
+    return st
+
+
+def join_side_streams():
+    """Current stream(s) wait for every weight-gradient side stream."""
+    for idx, st in _side_streams.items():
+        torch.cuda.current_stream(idx).wait_stream(st)
 
 
 def _direct(*params):
@@ -350,12 +382,24 @@ def _wgrad(dy, x, weight, bias, M, N, K):
     """Linear weight/bias gradients on msu_linear_wgrad; (None, None) when accumulated
     straight into the trainer's flat .grad views."""
     L = _lib.lib()
-    ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
     if _direct(weight) and (bias is None or _direct(bias)):
-        _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(weight.grad),
-                  _p(None if bias is None else bias.grad), _p(ws), M, N, K, 1, _s(x))
+        if _side_enabled:
+            main = torch.cuda.current_stream(x.device)
+            side = _side_stream_for(x.device)
+            side.wait_stream(main)  # dy and x are ready
+            with torch.cuda.stream(side):
+                ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
+                _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(weight.grad),
+                          _p(None if bias is None else bias.grad), _p(ws), M, N, K, 1, side.cuda_stream)
+            dy.record_stream(side)  # their memory is not reused by the main stream meanwhile
+            x.record_stream(side)
+        else:
+            ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
+            _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(weight.grad),
+                      _p(None if bias is None else bias.grad), _p(ws), M, N, K, 1, _s(x))
         _notify(weight, bias)
         return None, None
+    ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
     dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
     db = torch.empty(N, device=x.device, dtype=torch.float32) if bias is not None else None
     _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(dw), _p(db), _p(ws), M, N, K, 0, _s(x))

@@ -128,7 +128,15 @@ class GradBucketer:
     def _launch(self, b):
         g, s, e = self.buckets[b]
         self.launched[b] = True
-        self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+        side = ops.side_stream(g.grad.device)
+        if side is None:
+            self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+            return
+        # the bucket's gradients come from both streams: issue from the side stream after it
+        # has caught up with the main stream's work so far
+        side.wait_stream(torch.cuda.current_stream(g.grad.device))
+        with torch.cuda.stream(side):
+            self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
 
     def _hook(self, p):
         b = self.param_bucket[id(p)]
@@ -204,6 +212,7 @@ class Trainer:
         loss.backward()
         if self.reducer is not None:
             self.reducer.finish()
+        ops.join_side_streams()  # weight gradients issued on the side stream
         self.step_count += 1
         inv = self.inv_world if self.world_size > 1 else None
         for g in self.groups:

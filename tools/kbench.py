@@ -57,6 +57,16 @@ def attn():
                       f"({byts/ms/1e6:6.0f} GB/s, {nwin*nh/ms/1e3:6.1f} Mitem/s)  bwd {msb*1e3:7.1f} us")
 
 
+def stream():
+    """Reference streaming rates: torch copy / sum of a 512 MB bf16 tensor."""
+    x = torch.randn(256 << 20, device=DEV, dtype=torch.bfloat16)
+    y = torch.empty_like(x)
+    ms = timeit(lambda: y.copy_(x))
+    print(f"copy 512 MB: {ms*1e3:7.1f} us  {2 * x.numel() * 2 / ms / 1e6:6.0f} GB/s (read+write)")
+    ms = timeit(lambda: x.sum())
+    print(f"sum  512 MB: {ms*1e3:7.1f} us  {x.numel() * 2 / ms / 1e6:6.0f} GB/s (read)")
+
+
 def wgrad():
     from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
     shapes = [(B * 65536, 288, 96), (B * 65536, 96, 96), (B * 65536, 384, 96), (B * 65536, 96, 384),
@@ -153,6 +163,6 @@ def tok():
 
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
-    for name, fn in (("attn", attn), ("wgrad", wgrad), ("conv", conv), ("ln", ln), ("tok", tok)):
+    for name, fn in (("attn", attn), ("wgrad", wgrad), ("conv", conv), ("ln", ln), ("tok", tok), ("stream", stream)):
         if what in (name, "all"):
             fn()
