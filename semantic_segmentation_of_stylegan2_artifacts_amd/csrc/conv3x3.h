@@ -16,6 +16,7 @@
 
 #include "common.h"
 #include "mfma_frag.h"
+#include "reduce.h"
 
 // MSU_EXP: ablation bits for timing experiments only (tools/build_exp.sh); 0 in every real build
 #ifndef MSU_EXP
@@ -800,26 +801,16 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
   }
 }
 
-// sum partials -> dW[co][ci][3][3] (torch Conv2d layout) and db[co]
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* part, const float* dbpart,
-                                                           int nchunk, int Cout, int Cin, int CinP,
-                                                           float* dW, float* db) {
+// chunk-summed partial [dy][co][dx][ci] -> dW[co][ci][3][3] (torch Conv2d layout)
+__global__ void __launch_bounds__(256) wgrad_permute_kernel(const float* __restrict__ sum, int Cout, int Cin,
+                                                            int CinP, float* __restrict__ dW) {
   const long n = (long)Cout * Cin * 9;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i < n) {
     const int co = (int)(i / (Cin * 9));
     const int rem = (int)(i - (long)co * Cin * 9);
     const int ci = rem / 9, tap = rem % 9, dy = tap / 3, dx = tap % 3;
-    const long slab = (long)Cout * 3 * CinP;
-    float s = 0.f;
-    for (int c = 0; c < nchunk; ++c)
-      s += part[((long)c * 3 + dy) * slab + ((long)co * 3 + dx) * CinP + ci];
-    dW[i] = s;
-  }
-  if (db && i < Cout) {
-    float s = 0.f;
-    for (int c = 0; c < nchunk; ++c) s += dbpart[(long)c * Cout + i];
-    db[i] = s;
+    dW[i] = sum[((long)dy * Cout * 3 + (long)co * 3 + dx) * CinP + ci];
   }
 }
 

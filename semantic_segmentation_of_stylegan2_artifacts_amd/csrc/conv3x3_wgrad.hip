@@ -6,7 +6,8 @@ extern "C" {
 long msu_conv3x3_wgrad_workspace(int nchunk, int Cin, int Cout, int dtype, int unused) {
   (void)dtype; (void)unused;
   const int CinP = (Cin + 31) / 32 * 32;
-  return (long)nchunk * 3 * Cout * 3 * CinP + (long)nchunk * Cout;
+  // chunk partials [nchunk][3][Cout][3][CinP] + bias partials [nchunk][Cout] + their sum
+  return (long)(nchunk + 1) * 3 * Cout * 3 * CinP + (long)nchunk * Cout;
 }
 
 // dW [Cout][Cin][3][3] f32 and db [Cout] f32 (db may be null).  in_mode as in fwd.
@@ -46,9 +47,15 @@ int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, flo
   }
 #undef MSU_WG
   if (rc) return rc;
+  // deterministic chunk sums (one launch for the weight slab and the bias), then the
+  // [dy][co][dx][ci] -> [co][ci][dy][dx] permutation
+  const long slab = 3L * Cout * 3 * g.CinP;
+  float* sum = dbpart + (long)nchunk * Cout;
+  const ColSeg segs[2] = {{part, slab, slab, sum}, {dbpart, Cout, Cout, db}};
+  colsum_multi(segs, db ? 2 : 1, nchunk, 0, st);
   const long n = (long)Cout * Cin * 9;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part,
-                     dbpart, nchunk, Cout, Cin, g.CinP, dW, db);
+  hipLaunchKernelGGL(wgrad_permute_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sum, Cout, Cin,
+                     g.CinP, dW);
   return MSU_CHECK_LAUNCH();
 }
 

@@ -98,6 +98,24 @@ def join_side_streams():
         torch.cuda.current_stream(idx).wait_stream(st)
 
 
+_join_queued = False
+
+
+def _end_of_backward():
+    global _join_queued
+    _join_queued = False
+    join_side_streams()
+
+
+def _join_at_end_of_backward():
+    """Once per backward pass: when it ends, the main stream waits for the side stream, so
+    .grad read after ``backward()`` returns is complete (overlap stays inside backward)."""
+    global _join_queued
+    if not _join_queued:
+        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+        _join_queued = True
+
+
 def _direct(*params):
     return all(p is not None and getattr(p, "_msu_direct", False) and p.grad is not None for p in params)
 
@@ -393,6 +411,7 @@ def _wgrad(dy, x, weight, bias, M, N, K):
                           _p(None if bias is None else bias.grad), _p(ws), M, N, K, 1, side.cuda_stream)
             dy.record_stream(side)  # their memory is not reused by the main stream meanwhile
             x.record_stream(side)
+            _join_at_end_of_backward()
         else:
             ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
             _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(weight.grad),
