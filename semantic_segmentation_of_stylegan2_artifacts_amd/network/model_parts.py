@@ -477,10 +477,20 @@ class MSUNetSys(nn.Module):
         return [self.layers_cent1[self.num_layers - 2], self.layers_cent2[self.num_layers - 3]]
 
     def _run_dead(self, mod, x):
+        """Run a branch whose result the reference discards.  On a GPU it goes to the side
+        stream (ops.side stream, joined with the weight-gradient work at the end of backward):
+        nothing reads its output, so it overlaps the rest of the forward pass."""
         if self.skip_dead_branches:
             return
-        with torch.no_grad():
+        if not x.is_cuda:
+            with torch.no_grad():
+                mod(x)
+            return
+        side = ops._side_stream_for(x.device)
+        side.wait_stream(torch.cuda.current_stream(x.device))
+        with torch.no_grad(), torch.cuda.stream(side):
             mod(x)
+        x.record_stream(side)
 
     def forward_features(self, x):
         """``model_parts.py:775-815``."""
