@@ -116,6 +116,7 @@ class GradBucketer:
                     start, count = end, 0
             if count:
                 self.buckets.append([g, start, g.numel])
+        self.main_stream = None  # the stream the training step runs on (set per step)
         self.expected = None    # accumulations per bucket, learned on the first step
         self.pending = [0] * len(self.buckets)
         self.launched = [False] * len(self.buckets)
@@ -133,8 +134,10 @@ class GradBucketer:
             self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
             return
         # the bucket's gradients come from both streams: issue from the side stream after it
-        # has caught up with the main stream's work so far
-        side.wait_stream(torch.cuda.current_stream(g.grad.device))
+        # has caught up with the main stream's work so far (the hook may fire while autograd
+        # runs a side-stream node, so the main stream is named explicitly)
+        main = self.main_stream if self.main_stream is not None else torch.cuda.current_stream(g.grad.device)
+        side.wait_stream(main)
         with torch.cuda.stream(side):
             self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
 
@@ -205,6 +208,8 @@ class Trainer:
         """One training step; returns the (device) loss of this rank's batch."""
         self.model.train()
         ops.set_grad_ready_callback(self.reducer._hook if self.reducer is not None else None)
+        if self.reducer is not None and torch.device(self.device).type == "cuda":
+            self.reducer.main_stream = torch.cuda.current_stream(self.device)
         if self.amp_dtype == torch.bfloat16:
             for g in self.groups:
                 g.refresh_shadow()
