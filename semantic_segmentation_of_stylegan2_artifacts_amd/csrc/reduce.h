@@ -75,8 +75,9 @@ inline void colsum_multi(const ColSeg* segs, int nseg, int nparts, int accumulat
     total += segs[j].n;
   }
   const int V = v4 ? 4 : 1;
-  // narrow reductions (LayerNorm affine, biases: ~1000 parts) want many part-lanes in flight
-  const int PL = total / V <= 1024 ? 32 : 8;
+  // narrow reductions (LayerNorm affine, biases: ~1000 parts) want many part-lanes in flight:
+  // with 128 part-lanes a 1024-part reduction is one round of 8 loads per thread
+  const int PL = total / V <= 256 ? 128 : (total / V <= 1024 ? 32 : 8);
   const int NC = 256 / PL;
   ColSegs sg{};
   int blocks = 0;
@@ -91,10 +92,12 @@ inline void colsum_multi(const ColSeg* segs, int nseg, int nparts, int accumulat
   sg.nseg = nseg;
   if (blocks == 0) return;
   if (V == 4) {
-    if (PL == 32) hipLaunchKernelGGL((colsum_kernel<32, 4>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
+    if (PL == 128) hipLaunchKernelGGL((colsum_kernel<128, 4>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
+    else if (PL == 32) hipLaunchKernelGGL((colsum_kernel<32, 4>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
     else hipLaunchKernelGGL((colsum_kernel<8, 4>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
   } else {
-    if (PL == 32) hipLaunchKernelGGL((colsum_kernel<32, 1>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
+    if (PL == 128) hipLaunchKernelGGL((colsum_kernel<128, 1>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
+    else if (PL == 32) hipLaunchKernelGGL((colsum_kernel<32, 1>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
     else hipLaunchKernelGGL((colsum_kernel<8, 1>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
   }
 }

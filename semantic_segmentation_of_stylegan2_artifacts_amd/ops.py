@@ -101,6 +101,24 @@ def join_side_streams():
 _join_queued = False
 
 
+def _guard_side_write(p, ev):
+    """p.grad was just updated on the side stream (event ev).  If autograd later accumulates
+    another gradient into p on the main stream (e.g. the qkv bias: its Linear adds db here,
+    the attention op returns the padded tokens' share), that AccumulateGrad must wait for it:
+    a tensor hook on p makes the current stream wait for the last such event first."""
+    p._msu_side_event = ev
+    if not getattr(p, "_msu_side_hooked", False):
+        def hook(grad, p=p):
+            # called with None when the backward that owns p returned no gradient (direct
+            # accumulation): nothing will be added, nothing to wait for
+            e = getattr(p, "_msu_side_event", None)
+            if grad is not None and e is not None:
+                torch.cuda.current_stream(p.device).wait_event(e)
+            return grad
+        p.register_hook(hook)
+        p._msu_side_hooked = True
+
+
 def _end_of_backward():
     global _join_queued
     _join_queued = False
@@ -325,6 +343,8 @@ class _WindowAttention(torch.autograd.Function):
         _lib.call("msu_win_attn_fwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(out), _p(ws), B, H, W,
                   C, num_heads, shift, float(p_drop), seed, _s(qkv))
         ctx.save_for_backward(qkv, qkv_bias, table)
+        # the parameter itself when it reached us uncast (trainer flat buffers: direct .grad)
+        ctx.bias_param = qkv_bias if isinstance(qkv_bias, torch.nn.Parameter) else None
         ctx.cfg = (num_heads, shift, float(p_drop), seed)
         return out
 
@@ -343,6 +363,17 @@ class _WindowAttention(torch.autograd.Function):
         dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
         _lib.call("msu_win_attn_bwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
                   _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _s(qkv))
+        bp = ctx.bias_param
+        if bp is not None and _side_enabled and _direct(bp):
+            # the qkv bias also receives its Linear's db on the side stream: add this share
+            # there too, so every write to its .grad is ordered on one stream
+            side = _side_stream_for(qkv.device)
+            side.wait_stream(torch.cuda.current_stream(qkv.device))
+            with torch.cuda.stream(side):
+                bp.grad.add_(dbias)
+            dbias.record_stream(side)
+            _notify(bp)
+            return dqkv, None, dtable, None, None, None, None
         return dqkv, dbias, dtable, None, None, None, None
 
 
@@ -411,6 +442,11 @@ def _wgrad(dy, x, weight, bias, M, N, K):
                           _p(None if bias is None else bias.grad), _p(ws), M, N, K, 1, side.cuda_stream)
             dy.record_stream(side)  # their memory is not reused by the main stream meanwhile
             x.record_stream(side)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            _guard_side_write(weight, ev)
+            if bias is not None:
+                _guard_side_write(bias, ev)
             _join_at_end_of_backward()
         else:
             ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
