@@ -188,6 +188,7 @@ class Trainer:
                                    tversky_bce_mix=t.LOSS_TVERSKY_BCE_MIX)
         self.world_size = world_size
         self.step_count = 0
+        self._shadow_fresh = False
         self.inv_world = torch.full((1,), 1.0 / world_size, device=device, dtype=torch.float32)
         self.reducer = GradBucketer(self.groups, bucket_mb << 20, process_group) if world_size > 1 else None
 
@@ -210,9 +211,10 @@ class Trainer:
         ops.set_grad_ready_callback(self.reducer._hook if self.reducer is not None else None)
         if self.reducer is not None and torch.device(self.device).type == "cuda":
             self.reducer.main_stream = torch.cuda.current_stream(self.device)
-        if self.amp_dtype == torch.bfloat16:
+        if self.amp_dtype == torch.bfloat16 and not self._shadow_fresh:
             for g in self.groups:
                 g.refresh_shadow()
+        self._shadow_fresh = False
         loss = self.forward_loss(images, labels)
         loss.backward()
         if self.reducer is not None:
@@ -226,4 +228,7 @@ class Trainer:
             g.grad.zero_()
             if self.amp_dtype == torch.bfloat16:
                 g.refresh_shadow()  # keeps evaluation between steps on the updated weights
+        # the next step's refresh is skipped; a write through a parameter in between bumps its
+        # version and the Linear ops cast that weight themselves (ops._shadow)
+        self._shadow_fresh = self.amp_dtype == torch.bfloat16
         return loss.detach()

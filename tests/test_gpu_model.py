@@ -82,3 +82,38 @@ def test_msunet_input_channel_check():
     m = MSUNet(cfg, img_size=224).to(DEV)
     with pytest.raises(ValueError):
         m(torch.zeros(1, 4, 224, 224, device=DEV))
+
+
+def test_side_stream_paths_are_exact():
+    """The discarded branches on the side stream change nothing (same logits with them
+    skipped), and the gradients with the side stream equal the single-stream ones (same
+    kernels; only the qkv bias sums its two shares in the other order: f32 rounding)."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import FlatGroup
+    spec = cases.model_cases()["swinT224"]
+    cfg = make_cfg(**spec["cfg"])
+    params = cases.model_params(cfg, spec["seed"])
+    x, target = cases.model_inputs(cfg, spec["batch"], spec["seed"])
+    grads = {}
+    for side in (True, False):
+        model = _build(cfg)
+        model.load_state_dict(params, strict=True)
+        model = model.to(DEV).train()
+        named = [(n, p) for n, p in model.named_parameters()
+                 if not any(p is q for m in model.dead_modules() for q in m.parameters())]
+        grp = FlatGroup(named, 0.0, torch.device(DEV))
+        old = ops._side_enabled
+        ops._side_enabled = side
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = model(x.to(DEV))
+                model.skip_dead_branches = True
+                out_skip = model(x.to(DEV))
+                model.skip_dead_branches = False
+            assert torch.equal(out, out_skip)
+            out.float().square().mean().backward()
+            torch.cuda.synchronize()
+        finally:
+            ops._side_enabled = old
+        grads[side] = grp.grad.clone()
+    torch.testing.assert_close(grads[True], grads[False], rtol=1e-6, atol=1e-9)
