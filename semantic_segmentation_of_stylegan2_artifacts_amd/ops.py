@@ -73,6 +73,7 @@ def set_grad_ready_callback(fn):
 # latency-bound at stages 1-3) instead of sitting on it.  The trainer joins the side stream
 # before the optimizer (join_side_streams) and the bucketed all-reduce is issued from it.
 _side_enabled = os.environ.get("MSU_WGRAD_SIDE", "1") != "0"
+_SIDE_PRIORITY = int(os.environ.get("MSU_SIDE_PRIORITY", "1"))  # A/B switch (0: same as main)
 _side_streams = {}
 
 
@@ -88,7 +89,9 @@ def _side_stream_for(device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _side_streams.get(idx)
     if st is None:
-        st = _side_streams[idx] = torch.cuda.Stream(device=idx)
+        # lowest priority: when both streams have work queued, the dispatcher serves the
+        # main (critical-path) stream's workgroups first
+        st = _side_streams[idx] = torch.cuda.Stream(device=idx, priority=_SIDE_PRIORITY)
     return st
 
 
