@@ -52,15 +52,31 @@ def _next_seed():
     return _seed_rng.getrandbits(62)
 
 
+_SCALE_POOL = {}
+_POOL_ROWS = 64
+
+
 def _drop_path_scale(p, training, B, device):
-    """torchvision StochasticDepth(p, 'row'): per-sample Bernoulli(1-p)/(1-p) or None."""
+    """torchvision StochasticDepth(p, 'row'): per-sample Bernoulli(1-p)/(1-p) or None.
+    Draws come from a per-(p, B, device) pool refilled 64 rows at a time (one Bernoulli
+    kernel and one divide per 64 calls instead of three tiny kernels per call); each call
+    takes a fresh row, so draws stay independent and identically distributed."""
     if not training or p == 0.0:
         return None
     survival = 1.0 - p
-    noise = torch.empty(B, device=device, dtype=torch.float32).bernoulli_(survival)
-    if survival > 0.0:
-        noise.div_(survival)
-    return noise
+    device = torch.device(device)
+    # one pool per stream: a row is read on the stream whose kernel produced it
+    sid = torch.cuda.current_stream(device).stream_id if device.type == "cuda" else 0
+    key = (float(p), int(B), str(device), sid)
+    pool = _SCALE_POOL.get(key)
+    if pool is None or pool[1] >= _POOL_ROWS:
+        noise = torch.empty(_POOL_ROWS, B, device=device, dtype=torch.float32).bernoulli_(survival)
+        if survival > 0.0:
+            noise.div_(survival)
+        pool = _SCALE_POOL[key] = [noise, 0]
+    row = pool[0][pool[1]]
+    pool[1] += 1
+    return row
 
 
 # ============================================================================ Swin block
