@@ -136,6 +136,11 @@ int msu_gelu_fwd(int dtype, const void* x, void* y, long n, void* stream);
 int msu_gelu_bwd(int dtype, const void* x, const void* dy, void* dx, long n, void* stream);
 /* PatchEmbed.proj im2col (model_parts.py:211, :222): img [B,Cin,H,W] f32 ->
  * [B*(H/p)*(W/p), Cin*p*p] in (c, ky, kx) order. */
+/* out = a + b * scale[i / per_sample] (a may be NULL: out = b * scale[...]); n, per_sample
+ * multiples of 4.  The Swin block's residual add with StochasticDepth's per-sample scale
+ * (torchvision SwinTransformerBlock: x + stochastic_depth(f(x))) and its branch gradient. */
+int msu_residual(int dtype, const void* a, const void* b, const float* scale, void* out, long n, long per_sample,
+                 void* stream);
 int msu_patchify(int dtype, const float* img, void* out, int B, int Cin, int H, int W, int p,
                  void* stream);
 

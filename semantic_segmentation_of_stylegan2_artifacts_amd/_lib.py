@@ -31,6 +31,7 @@ SIGNATURES = {
     "msu_win_attn_bwd": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P]),
     "msu_gelu_fwd": (I, [I, P, P, L, P]),
     "msu_gelu_bwd": (I, [I, P, P, P, L, P]),
+    "msu_residual": (I, [I, P, P, P, P, L, L, P]),
     "msu_patchify": (I, [I, P, P, I, I, I, I, I, P]),
     "msu_dynloss_nblk": (I, [L]),
     "msu_dynloss_fwd": (I, [I, P, P, I, L, F, F, F, P, I, P, P, P]),

@@ -30,6 +30,23 @@ __global__ void __launch_bounds__(256) gelu_bwd_kernel(const T* x, const T* dy, 
   }
 }
 
+// out = a + b * scale[sample] (a may be null: out = b * scale[sample]): the residual add with
+// StochasticDepth's per-sample scale (torchvision SwinTransformerBlock: x + stochastic_depth(f(x)))
+// in one pass, and its backward for the branch (dy * scale[sample]).
+template <typename T>
+__global__ void __launch_bounds__(256) residual_kernel(const T* a, const T* b, const float* scale, T* out,
+                                                       long n4, long per_sample4) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const float s = scale[i / per_sample4];
+    float vb[4], va[4] = {0.f, 0.f, 0.f, 0.f};
+    Vec4<T>::load(b + 4 * i, vb);
+    if (a) Vec4<T>::load(a + 4 * i, va);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) vb[e] = fmaf(vb[e], s, va[e]);
+    Vec4<T>::store(out + 4 * i, vb);
+  }
+}
+
 // img [B, Cin, H, W] f32 -> cols [B*(H/p)*(W/p), Cin*p*p] in (c, ky, kx) order = conv weight order
 template <typename T>
 __global__ void __launch_bounds__(256) patchify_kernel(const float* img, T* out, int B, int Cin,
@@ -251,6 +268,19 @@ int msu_gelu_bwd(int dtype, const void* x, const void* dy, void* dx, long n, voi
   else
     hipLaunchKernelGGL(gelu_bwd_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, st,
                        (const float*)x, (const float*)dy, (float*)dx, n / 4);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_residual(int dtype, const void* a, const void* b, const float* scale, void* out, long n, long per_sample,
+                 void* stream) {
+  if (n % 4 || per_sample % 4 || per_sample <= 0 || scale == nullptr) return -2;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MSU_BF16)
+    hipLaunchKernelGGL(residual_kernel<bf16_t>, dim3(grid_for(n / 4)), dim3(256), 0, st, (const bf16_t*)a,
+                       (const bf16_t*)b, scale, (bf16_t*)out, n / 4, per_sample / 4);
+  else
+    hipLaunchKernelGGL(residual_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, st, (const float*)a,
+                       (const float*)b, scale, (float*)out, n / 4, per_sample / 4);
   return MSU_CHECK_LAUNCH();
 }
 

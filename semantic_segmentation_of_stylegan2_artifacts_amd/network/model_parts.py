@@ -179,9 +179,11 @@ def materialize(state):
     if not isinstance(state, tuple):
         return state
     x, br, sc = state
-    br = br.to(x.dtype)
     if sc is None:
-        return x + br
+        return x + br.to(x.dtype)
+    if x.is_cuda and x.dtype == br.dtype and x[0].numel() % 4 == 0:
+        return ops.residual_add(x, br, sc)
+    br = br.to(x.dtype)
     return x + br * sc.view(-1, *([1] * (br.dim() - 1))).to(br.dtype)
 
 

@@ -633,6 +633,36 @@ def _shadow(param, dt):
     return param.to(dt)
 
 
+# ----------------------------------------------------------------------------- residual
+class _Residual(torch.autograd.Function):
+    """x + br * scale[sample] in one pass (StochasticDepth 'row' scale); backward: dx = dy,
+    dbr = dy * scale[sample]."""
+
+    @staticmethod
+    def forward(ctx, x, br, scale):
+        _need_cuda(x, br)
+        out = torch.empty_like(x)
+        _lib.call("msu_residual", _dt(x), _p(x), _p(br), _p(scale), _p(out), x.numel(), x[0].numel(), _s(x))
+        ctx.save_for_backward(scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        (scale,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dbr = torch.empty_like(dy)
+        _lib.call("msu_residual", _dt(dy), None, _p(dy), _p(scale), _p(dbr), dy.numel(), dy[0].numel(), _s(dy))
+        return dy, dbr, None
+
+
+def residual_add(x, br, scale):
+    """``x + br * scale.view(B, 1, ...)`` (per-sample scale; plain add when scale is None)."""
+    dt = act_dtype()
+    if scale is None:
+        return x + br.to(x.dtype)
+    return _Residual.apply(_as(x, dt), _as(br, dt), _f32(scale))
+
+
 # ----------------------------------------------------------------------------- GELU
 class _Gelu(torch.autograd.Function):
     @staticmethod

@@ -518,3 +518,26 @@ def test_window_attention_bf16_dropout_consistency():
     y2.backward(dy)
     rhs_wrong = (q2.grad[..., 2 * C:].float() * q2[..., 2 * C:].float()).sum().item()
     assert abs(lhs - rhs_wrong) > 4e-3 * terms.abs().sum().item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_residual_add(dtype):
+    """ops.residual_add = x + br * scale[sample] (StochasticDepth row scale) and its grads."""
+    ops = _ops()
+    g = _g(77)
+    x = torch.randn(3, 9, 7, 16, generator=g)
+    br = torch.randn(3, 9, 7, 16, generator=g)
+    sc = torch.tensor([0.0, 1.25, 1.25])
+    dy = torch.randn(3, 9, 7, 16, generator=g)
+    xr, brr = x.clone().requires_grad_(True), br.clone().requires_grad_(True)
+    yr = xr + brr * sc.view(-1, 1, 1, 1)
+    yr.backward(dy)
+    xg = x.to(DEV, dtype).requires_grad_(True)
+    bg = br.to(DEV, dtype).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        y = ops.residual_add(xg, bg, sc.to(DEV))
+    y.backward(dy.to(DEV, dtype))
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    _close(y, yr, tol, tol, "y")
+    _close(xg.grad, xr.grad, tol, tol, "dx")
+    _close(bg.grad, brr.grad, tol, tol, "dbr")
