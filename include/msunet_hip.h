@@ -81,6 +81,13 @@ int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const fl
                      const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                      float* workspace, int B, int H, int W, int C, int nh, int shift,
                      float p_drop, unsigned long long seed, void* stream);
+/* As msu_win_attn_bwd; the parameter-gradient tail (relative-table and qkv-bias reductions)
+ * runs on param_stream, ordered after the backward kernel by an event (null: on stream).
+ * dqkv is complete when `stream` is; dtable / dqkv_bias_pad when `param_stream` is. */
+int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const float* table,
+                      const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
+                      float* workspace, int B, int H, int W, int C, int nh, int shift,
+                      float p_drop, unsigned long long seed, void* stream, void* param_stream);
 
 /* ---------------------------------------------------------------- refine convs
  * FinalPatchExpand_X4_V2.refine1 / refine2 (model_parts.py:447-448, :468-471): 3x3, pad 1,

@@ -144,3 +144,18 @@ __device__ __attribute__((aligned(16))) uint32_t g_zero_region[1024];
 MSU_DEV const void* zero_src(int slot) { return g_zero_region + 4 * (slot & 255); }
 
 #define MSU_CHECK_LAUNCH() (hipGetLastError() == hipSuccess ? 0 : -1)
+
+// Order stream `pst` after the work queued so far on `st` (an event; one per host thread,
+// reused: each record captures the state at that moment).  pst == st or null: nothing.
+// Lets an entry point put its parameter-gradient tail on the caller's side stream.
+inline int attn_param_stream(hipStream_t st, hipStream_t& pst) {
+  if (pst == nullptr || pst == st) {
+    pst = st;
+    return 0;
+  }
+  static thread_local hipEvent_t ev = nullptr;
+  if (ev == nullptr && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
+  if (hipEventRecord(ev, st) != hipSuccess) return -1;
+  if (hipStreamWaitEvent(pst, ev, 0) != hipSuccess) return -1;
+  return 0;
+}

@@ -400,7 +400,8 @@ int msu_attn_mfma_fwd(const void* qkv, const float* qkv_bias, const float* table
                       float* bias_img, hipStream_t st);
 int msu_attn_mfma_bwd(const void* qkv, const float* qkv_bias, const float* table, const void* dout,
                       void* dqkv, float* dtable, float* dqkv_bias_pad, float* ws, int B, int H, int W,
-                      int C, int nh, int shift, float p_drop, unsigned long long seed, hipStream_t st);
+                      int C, int nh, int shift, float p_drop, unsigned long long seed, hipStream_t st,
+                      hipStream_t pst);
 long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh);
 long msu_attn_mfma_fwd_workspace(int C, int nh);
 
@@ -446,18 +447,19 @@ long msu_win_attn_bwd_workspace(int dtype, int B, int H, int W, int C, int nh) {
   return nblk * nh * NT * NT + (long)nh * NT * NT + nblk * 3 * C;
 }
 
-int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
-                     const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
-                     float* workspace, int B, int H, int W, int C, int nh, int shift,
-                     float p_drop, unsigned long long seed, void* stream) {
+int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const float* table,
+                      const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
+                      float* workspace, int B, int H, int W, int C, int nh, int shift,
+                      float p_drop, unsigned long long seed, void* stream, void* param_stream) {
   if (C != nh * HD) return -2;
   if ((long)B * H * W >= (1L << 31)) return -2;
   const WinGeom g = make_geom(B, H, W, C, nh, shift);
   hipStream_t st = (hipStream_t)stream;
+  hipStream_t pst = (hipStream_t)param_stream;
   if (g.nwin == 0) return 0;
   if (dtype == MSU_BF16)
     return msu_attn_mfma_bwd(qkv, qkv_bias, table, dout, dqkv, dtable, dqkv_bias_pad, workspace, B, H, W,
-                             C, nh, shift, p_drop, seed, st);
+                             C, nh, shift, p_drop, seed, st, pst);
   const int nblk = f32_bwd_blocks(g.nwin, nh);
   const float scale = 1.0f / sqrtf((float)HD);
   float* dB_part = workspace;
@@ -466,12 +468,22 @@ int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const fl
   hipLaunchKernelGGL(win_attn_bwd_kernel<float>, dim3(nblk, nh), dim3(64), 0, st,
                      (const float*)qkv, qkv_bias, table, (const float*)dout, (float*)dqkv,
                      dB_part, qb_part, g, scale, p_drop, (uint64_t)seed, nblk);
+  const int rc = attn_param_stream(st, pst);
+  if (rc) return rc;
   const long nB = (long)nh * NT * NT;
-  colsum(dB_part, nblk, nB, nB, dB, 0, st);
-  hipLaunchKernelGGL(rel_table_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, st,
+  colsum(dB_part, nblk, nB, nB, dB, 0, pst);
+  hipLaunchKernelGGL(rel_table_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, pst,
                      dB, nh, dtable);
-  colsum(qb_part, nblk, 3L * C, 3L * C, dqkv_bias_pad, 0, st);
+  colsum(qb_part, nblk, 3L * C, 3L * C, dqkv_bias_pad, 0, pst);
   return MSU_CHECK_LAUNCH();
+}
+
+int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
+                     const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
+                     float* workspace, int B, int H, int W, int C, int nh, int shift,
+                     float p_drop, unsigned long long seed, void* stream) {
+  return msu_win_attn_bwd2(dtype, qkv, qkv_bias, table, dout, dqkv, dtable, dqkv_bias_pad, workspace, B, H, W,
+                           C, nh, shift, p_drop, seed, stream, nullptr);
 }
 
 }  // extern "C"

@@ -731,7 +731,8 @@ int msu_attn_mfma_fwd(const void* qkv, const float* qkv_bias, const float* table
 
 int msu_attn_mfma_bwd(const void* qkv, const float* qkv_bias, const float* table, const void* dout,
                       void* dqkv, float* dtable, float* dqkv_bias_pad, float* ws, int B, int H, int W,
-                      int C, int nh, int shift, float p_drop, unsigned long long seed, hipStream_t st) {
+                      int C, int nh, int shift, float p_drop, unsigned long long seed, hipStream_t st,
+                      hipStream_t pst) {
   const Geom g = make_geom(B, H, W, C, nh, shift);
   if (g.nwin == 0) return 0;
   const float scale = 1.0f / sqrtf((float)HD);
@@ -747,8 +748,11 @@ int msu_attn_mfma_bwd(const void* qkv, const float* qkv_bias, const float* table
   hipLaunchKernelGGL(attn_bwd_mfma<BWD_WAVES>, dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
                      (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
                      p_drop, (uint64_t)seed, nblk);
+  // parameter-gradient reductions: on pst (after the backward kernel) when given
+  const int rc = attn_param_stream(st, pst);
+  if (rc) return rc;
   const ColSeg segs[2] = {{dB_part, (long)nh * 4096, (long)nh * 4096, dimg}, {qb_part, 3L * C, 3L * C, dqkv_bias_pad}};
-  colsum_multi(segs, 2, (int)parts, 0, st);
-  hipLaunchKernelGGL(bias_image_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, st, dimg, nh, dtable);
+  colsum_multi(segs, 2, (int)parts, 0, pst);
+  hipLaunchKernelGGL(bias_image_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, pst, dimg, nh, dtable);
   return MSU_CHECK_LAUNCH();
 }

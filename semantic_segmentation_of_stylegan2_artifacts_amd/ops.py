@@ -348,6 +348,7 @@ class _WindowAttention(torch.autograd.Function):
         ctx.save_for_backward(qkv, qkv_bias, table)
         # the parameter itself when it reached us uncast (trainer flat buffers: direct .grad)
         ctx.bias_param = qkv_bias if isinstance(qkv_bias, torch.nn.Parameter) else None
+        ctx.table_param = table if isinstance(table, torch.nn.Parameter) else None
         ctx.cfg = (num_heads, shift, float(p_drop), seed)
         return out
 
@@ -362,21 +363,34 @@ class _WindowAttention(torch.autograd.Function):
         ws = torch.empty(L.msu_win_attn_bwd_workspace(_dt(qkv), B, H, W, C, nh), device=qkv.device,
                          dtype=torch.float32)
         dqkv = torch.empty_like(qkv)
+        bp, tp = ctx.bias_param, ctx.table_param
+        if bp is not None and tp is not None and _side_enabled and _direct(bp, tp):
+            # parameter-gradient tail on the side stream: the relative-table / qkv-bias
+            # reductions and their .grad adds (the qkv bias also receives its Linear's db
+            # there, so every write to its .grad is ordered on one stream)
+            main = torch.cuda.current_stream(qkv.device)
+            side = _side_stream_for(qkv.device)
+            with torch.cuda.stream(side):
+                dtable = torch.empty_like(table)
+                dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
+            _lib.call("msu_win_attn_bwd2", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
+                      _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, main.cuda_stream,
+                      side.cuda_stream)
+            ws.record_stream(side)
+            with torch.cuda.stream(side):
+                bp.grad.add_(dbias)
+                tp.grad.add_(dtable)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            _guard_side_write(bp, ev)
+            _guard_side_write(tp, ev)
+            _join_at_end_of_backward()
+            _notify(bp, tp)
+            return dqkv, None, None, None, None, None, None
         dtable = torch.empty_like(table)
         dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
         _lib.call("msu_win_attn_bwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
                   _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _s(qkv))
-        bp = ctx.bias_param
-        if bp is not None and _side_enabled and _direct(bp):
-            # the qkv bias also receives its Linear's db on the side stream: add this share
-            # there too, so every write to its .grad is ordered on one stream
-            side = _side_stream_for(qkv.device)
-            side.wait_stream(torch.cuda.current_stream(qkv.device))
-            with torch.cuda.stream(side):
-                bp.grad.add_(dbias)
-            dbias.record_stream(side)
-            _notify(bp)
-            return dqkv, None, dtable, None, None, None, None
         return dqkv, dbias, dtable, None, None, None, None
 
 
