@@ -2,8 +2,14 @@
 // FinalPatchExpand_X4_V2.act), the 4x4/s4 patch-embed im2col (PatchEmbed.proj,
 // model_parts.py:211,222), DynamicLoss fwd/bwd (loss/DynamicLoss.py:82-111) and the fused
 // AdamW step over flat parameter buffers (trainer.py:143-152, torch.optim.AdamW semantics).
-// All HBM-bound: vectorised 4-wide, grid-stride, f32 math.
+// All HBM-bound: vectorised 4-wide, grid-stride, f32 math.  GELU: libm erff for f32 (the
+// parity path), the one-exp / one-rcp erf of common.h for bf16 (|error| <= 1.5e-7, far below
+// bf16 rounding; libm erff made the bf16 kernels VALU-bound).
 #include "common.h"
+
+#ifndef MSU_EXP
+#define MSU_EXP 0
+#endif
 
 namespace {
 
@@ -13,7 +19,7 @@ __global__ void __launch_bounds__(256) gelu_fwd_kernel(const T* x, T* y, long n4
     float v[4];
     Vec4<T>::load(x + 4 * i, v);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+    for (int e = 0; e < 4; ++e) v[e] = (sizeof(T) == 2 && !(MSU_EXP & 1)) ? gelu_fast(v[e]) : gelu_f(v[e]);
     Vec4<T>::store(y + 4 * i, v);
   }
 }
@@ -25,7 +31,7 @@ __global__ void __launch_bounds__(256) gelu_bwd_kernel(const T* x, const T* dy, 
     Vec4<T>::load(x + 4 * i, v);
     Vec4<T>::load(dy + 4 * i, d);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) d[e] *= gelu_grad_f(v[e]);
+    for (int e = 0; e < 4; ++e) d[e] *= (sizeof(T) == 2 && !(MSU_EXP & 1)) ? gelu_grad_fast(v[e]) : gelu_grad_f(v[e]);
     Vec4<T>::store(dx + 4 * i, d);
   }
 }
