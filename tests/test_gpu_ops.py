@@ -541,3 +541,31 @@ def test_residual_add(dtype):
     _close(y, yr, tol, tol, "y")
     _close(xg.grad, xr.grad, tol, tol, "dx")
     _close(bg.grad, brr.grad, tol, tol, "dbr")
+
+
+def test_window_attention_param_tail_on_side_stream():
+    """With direct .grad parameters the relative-table / qkv-bias gradient tail runs on the
+    side stream (msu_win_attn_bwd2) and is added there: same gradients as the autograd path."""
+    ops = _ops()
+    B, H, W, nh, shift = 2, 20, 27, 2, 3
+    C = 32 * nh
+    g = _g(4242)
+    qkv = torch.randn(B, H, W, 3 * C, generator=g).to(DEV, torch.bfloat16)
+    qb = (0.3 * torch.randn(3 * C, generator=g)).to(DEV)
+    table = torch.randn(169, nh, generator=g).to(DEV)
+    dy = torch.randn(B, H, W, C, generator=g).to(DEV, torch.bfloat16)
+    res = {}
+    for direct in (False, True):
+        q = qkv.clone().requires_grad_(True)
+        pb, pt = torch.nn.Parameter(qb.clone()), torch.nn.Parameter(table.clone())
+        if direct:
+            for p in (pb, pt):
+                p.grad = torch.zeros_like(p)
+                p._msu_direct = True
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = ops.window_attention(q, pb, pt, nh, shift)
+        y.backward(dy)
+        torch.cuda.synchronize()
+        res[direct] = (q.grad.float(), pb.grad.clone(), pt.grad.clone())
+    for a, b, what in zip(res[True], res[False], ("dqkv", "dbias", "dtable")):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7, msg=what)
