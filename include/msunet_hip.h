@@ -131,8 +131,10 @@ int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float*
  *   epi 1  torchvision MLP mlp.0 + mlp.1 (Linear -> GELU): Y = H = A.W^T + b, Y2 = GELU(H);
  *   epi 2  input gradient of mlp.3 through mlp.1: Y = (A.W^T) * GELU'(H) (no bias).
  * msu_tok_gemm_supported() says whether a shape is covered (N % 32 == 0, K % 48 or 128 == 0
- * and an LDS plan exists); uncovered shapes are the caller's to route to a library GEMM. */
+ * and an LDS plan exists), msu_tok_gemm_supported_epi() the same for one epilogue (the GELU
+ * epilogues cap the column chunk); uncovered shapes are the caller's to route to a library GEMM. */
 int msu_tok_gemm_supported(long M, int N, int K);
+int msu_tok_gemm_supported_epi(long M, int N, int K, int epi);
 int msu_tok_gemm(const void* A, const void* A2, int K1, const void* W, const float* bias, void* Y,
                  void* Y2, const void* H, long M, int N, int K, int epi, void* stream);
 int msu_tok_gemm_plan(long M, int N, int K, long* out6);

@@ -49,6 +49,7 @@ SIGNATURES = {
     "msu_wgrad_workspace": (L, [L, I, I]),
     "msu_linear_wgrad": (I, [I, P, P, P, P, P, L, I, I, I, P]),
     "msu_tok_gemm_supported": (I, [L, I, I]),
+    "msu_tok_gemm_supported_epi": (I, [L, I, I, I]),
     "msu_tok_gemm": (I, [P, P, I, P, P, P, P, P, L, I, I, I, P]),
     "msu_tok_gemm_plan": (I, [L, I, I, P]),
     "msu_metrics_nblk": (I, [L]),

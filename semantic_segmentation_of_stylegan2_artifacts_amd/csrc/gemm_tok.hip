@@ -68,6 +68,12 @@ int msu_tok_gemm_supported(long M, int N, int K) {
   return tok_plan(M, N, K).nc ? 1 : 0;
 }
 
+// Same for a given epilogue (the GELU epilogues cap the chunk width at 192 columns).
+int msu_tok_gemm_supported_epi(long M, int N, int K, int epi) {
+  if (M <= 0 || N % 32 || K % 16 || epi < 0 || epi > 2) return 0;
+  return tok_plan(M, N, K, epi).nc ? 1 : 0;
+}
+
 // Y[M][N] = epi(A . W^T + bias), bf16 in / out.  epi 0: plain (+ bias); 1: Y = H and
 // Y2 = GELU(H) (needs bias); 2: Y = (A . W^T) * GELU'(H) (no bias).  A2 != null: columns
 // [K1, K) of A come from A2 ([M][K - K1]; needs bias).

@@ -418,6 +418,20 @@ def tok_supported(M, N, K):
     return r
 
 
+def tok_supported_epi(M, N, K, epi):
+    """``tok_supported`` for one epilogue (TOK_GELU_* plans cap the column chunk at 192)."""
+    key = (int(M), int(N), int(K), int(epi))
+    r = _tok_cache.get(key)
+    if r is None:
+        r = _tok_cache[key] = bool(_lib.lib().msu_tok_gemm_supported_epi(*key))
+    return r
+
+
+# GELU-epilogue GEMMs of the MLP on the token GEMM from this many tokens up (A/B switch
+# MSU_MLP_TOK_MIN_M): below it hipBLASLt + the standalone GELU kernels.
+_MLP_TOK_MIN_M = int(os.environ.get("MSU_MLP_TOK_MIN_M", "131072"))
+
+
 def tok_preferred(M, N, K):
     """Token GEMM where it beats hipBLASLt (measured, tools/kbench.py tok): the HBM-bound
     stage-0 shapes (M >= 256k tokens) and small weights (N*K <= 576*192); wider weights at
@@ -601,7 +615,24 @@ def mlp_fusable(x, fc1_weight, fc2_weight):
         return False
     Hd, C = fc1_weight.shape
     M = x.numel() // C
-    return (tok_preferred(M, Hd, C) and tok_preferred(M, C, Hd) and fc2_weight.shape == (C, Hd))
+    if fc2_weight.shape != (C, Hd):
+        return False
+    if tok_preferred(M, Hd, C) and tok_preferred(M, C, Hd):
+        return True
+    # the two GELU-epilogue GEMMs (mlp.0 forward, mlp.3 input gradient: both [M,C]x[C,Hd])
+    # on the token GEMM, the other two on whichever GEMM is preferred for their shape
+    return (M >= _MLP_TOK_MIN_M and tok_supported_epi(M, Hd, C, TOK_GELU_DUAL) and
+            tok_supported_epi(M, Hd, C, TOK_GELU_GRAD))
+
+
+def _mm(a, w, bias=None):
+    """bf16 a . w^T (+ bias) on the token GEMM where preferred, else hipBLASLt."""
+    N, K = w.shape
+    M = a.numel() // K
+    if tok_preferred(M, N, K):
+        return tok_gemm(a, w, bias)
+    with torch.autocast("cuda", enabled=False):
+        return torch.nn.functional.linear(a, w, None if bias is None else bias.to(torch.bfloat16))
 
 
 class _Mlp(torch.autograd.Function):
@@ -613,7 +644,7 @@ class _Mlp(torch.autograd.Function):
         W1 = _shadow(w1, torch.bfloat16)
         W2 = _shadow(w2, torch.bfloat16)
         h, g = tok_gemm(x, W1, _f32(b1), TOK_GELU_DUAL)
-        y = tok_gemm(g, W2, _f32(b2))
+        y = _mm(g, W2, _f32(b2))
         ctx.save_for_backward(x, h, g, W1, W2)
         ctx.params = (w1, b1, w2, b2)
         return y
@@ -628,7 +659,7 @@ class _Mlp(torch.autograd.Function):
         dw2, db2 = _wgrad(dy, g, w2, b2, M, C, Hd)
         dh = tok_gemm(dy, _wt(W2), None, TOK_GELU_GRAD, h=h)
         dw1, db1 = _wgrad(dh, x, w1, b1, M, Hd, C)
-        dx = tok_gemm(dh, _wt(W1)) if ctx.needs_input_grad[0] else None
+        dx = _mm(dh, _wt(W1)) if ctx.needs_input_grad[0] else None
         return dx, dw1, db1, dw2, db2
 
 

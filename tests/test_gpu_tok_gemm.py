@@ -128,6 +128,16 @@ def test_fused_mlp_matches_fp32(M, C):
         assert err <= 3e-2 * r.abs().max().item(), f"{name}: {err:.3e} vs {r.abs().max().item():.3e}"
 
 
+@pytest.mark.parametrize("M,C", [(1024, 384), (2048, 192)])
+def test_fused_mlp_mixed_routing(M, C, monkeypatch):
+    """Stage-1/2 widths: the GELU-epilogue GEMMs on the token GEMM, mlp.3 forward and mlp.0's
+    input gradient on hipBLASLt (ops._mm) -- same numerics bar as the all-token-GEMM MLP."""
+    ops = _ops()
+    monkeypatch.setattr(ops, "_MLP_TOK_MIN_M", 0)
+    assert not (ops.tok_preferred(M, 4 * C, C) and ops.tok_preferred(M, C, 4 * C))
+    test_fused_mlp_matches_fp32(M, C)
+
+
 def test_linear_uses_tok_gemm_and_matches():
     """ops.linear in bf16 routes through the token GEMM for covered shapes (fwd + dgrad)."""
     ops = _ops()

@@ -158,6 +158,15 @@ def tok():
                 wt = w.contiguous()
                 mg = timeit(lambda: ops.tok_gemm(dy, wt, None, ops.TOK_GELU_GRAD, h=h))
                 line += f" dual {md*1e3:6.1f} us ({(byts + M*N*2)/md/1e6:5.0f} GB/s) ggrad {mg*1e3:6.1f} us ({(byts + M*N*2)/mg/1e6:5.0f} GB/s)"
+                # the unfused alternative: hipBLASLt + standalone GELU fwd / bwd kernels
+                with torch.no_grad():
+                    yb = torch.nn.functional.linear(a, w, bb)
+                    mgf = timeit(lambda: ops.gelu(yb))
+                    mdg = timeit(lambda: torch.matmul(dy, w.t()))  # dY[M,K] . W3^T with W3 = w^T: [M,N]
+                    dh = torch.empty_like(h)
+                    mgb = timeit(lambda: ops._lib.call("msu_gelu_bwd", ops._dt(h), ops._p(h), ops._p(yb),
+                                                       ops._p(dh), h.numel(), ops._s(h)))
+                line += f" | blas+gelu fwd {(mt+mgf)*1e3:6.1f} us, blas dgrad+gelu' {(mdg+mgb)*1e3:6.1f} us"
         print(line, flush=True)
 
 
