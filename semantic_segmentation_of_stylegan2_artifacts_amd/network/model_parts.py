@@ -518,6 +518,8 @@ class MSUNetSys(nn.Module):
         x = self.pos_drop(x)
         xd = []
         L = self.num_layers
+        dead = []  # issued after the stage's own blocks: the main stream is not starved while
+        # the host launches a branch nobody reads
         for i, layer in enumerate(self.layers):
             if i == 1:
                 x2 = x
@@ -528,7 +530,7 @@ class MSUNetSys(nn.Module):
                         x2 = _skip_fuse(self.concat_back_dim[k + 2], x2, xd[i - k])
                         xd[i - k] = x2
                         if k == L - 3:
-                            self._run_dead(mod, x2)
+                            dead.append((mod, x2))
                         else:
                             x2 = mod(x2)
             if i == 2:
@@ -540,11 +542,14 @@ class MSUNetSys(nn.Module):
                         x1 = _skip_fuse(self.concat_back_dim[k + 1], x1, xd[i - k])
                         xd[i - k] = x1
                         if k == L - 2:
-                            self._run_dead(mod, x1)
+                            dead.append((mod, x1))
                         else:
                             x1 = mod(x1)
             xd.append(x)
             x = layer(x)
+            for mod, xin in dead:
+                self._run_dead(mod, xin)
+            dead.clear()
         x = ops.layer_norm(x, self.norm.weight, self.norm.bias, self.norm.eps)
         return x, xd
 
