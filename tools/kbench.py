@@ -132,6 +132,20 @@ def ln():
               f"bwd {msb*1e3:.1f} us ({3*rows*C*2/msb/1e6:.0f} GB/s)")
 
 
+def lnadd():
+    """Residual add + LN (the Swin block's norm2 / next norm1) backward with both output
+    gradients, as the block runs it: dres = the residual stream's gradient."""
+    for rows, C in ((B * 65536, 96), (B * 16384, 192), (B * 4096, 384)):
+        a = torch.randn(rows, C, device=DEV, dtype=torch.bfloat16).requires_grad_(True)
+        b = torch.randn(rows, C, device=DEV, dtype=torch.bfloat16).requires_grad_(True)
+        w = torch.randn(C, device=DEV)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            s, y = ops.add_layer_norm(a, b, None, w, w)
+        dy, ds = torch.randn_like(y), torch.randn_like(s)
+        msb = timeit(lambda: torch.autograd.grad([y, s], [a, b], [dy, ds], retain_graph=True))
+        print(f"LN+add rows={rows} C={C}: bwd {msb*1e3:.1f} us ({5*rows*C*2/msb/1e6:.0f} GB/s)", flush=True)
+
+
 def tok():
     """Token GEMM vs hipBLASLt (F.linear) at the Swin-T 1024^2 bs8 shapes."""
     shapes = [(B * 65536, 288, 96), (B * 65536, 96, 96), (B * 65536, 384, 96), (B * 65536, 96, 384),
@@ -172,6 +186,6 @@ def tok():
 
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
-    for name, fn in (("attn", attn), ("wgrad", wgrad), ("conv", conv), ("ln", ln), ("tok", tok), ("stream", stream)):
+    for name, fn in (("attn", attn), ("wgrad", wgrad), ("conv", conv), ("ln", ln), ("lnadd", lnadd), ("tok", tok), ("stream", stream)):
         if what in (name, "all"):
             fn()
