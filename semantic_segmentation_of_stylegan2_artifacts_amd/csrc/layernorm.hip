@@ -303,9 +303,12 @@ int launch_fwd(const LnArgs& a, hipStream_t st, int max_blocks) {
   };
   // rows of <= 16 chunks (C <= 128 bf16) read by 16 lanes each (one 16-B chunk per lane, whole
   // rows per load instruction) instead of 4 lanes x 4 chunks: bench 153.5 vs 152.8 img/s
-  // (A/B switch MSU_LN_WIDE=0 restores the 4-lane rows)
-  static const int wide = getenv("MSU_LN_WIDE") ? atoi(getenv("MSU_LN_WIDE")) : 1;
+  // and the same up to C <= 512 on 32 / 64 lanes: +0.25 % more (3 of 3 pairs).  A/B switch
+  // MSU_LN_WIDE: 0 = 4-lane rows, 1 = one chunk per lane up to C = 128 only)
+  static const int wide = getenv("MSU_LN_WIDE") ? atoi(getenv("MSU_LN_WIDE")) : 2;
   if (wide && nchunk <= 16) return go(ln_fwd_kernel<T, MODE, 16, 1>, 16);
+  if (wide >= 2 && nchunk <= 32) return go(ln_fwd_kernel<T, MODE, 32, 1>, 32);
+  if (wide >= 2 && nchunk <= 64) return go(ln_fwd_kernel<T, MODE, 64, 1>, 64);
   if (nchunk <= 4 * 4) return go(ln_fwd_kernel<T, MODE, 4, 4>, 4);
   if (nchunk <= 8 * 4) return go(ln_fwd_kernel<T, MODE, 8, 4>, 8);
   if (nchunk <= 16 * 4) return go(ln_fwd_kernel<T, MODE, 16, 4>, 16);
@@ -322,8 +325,10 @@ int launch_bwd(const LnBwdArgs& a, hipStream_t st, int nblocks) {
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(256), 0, st, a);
     return MSU_CHECK_LAUNCH();
   };
-  static const int wide = getenv("MSU_LN_WIDE") ? atoi(getenv("MSU_LN_WIDE")) : 1;  // see launch_fwd
+  static const int wide = getenv("MSU_LN_WIDE") ? atoi(getenv("MSU_LN_WIDE")) : 2;  // see launch_fwd
   if (wide && nchunk <= 16) return go(ln_bwd_kernel<T, MODE, 16, 1>);
+  if (wide >= 2 && nchunk <= 32) return go(ln_bwd_kernel<T, MODE, 32, 1>);
+  if (wide >= 2 && nchunk <= 64) return go(ln_bwd_kernel<T, MODE, 64, 1>);
   if (nchunk <= 4 * 3) return go(ln_bwd_kernel<T, MODE, 4, 3>);  // C = 96 bf16: no idle slot
   if (nchunk <= 4 * 4) return go(ln_bwd_kernel<T, MODE, 4, 4>);
   if (nchunk <= 8 * 4) return go(ln_bwd_kernel<T, MODE, 8, 4>);
