@@ -85,6 +85,47 @@ def conv_roofline(device, batch, img, C):
             "flops_per_launch": flops, "ms_per_launch": round(ms, 4)}
 
 
+def attention_roofline(device, batch, img, C, heads):
+    """Window attention (the north star's second named kernel): the stage-0 shifted block's
+    msu_win_attn_fwd launch at the bench shape, timed with HIP events on the launching
+    (current) stream.  Algorithmic work per window x head: 4*49*49*32 FLOP (QK^T and PV) and
+    q, k, v in + o out; the padded grid (ceil(H/7)^2 windows per image) is what the kernel
+    computes.  The timed call includes the tiny aux kernel (bias image, scaled qkv bias) that
+    precedes every attention launch.  HBM-bound (AI ~ 25 FLOP/B); both fractions are reported."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    res = img // 4
+    g = torch.Generator(device="cpu").manual_seed(2)
+    qkv = torch.randn(batch, res, res, 3 * C, generator=g).to(device, torch.bfloat16)
+    qb = torch.zeros(3 * C, device=device)
+    tb = (0.02 * torch.randn(169, heads, generator=g)).to(device)
+    s = torch.cuda.current_stream(device)
+
+    def launch():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            ops.window_attention(qkv, qb, tb, heads, 3, 0.0, 1)
+
+    for _ in range(3):
+        launch()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 10
+    e0.record(s)
+    for _ in range(n):
+        launch()
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    nwin = batch * ((res + 6) // 7) ** 2
+    flops = 4.0 * 49 * 49 * 32 * nwin * heads
+    byts = batch * res * res * 4 * C * 2
+    return {"kernel": "attn_fwd_mfma (stage-0 shifted window attention fwd, bf16 MFMA)", "bound": "hbm",
+            "achieved": round(byts / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "mfma_tflops": round(flops / (ms * 1e-3) / 1e12, 1),
+            "mfma_frac": round(flops / (ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+            "bytes_per_launch": byts, "flops_per_launch": flops, "ms_per_launch": round(ms, 4)}
+
+
 def cpu_baseline(seconds_budget=25.0):
     """The CPU oracle (pure PyTorch fp32 restatement of the reference path) timing one
     training step (fwd + DynamicLoss + bwd + AdamW) of Swin-T MS-UNet on 4 x 256^2
@@ -229,6 +270,8 @@ def main():
         }
         if not args.no_roofline:
             res["roofline"] = conv_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM)
+            res["roofline_attention"] = attention_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM,
+                                                           cfg.MODEL.SWIN.NUM_HEADS[0])
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline()
             res["dice_vs_ref"] = dice_vs_reference(device)
