@@ -35,8 +35,14 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream
+
+
 def _s(t):
-    return torch.cuda.current_stream(t.device).cuda_stream
+    """hipStream_t (as int) of the current stream on t's device.  The raw getter skips the
+    Python Stream object torch.cuda.current_stream builds: a few µs per launch of host time,
+    which is what bounds the short stage-2/3 kernels."""
+    return _raw_stream(t.get_device())
 
 
 def act_dtype(device_type="cuda"):
