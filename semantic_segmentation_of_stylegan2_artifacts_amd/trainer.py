@@ -21,12 +21,17 @@ Here:
   ``grad is None``.
 """
 import math
+import os
 
 import torch
 import torch.distributed as dist
 
 from . import ops
 from .loss import DynamicLoss
+
+# A/B switch: mark the bf16 shadow's parameter versions before AdamW (host-only work while
+# the GPU is still busy) instead of after the step's last launch
+_EARLY_MARK = os.environ.get("MSU_EARLY_SHADOW_MARK", "1") != "0"
 
 
 def is_no_decay(name, param):
@@ -85,7 +90,15 @@ class FlatGroup:
         a raw pointer).  Each parameter records its version: an in-place write made through
         the parameter itself (load_state_dict, ``p.copy_``) bumps it and makes the Linear ops
         cast that weight again until the next refresh."""
+        self.copy_shadow()
+        self.mark_shadow()
+
+    def copy_shadow(self):
         self.shadow.copy_(self.data)
+
+    def mark_shadow(self):
+        """Host-only half of the refresh: the raw-pointer AdamW and the shadow copy do not
+        bump parameter versions, so this can run while the GPU is still in backward."""
         for p in self.params:
             p._msu_shadow_ver = p._version
 
@@ -223,12 +236,21 @@ class Trainer:
         ops.join_side_streams()  # weight gradients issued on the side stream
         self.step_count += 1
         inv = self.inv_world if self.world_size > 1 else None
+        bf16 = self.amp_dtype == torch.bfloat16
+        if bf16 and _EARLY_MARK:
+            # the per-parameter Python loop runs now, while the GPU still has backward work
+            # queued, not after the last launch of the step (it left the GPU idle there)
+            for g in self.groups:
+                g.mark_shadow()
         for g in self.groups:
             ops.adamw_(g.data, g.grad, g.exp_avg, g.exp_avg_sq, self.lr, self.betas[0], self.betas[1],
                        self.eps, g.weight_decay, self.step_count, inv_scale=inv)
             g.grad.zero_()
-            if self.amp_dtype == torch.bfloat16:
-                g.refresh_shadow()  # keeps evaluation between steps on the updated weights
+            if bf16:  # keeps evaluation between steps on the updated weights
+                if _EARLY_MARK:
+                    g.copy_shadow()
+                else:
+                    g.refresh_shadow()
         # the next step's refresh is skipped; a write through a parameter in between bumps its
         # version and the Linear ops cast that weight themselves (ops._shadow)
         self._shadow_fresh = self.amp_dtype == torch.bfloat16
