@@ -685,8 +685,9 @@ int msu_ln_part_blocks(long rows, int C) {
   (void)C;
   // >= 16 rows per block (the per-block parameter-gradient reduction amortises) and enough
   // blocks to fill the CUs at the deep stages (8192 rows x 768: 512 blocks, not 64)
+  static const long cap = getenv("MSU_LN_PARTS_MAX") ? atol(getenv("MSU_LN_PARTS_MAX")) : 1024;  // A/B switch
   long nb = (rows + 15) / 16;
-  if (nb > 1024) nb = 1024;
+  if (nb > cap) nb = cap;
   return nb < 1 ? 1 : (int)nb;
 }
 
