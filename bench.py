@@ -221,7 +221,7 @@ def main():
     model = MSUNet(cfg, img_size=args.img, num_classes=1).to(device)
     model.ms_unet.skip_dead_branches = args.skip_dead
     trainer = Trainer(model, cfg, device, world_size=world,
-                      process_group=dist.group.WORLD if world > 1 else None)
+                      process_group=dist.group.WORLD if world > 1 else None, rank=rank, seed=cfg.SEED)
     pool = batch_pool(2, args.batch, args.img, device, cfg.SEED + 1000 * rank)
 
     for i in range(args.warmup):

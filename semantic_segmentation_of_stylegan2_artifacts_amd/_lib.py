@@ -39,6 +39,9 @@ SIGNATURES = {
     "msu_dynloss_bwd": (I, [I, P, P, P, P, P, I, L, F, F, F, P, P]),
     "msu_adamw": (I, [P, P, P, P, L, F, F, F, F, F, I, P, P, P]),
     "msu_nonfinite": (I, [P, L, P, P]),
+    "msu_nonfinite2": (I, [P, L, P, L, P, P]),
+    "msu_adamw_dev": (I, [P, P, P, P, L, P, F, F, F, F, P, P, P]),
+    "msu_step_advance": (I, [P, P, P]),
     "msu_cast": (I, [I, P, P, L, P]),
     "msu_conv3x3_fwd": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),
     "msu_conv3x3_fwd2": (I, [I, I, P, P, P, P, P, I, I, I, I, I, P]),

@@ -229,6 +229,48 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
   }
 }
 
+// Device-resident hyper-parameters (hyper = {lr, step}): the launch carries no per-step host
+// scalars, so a step can be replayed from a HIP graph and a skipped step (found_inf, the
+// GradScaler rule of trainer.py:315-316) leaves the step count where it was.  Bias
+// corrections are formed in double from the device step, as torch computes them on the host.
+__global__ void __launch_bounds__(256) adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v, long n,
+                                                        const float* hyper, float b1, float b2, float eps,
+                                                        float wd, const float* inv_scale,
+                                                        const float* found_inf) {
+  if (found_inf && found_inf[0] != 0.f) return;
+  const float lr = hyper[0];
+  const double step = (double)hyper[1];
+  const float bc1 = (float)(1.0 - pow((double)b1, step));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, step));
+  const float is = inv_scale ? inv_scale[0] : 1.f;
+  const float step_size = lr / bc1;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float gi = g[i] * is;
+    float pi = p[i] * (1.f - lr * wd);
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    pi -= step_size * mi / (sqrtf(vi) / bc2_sqrt + eps);
+    p[i] = pi;
+  }
+}
+
+// hyper[1] += 1 unless the step is skipped (one thread)
+__global__ void step_advance_kernel(float* hyper, const float* found_inf) {
+  if (threadIdx.x == 0 && !(found_inf && found_inf[0] != 0.f)) hyper[1] = hyper[1] + 1.f;
+}
+
+// any non-finite in x0[0:n0] or x1[0:n1] -> flag[0] = 1 (flag zeroed by the caller)
+__global__ void __launch_bounds__(256) nonfinite2_kernel(const float* x0, long n0, const float* x1, long n1,
+                                                         float* flag) {
+  bool bad = false;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n0 + n1; i += (long)gridDim.x * 256)
+    bad |= !isfinite(i < n0 ? x0[i] : x1[i - n0]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) flag[0] = 1.f;
+}
+
 // any non-finite in x -> flag[0] = 1 (flag must be zeroed by the caller)
 __global__ void __launch_bounds__(256) nonfinite_kernel(const float* x, long n, float* flag) {
   bool bad = false;
@@ -350,6 +392,29 @@ int msu_adamw(float* p, const float* g, float* m, float* v, long n, float lr, fl
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream,
                      p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, (float)bc1,
                      (float)sqrt(bc2), inv_scale, found_inf);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_adamw_dev(float* p, const float* g, float* m, float* v, long n, const float* hyper, float beta1,
+                  float beta2, float eps, float weight_decay, const float* inv_scale, const float* found_inf,
+                  void* stream) {
+  if (n == 0) return 0;
+  if (hyper == nullptr) return -2;
+  hipLaunchKernelGGL(adamw_dev_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream,
+                     p, g, m, v, n, hyper, beta1, beta2, eps, weight_decay, inv_scale, found_inf);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_step_advance(float* hyper, const float* found_inf, void* stream) {
+  if (hyper == nullptr) return -2;
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper, found_inf);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_nonfinite2(const float* x0, long n0, const float* x1, long n1, float* flag, void* stream) {
+  if (n0 + n1 == 0) return 0;
+  hipLaunchKernelGGL(nonfinite2_kernel, dim3(grid_for(n0 + n1, 256, 16384)), dim3(256), 0, (hipStream_t)stream,
+                     x0, n0, x1, n1, flag);
   return MSU_CHECK_LAUNCH();
 }
 

@@ -427,7 +427,8 @@ int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const fl
                      float p_drop, unsigned long long seed, void* stream) {
   if (C != nh * HD) return -2;
   const WinGeom g = make_geom(B, H, W, C, nh, shift);
-  if ((long)B * H * W >= (1L << 31)) return -2;
+  // the MFMA kernels address qkv / dqkv rows with 32-bit products tok * 3C
+  if ((long)B * H * W * 3 * C >= (1L << 32)) return -2;
   const long items = g.nwin * nh;
   if (items == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
@@ -452,7 +453,8 @@ int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const f
                       float* workspace, int B, int H, int W, int C, int nh, int shift,
                       float p_drop, unsigned long long seed, void* stream, void* param_stream) {
   if (C != nh * HD) return -2;
-  if ((long)B * H * W >= (1L << 31)) return -2;
+  // the MFMA kernels address qkv / dqkv rows with 32-bit products tok * 3C
+  if ((long)B * H * W * 3 * C >= (1L << 32)) return -2;
   const WinGeom g = make_geom(B, H, W, C, nh, shift);
   hipStream_t st = (hipStream_t)stream;
   hipStream_t pst = (hipStream_t)param_stream;

@@ -52,6 +52,13 @@ def _next_seed():
     return _seed_rng.getrandbits(62)
 
 
+def reseed(seed):
+    """Restart the attention-dropout seed stream (per rank under data parallelism) and drop
+    the pooled stochastic-depth draws made under the previous seed."""
+    _seed_rng.seed(int(seed) ^ 0x5EED)
+    _SCALE_POOL.clear()
+
+
 _SCALE_POOL = {}
 _POOL_ROWS = 64
 

@@ -1011,5 +1011,23 @@ def adamw_(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay
               beta2, eps, weight_decay, int(step), _p(inv_scale), _p(found_inf), _s(param))
 
 
-def nonfinite_(x, flag):
-    _lib.call("msu_nonfinite", _p(x), x.numel(), _p(flag), _s(x))
+def nonfinite_(x, flag, x2=None):
+    """flag[0] = 1 if x (or x2) holds an inf / NaN (flag is zeroed by the caller)."""
+    if x2 is None:
+        _lib.call("msu_nonfinite", _p(x), x.numel(), _p(flag), _s(x))
+    else:
+        _lib.call("msu_nonfinite2", _p(x), x.numel(), _p(x2), x2.numel(), _p(flag), _s(x))
+
+
+def adamw_dev_(param, grad, exp_avg, exp_avg_sq, hyper, beta1, beta2, eps, weight_decay, inv_scale=None,
+               found_inf=None):
+    """AdamW over flat f32 buffers with lr and step read from the device tensor
+    ``hyper = [lr, step]``; no update at all when found_inf[0] != 0."""
+    _need_cuda(param)
+    _lib.call("msu_adamw_dev", _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), _p(hyper),
+              beta1, beta2, eps, weight_decay, _p(inv_scale), _p(found_inf), _s(param))
+
+
+def step_advance_(hyper, found_inf=None):
+    """hyper[1] += 1 unless found_inf[0] != 0 (a skipped step is not counted)."""
+    _lib.call("msu_step_advance", _p(hyper), _p(found_inf), _s(hyper))

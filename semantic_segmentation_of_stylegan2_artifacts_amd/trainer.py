@@ -173,12 +173,26 @@ class GradBucketer:
         self.launched = [False] * len(self.buckets)
 
 
+def reseed(seed, rank=0):
+    """Per-rank randomness for data parallelism: the model is built from the shared seed
+    (identical initial weights on every rank), then every rank draws its own drop-path and
+    dropout masks (torch CPU/HIP generators and the attention-dropout seed stream), so the
+    global batch sees independent masks per sample, as the reference's single process does."""
+    from .network import model_parts
+    s = int(seed) + 1_000_003 * int(rank)
+    torch.manual_seed(s)  # seeds the HIP generators of every device too
+    model_parts.reseed(s)
+
+
 class Trainer:
     def __init__(self, model, config, device, lr=None, amp_dtype=torch.bfloat16, bucket_mb=32,
-                 world_size=1, process_group=None):
+                 world_size=1, process_group=None, rank=0, seed=None, skip_nonfinite=True):
         self.model = model
         self.device = device
         self.amp_dtype = amp_dtype
+        self.rank = rank
+        if seed is not None:
+            reseed(seed, rank)
         core = model.ms_unet if hasattr(model, "ms_unet") else model
         dead = set()
         if hasattr(core, "dead_modules"):
@@ -195,7 +209,14 @@ class Trainer:
         opt = config.TRAIN.OPTIMIZER
         self.betas = tuple(opt.BETAS)
         self.eps = float(opt.EPS)
+        # device-resident step scalars {lr, step}: AdamW reads them on the GPU, so a skipped
+        # (non-finite) step is not counted without a host sync, and the launch is replayable
+        self.hyper = torch.zeros(2, device=device, dtype=torch.float32)
         self.lr = float(config.TRAIN.BASE_LR if lr is None else lr)
+        # GradScaler semantics (trainer.py:182,315-316): a step whose gradients hold an inf /
+        # NaN leaves parameters and moments untouched
+        self.skip_nonfinite = skip_nonfinite
+        self.found_inf = torch.zeros(1, device=device, dtype=torch.float32)
         t = config.TRAIN
         self.loss_fn = DynamicLoss(alpha=t.TVERSKY_LOSS_ALPHA, beta=t.TVERSKY_LOSS_BETA,
                                    tversky_bce_mix=t.LOSS_TVERSKY_BCE_MIX)
@@ -203,7 +224,21 @@ class Trainer:
         self.step_count = 0
         self._shadow_fresh = False
         self.inv_world = torch.full((1,), 1.0 / world_size, device=device, dtype=torch.float32)
-        self.reducer = GradBucketer(self.groups, bucket_mb << 20, process_group) if world_size > 1 else None
+        self.reducer = (GradBucketer(self.groups, int(bucket_mb * (1 << 20)), process_group)
+                        if world_size > 1 else None)
+
+    @property
+    def lr(self):
+        return self._lr
+
+    @lr.setter
+    def lr(self, value):
+        self._lr = float(value)
+        self.hyper[0:1].fill_(self._lr)
+
+    def optimizer_steps(self):
+        """AdamW steps actually applied (skipped non-finite steps excluded); syncs."""
+        return int(self.hyper[1].item())
 
     def num_params(self):
         return sum(g.count for g in self.groups)
@@ -242,9 +277,17 @@ class Trainer:
             # queued, not after the last launch of the step (it left the GPU idle there)
             for g in self.groups:
                 g.mark_shadow()
+        found = None
+        if self.skip_nonfinite:
+            # after the all-reduce: an inf on any rank reaches every rank's sum, so all ranks
+            # skip together
+            found = self.found_inf
+            found.zero_()
+            ops.nonfinite_(self.groups[0].grad, found, self.groups[1].grad)
+        ops.step_advance_(self.hyper, found)
         for g in self.groups:
-            ops.adamw_(g.data, g.grad, g.exp_avg, g.exp_avg_sq, self.lr, self.betas[0], self.betas[1],
-                       self.eps, g.weight_decay, self.step_count, inv_scale=inv)
+            ops.adamw_dev_(g.data, g.grad, g.exp_avg, g.exp_avg_sq, self.hyper, self.betas[0], self.betas[1],
+                           self.eps, g.weight_decay, inv_scale=inv, found_inf=found)
             g.grad.zero_()
             if bf16:  # keeps evaluation between steps on the updated weights
                 if _EARLY_MARK:

@@ -96,6 +96,11 @@ def model_cases():
                                  num_heads=[1, 2, 4, 8], drop_path_rate=0.0), batch=1, seed=12),
         "swinT224": dict(cfg=dict(img_size=224, embed_dim=96, depths=[2, 2, 2, 2],
                                   num_heads=[3, 6, 12, 24], drop_path_rate=0.0), batch=1, seed=13),
+        # the Swin-S / Swin-B stacks (depth-18 stage 2, C=128 for B) at 224^2
+        "swinS224": dict(cfg=dict(img_size=224, embed_dim=96, depths=[2, 2, 18, 2],
+                                  num_heads=[3, 6, 12, 24], drop_path_rate=0.0), batch=1, seed=14),
+        "swinB224": dict(cfg=dict(img_size=224, embed_dim=128, depths=[2, 2, 18, 2],
+                                  num_heads=[4, 8, 16, 32], drop_path_rate=0.0), batch=2, seed=15),
     }
 
 

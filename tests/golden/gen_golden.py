@@ -141,8 +141,10 @@ def gen_ops():
     print("ops_reference.npz:", len(out), "arrays")
 
 
-def gen_msunet():
+def gen_msunet(only=None):
     for name, spec in cases.model_cases().items():
+        if only and name not in only:
+            continue
         cfg = make_cfg(**spec["cfg"])
         model = ref_msunetsys(cfg)
         params = cases.model_params(cfg, spec["seed"])
@@ -197,6 +199,10 @@ if __name__ == "__main__":
     sys.path.insert(0, REF)
     install_shims()
     torch.set_num_threads(8)
+    only = sys.argv[1:]  # model case names: regenerate just those fixtures
+    if only:
+        gen_msunet(only)
+        sys.exit(0)
     gen_dynamic_loss()
     gen_ops()
     gen_msunet()

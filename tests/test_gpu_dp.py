@@ -1,0 +1,128 @@
+"""GPU: the data-parallel PRODUCT path with two ranks on one device.
+
+Two processes (gloo process group, both on cuda:0) drive the real ``Trainer``: parameters in
+flat buffers, backward kernels accumulating straight into ``.grad`` and reporting through
+``ops._notify``, Linear weight gradients and attention parameter tails on the side stream,
+``GradBucketer`` issuing each bucket's all-reduce from the side stream as its accumulation
+count is reached (learned on step 0, overlapped with backward from step 1 on).  Checks:
+
+* the all-reduced gradient of two ranks with one image each equals the single-process
+  gradient of the 2-image global batch (the reference's nn.DataParallel semantics,
+  trainer.py:96-97: mean over the global batch), on the first (post-backward) and second
+  (overlapped) step, with small 64 KB buckets so that many launch mid-backward;
+* after three full Trainer steps the parameters and AdamW moments are bitwise identical
+  on both ranks (fp32 and bf16 training modes).
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import cases  # noqa: E402
+from oracle.msunet import make_cfg  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _build():
+    from semantic_segmentation_of_stylegan2_artifacts_amd.network.model_parts import MSUNetSys
+    spec = cases.model_cases()["swinT224"]
+    cfg = make_cfg(**spec["cfg"])
+    m = MSUNetSys(img_size=cfg["img_size"], embed_dim=cfg["embed_dim"], depths=cfg["depths"],
+                  num_heads=cfg["num_heads"], drop_rate=0.0, attn_drop_rate=0.0, drop_path_rate=0.0)
+    m.load_state_dict(cases.model_params(cfg, spec["seed"]), strict=True)
+    x, t = cases.model_inputs(cfg, 2, spec["seed"])
+    return m, x, t
+
+
+def _conf():
+    from semantic_segmentation_of_stylegan2_artifacts_amd import load_config
+    return load_config(None, "swin_t", **{"TRAIN.BASE_LR": 1e-3})
+
+
+def _worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import Trainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    out = {}
+    for amp in (torch.float32, torch.bfloat16):
+        model, x, t = _build()
+        model = model.to(dev).train()
+        x, t = x[rank:rank + 1].to(dev), t[rank:rank + 1].to(dev)
+        # ~64 KB buckets: many all-reduces launch mid-backward
+        tr = Trainer(model, _conf(), dev, amp_dtype=amp, bucket_mb=1 / 16, world_size=world,
+                     process_group=dist.group.WORLD, rank=rank, seed=0)
+        if amp == torch.float32:
+            # the gradient exchange exactly as Trainer.step runs it, captured before AdamW
+            for step in range(2):
+                ops.set_grad_ready_callback(tr.reducer._hook)
+                tr.reducer.main_stream = torch.cuda.current_stream(dev)
+                loss = tr.forward_loss(x, t)
+                loss.backward()
+                if step == 1:
+                    launched_early = sum(tr.reducer.launched)
+                tr.reducer.finish()
+                ops.join_side_streams()
+                out[f"grad{step}"] = torch.cat([g.grad.clone() for g in tr.groups]).cpu()
+                for g in tr.groups:
+                    g.grad.zero_()
+            out["launched_early"] = launched_early
+            out["nbuckets"] = len(tr.reducer.buckets)
+            # (name, offset into the concatenated flat gradient) per parameter
+            base, layout = 0, []
+            for g in tr.groups:
+                layout += [(n, base + o) for n, o in zip(g.names, g.offsets)]
+                base += g.numel
+            out["names"] = [n for n, _ in layout]
+            out["offsets"] = [o for _, o in layout]
+        for _ in range(3):
+            tr.step(x, t)
+        torch.cuda.synchronize()
+        tag = "f32" if amp == torch.float32 else "bf16"
+        out[f"state_{tag}"] = torch.cat([torch.cat([g.data, g.exp_avg, g.exp_avg_sq]) for g in tr.groups]).cpu()
+        ops.set_grad_ready_callback(None)
+    torch.save(out, os.path.join(outdir, f"rank{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_dp_product_path_two_ranks_one_gpu(tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [torch.load(os.path.join(tmp_path, f"rank{k}.pt"), weights_only=True) for k in range(world)]
+    assert r[0]["nbuckets"] > 20
+    assert r[1]["launched_early"] > 0, "no bucket all-reduce overlapped backward"
+    for key in ("grad0", "grad1", "state_f32", "state_bf16"):
+        assert torch.equal(r[0][key], r[1][key]), f"ranks disagree on {key}"
+
+    # single process, global batch of 2, plain autograd on the same weights (fp32 mode)
+    from semantic_segmentation_of_stylegan2_artifacts_amd.loss import DynamicLoss
+    model, x, t = _build()
+    model = model.cuda().train()
+    loss = DynamicLoss(alpha=0.2, beta=0.8, tversky_bce_mix=0.45)(model(x.cuda()), t.cuda())
+    loss.backward()
+    params = dict(model.named_parameters())
+    conf = _conf()
+    assert conf.TRAIN.TVERSKY_LOSS_ALPHA == 0.2 and conf.TRAIN.LOSS_TVERSKY_BCE_MIX == 0.45
+    for step in ("grad0", "grad1"):
+        flat = r[0][step]
+        worst = 0.0
+        for name, off in zip(r[0]["names"], r[0]["offsets"]):
+            ref = params[name].grad
+            got = flat[off: off + ref.numel()].view_as(ref) * 0.5  # sum over ranks -> global mean
+            scale = ref.abs().max().item() + 1e-12
+            worst = max(worst, (got - ref.cpu()).abs().max().item() / scale)
+        assert worst < 1e-4, (step, worst)
