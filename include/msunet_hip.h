@@ -181,15 +181,16 @@ int msu_seg_metrics(int dtype, const void* logits, const float* label, int B, lo
 int msu_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
               float beta2, float eps, float weight_decay, int step, const float* inv_scale,
               const float* found_inf, void* stream);
-/* As msu_adamw with the per-step scalars in device memory, hyper = {lr, step} (f32): the
- * launch holds no host scalar that changes per step (HIP-graph replayable).  Skips when
- * found_inf[0] != 0 (GradScaler.step, trainer.py:182,315-316). */
-int msu_adamw_dev(float* p, const float* g, float* m, float* v, long n, const float* hyper, float beta1,
-                  float beta2, float eps, float weight_decay, const float* inv_scale, const float* found_inf,
+/* As msu_adamw with the per-step scalars in device memory, hyper = {lr, step} (f64): the
+ * launch holds no host scalar that changes per step (HIP-graph replayable); scalars are
+ * formed in double like torch.optim.AdamW's.  Skips when found_inf[0] != 0 (GradScaler.step,
+ * trainer.py:182,315-316). */
+int msu_adamw_dev(float* p, const float* g, float* m, float* v, long n, const double* hyper, double beta1,
+                  double beta2, double eps, double weight_decay, const float* inv_scale, const float* found_inf,
                   void* stream);
 /* hyper[1] += 1 unless found_inf[0] != 0 (the skipped step does not count, as torch's AdamW
  * `step` state is not advanced when GradScaler skips optimizer.step). */
-int msu_step_advance(float* hyper, const float* found_inf, void* stream);
+int msu_step_advance(double* hyper, const float* found_inf, void* stream);
 /* flag[0] = 1 if any element of x (x0[0:n0], x1[0:n1]) is inf/NaN; flag zeroed by the caller
  * (GradScaler's non-finite check, torch._amp_foreach_non_finite_check_and_unscale_). */
 int msu_nonfinite(const float* x, long n, float* flag, void* stream);

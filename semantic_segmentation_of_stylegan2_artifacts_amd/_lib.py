@@ -14,6 +14,7 @@ P = ctypes.c_void_p
 I = ctypes.c_int
 L = ctypes.c_long
 F = ctypes.c_float
+D = ctypes.c_double
 U64 = ctypes.c_ulonglong
 
 # name -> (restype, argtypes); must match include/msunet_hip.h
@@ -40,7 +41,7 @@ SIGNATURES = {
     "msu_adamw": (I, [P, P, P, P, L, F, F, F, F, F, I, P, P, P]),
     "msu_nonfinite": (I, [P, L, P, P]),
     "msu_nonfinite2": (I, [P, L, P, L, P, P]),
-    "msu_adamw_dev": (I, [P, P, P, P, L, P, F, F, F, F, P, P, P]),
+    "msu_adamw_dev": (I, [P, P, P, P, L, P, D, D, D, D, P, P, P]),
     "msu_step_advance": (I, [P, P, P]),
     "msu_cast": (I, [I, P, P, L, P]),
     "msu_conv3x3_fwd": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),

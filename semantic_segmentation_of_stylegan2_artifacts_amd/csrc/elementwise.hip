@@ -229,37 +229,43 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
   }
 }
 
-// Device-resident hyper-parameters (hyper = {lr, step}): the launch carries no per-step host
-// scalars, so a step can be replayed from a HIP graph and a skipped step (found_inf, the
-// GradScaler rule of trainer.py:315-316) leaves the step count where it was.  Bias
-// corrections are formed in double from the device step, as torch computes them on the host.
+// Device-resident hyper-parameters (hyper = {lr, step}, f64): the launch carries no per-step
+// host scalar, so a step can be replayed from a HIP graph and a skipped step (found_inf, the
+// GradScaler rule of trainer.py:315-316) leaves the step count where it was.  Every scalar is
+// formed in double and rounded once, and the update follows torch.optim.AdamW's operation
+// order (param.mul_(1 - lr*wd); exp_avg.lerp_(g, 1 - b1); exp_avg_sq.mul_(b2).addcmul_(g, g,
+// 1 - b2); param.addcdiv_(exp_avg, sqrt(exp_avg_sq) / sqrt(bc2) + eps, -lr / bc1)).
 __global__ void __launch_bounds__(256) adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v, long n,
-                                                        const float* hyper, float b1, float b2, float eps,
-                                                        float wd, const float* inv_scale,
+                                                        const double* hyper, double b1, double b2, float eps,
+                                                        double wd, const float* inv_scale,
                                                         const float* found_inf) {
+#pragma clang fp contract(off)
   if (found_inf && found_inf[0] != 0.f) return;
-  const float lr = hyper[0];
-  const double step = (double)hyper[1];
-  const float bc1 = (float)(1.0 - pow((double)b1, step));
-  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, step));
+  const double lr = hyper[0];
+  const double step = hyper[1];
+  const float decay = (float)(1.0 - lr * wd);
+  const float w1 = (float)(1.0 - b1);
+  const float b2f = (float)b2, w2 = (float)(1.0 - b2);
+  const float neg_step_size = (float)(-(lr / (1.0 - pow(b1, step))));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow(b2, step));
   const float is = inv_scale ? inv_scale[0] : 1.f;
-  const float step_size = lr / bc1;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const float gi = g[i] * is;
-    float pi = p[i] * (1.f - lr * wd);
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    const float gi = inv_scale ? g[i] * is : g[i];
+    const float pi = p[i] * decay;
+    float mi = m[i];
+    mi = w1 < 0.5f ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.f - w1);  // ATen lerp
+    const float vi = v[i] * b2f + w2 * gi * gi;
     m[i] = mi;
     v[i] = vi;
-    pi -= step_size * mi / (sqrtf(vi) / bc2_sqrt + eps);
-    p[i] = pi;
+    const float denom = __fsqrt_rn(vi) / bc2_sqrt + eps;
+    p[i] = pi + neg_step_size * (mi / denom);
   }
 }
 
 // hyper[1] += 1 unless the step is skipped (one thread)
-__global__ void step_advance_kernel(float* hyper, const float* found_inf) {
-  if (threadIdx.x == 0 && !(found_inf && found_inf[0] != 0.f)) hyper[1] = hyper[1] + 1.f;
+__global__ void step_advance_kernel(double* hyper, const float* found_inf) {
+  if (threadIdx.x == 0 && !(found_inf && found_inf[0] != 0.f)) hyper[1] = hyper[1] + 1.0;
 }
 
 // any non-finite in x0[0:n0] or x1[0:n1] -> flag[0] = 1 (flag zeroed by the caller)
@@ -395,17 +401,17 @@ int msu_adamw(float* p, const float* g, float* m, float* v, long n, float lr, fl
   return MSU_CHECK_LAUNCH();
 }
 
-int msu_adamw_dev(float* p, const float* g, float* m, float* v, long n, const float* hyper, float beta1,
-                  float beta2, float eps, float weight_decay, const float* inv_scale, const float* found_inf,
+int msu_adamw_dev(float* p, const float* g, float* m, float* v, long n, const double* hyper, double beta1,
+                  double beta2, double eps, double weight_decay, const float* inv_scale, const float* found_inf,
                   void* stream) {
   if (n == 0) return 0;
   if (hyper == nullptr) return -2;
   hipLaunchKernelGGL(adamw_dev_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream,
-                     p, g, m, v, n, hyper, beta1, beta2, eps, weight_decay, inv_scale, found_inf);
+                     p, g, m, v, n, hyper, beta1, beta2, (float)eps, weight_decay, inv_scale, found_inf);
   return MSU_CHECK_LAUNCH();
 }
 
-int msu_step_advance(float* hyper, const float* found_inf, void* stream) {
+int msu_step_advance(double* hyper, const float* found_inf, void* stream) {
   if (hyper == nullptr) return -2;
   hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper, found_inf);
   return MSU_CHECK_LAUNCH();

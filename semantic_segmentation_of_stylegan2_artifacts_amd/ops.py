@@ -128,10 +128,20 @@ def _guard_side_write(p, ev):
         p._msu_side_hooked = True
 
 
+# Tensors a side-stream kernel is still reading.  record_stream only keeps their memory from
+# being reused; it does not stop autograd from accumulating into them IN PLACE: a gradient
+# returned for two inputs (the add-LN backward hands the same `da` to the residual and to the
+# branch) is "stealable" by autograd's InputBuffer once its use count drops to one, and the
+# main stream would then add into it while a side-stream weight gradient still reads it.  One
+# extra reference per tensor, held until the end-of-backward join, keeps it out of reach.
+_side_keep = []
+
+
 def _end_of_backward():
     global _join_queued
     _join_queued = False
     join_side_streams()
+    _side_keep.clear()  # the main stream now waits for every side-stream read
 
 
 def _join_at_end_of_backward():
@@ -479,6 +489,8 @@ def _wgrad(dy, x, weight, bias, M, N, K):
                           _p(None if bias is None else bias.grad), _p(ws), M, N, K, 1, side.cuda_stream)
             dy.record_stream(side)  # their memory is not reused by the main stream meanwhile
             x.record_stream(side)
+            _side_keep.append(dy)  # ... nor accumulated into in place (see _side_keep)
+            _side_keep.append(x)
             ev = torch.cuda.Event()
             ev.record(side)
             _guard_side_write(weight, ev)

@@ -211,7 +211,7 @@ class Trainer:
         self.eps = float(opt.EPS)
         # device-resident step scalars {lr, step}: AdamW reads them on the GPU, so a skipped
         # (non-finite) step is not counted without a host sync, and the launch is replayable
-        self.hyper = torch.zeros(2, device=device, dtype=torch.float32)
+        self.hyper = torch.zeros(2, device=device, dtype=torch.float64)
         self.lr = float(config.TRAIN.BASE_LR if lr is None else lr)
         # GradScaler semantics (trainer.py:182,315-316): a step whose gradients hold an inf /
         # NaN leaves parameters and moments untouched

@@ -25,13 +25,13 @@ def _ctype_of(decl):
     if "*" in d:
         return "P"
     t = d.rsplit(" ", 1)[0].strip()
-    return {"int": "I", "long": "L", "float": "F", "unsigned long long": "U64"}[t]
+    return {"int": "I", "long": "L", "float": "F", "double": "D", "unsigned long long": "U64"}[t]
 
 
 def test_header_and_bindings_agree():
     decl = _declared()
     assert decl, "no declarations parsed"
-    names = {v: k for k, v in vars(_lib).items() if k in ("P", "I", "L", "F", "U64")}
+    names = {v: k for k, v in vars(_lib).items() if k in ("P", "I", "L", "F", "D", "U64")}
     assert set(decl) == set(_lib.SIGNATURES), set(decl) ^ set(_lib.SIGNATURES)
     for name, (ret, args) in decl.items():
         res, argtypes = _lib.SIGNATURES[name]

@@ -119,10 +119,12 @@ def test_dp_product_path_two_ranks_one_gpu(tmp_path):
     assert conf.TRAIN.TVERSKY_LOSS_ALPHA == 0.2 and conf.TRAIN.LOSS_TVERSKY_BCE_MIX == 0.45
     for step in ("grad0", "grad1"):
         flat = r[0][step]
-        worst = 0.0
+        errs = []
         for name, off in zip(r[0]["names"], r[0]["offsets"]):
             ref = params[name].grad
             got = flat[off: off + ref.numel()].view_as(ref) * 0.5  # sum over ranks -> global mean
             scale = ref.abs().max().item() + 1e-12
-            worst = max(worst, (got - ref.cpu()).abs().max().item() / scale)
-        assert worst < 1e-4, (step, worst)
+            errs.append(((got - ref.cpu()).abs().max().item() / scale, name))
+        errs.sort(reverse=True)
+        bad = [e for e in errs if e[0] >= 1e-4]
+        assert not bad, (step, len(bad), bad[:8])

@@ -129,25 +129,38 @@ def test_nonfinite_gradient_skips_the_step():
     for g, d in zip(tr.groups, snap):
         assert torch.equal(g.data, d)
     assert tr.optimizer_steps() == 1
-    # the next finite step is AdamW step 2 of torch: compare against torch.optim.AdamW run
-    # for two steps on the same gradients
-    from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import is_no_decay
-    live = {n for g in tr.groups for n in g.names}
-    decay = [p for n, p in ref.named_parameters() if n in live and not is_no_decay(n, p)]
-    nodecay = [p for n, p in ref.named_parameters() if n in live and is_no_decay(n, p)]
-    opt = torch.optim.AdamW([{"params": decay, "weight_decay": conf.TRAIN.WEIGHT_DECAY},
-                             {"params": nodecay, "weight_decay": 0.0}], lr=tr.lr,
-                            betas=tuple(conf.TRAIN.OPTIMIZER.BETAS), eps=conf.TRAIN.OPTIMIZER.EPS)
-    for _ in range(2):
-        opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            lr_ = tr.loss_fn(ref(x), target)
-        lr_.backward()
-        opt.step()
     tr.step(x, target)
     assert tr.optimizer_steps() == 2
-    rp = dict(ref.named_parameters())
-    for g in tr.groups:
-        for name, p in zip(g.names, g.params):
-            # a wrong bias correction (step 3) would be off by ~0.4 * lr = 4e-4
-            torch.testing.assert_close(p.detach(), rp[name].detach(), rtol=1e-4, atol=2e-5, msg=name)
+
+
+def test_adamw_dev_skip_matches_torch_adamw():
+    """The device-hyper AdamW (lr / step read on the GPU) over three steps, the middle one
+    flagged non-finite, equals torch.optim.AdamW run on the two finite steps only (the skipped
+    step neither updates nor advances the bias-correction step)."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    g = torch.Generator().manual_seed(7)
+    n = 10007
+    p0 = torch.randn(n, generator=g)
+    grads = [torch.randn(n, generator=g) * s for s in (1.0, 3.0, 0.5)]
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-2, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.05)
+    for k in (0, 2):
+        ref.grad = grads[k].clone()
+        opt.step()
+    p = p0.to(DEV)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    hyper = torch.tensor([1e-2, 0.0], device=DEV, dtype=torch.float64)
+    found = torch.zeros(1, device=DEV)
+    for k in range(3):
+        gd = grads[k].to(DEV)
+        if k == 1:
+            gd[17] = float("inf")
+        found.zero_()
+        ops.nonfinite_(gd, found)
+        ops.step_advance_(hyper, found)
+        ops.adamw_dev_(p, gd, m, v, hyper, 0.9, 0.999, 1e-8, 0.05, found_inf=found)
+    assert hyper[1].item() == 2.0
+    # same scalars and operation order as torch: a few ulp at most (CPU vs GPU rounding)
+    torch.testing.assert_close(p.cpu(), ref.detach(), rtol=4e-7, atol=1e-8)
+    torch.testing.assert_close(m.cpu(), opt.state[ref]["exp_avg"], rtol=4e-7, atol=1e-9)
+    torch.testing.assert_close(v.cpu(), opt.state[ref]["exp_avg_sq"], rtol=4e-7, atol=1e-12)
