@@ -7,7 +7,8 @@
  * values.  Return value: 0 on success, -2 bad shape/arguments, -3 unsupported mode,
  * -4 LDS budget exceeded, -1 launch error.
  *
- * dtype: 0 = f32 activations (parity mode), 1 = bf16 activations (training mode).
+ * dtype: 0 = f32 activations (parity mode), 1 = bf16 activations (training mode), 2 = f16
+ * activations (the reference's torch.amp.autocast(float16) step, trainer.py:308).
  * Parameters, statistics and parameter gradients are always f32.
  *
  * The reference path is Python (network/model_parts.py, torchvision SwinTransformerBlock,
@@ -123,7 +124,8 @@ int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float*
                      long M, int N, int K, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------- Linear forward / input gradient
- * Token GEMM (bf16 in/out, f32 accumulate) for the same Linears as msu_linear_wgrad:
+ * Token GEMM (dtype 1 bf16 / 2 f16 in and out, f32 accumulate) for the same Linears as
+ * msu_linear_wgrad:
  * Y[M][N] = epi(A[M][K] . W[N][K]^T + bias[N]); input gradients pass W^T ([K][N]).
  *   epi 0  plain, optional bias; A2 != null: A's columns [K1, K) come from A2 ([M][K-K1]) --
  *          the skip-fusion torch.cat([x, skip], -1) -> concat_back_dim (model_parts.py:792-794,
@@ -135,7 +137,7 @@ int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float*
  * epilogues cap the column chunk); uncovered shapes are the caller's to route to a library GEMM. */
 int msu_tok_gemm_supported(long M, int N, int K);
 int msu_tok_gemm_supported_epi(long M, int N, int K, int epi);
-int msu_tok_gemm(const void* A, const void* A2, int K1, const void* W, const float* bias, void* Y,
+int msu_tok_gemm(int dtype, const void* A, const void* A2, int K1, const void* W, const float* bias, void* Y,
                  void* Y2, const void* H, long M, int N, int K, int epi, void* stream);
 int msu_tok_gemm_plan(long M, int N, int K, long* out6);
 

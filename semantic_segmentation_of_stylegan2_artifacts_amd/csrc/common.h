@@ -1,6 +1,9 @@
 // Shared device helpers for the MS-UNet gfx950 kernels.
-// Activations are either f32 (parity mode) or bf16 (training mode); every reduction and
-// every normalisation statistic is computed in f32.
+// Activations are f32 (parity mode), bf16 (training mode) or f16 (the reference's
+// torch.amp.autocast(float16), trainer.py:308); every reduction and every normalisation
+// statistic is computed in f32.  The two 16-bit formats share every kernel: the storage is
+// moved as raw 16-bit words (bf16x8 below is only a 16-byte operand container) and only the
+// conversions and the MFMA opcode depend on the format (Fmt16<T>).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
@@ -14,8 +17,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // register-resident 16-B chunk
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t bf16_t;  // storage type of a bf16 activation
+typedef _Float16 f16_t;   // storage type of an f16 activation
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-enum MsuDtype { MSU_F32 = 0, MSU_BF16 = 1 };
+enum MsuDtype { MSU_F32 = 0, MSU_BF16 = 1, MSU_F16 = 2 };
 
 // ------------------------------------------------------------------ scalar conversion
 MSU_DEV float to_f32(float v) { return v; }
@@ -25,6 +30,49 @@ template <> MSU_DEV float from_f32<float>(float v) { return v; }
 template <> MSU_DEV bf16_t from_f32<bf16_t>(float v) {
   __hip_bfloat16 h = __float2bfloat16(v);  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
   return *reinterpret_cast<bf16_t*>(&h);
+}
+
+MSU_DEV float to_f32(f16_t v) { return (float)v; }
+template <> MSU_DEV f16_t from_f32<f16_t>(float v) { return (f16_t)v; }  // v_cvt_f16_f32 (RNE)
+
+// ------------------------------------------------------------------ 16-bit formats
+// Raw-word view of a 16-bit activation format: encode / decode through a uint32 word pair and
+// the matching MFMA opcodes on 8-element operands held in a bf16x8 container.
+template <typename T> struct Fmt16;
+template <> struct Fmt16<bf16_t> {
+  static MSU_DEV uint32_t bits(float v) { return (uint32_t)from_f32<bf16_t>(v); }
+  static MSU_DEV float lo(uint32_t w) { return __uint_as_float(w << 16); }
+  static MSU_DEV float hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+  static MSU_DEV f32x16 mma32(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  static MSU_DEV f32x4 mma16(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Fmt16<f16_t> {
+  static MSU_DEV uint32_t bits(float v) { return (uint32_t)__builtin_bit_cast(uint16_t, (f16_t)v); }
+  static MSU_DEV float lo(uint32_t w) { return (float)__builtin_bit_cast(f16_t, (uint16_t)(w & 0xffffu)); }
+  static MSU_DEV float hi(uint32_t w) { return (float)__builtin_bit_cast(f16_t, (uint16_t)(w >> 16)); }
+  static MSU_DEV f32x16 mma32(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                  0, 0, 0);
+  }
+  static MSU_DEV f32x4 mma16(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                  0, 0, 0);
+  }
+};
+// two values -> one packed 32-bit word (lo in bits 0-15)
+template <typename T> MSU_DEV uint32_t pack2(float lo, float hi) {
+  return Fmt16<T>::bits(lo) | (Fmt16<T>::bits(hi) << 16);
+}
+// the 16-bit word of a stored value (for hi/lo splits: bits of from_f32<T>(v))
+template <typename T> MSU_DEV float round16(float v) { return to_f32(from_f32<T>(v)); }
+// a bf16x8 container of eight constants
+template <typename T> MSU_DEV bf16x8 splat8(float a0, float a1, float rest) {
+  u32x4 w = {pack2<T>(a0, a1), pack2<T>(rest, rest), pack2<T>(rest, rest), pack2<T>(rest, rest)};
+  return __builtin_bit_cast(bf16x8, w);
 }
 
 // ------------------------------------------------------------------ 4-wide vector I/O
@@ -49,6 +97,20 @@ template <> struct Vec4<bf16_t> {
     uint2 q;
     q.x = (uint32_t)from_f32<bf16_t>(v[0]) | ((uint32_t)from_f32<bf16_t>(v[1]) << 16);
     q.y = (uint32_t)from_f32<bf16_t>(v[2]) | ((uint32_t)from_f32<bf16_t>(v[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = q;
+  }
+};
+
+template <> struct Vec4<f16_t> {
+  static MSU_DEV void load(const f16_t* p, float (&v)[4]) {
+    uint2 q = *reinterpret_cast<const uint2*>(p);
+    v[0] = Fmt16<f16_t>::lo(q.x); v[1] = Fmt16<f16_t>::hi(q.x);
+    v[2] = Fmt16<f16_t>::lo(q.y); v[3] = Fmt16<f16_t>::hi(q.y);
+  }
+  static MSU_DEV void store(f16_t* p, const float (&v)[4]) {
+    uint2 q;
+    q.x = pack2<f16_t>(v[0], v[1]);
+    q.y = pack2<f16_t>(v[2], v[3]);
     *reinterpret_cast<uint2*>(p) = q;
   }
 };
@@ -144,6 +206,36 @@ __device__ __attribute__((aligned(16))) uint32_t g_zero_region[1024];
 MSU_DEV const void* zero_src(int slot) { return g_zero_region + 4 * (slot & 255); }
 
 #define MSU_CHECK_LAUNCH() (hipGetLastError() == hipSuccess ? 0 : -1)
+
+// Run a statement with T bound to the storage type of `dtype` (f32 / bf16 / f16).
+#define MSU_DISPATCH(dtype, T, ...)          \
+  switch (dtype) {                           \
+    case MSU_BF16: {                         \
+      typedef bf16_t T;                      \
+      __VA_ARGS__;                           \
+    } break;                                 \
+    case MSU_F16: {                          \
+      typedef f16_t T;                       \
+      __VA_ARGS__;                           \
+    } break;                                 \
+    default: {                               \
+      typedef float T;                       \
+      __VA_ARGS__;                           \
+    }                                        \
+  }
+// the 16-bit formats only (f32 handled by the caller)
+#define MSU_DISPATCH16(dtype, T, ...)        \
+  switch (dtype) {                           \
+    case MSU_F16: {                          \
+      typedef f16_t T;                       \
+      __VA_ARGS__;                           \
+    } break;                                 \
+    default: {                               \
+      typedef bf16_t T;                      \
+      __VA_ARGS__;                           \
+    }                                        \
+  }
+inline bool msu_is16(int dtype) { return dtype == MSU_BF16 || dtype == MSU_F16; }
 
 // Order stream `pst` after the work queued so far on `st` (an event; one per host thread,
 // reused: each record captures the state at that moment).  pst == st or null: nothing.

@@ -100,16 +100,15 @@ MSU_DEV void stage_halo(const T* X, T* sX, int b, int y_first, int nrows, int x0
 
 // acc += A(16 x 32) B(32 x 16) with both operands k-contiguous in LDS.
 template <typename T> struct KC;
-template <> struct KC<bf16_t> {
-  static MSU_DEV void mma(f32x4& acc, const bf16_t* A, int lda, const bf16_t* B, int ldb, int lane) {
+template <typename T> struct KC16 {
+  static MSU_DEV void mma(f32x4& acc, const T* A, int lda, const T* B, int ldb, int lane) {
     const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + (lane & 15) * lda + 8 * (lane >> 4));
     const bf16x8 b = *reinterpret_cast<const bf16x8*>(B + (lane & 15) * ldb + 8 * (lane >> 4));
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-  }
-  static MSU_DEV bf16x8 fragA(const bf16_t* A, int lda, int lane) {
-    return *reinterpret_cast<const bf16x8*>(A + (lane & 15) * lda + 8 * (lane >> 4));
+    acc = Fmt16<T>::mma16(a, b, acc);
   }
 };
+template <> struct KC<bf16_t> : KC16<bf16_t> {};
+template <> struct KC<f16_t> : KC16<f16_t> {};
 template <> struct KC<float> {
   static MSU_DEV void mma(f32x4& acc, const float* A, int lda, const float* B, int ldb, int lane) {
     const float* pa = A + (lane & 15) * lda + (lane >> 4);
@@ -235,8 +234,8 @@ __global__ void __launch_bounds__(64 * (TH / MT)) conv3x3_kernel(const T* __rest
   }
 }
 
-// ------------------------------------------------------------------ bf16 fwd / dgrad, v2
-// Persistent implicit GEMM on v_mfma_f32_32x32x16_bf16 (Cout = 32*NCT, CinP = 16*KS).  One
+// ------------------------------------------------------------------ 16-bit fwd / dgrad, v2
+// Persistent implicit GEMM on v_mfma_f32_32x32x16_{bf16,f16} (raw 16-bit storage; T = format) (Cout = 32*NCT, CinP = 16*KS).  One
 // workgroup of NW waves per CU loops over output tiles of NW*MT rows x 32 pixels x all
 // Cout; wave w owns MT image rows.  D[co][pixel] = W_tap[co][ci] * X[ci][pixel]: the weight
 // fragment is the A operand, so each lane ends with 4 consecutive output channels of one
@@ -251,22 +250,18 @@ __global__ void __launch_bounds__(64 * (TH / MT)) conv3x3_kernel(const T* __rest
 //     GELU' epilogue.
 // Index math of the halo chunks goes through opaque() so it is recomputed per tile instead
 // of pinning registers for the whole persistent loop.
-MSU_DEV void unpack8(const u32x4& q, float (&v)[8]) {
-  const uint32_t w[4] = {q[0], q[1], q[2], q[3]};
+template <typename T> MSU_DEV void unpack8(const u32x4& q, float (&v)[8]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    v[2 * i] = Fmt16<T>::lo(q[i]);
+    v[2 * i + 1] = Fmt16<T>::hi(q[i]);
   }
 }
-MSU_DEV uint32_t pack2(float a, float b) {
-  return (uint32_t)from_f32<bf16_t>(a) | ((uint32_t)from_f32<bf16_t>(b) << 16);
-}
-MSU_DEV u32x4 gelu8(const u32x4& q) {
+template <typename T> MSU_DEV u32x4 gelu8(const u32x4& q) {
   float v[8];
-  unpack8(q, v);
-  return u32x4{pack2(gelu_fast(v[0]), gelu_fast(v[1])), pack2(gelu_fast(v[2]), gelu_fast(v[3])),
-               pack2(gelu_fast(v[4]), gelu_fast(v[5])), pack2(gelu_fast(v[6]), gelu_fast(v[7]))};
+  unpack8<T>(q, v);
+  return u32x4{pack2<T>(gelu_fast(v[0]), gelu_fast(v[1])), pack2<T>(gelu_fast(v[2]), gelu_fast(v[3])),
+               pack2<T>(gelu_fast(v[4]), gelu_fast(v[5])), pack2<T>(gelu_fast(v[6]), gelu_fast(v[7]))};
 }
 
 template <int I> using IC = std::integral_constant<int, I>;
@@ -275,8 +270,8 @@ MSU_DEV void static_for(F&& f, std::integer_sequence<int, Is...>) {
   (f(IC<Is>{}), ...);
 }
 
-template <int NCT, int KS, int NW, int MT, bool WDB, bool IN_D2S, bool IN_GELU, bool OUT_D2S, bool OUT_GGRAD,
-          bool BIAS, bool DUAL>
+template <typename T, int NCT, int KS, int NW, int MT, bool WDB, bool IN_D2S, bool IN_GELU, bool OUT_D2S,
+          bool OUT_GGRAD, bool BIAS, bool DUAL>
 __global__ void __launch_bounds__(64 * NW) conv3x3_v2_kernel(const bf16_t* __restrict__ X,
                                                          const bf16_t* __restrict__ Wt,
                                                          const float* __restrict__ bias,
@@ -376,7 +371,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_v2_kernel(const bf16_t* __res
   load_halo(tile);
   if constexpr (IN_GELU && !(MSU_EXP & 2)) {
 #pragma unroll
-    for (int c = 0; c < NHC; ++c) hr[c] = gelu8(hr[c]);
+    for (int c = 0; c < NHC; ++c) hr[c] = gelu8<T>(hr[c]);
   }
   store_halo();
   load_w(0, w0);
@@ -420,7 +415,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_v2_kernel(const bf16_t* __res
         constexpr int c1 = (c0 + (NHC + 2) / 3) < NHC ? (c0 + (NHC + 2) / 3) : NHC;
         if ((wave < NW / 2) == (tap <= 4)) {
 #pragma unroll
-          for (int c = c0; c < c1; ++c) hr[c] = gelu8(hr[c]);
+          for (int c = c0; c < c1; ++c) hr[c] = gelu8<T>(hr[c]);
         }
       }
       if constexpr (OUT_GGRAD && tap == 5) {
@@ -460,7 +455,7 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_v2_kernel(const bf16_t* __res
             if constexpr (MSU_EXP & 32)
               acc[m][n][0] += (float)wf[cur][n][0] * (float)xa[cur][m][1];
             else
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[cur][n], xa[cur][m], acc[m][n], 0, 0, 0);
+              acc[m][n] = Fmt16<T>::mma32(wf[cur][n], xa[cur][m], acc[m][n]);
           }
         __builtin_amdgcn_sched_barrier(0);
       }, std::make_integer_sequence<int, KS>{});
@@ -507,13 +502,13 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_v2_kernel(const bf16_t* __res
               const u32x4 t = sp[m][n][pp];
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
-                v[2 * i] *= gelu_grad_fast(__uint_as_float(t[i] << 16));
-                v[2 * i + 1] *= gelu_grad_fast(__uint_as_float(t[i] & 0xffff0000u));
+                v[2 * i] *= gelu_grad_fast(Fmt16<T>::lo(t[i]));
+                v[2 * i + 1] *= gelu_grad_fast(Fmt16<T>::hi(t[i]));
               }
             }
-            const u32x4 pk = {pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])};
+            const u32x4 pk = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
             if (!(MSU_EXP & 1) || v[0] == 1.2345e-30f) *reinterpret_cast<u32x4*>(Y + out_off(b, y, xo, co)) = pk;
-            if constexpr (DUAL) *reinterpret_cast<u32x4*>(Y2 + out_off(b, y, xo, co)) = gelu8(pk);
+            if constexpr (DUAL) *reinterpret_cast<u32x4*>(Y2 + out_off(b, y, xo, co)) = gelu8<T>(pk);
           }
         }
     }
@@ -622,7 +617,7 @@ __global__ void __launch_bounds__(64 * NT) conv3x3_wgrad_kernel(const T* __restr
 // DMAs land (vmcnt), each wave GELU-converts the halo slots it wrote, in place, so no
 // registers are held across the tile and no extra barrier is needed.
 // Partials: [block][dy][co][dx][ci] + db [block][co], the layout wgrad_reduce_kernel sums.
-template <bool IN_D2S, bool IN_GELU>
+template <typename T, bool IN_D2S, bool IN_GELU>
 __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __restrict__ X,
                                                                const bf16_t* __restrict__ DY,
                                                                float* __restrict__ part,
@@ -691,7 +686,7 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
         const int s = 64 * k + ln;
         if (k < NINS && s / SLOTS < HPIX && s % SLOTS < SLOTS - 1) {
           u32x4* p = reinterpret_cast<u32x4*>(lds + buf * BUF + 8 * s);
-          *p = gelu8(*p);
+          *p = gelu8<T>(*p);
         }
       }
     }
@@ -733,8 +728,8 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
 #pragma unroll
       for (int p = 0; p < DPIX / 16; ++p) {
         vreg_pin(v[p]);
-        dbacc[0] += __uint_as_float(v[p] << 16);
-        dbacc[1] += __uint_as_float(v[p] & 0xffff0000u);
+        dbacc[0] += Fmt16<T>::lo(v[p]);
+        dbacc[1] += Fmt16<T>::hi(v[p]);
       }
     }
     // lane part of a k-strided fragment read: pixels 2(4g + q) + half (+16 for the second
@@ -762,7 +757,7 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
         for (int i = 0; i < 3; ++i)
 #pragma unroll
           for (int j = 0; j < 3; ++j)
-            acc[d][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[d][i][j], 0, 0, 0);
+            acc[d][i][j] = Fmt16<T>::mma16(af[i], bf[j], acc[d][i][j]);
         __builtin_amdgcn_sched_barrier(0);
       });
     });
@@ -857,14 +852,14 @@ int num_cus() {
   return n;
 }
 
-template <int NCT, int KS, int NW, int MT, bool WDB, bool IN_D2S, bool IN_GELU, bool OUT_D2S, bool OUT_GGRAD,
-          bool BIAS, bool DUAL>
+template <typename T, int NCT, int KS, int NW, int MT, bool WDB, bool IN_D2S, bool IN_GELU, bool OUT_D2S,
+          bool OUT_GGRAD, bool BIAS, bool DUAL>
 int launch_v2(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S,
               bf16_t* Y, bf16_t* Y2, hipStream_t st) {
   constexpr int PS = KS * 16 + 8, TH = NW * MT;
   constexpr size_t lds = sizeof(bf16_t) * ((size_t)(TH + 2) * 34 * PS + (WDB ? 2 : 1) * (size_t)NCT * 32 * PS);
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = conv3x3_v2_kernel<NCT, KS, NW, MT, WDB, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS, DUAL>;
+  auto kern = conv3x3_v2_kernel<T, NCT, KS, NW, MT, WDB, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS, DUAL>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -886,7 +881,10 @@ int conv_nt(const ConvGeom& g, const void* X, const void* Wt, const float* bias,
   if constexpr (sizeof(T) == 2) {
     // the Swin-T/S decoder head width takes the persistent v2 kernel
     if (g.Cout == 96 && g.CinP == 96)
-      return launch_v2<3, 6, 8, 1, true, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS, DUAL>(g, x, w, bias, s, y, y2, st);
+      return launch_v2<T, 3, 6, 8, 1, true, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS, DUAL>(g, (const bf16_t*)x,
+                                                                                          (const bf16_t*)w, bias,
+                                                                                          (const bf16_t*)s, (bf16_t*)y,
+                                                                                          (bf16_t*)y2, st);
   }
   switch (g.Cout / 16) {
     case 1: return launch_conv<T, 1, IN_D2S, IN_GELU, OUT_D2S, OUT_GGRAD, BIAS, DUAL>(g, x, w, bias, s, y, y2, st);
@@ -918,13 +916,13 @@ int launch_wgrad_nti(const ConvGeom& g, const T* X, const T* DY, float* part, fl
   return -2;
 }
 
-template <bool IN_D2S, bool IN_GELU>
+template <typename T, bool IN_D2S, bool IN_GELU>
 int launch_wgrad_v2(const ConvGeom& g, const bf16_t* X, const bf16_t* DY, float* part, float* dbpart,
                     int nblocks, hipStream_t st) {
   constexpr int nins = ((6 * 34 + 4 * 32) * 13 + 63) / 64;
   constexpr size_t lds = 2 * sizeof(bf16_t) * (size_t)nins * 64 * 8;
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = conv3x3_wgrad_v2_kernel<IN_D2S, IN_GELU>;
+  auto kern = conv3x3_wgrad_v2_kernel<T, IN_D2S, IN_GELU>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -11,7 +11,7 @@ int msu_conv3x3_fwd2(int dtype, int in_mode, const void* X, const void* Wt, cons
   if (Cout % 16 || Cin % 8 || Cout > 128 || Cin > 128) return -2;
   if ((in_mode & 2) && (H % 4 || W % 4)) return -2;
   if (Y2 && (in_mode & 1)) return -2;
-  const ConvGeom g = make_geom(B, H, W, Cin, Cout, dtype == MSU_BF16 ? 2 : 4);
+  const ConvGeom g = make_geom(B, H, W, Cin, Cout, msu_is16(dtype) ? 2 : 4);
   hipStream_t st = (hipStream_t)stream;
   if (bias == nullptr) return -2;
 #define MSU_FWD(T, D2S, GL, DU) return conv_nt<T, D2S, GL, false, false, true, DU>(g, X, Wt, bias, nullptr, Y, Y2, st)
@@ -26,6 +26,8 @@ int msu_conv3x3_fwd2(int dtype, int in_mode, const void* X, const void* Wt, cons
   }
   if (dtype == MSU_BF16) {
     MSU_FWD_ALL(bf16_t)
+  } else if (dtype == MSU_F16) {
+    MSU_FWD_ALL(f16_t)
   } else {
     MSU_FWD_ALL(float)
   }
@@ -47,13 +49,18 @@ int msu_conv3x3_dgrad(int dtype, int out_mode, const void* dY, const void* Wflip
                       void* dX, int B, int H, int W, int Cin, int Cout, void* stream) {
   if (Cout % 16 || Cin % 16 || Cout > 128 || Cin > 128) return -2;
   if ((out_mode & 2) && (H % 4 || W % 4)) return -2;
-  const ConvGeom g = make_geom(B, H, W, Cout, Cin, dtype == MSU_BF16 ? 2 : 4);
+  const ConvGeom g = make_geom(B, H, W, Cout, Cin, msu_is16(dtype) ? 2 : 4);
   hipStream_t st = (hipStream_t)stream;
 #define MSU_DG(T, D2S, GG) return conv_nt<T, false, false, D2S, GG, false>(g, dY, Wflip, nullptr, S, dX, nullptr, st)
   if (dtype == MSU_BF16) {
     switch (out_mode & 3) {
       case 1: MSU_DG(bf16_t, false, true);
       case 3: MSU_DG(bf16_t, true, true);
+    }
+  } else if (dtype == MSU_F16) {
+    switch (out_mode & 3) {
+      case 1: MSU_DG(f16_t, false, true);
+      case 3: MSU_DG(f16_t, true, true);
     }
   } else {
     switch (out_mode & 3) {

@@ -16,27 +16,29 @@ int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, flo
                       int Cout, void* stream) {
   (void)unused;
   if (Cout % 16 || Cin % 8 || Cout > 128 || Cin > 128 || nchunk < 1) return -2;
-  const ConvGeom g = make_geom(B, H, W, Cin, Cout, dtype == MSU_BF16 ? 2 : 4);
+  const ConvGeom g = make_geom(B, H, W, Cin, Cout, msu_is16(dtype) ? 2 : 4);
   hipStream_t st = (hipStream_t)stream;
   float* part = workspace;
   float* dbpart = workspace + (long)nchunk * 3 * Cout * 3 * g.CinP;
   int rc = -3;
 #define MSU_WG(T, D2S, GL) rc = wgrad_nt<T, D2S, GL>(g, X, dY, part, dbpart, nchunk, st)
-  if (dtype == MSU_BF16 && Cin == 96 && Cout == 96) {
+  if (msu_is16(dtype) && Cin == 96 && Cout == 96) {
     const bf16_t* x = (const bf16_t*)X; const bf16_t* d = (const bf16_t*)dY;
-    switch (in_mode & 3) {
-      case 0: rc = launch_wgrad_v2<false, false>(g, x, d, part, dbpart, nchunk, st); break;
-      case 1: rc = launch_wgrad_v2<false, true>(g, x, d, part, dbpart, nchunk, st); break;
-      case 2: rc = launch_wgrad_v2<true, false>(g, x, d, part, dbpart, nchunk, st); break;
-      case 3: rc = launch_wgrad_v2<true, true>(g, x, d, part, dbpart, nchunk, st); break;
-    }
-  } else if (dtype == MSU_BF16) {
-    switch (in_mode & 3) {
-      case 0: MSU_WG(bf16_t, false, false); break;
-      case 1: MSU_WG(bf16_t, false, true); break;
-      case 2: MSU_WG(bf16_t, true, false); break;
-      case 3: MSU_WG(bf16_t, true, true); break;
-    }
+    MSU_DISPATCH16(dtype, T,
+      switch (in_mode & 3) {
+        case 0: rc = launch_wgrad_v2<T, false, false>(g, x, d, part, dbpart, nchunk, st); break;
+        case 1: rc = launch_wgrad_v2<T, false, true>(g, x, d, part, dbpart, nchunk, st); break;
+        case 2: rc = launch_wgrad_v2<T, true, false>(g, x, d, part, dbpart, nchunk, st); break;
+        case 3: rc = launch_wgrad_v2<T, true, true>(g, x, d, part, dbpart, nchunk, st); break;
+      });
+  } else if (msu_is16(dtype)) {
+    MSU_DISPATCH16(dtype, T,
+      switch (in_mode & 3) {
+        case 0: MSU_WG(T, false, false); break;
+        case 1: MSU_WG(T, false, true); break;
+        case 2: MSU_WG(T, true, false); break;
+        case 3: MSU_WG(T, true, true); break;
+      });
   } else {
     switch (in_mode & 3) {
       case 0: MSU_WG(float, false, false); break;

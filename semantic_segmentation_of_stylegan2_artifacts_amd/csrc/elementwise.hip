@@ -304,24 +304,16 @@ extern "C" {
 int msu_gelu_fwd(int dtype, const void* x, void* y, long n, void* stream) {
   if (n % 4) return -2;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MSU_BF16)
-    hipLaunchKernelGGL(gelu_fwd_kernel<bf16_t>, dim3(grid_for(n / 4)), dim3(256), 0, st,
-                       (const bf16_t*)x, (bf16_t*)y, n / 4);
-  else
-    hipLaunchKernelGGL(gelu_fwd_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, st,
-                       (const float*)x, (float*)y, n / 4);
+  MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(gelu_fwd_kernel<T>, dim3(grid_for(n / 4)), dim3(256), 0, st,
+                                            (const T*)x, (T*)y, n / 4));
   return MSU_CHECK_LAUNCH();
 }
 
 int msu_gelu_bwd(int dtype, const void* x, const void* dy, void* dx, long n, void* stream) {
   if (n % 4) return -2;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MSU_BF16)
-    hipLaunchKernelGGL(gelu_bwd_kernel<bf16_t>, dim3(grid_for(n / 4)), dim3(256), 0, st,
-                       (const bf16_t*)x, (const bf16_t*)dy, (bf16_t*)dx, n / 4);
-  else
-    hipLaunchKernelGGL(gelu_bwd_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, st,
-                       (const float*)x, (const float*)dy, (float*)dx, n / 4);
+  MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(gelu_bwd_kernel<T>, dim3(grid_for(n / 4)), dim3(256), 0, st,
+                                            (const T*)x, (const T*)dy, (T*)dx, n / 4));
   return MSU_CHECK_LAUNCH();
 }
 
@@ -329,12 +321,8 @@ int msu_residual(int dtype, const void* a, const void* b, const float* scale, vo
                  void* stream) {
   if (n % 4 || per_sample % 4 || per_sample <= 0 || scale == nullptr) return -2;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MSU_BF16)
-    hipLaunchKernelGGL(residual_kernel<bf16_t>, dim3(grid_for(n / 4)), dim3(256), 0, st, (const bf16_t*)a,
-                       (const bf16_t*)b, scale, (bf16_t*)out, n / 4, per_sample / 4);
-  else
-    hipLaunchKernelGGL(residual_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, st, (const float*)a,
-                       (const float*)b, scale, (float*)out, n / 4, per_sample / 4);
+  MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(residual_kernel<T>, dim3(grid_for(n / 4)), dim3(256), 0, st,
+                                            (const T*)a, (const T*)b, scale, (T*)out, n / 4, per_sample / 4));
   return MSU_CHECK_LAUNCH();
 }
 
@@ -343,12 +331,8 @@ int msu_patchify(int dtype, const float* img, void* out, int B, int Cin, int H, 
   if (H % p || W % p) return -2;
   hipStream_t st = (hipStream_t)stream;
   const long n = (long)B * Cin * H * W;
-  if (dtype == MSU_BF16)
-    hipLaunchKernelGGL(patchify_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, img,
-                       (bf16_t*)out, B, Cin, H, W, p);
-  else
-    hipLaunchKernelGGL(patchify_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, img,
-                       (float*)out, B, Cin, H, W, p);
+  MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(patchify_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, img,
+                                            (T*)out, B, Cin, H, W, p));
   return MSU_CHECK_LAUNCH();
 }
 
@@ -363,12 +347,8 @@ int msu_dynloss_fwd(int dtype, const void* logits, const float* target, int B, l
                     float alpha, float beta, float mix, float* part, int nblk, float* loss,
                     float* coef, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MSU_BF16)
-    hipLaunchKernelGGL(dynloss_partial_kernel<bf16_t>, dim3(nblk, B), dim3(256), 0, st,
-                       (const bf16_t*)logits, target, N, nblk, part);
-  else
-    hipLaunchKernelGGL(dynloss_partial_kernel<float>, dim3(nblk, B), dim3(256), 0, st,
-                       (const float*)logits, target, N, nblk, part);
+  MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(dynloss_partial_kernel<T>, dim3(nblk, B), dim3(256), 0, st,
+                                            (const T*)logits, target, N, nblk, part));
   if (B > 64) return -2;
   hipLaunchKernelGGL(dynloss_final_kernel, dim3(1), dim3(512), 0, st, part, B, nblk, N, alpha, beta,
                      mix, 1e-6f, loss, coef);
@@ -380,12 +360,9 @@ int msu_dynloss_bwd(int dtype, const void* logits, const float* target, const fl
                     float mix, float* dlogits, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const long n = (long)B * N;
-  if (dtype == MSU_BF16)
-    hipLaunchKernelGGL(dynloss_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st,
-                       (const bf16_t*)logits, target, coef, loss, gout, N, B, alpha, beta, mix, dlogits);
-  else
-    hipLaunchKernelGGL(dynloss_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st,
-                       (const float*)logits, target, coef, loss, gout, N, B, alpha, beta, mix, dlogits);
+  MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(dynloss_bwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st,
+                                            (const T*)logits, target, coef, loss, gout, N, B, alpha, beta, mix,
+                                            dlogits));
   return MSU_CHECK_LAUNCH();
 }
 
@@ -432,10 +409,7 @@ int msu_nonfinite(const float* x, long n, float* flag, void* stream) {
 
 int msu_cast(int dtype, const float* x, void* y, long n, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MSU_BF16)
-    hipLaunchKernelGGL(cast_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, x, (bf16_t*)y, n);
-  else
-    hipLaunchKernelGGL(cast_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, x, (float*)y, n);
+  MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(cast_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, x, (T*)y, n));
   return MSU_CHECK_LAUNCH();
 }
 

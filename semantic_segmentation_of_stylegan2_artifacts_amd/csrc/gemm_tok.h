@@ -1,5 +1,5 @@
 // Token GEMM: Y[M][N] = epi(A[M][K] . W[N][K]^T (+ bias)) for the Linear layers of the Swin
-// blocks and MS-UNet glue (bf16 in / bf16 out, f32 accumulate).
+// blocks and MS-UNet glue (bf16 or f16 in / out, f32 accumulate).
 //
 // Replaces the forward and input-gradient GEMMs of torchvision's block Linears (qkv / proj /
 // mlp.0 / mlp.3, called from model_parts.py:170 / :538), PatchMerging.reduction
@@ -56,9 +56,8 @@ struct TokArgs {
   int rgroups;       // row groups (gridDim.x / nchunk)
 };
 
-MSU_DEV uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)from_f32<bf16_t>(lo) | ((uint32_t)from_f32<bf16_t>(hi) << 16);
-}
+// Storage pointers are raw 16-bit words (bf16_t); the kernel's T (bf16_t / f16_t) says how
+// they are interpreted (conversions, MFMA opcode).
 
 template <int KC>
 struct StageGeom {
@@ -101,7 +100,7 @@ constexpr int stage_cols() {
        : (NC % 64 == 0 && 32 * (64 * 2 + 16) <= bytes)   ? 64 : 32;
 }
 
-template <int KC, int NC, int NST, int NW, int EPI, bool BIAS, bool CONCAT>
+template <typename T, int KC, int NC, int NST, int NW, int EPI, bool BIAS, bool CONCAT>
 __global__ void __launch_bounds__(64 * NW) tokgemm_kernel(TokArgs a) {
   constexpr int WPB = NW;
   using G = StageGeom<KC>;
@@ -134,15 +133,15 @@ __global__ void __launch_bounds__(64 * NW) tokgemm_kernel(TokArgs a) {
           *reinterpret_cast<const uint4*>(a.W + (long)(n0 + r) * K + 8 * c);
     }
     if (BIAS) {
-      // bias as an extra k-block: bf16 hi + lo parts (~16 significant bits) times a ones column
+      // bias as an extra k-block: 16-bit hi + lo parts (~16 / 22 significant bits for bf16 /
+      // f16) times a ones column
       for (int i = tid; i < NC * 2; i += 64 * WPB) {
         const int r = i >> 1, half = i & 1;
         uint4 q = make_uint4(0, 0, 0, 0);
         if (half == 0) {
           const float bv = a.bias[n0 + r];
-          const bf16_t hi = from_f32<bf16_t>(bv);
-          const bf16_t lo = from_f32<bf16_t>(bv - to_f32(hi));
-          q.x = (uint32_t)hi | ((uint32_t)lo << 16);
+          const float hi = round16<T>(bv);
+          q.x = pack2<T>(hi, bv - hi);
         }
         *reinterpret_cast<uint4*>(sW + r * LDW + K + 8 * half) = q;
       }
@@ -250,19 +249,16 @@ __global__ void __launch_bounds__(64 * NW) tokgemm_kernel(TokArgs a) {
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
           const bf16x8 wx = *reinterpret_cast<const bf16x8*>(wk + n * 32 * LDW + 16 * kk);
-          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wx, bx, acc[n], 0, 0, 0);
+          acc[n] = Fmt16<T>::mma32(wx, bx, acc[n]);
         }
       }
       if (BIAS && last) {
         // + bias: the W image's bias k-block times a ones column (k = 0, 1 of lanes 0-31)
-        bf16x8 ones;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) ones[e] = (__bf16)0.0f;
-        if (lane < 32) { ones[0] = (__bf16)1.0f; ones[1] = (__bf16)1.0f; }
+        const bf16x8 ones = lane < 32 ? splat8<T>(1.0f, 1.0f, 0.0f) : splat8<T>(0.0f, 0.0f, 0.0f);
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
           const bf16x8 wx = *reinterpret_cast<const bf16x8*>(wfrag + K + n * 32 * LDW);
-          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wx, ones, acc[n], 0, 0, 0);
+          acc[n] = Fmt16<T>::mma32(wx, ones, acc[n]);
         }
       }
     }
@@ -306,17 +302,17 @@ __global__ void __launch_bounds__(64 * NW) tokgemm_kernel(TokArgs a) {
           if constexpr (GGRAD) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              v[2 * i] *= gelu_grad_fast(__uint_as_float(hv[p][i] << 16));
-              v[2 * i + 1] *= gelu_grad_fast(__uint_as_float(hv[p][i] & 0xffff0000u));
+              v[2 * i] *= gelu_grad_fast(Fmt16<T>::lo(hv[p][i]));
+              v[2 * i + 1] *= gelu_grad_fast(Fmt16<T>::hi(hv[p][i]));
             }
           }
           if (EPI == EPI_GELU_DUAL && out == 1) {
-            // GELU of the bf16-rounded pre-activation, as the unfused GELU kernel would see it
+            // GELU of the rounded pre-activation, as the unfused GELU kernel would see it
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = gelu_fast(to_f32(from_f32<bf16_t>(v[i])));
+            for (int i = 0; i < 8; ++i) v[i] = gelu_fast(round16<T>(v[i]));
           }
-          const u32x4 pk = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                            pack_bf16x2(v[6], v[7])};
+          const u32x4 pk = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                            pack2<T>(v[6], v[7])};
           ds_write16_untracked(sbase + fr * RSTR + (16 * pp + (lane >= 32 ? 8 : 0)) * 2, pk);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -361,9 +357,9 @@ inline size_t plan_lds(int kc, int nc, int nst, int K, int nw = 4) {
   return (size_t)nc * (K + 16 + 8) * 2 + (size_t)nw * nst * stage;  // W image incl. bias block
 }
 
-template <int KC, int NC, int NST, int NW, int EPI, bool BIAS, bool CONCAT>
+template <typename T, int KC, int NC, int NST, int NW, int EPI, bool BIAS, bool CONCAT>
 int launch_tok(const TokPlan& p, TokArgs a, hipStream_t st) {
-  auto kern = tokgemm_kernel<KC, NC, NST, NW, EPI, BIAS, CONCAT>;
+  auto kern = tokgemm_kernel<T, KC, NC, NST, NW, EPI, BIAS, CONCAT>;
   static size_t attr = 0;
   if (attr < p.lds) {
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds) != hipSuccess)
@@ -377,10 +373,10 @@ int launch_tok(const TokPlan& p, TokArgs a, hipStream_t st) {
 }
 
 // epilogue variants instantiated per (KC, NC, NST); FULL = all five, else plain (+bias) only
-template <int KC, int NC, int NST, int NW, bool FULL>
+template <typename T, int KC, int NC, int NST, int NW, bool FULL>
 int dispatch_epi(const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st) {
 #define MSU_TOK(E, B, C) \
-  if (epi == E && bias == B && concat == C) return launch_tok<KC, NC, NST, NW, E, B, C>(p, a, st);
+  if (epi == E && bias == B && concat == C) return launch_tok<T, KC, NC, NST, NW, E, B, C>(p, a, st);
   MSU_TOK(EPI_PLAIN, true, false)
   MSU_TOK(EPI_PLAIN, false, false)
   if constexpr (FULL) {
@@ -392,21 +388,21 @@ int dispatch_epi(const TokPlan& p, const TokArgs& a, int epi, bool bias, bool co
   return -3;
 }
 
-template <int KC, bool FULL>
+template <typename T, int KC, bool FULL>
 int dispatch_nc(const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st) {
-#define MSU_NC(NC)                                                                                   \
-  if (p.nc == NC) {                                                                                  \
-    if (p.nst == 3) return dispatch_epi<KC, NC, 3, 4, FULL>(p, a, epi, bias, concat, st);           \
-    if (p.nst == 2 && p.nw == 8) return dispatch_epi<KC, NC, 2, 8, FULL>(p, a, epi, bias, concat, st); \
-    if (p.nst == 2) return dispatch_epi<KC, NC, 2, 4, FULL>(p, a, epi, bias, concat, st);           \
+#define MSU_NC(NC)                                                                                      \
+  if (p.nc == NC) {                                                                                     \
+    if (p.nst == 3) return dispatch_epi<T, KC, NC, 3, 4, FULL>(p, a, epi, bias, concat, st);           \
+    if (p.nst == 2 && p.nw == 8) return dispatch_epi<T, KC, NC, 2, 8, FULL>(p, a, epi, bias, concat, st); \
+    if (p.nst == 2) return dispatch_epi<T, KC, NC, 2, 4, FULL>(p, a, epi, bias, concat, st);           \
   }
   MSU_NC(384) MSU_NC(288) MSU_NC(256) MSU_NC(192) MSU_NC(128) MSU_NC(96) MSU_NC(64)
 #undef MSU_NC
   return -3;
 }
 
-int dispatch_k96(const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st);
-int dispatch_k128(const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st);
-int dispatch_k48(const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st);
+int dispatch_k96(int dtype, const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st);
+int dispatch_k128(int dtype, const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st);
+int dispatch_k48(int dtype, const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st);
 
 }  // namespace msu_tok

@@ -77,8 +77,9 @@ int msu_tok_gemm_supported_epi(long M, int N, int K, int epi) {
 // Y[M][N] = epi(A . W^T + bias), bf16 in / out.  epi 0: plain (+ bias); 1: Y = H and
 // Y2 = GELU(H) (needs bias); 2: Y = (A . W^T) * GELU'(H) (no bias).  A2 != null: columns
 // [K1, K) of A come from A2 ([M][K - K1]; needs bias).
-int msu_tok_gemm(const void* A, const void* A2, int K1, const void* W, const float* bias, void* Y, void* Y2,
-                 const void* H, long M, int N, int K, int epi, void* stream) {
+int msu_tok_gemm(int dtype, const void* A, const void* A2, int K1, const void* W, const float* bias, void* Y,
+                 void* Y2, const void* H, long M, int N, int K, int epi, void* stream) {
+  if (!msu_is16(dtype)) return -3;
   if (M < 0 || N % 32 || K % 16) return -2;
   if (M == 0) return 0;
   if (A2 != nullptr && (K1 <= 0 || K1 >= K || K1 % 8)) return -2;
@@ -106,9 +107,9 @@ int msu_tok_gemm(const void* A, const void* A2, int K1, const void* W, const flo
   const bool has_bias = bias != nullptr, concat = A2 != nullptr;
   int rc = -3;
   switch (p.kc) {
-    case 96: rc = dispatch_k96(p, a, epi, has_bias, concat, st); break;
-    case 128: rc = dispatch_k128(p, a, epi, has_bias, concat, st); break;
-    case 48: rc = dispatch_k48(p, a, epi, has_bias, concat, st); break;
+    case 96: rc = dispatch_k96(dtype, p, a, epi, has_bias, concat, st); break;
+    case 128: rc = dispatch_k128(dtype, p, a, epi, has_bias, concat, st); break;
+    case 48: rc = dispatch_k48(dtype, p, a, epi, has_bias, concat, st); break;
   }
   if (rc) return rc;
   return MSU_CHECK_LAUNCH();

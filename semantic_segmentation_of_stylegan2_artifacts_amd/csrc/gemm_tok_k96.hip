@@ -2,7 +2,8 @@
 #include "gemm_tok.h"
 
 namespace msu_tok {
-int dispatch_k96(const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st) {
-  return dispatch_nc<96, true>(p, a, epi, bias, concat, st);
+int dispatch_k96(int dtype, const TokPlan& p, const TokArgs& a, int epi, bool bias, bool concat, hipStream_t st) {
+  if (dtype == MSU_F16) return dispatch_nc<f16_t, 96, true>(p, a, epi, bias, concat, st);
+  return dispatch_nc<bf16_t, 96, true>(p, a, epi, bias, concat, st);
 }
 }  // namespace msu_tok

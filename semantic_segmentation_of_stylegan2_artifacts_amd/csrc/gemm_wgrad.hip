@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ dY, co
 // global_load_lds_dwordx4 (pad slots re-read chunk 0 of their row; rows past the block's
 // range read the spread zero region); a ring of NST stages keeps NST-1 in flight; raw
 // s_barrier + counted vmcnt keep the prefetch alive across barriers.
-template <int NTW, int WN, int NST>
+template <typename T, int NTW, int WN, int NST>
 __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                                          float* __restrict__ part, float* __restrict__ dbpart,
                                                          long M, int N, int K, long mchunk) {
@@ -206,9 +206,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
     for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const bool do_bias = dbpart != nullptr && tk == 0;
-  bf16x8 ones;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  const bf16x8 ones = splat8<T>(1.0f, 1.0f, 1.0f);
   // lane part of a k-strided fragment read (ds_read_b64_tr_b16), columns 4p.  The k order
   // is free (both operands use the same one): each 32-lane half reads 8 rows of one parity,
   // 2(4g + q) + half (g = lane group within the half), and the second half of the fragment
@@ -254,10 +252,10 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
         if constexpr (MSU_EXP & 1)
           acc[i][j][0] += (float)af[i & 1][j] * (float)bf[j][i];
         else
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i & 1], bf[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = Fmt16<T>::mma16(af[i & 1], bf[j], acc[i][j]);
       }
       if constexpr (!(MSU_EXP & 1))
-        accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i & 1], ones, accb[i], 0, 0, 0);  // unconditional
+        accb[i] = Fmt16<T>::mma16(af[i & 1], ones, accb[i]);  // unconditional
       if constexpr (i + 1 < NTW) lds_wait_tie<0>(af[(i + 1) & 1]);
     });
   }
@@ -356,7 +354,7 @@ inline WavePlan wave_plan(long M, int N, int K) {
   return p;
 }
 
-template <int NTW, int WN, int NST>
+template <typename T, int NTW, int WN, int NST>
 void launch_wave(dim3 grid, const bf16_t* dY, const bf16_t* X, float* part, float* dbpart, long M, int N, int K,
                  long mchunk, hipStream_t st) {
   constexpr int WM = 4 / WN, WT = 16 * NTW, RS = 32 * WM;
@@ -364,7 +362,7 @@ void launch_wave(dim3 grid, const bf16_t* dY, const bf16_t* X, float* part, floa
   constexpr int INS = ((SLOTS + 63) / 64 + 3) / 4 * 4;
   constexpr size_t lds = (size_t)NST * INS * 64 * 16;
   if constexpr (lds <= 160 * 1024) {  // ring depths the plan never picks are not instantiated
-    auto kern = wgrad_wave_kernel<NTW, WN, NST>;
+    auto kern = wgrad_wave_kernel<T, NTW, WN, NST>;
     static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -374,6 +372,7 @@ void launch_wave(dim3 grid, const bf16_t* dY, const bf16_t* X, float* part, floa
   }
 }
 
+template <typename T>
 int run_wave(const WavePlan& p, const bf16_t* dY, const bf16_t* X, float* part, float* dbpart, long M, int N, int K,
              hipStream_t st) {
   const int wt = 16 * p.ntw, wm = 4 / p.wn, rs = 32 * wm;
@@ -383,10 +382,10 @@ int run_wave(const WavePlan& p, const bf16_t* dY, const bf16_t* X, float* part, 
 #define MSU_WAVE(NTW, WN)                                                                                   \
   if (p.ntw == NTW && p.wn == WN) {                                                                         \
     switch (p.nst) {                                                                                        \
-      case 3: launch_wave<NTW, WN, 3>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;            \
-      case 4: launch_wave<NTW, WN, 4>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;            \
-      case 5: launch_wave<NTW, WN, 5>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;            \
-      case 6: launch_wave<NTW, WN, 6>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;            \
+      case 3: launch_wave<T, NTW, WN, 3>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;         \
+      case 4: launch_wave<T, NTW, WN, 4>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;         \
+      case 5: launch_wave<T, NTW, WN, 5>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;         \
+      case 6: launch_wave<T, NTW, WN, 6>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;         \
     }                                                                                                       \
   }
   MSU_WAVE(6, 1) MSU_WAVE(6, 2) MSU_WAVE(6, 4) MSU_WAVE(8, 1) MSU_WAVE(8, 2) MSU_WAVE(8, 4)
@@ -434,12 +433,13 @@ int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float*
     return MSU_CHECK_LAUNCH();
   }
   static const bool generic_only = getenv("MSU_WGRAD_GENERIC") != nullptr;  // A/B timing switch
-  if (dtype == MSU_BF16 && !generic_only) {
+  if (msu_is16(dtype) && !generic_only) {
     const WavePlan p = wave_plan(M, N, K);
     if (p.ntw) {
       float* part = workspace;
       float* dbpart = db ? workspace + (long)p.slabs() * N * K : nullptr;
-      const int rc = run_wave(p, (const bf16_t*)dY, (const bf16_t*)X, part, dbpart, M, N, K, st);
+      int rc = -3;
+      MSU_DISPATCH16(dtype, T, rc = run_wave<T>(p, (const bf16_t*)dY, (const bf16_t*)X, part, dbpart, M, N, K, st));
       if (rc) return rc;
       const ColSeg segs[2] = {{part, (long)N * K, (long)N * K, dW}, {dbpart, N, N, db}};
       colsum_multi(segs, db ? 2 : 1, p.slabs(), accumulate, st);
@@ -453,21 +453,13 @@ int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float*
   float* dbpart = db ? workspace + (long)S * N * K : nullptr;
   const int bt = tile_of(N, K);
   const dim3 grid((unsigned)(((N + bt - 1) / bt) * ((K + bt - 1) / bt)), (unsigned)S);
-  if (dtype == MSU_BF16) {
+  MSU_DISPATCH(dtype, T,
     if (bt == 96)
-      hipLaunchKernelGGL((wgrad_kernel<bf16_t, 3>), grid, dim3(256), 0, st, (const bf16_t*)dY,
-                         (const bf16_t*)X, part, dbpart, M, N, K, mchunk);
+      hipLaunchKernelGGL((wgrad_kernel<T, 3>), grid, dim3(256), 0, st, (const T*)dY, (const T*)X, part, dbpart, M,
+                         N, K, mchunk);
     else
-      hipLaunchKernelGGL((wgrad_kernel<bf16_t, 4>), grid, dim3(256), 0, st, (const bf16_t*)dY,
-                         (const bf16_t*)X, part, dbpart, M, N, K, mchunk);
-  } else {
-    if (bt == 96)
-      hipLaunchKernelGGL((wgrad_kernel<float, 3>), grid, dim3(256), 0, st, (const float*)dY,
-                         (const float*)X, part, dbpart, M, N, K, mchunk);
-    else
-      hipLaunchKernelGGL((wgrad_kernel<float, 4>), grid, dim3(256), 0, st, (const float*)dY,
-                         (const float*)X, part, dbpart, M, N, K, mchunk);
-  }
+      hipLaunchKernelGGL((wgrad_kernel<T, 4>), grid, dim3(256), 0, st, (const T*)dY, (const T*)X, part, dbpart, M,
+                         N, K, mchunk));
   const ColSeg segs[2] = {{part, (long)N * K, (long)N * K, dW}, {dbpart, N, N, db}};
   colsum_multi(segs, db ? 2 : 1, S, accumulate, st);
   return MSU_CHECK_LAUNCH();

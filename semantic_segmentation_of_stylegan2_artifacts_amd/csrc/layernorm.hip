@@ -17,33 +17,35 @@ namespace {
 
 enum InMode { IN_PLAIN = 0, IN_ADD = 1, IN_MERGE = 2, IN_D2S2 = 3 };
 
-// 16-byte row chunks: 4 f32 or 8 bf16 elements per lane access
+// 16-byte row chunks: 4 f32 or 8 16-bit elements per lane access
 template <typename T> struct VecW;
 template <> struct VecW<float> {
   static constexpr int W = 4;
   static MSU_DEV void load(const float* p, float (&v)[4]) { Vec4<float>::load(p, v); }
   static MSU_DEV void store(float* p, const float (&v)[4]) { Vec4<float>::store(p, v); }
 };
-template <> struct VecW<bf16_t> {
+template <typename T> struct VecW16 {
   static constexpr int W = 8;
-  static MSU_DEV void load(const bf16_t* p, float (&v)[8]) {
+  static MSU_DEV void load(const T* p, float (&v)[8]) {
     const uint4 q = *reinterpret_cast<const uint4*>(p);
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      v[2 * i] = __uint_as_float(w[i] << 16);
-      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      v[2 * i] = Fmt16<T>::lo(w[i]);
+      v[2 * i + 1] = Fmt16<T>::hi(w[i]);
     }
   }
-  static MSU_DEV void store(bf16_t* p, const float (&v)[8]) {
+  static MSU_DEV void store(T* p, const float (&v)[8]) {
     uint4 q;
-    q.x = (uint32_t)from_f32<bf16_t>(v[0]) | ((uint32_t)from_f32<bf16_t>(v[1]) << 16);
-    q.y = (uint32_t)from_f32<bf16_t>(v[2]) | ((uint32_t)from_f32<bf16_t>(v[3]) << 16);
-    q.z = (uint32_t)from_f32<bf16_t>(v[4]) | ((uint32_t)from_f32<bf16_t>(v[5]) << 16);
-    q.w = (uint32_t)from_f32<bf16_t>(v[6]) | ((uint32_t)from_f32<bf16_t>(v[7]) << 16);
+    q.x = pack2<T>(v[0], v[1]);
+    q.y = pack2<T>(v[2], v[3]);
+    q.z = pack2<T>(v[4], v[5]);
+    q.w = pack2<T>(v[6], v[7]);
     *reinterpret_cast<uint4*>(p) = q;
   }
 };
+template <> struct VecW<bf16_t> : VecW16<bf16_t> {};
+template <> struct VecW<f16_t> : VecW16<f16_t> {};
 template <int VW> MSU_DEV void load_f32(const float* p, float (&v)[VW]) {
 #pragma unroll
   for (int i = 0; i < VW; i += 4) {
@@ -341,18 +343,20 @@ int launch_bwd(const LnBwdArgs& a, hipStream_t st, int nblocks) {
 
 template <int MODE>
 int fwd_dispatch(int dtype, const LnArgs& a, hipStream_t st) {
-  if (a.C % (dtype == MSU_BF16 ? 8 : 4) != 0 || a.C > 2048) return -2;
+  if (a.C % (msu_is16(dtype) ? 8 : 4) != 0 || a.C > 2048) return -2;
   if (a.rows == 0) return 0;
   static const int maxb = getenv("MSU_LN_FWD_BLOCKS") ? atoi(getenv("MSU_LN_FWD_BLOCKS")) : 16384;  // A/B switch: 16384 vs 4096 vs 2048 = 154.06 / 153.82 / 152.78 img/s
-  return dtype == MSU_BF16 ? launch_fwd<bf16_t, MODE>(a, st, maxb) : launch_fwd<float, MODE>(a, st, maxb);
+  MSU_DISPATCH(dtype, T, return launch_fwd<T, MODE>(a, st, maxb));
+  return -3;
 }
 
 template <int MODE>
 int bwd_dispatch(int dtype, const LnBwdArgs& a, float* dgamma, float* dbeta, int nparts, int accumulate,
                  hipStream_t st) {
-  if (a.C % (dtype == MSU_BF16 ? 8 : 4) != 0 || a.C > 2048) return -2;
+  if (a.C % (msu_is16(dtype) ? 8 : 4) != 0 || a.C > 2048) return -2;
   if (a.rows == 0) return 0;
-  int rc = dtype == MSU_BF16 ? launch_bwd<bf16_t, MODE>(a, st, nparts) : launch_bwd<float, MODE>(a, st, nparts);
+  int rc = -3;
+  MSU_DISPATCH(dtype, T, rc = launch_bwd<T, MODE>(a, st, nparts));
   if (rc) return rc;
   if (dbeta == dgamma + a.C) {  // contiguous [dgamma | dbeta]: one reduction launch
     colsum(a.part, nparts, 2L * a.C, 2L * a.C, dgamma, accumulate, st);
@@ -488,14 +492,10 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(const float* dlogit, cons
   }
 }
 
-// bf16, C % 32 == 0: 4 lanes per row, 16-B loads (KC chunks of 8 channels per lane), the
+// 16-bit, C % 32 == 0: 4 lanes per row, 16-B loads (KC chunks of 8 channels per lane), the
 // lane's gamma*w / beta*w slices held in registers, two rows per iteration for ILP.
-MSU_DEV uint32_t pack2bf(float a, float b) {
-  return (uint32_t)from_f32<bf16_t>(a) | ((uint32_t)from_f32<bf16_t>(b) << 16);
-}
-
-template <int KC>
-__global__ void __launch_bounds__(256) head_fwd16_kernel(const bf16_t* z, const float* gamma, const float* beta,
+template <typename T, int KC>
+__global__ void __launch_bounds__(256) head_fwd16_kernel(const T* z, const float* gamma, const float* beta,
                                                          const float* w, float* logit, float* mean,
                                                          float* rstd, long rows, float eps) {
   constexpr int TPR = 4, C = 32 * KC, RPB = 256 / TPR;
@@ -521,8 +521,8 @@ __global__ void __launch_bounds__(256) head_fwd16_kernel(const bf16_t* z, const 
         const u32x4 q = *reinterpret_cast<const u32x4*>(z + r * C + (lane + TPR * k) * 8);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          v[h][k][2 * i] = __uint_as_float(q[i] << 16);
-          v[h][k][2 * i + 1] = __uint_as_float(q[i] & 0xffff0000u);
+          v[h][k][2 * i] = Fmt16<T>::lo(q[i]);
+          v[h][k][2 * i + 1] = Fmt16<T>::hi(q[i]);
         }
       }
     }
@@ -557,10 +557,10 @@ __global__ void __launch_bounds__(256) head_fwd16_kernel(const bf16_t* z, const 
 // dgamma_c = w_c A_c, dbeta_c = w_c D, dw_c = gamma_c A_c + beta_c D with A_c = sum_r dl xh_c,
 // D = sum_r dl: per block only A (per channel) and D are accumulated, reduced over the
 // block's 64 row groups in fixed order through LDS, and expanded into the [3][C] partial.
-template <int KC>
-__global__ void __launch_bounds__(256) head_bwd16_kernel(const float* dlogit, const bf16_t* z, const float* gamma,
+template <typename T, int KC>
+__global__ void __launch_bounds__(256) head_bwd16_kernel(const float* dlogit, const T* z, const float* gamma,
                                                          const float* beta, const float* w, const float* mean,
-                                                         const float* rstd, bf16_t* dz,
+                                                         const float* rstd, T* dz,
                                                          float* part /* [grid, 3, C] */, long rows) {
   constexpr int TPR = 4, C = 32 * KC, RPB = 256 / TPR;
   __shared__ float redA[RPB][C + 1];
@@ -585,8 +585,8 @@ __global__ void __launch_bounds__(256) head_bwd16_kernel(const float* dlogit, co
       const u32x4 q = *reinterpret_cast<const u32x4*>(z + r * C + (lane + TPR * k) * 8);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        xh[k][2 * i] = (__uint_as_float(q[i] << 16) - mu) * rs;
-        xh[k][2 * i + 1] = (__uint_as_float(q[i] & 0xffff0000u) - mu) * rs;
+        xh[k][2 * i] = (Fmt16<T>::lo(q[i]) - mu) * rs;
+        xh[k][2 * i + 1] = (Fmt16<T>::hi(q[i]) - mu) * rs;
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -605,7 +605,7 @@ __global__ void __launch_bounds__(256) head_bwd16_kernel(const float* dlogit, co
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = rs * (dl * gw[k][e] - s1 - xh[k][e] * s2);
       *reinterpret_cast<u32x4*>(dz + r * C + (lane + TPR * k) * 8) =
-          u32x4{pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7])};
+          u32x4{pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]), pack2<T>(o[4], o[5]), pack2<T>(o[6], o[7])};
     }
   }
 #pragma unroll
@@ -637,20 +637,17 @@ int msu_head_fwd(int dtype, const void* z, const float* gamma, const float* beta
   long nb = (rows + 31) / 32;
   if (nb > 8192) nb = 8192;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MSU_BF16 && (C == 96 || C == 128)) {
+  if (msu_is16(dtype) && (C == 96 || C == 128)) {
     long g = (rows + 127) / 128;
     if (g > 4096) g = 4096;
-    if (C == 96) hipLaunchKernelGGL((head_fwd16_kernel<3>), dim3(g), dim3(256), 0, st, (const bf16_t*)z, gamma, beta, w, logit, mean, rstd, rows, eps);
-    else hipLaunchKernelGGL((head_fwd16_kernel<4>), dim3(g), dim3(256), 0, st, (const bf16_t*)z, gamma, beta, w, logit, mean, rstd, rows, eps);
+    MSU_DISPATCH16(dtype, T,
+      if (C == 96) hipLaunchKernelGGL((head_fwd16_kernel<T, 3>), dim3(g), dim3(256), 0, st, (const T*)z, gamma, beta, w, logit, mean, rstd, rows, eps);
+      else hipLaunchKernelGGL((head_fwd16_kernel<T, 4>), dim3(g), dim3(256), 0, st, (const T*)z, gamma, beta, w, logit, mean, rstd, rows, eps));
     return MSU_CHECK_LAUNCH();
   }
-  if (dtype == MSU_BF16) {
-    if (C <= 128) hipLaunchKernelGGL((head_fwd_kernel<bf16_t, 4>), dim3(nb), dim3(256), 0, st, (const bf16_t*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps);
-    else hipLaunchKernelGGL((head_fwd_kernel<bf16_t, 8>), dim3(nb), dim3(256), 0, st, (const bf16_t*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps);
-  } else {
-    if (C <= 128) hipLaunchKernelGGL((head_fwd_kernel<float, 4>), dim3(nb), dim3(256), 0, st, (const float*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps);
-    else hipLaunchKernelGGL((head_fwd_kernel<float, 8>), dim3(nb), dim3(256), 0, st, (const float*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps);
-  }
+  MSU_DISPATCH(dtype, T,
+    if (C <= 128) hipLaunchKernelGGL((head_fwd_kernel<T, 4>), dim3(nb), dim3(256), 0, st, (const T*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps);
+    else hipLaunchKernelGGL((head_fwd_kernel<T, 8>), dim3(nb), dim3(256), 0, st, (const T*)z, gamma, beta, w, logit, mean, rstd, rows, C, eps));
   return MSU_CHECK_LAUNCH();
 }
 
@@ -662,16 +659,14 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
   if (C % 4 || C > 256) return -2;
   if (rows == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MSU_BF16 && C == 96)
-    hipLaunchKernelGGL((head_bwd16_kernel<3>), dim3(nparts), dim3(256), 0, st, dlogit, (const bf16_t*)z, gamma, beta, w, mean, rstd, (bf16_t*)dz, part, rows);
-  else if (dtype == MSU_BF16 && C == 128)
-    hipLaunchKernelGGL((head_bwd16_kernel<4>), dim3(nparts), dim3(256), 0, st, dlogit, (const bf16_t*)z, gamma, beta, w, mean, rstd, (bf16_t*)dz, part, rows);
-  else if (dtype == MSU_BF16) {
-    if (C <= 128) hipLaunchKernelGGL((head_bwd_kernel<bf16_t, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const bf16_t*)z, gamma, beta, w, mean, rstd, (bf16_t*)dz, part, rows, C);
-    else hipLaunchKernelGGL((head_bwd_kernel<bf16_t, 8>), dim3(nparts), dim3(256), 0, st, dlogit, (const bf16_t*)z, gamma, beta, w, mean, rstd, (bf16_t*)dz, part, rows, C);
+  if (msu_is16(dtype) && (C == 96 || C == 128)) {
+    MSU_DISPATCH16(dtype, T,
+      if (C == 96) hipLaunchKernelGGL((head_bwd16_kernel<T, 3>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows);
+      else hipLaunchKernelGGL((head_bwd16_kernel<T, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows));
   } else {
-    if (C <= 128) hipLaunchKernelGGL((head_bwd_kernel<float, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const float*)z, gamma, beta, w, mean, rstd, (float*)dz, part, rows, C);
-    else hipLaunchKernelGGL((head_bwd_kernel<float, 8>), dim3(nparts), dim3(256), 0, st, dlogit, (const float*)z, gamma, beta, w, mean, rstd, (float*)dz, part, rows, C);
+    MSU_DISPATCH(dtype, T,
+      if (C <= 128) hipLaunchKernelGGL((head_bwd_kernel<T, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows, C);
+      else hipLaunchKernelGGL((head_bwd_kernel<T, 8>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows, C));
   }
   if (dbeta == dgamma + C && dw == dgamma + 2 * C) {  // contiguous [dgamma | dbeta | dw]
     colsum(part, nparts, 3L * C, 3L * C, dgamma, 0, st);

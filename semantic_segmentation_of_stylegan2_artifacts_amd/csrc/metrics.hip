@@ -75,7 +75,7 @@ int msu_metrics_nblk(long N) {
   return (int)(nb < 1 ? 1 : nb);
 }
 
-// logits [B, N] (f32 or bf16), label [B, N] f32; part [B * nblk * 12] f32 scratch;
+// logits [B, N] (f32, bf16 or f16), label [B, N] f32; part [B * nblk * 12] f32 scratch;
 // out [B, 12] f64: sum(p g), sum(p^2), sum(g), sum(p), soft fp, soft fn, soft tn, tp, fp, fn,
 // tn, 0.
 int msu_seg_metrics(int dtype, const void* logits, const float* label, int B, long N, float threshold,
@@ -83,12 +83,8 @@ int msu_seg_metrics(int dtype, const void* logits, const float* label, int B, lo
   if (B <= 0 || N <= 0 || nblk <= 0) return -2;
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)nblk, (unsigned)B);
-  if (dtype == MSU_BF16)
-    hipLaunchKernelGGL(metrics_partial_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)logits, label, N,
-                       nblk, threshold, part);
-  else
-    hipLaunchKernelGGL(metrics_partial_kernel<float>, grid, dim3(256), 0, st, (const float*)logits, label, N, nblk,
-                       threshold, part);
+  MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(metrics_partial_kernel<T>, grid, dim3(256), 0, st, (const T*)logits,
+                                            label, N, nblk, threshold, part));
   hipLaunchKernelGGL(metrics_final_kernel, dim3((unsigned)((B * NQ + 3) / 4)), dim3(256), 0, st, part, B, nblk, out);
   return MSU_CHECK_LAUNCH();
 }

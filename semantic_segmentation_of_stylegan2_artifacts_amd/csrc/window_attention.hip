@@ -395,10 +395,10 @@ WinGeom make_geom(int B, int H, int W, int C, int nh, int shift) {
 }  // namespace
 
 // bf16 training path: window_attention_mfma.hip
-int msu_attn_mfma_fwd(const void* qkv, const float* qkv_bias, const float* table, void* out, int B,
+int msu_attn_mfma_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, void* out, int B,
                       int H, int W, int C, int nh, int shift, float p_drop, unsigned long long seed,
                       float* bias_img, hipStream_t st);
-int msu_attn_mfma_bwd(const void* qkv, const float* qkv_bias, const float* table, const void* dout,
+int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, const void* dout,
                       void* dqkv, float* dtable, float* dqkv_bias_pad, float* ws, int B, int H, int W,
                       int C, int nh, int shift, float p_drop, unsigned long long seed, hipStream_t st,
                       hipStream_t pst);
@@ -419,7 +419,7 @@ long msu_win_count(int B, int H, int W) { return make_geom(B, H, W, 32, 1, 0).nw
 
 long msu_win_attn_fwd_workspace(int dtype, int C, int nh) {
   (void)C;
-  return dtype == MSU_BF16 ? msu_attn_mfma_fwd_workspace(C, nh) : 1;
+  return msu_is16(dtype) ? msu_attn_mfma_fwd_workspace(C, nh) : 1;
 }
 
 int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
@@ -432,8 +432,8 @@ int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const fl
   const long items = g.nwin * nh;
   if (items == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == MSU_BF16)
-    return msu_attn_mfma_fwd(qkv, qkv_bias, table, out, B, H, W, C, nh, shift, p_drop, seed, workspace, st);
+  if (msu_is16(dtype))
+    return msu_attn_mfma_fwd(dtype, qkv, qkv_bias, table, out, B, H, W, C, nh, shift, p_drop, seed, workspace, st);
   const float scale = 1.0f / sqrtf((float)HD);
   const long nb = items < 262144 ? items : 262144;
   hipLaunchKernelGGL(win_attn_fwd_kernel<float>, dim3((unsigned)nb), dim3(64), 0, st,
@@ -443,7 +443,7 @@ int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const fl
 
 long msu_win_attn_bwd_workspace(int dtype, int B, int H, int W, int C, int nh) {
   const WinGeom g = make_geom(B, H, W, C, nh, 0);
-  if (dtype == MSU_BF16) return msu_attn_mfma_bwd_workspace(g.nwin, C, nh);
+  if (msu_is16(dtype)) return msu_attn_mfma_bwd_workspace(g.nwin, C, nh);
   const long nblk = f32_bwd_blocks(g.nwin, nh);
   return nblk * nh * NT * NT + (long)nh * NT * NT + nblk * 3 * C;
 }
@@ -459,8 +459,8 @@ int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const f
   hipStream_t st = (hipStream_t)stream;
   hipStream_t pst = (hipStream_t)param_stream;
   if (g.nwin == 0) return 0;
-  if (dtype == MSU_BF16)
-    return msu_attn_mfma_bwd(qkv, qkv_bias, table, dout, dqkv, dtable, dqkv_bias_pad, workspace, B, H, W,
+  if (msu_is16(dtype))
+    return msu_attn_mfma_bwd(dtype, qkv, qkv_bias, table, dout, dqkv, dtable, dqkv_bias_pad, workspace, B, H, W,
                              C, nh, shift, p_drop, seed, st, pst);
   const int nblk = f32_bwd_blocks(g.nwin, nh);
   const float scale = 1.0f / sqrtf((float)HD);

@@ -1,4 +1,4 @@
-// bf16 shifted-window attention on 32x32x16 MFMA, scores kept TRANSPOSED (keys on the
+// 16-bit (bf16 / f16) shifted-window attention on 32x32x16 MFMA, scores kept TRANSPOSED (keys on the
 // accumulator rows, queries on the lanes) -- the training-mode fast path of
 // msu_win_attn_fwd / msu_win_attn_bwd (torchvision shifted_window_attention semantics, see
 // window_attention.hip for the pad / roll / partition folding and the f32 parity kernel).
@@ -50,8 +50,10 @@ struct Geom {
   long nwin;
 };
 
+// T (bf16_t / f16_t): the 16-bit format of the raw words stored in qkv / dout / LDS
+template <typename T>
 MSU_DEV f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  return Fmt16<T>::mma32(a, b, c);
 }
 
 // row-major k-contiguous fragment: lane l -> row (l&31), k = k0 + 8(l>>5) .. +7
@@ -92,12 +94,12 @@ MSU_DEV bf16x8 frag_tr_q4(const bf16_t* img, int ld, int r0, int col0, int lane)
   return *reinterpret_cast<bf16x8*>(both);
 }
 
-// accumulator registers 8s..8s+7 -> bf16 fragment
+// accumulator registers 8s..8s+7 -> 16-bit fragment
+template <typename T>
 MSU_DEV bf16x8 pack8(const f32x16& a, int s) {
-  bf16x8 f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) f[e] = (__bf16)a[8 * s + e];
-  return f;
+  const u32x4 w = {pack2<T>(a[8 * s], a[8 * s + 1]), pack2<T>(a[8 * s + 2], a[8 * s + 3]),
+                   pack2<T>(a[8 * s + 4], a[8 * s + 5]), pack2<T>(a[8 * s + 6], a[8 * s + 7])};
+  return __builtin_bit_cast(bf16x8, w);
 }
 
 // accumulator row of register r for lane half h (32x32 C layout)
@@ -194,6 +196,7 @@ MSU_DEV void bias_init(f32x16 (&P)[2][2], const float* bimg, int lane) {
 }
 
 // P: the bias image (bias_init); + K Q^T, mask, softmax over j
+template <typename T>
 MSU_DEV void probs_T_from(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (&qb)[2][2],
                           const int* sReg, bool boundary, float scale, int lane) {
 #pragma unroll
@@ -201,7 +204,7 @@ MSU_DEV void probs_T_from(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf1
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-      for (int it = 0; it < 2; ++it) P[jt][it] = mfma32(ka[jt][ks], qb[it][ks], P[jt][it]);
+      for (int it = 0; it < 2; ++it) P[jt][it] = mfma32<T>(ka[jt][ks], qb[it][ks], P[jt][it]);
   const int h = lane >> 5;
   if (boundary) {
     const float mval = -100.0f / scale;
@@ -242,16 +245,16 @@ MSU_DEV void probs_T_from(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf1
   }
 }
 
-template <bool LANE_INNER = false>
+template <typename T, bool LANE_INNER = false>
 MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (&qb)[2][2],
                      const float* bimg, const int* sReg, bool boundary, float scale, int lane) {
   bias_init<LANE_INNER>(P, bimg, lane);
-  probs_T_from(P, ka, qb, sReg, boundary, scale, lane);
+  probs_T_from<T>(P, ka, qb, sReg, boundary, scale, lane);
 }
 
 struct Aux {
   const float* bimg;      // [nh][4096] bias image / scale
-  const bf16_t* biasrow;  // [3C] bf16 qkv bias (padded tokens' q|k|v)
+  const bf16_t* biasrow;  // [3C] 16-bit qkv bias (padded tokens' q|k|v)
   const bf16_t* zrow;     // [3C] zeros (row of a TOK_ZERO token, any column offset)
 };
 
@@ -269,7 +272,7 @@ struct FwdLds {
 // win + stride, ...; the HBM loads of window i+1 (token table, K / Q fragments, V rows) are
 // issued before window i is computed, so their latency hides under window i's MFMAs and
 // softmax instead of being paid per item.
-template <int WAVES>
+template <typename T, int WAVES>
 __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __restrict__ qkv, Aux aux,
                                                                bf16_t* __restrict__ out, Geom g, float scale,
                                                                float p_drop, uint64_t seed) {
@@ -342,7 +345,7 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
         qb[t][ks] = frag_rows(L.q, LD, 32 * t, 16 * ks, lane);
       }
     f32x16 P[2][2];
-    probs_T<true>(P, ka, qb, reinterpret_cast<const float*>(sBimg), L.reg[buf], bnd[buf], scale, lane);
+    probs_T<T, true>(P, ka, qb, reinterpret_cast<const float*>(sBimg), L.reg[buf], bnd[buf], scale, lane);
     if (p_drop > 0.f) {
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
@@ -361,7 +364,7 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
       for (int s = 0; s < 2; ++s) {
         const bf16x8 a = frag_tr_perm(L.v, LD, jt * 32 + 16 * s, 0, lane);
 #pragma unroll
-        for (int it = 0; it < 2; ++it) O[it] = mfma32(a, pack8(P[jt][it], s), O[it]);
+        for (int it = 0; it < 2; ++it) O[it] = mfma32<T>(a, pack8<T>(P[jt][it], s), O[it]);
       }
     // output through the q image (its fragments are consumed): lane -> query i, registers
     // 4gq..4gq+3 -> d = 8gq + 4hh .. +3; then 4 lanes per token store its 64-B slice
@@ -371,8 +374,8 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
         uint2 w;
-        w.x = (uint32_t)from_f32<bf16_t>(O[it][4 * gq]) | ((uint32_t)from_f32<bf16_t>(O[it][4 * gq + 1]) << 16);
-        w.y = (uint32_t)from_f32<bf16_t>(O[it][4 * gq + 2]) | ((uint32_t)from_f32<bf16_t>(O[it][4 * gq + 3]) << 16);
+        w.x = pack2<T>(O[it][4 * gq], O[it][4 * gq + 1]);
+        w.y = pack2<T>(O[it][4 * gq + 2], O[it][4 * gq + 3]);
         *reinterpret_cast<uint2*>(L.q + i * LD + 8 * gq + 4 * hh) = w;
       }
     }
@@ -408,7 +411,7 @@ struct BwdLds {
   int tok[2][64], reg[2][64];          // current / prefetched window
 };
 
-template <int WAVES>
+template <typename T, int WAVES>
 __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
     const bf16_t* __restrict__ qkv, Aux aux, const bf16_t* __restrict__ dout, bf16_t* __restrict__ dqkv,
     float* __restrict__ dB_part, float* __restrict__ qb_part, Geom g, float scale, float p_drop,
@@ -488,7 +491,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
       for (int a = 0; a < 2; ++a)
         for (int b = 0; b < 2; ++b) P[a][b][0] += (float)ka[a][b][0] * (float)qb[b][a][1];
     } else {
-      probs_T_from(P, ka, qb, sReg, boundary, scale, lane);
+      probs_T_from<T>(P, ka, qb, sReg, boundary, scale, lane);
     }
     // dPd^T[j][i] = sum_d V[j][d] dO[i][d]
     f32x16 D[2][2];
@@ -506,7 +509,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
 #pragma unroll
         for (int it = 0; it < 2; ++it) {
           if constexpr (MSU_EXP & 4) D[jt][it][ks] += (float)va[jt][ks][0] * (float)b[it][1];
-          else D[jt][it] = mfma32(va[jt][ks], b[it], D[jt][it]);
+          else D[jt][it] = mfma32<T>(va[jt][ks], b[it], D[jt][it]);
         }
     }
 #pragma unroll
@@ -539,10 +542,10 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
           }
           const int j0 = jt * 32 + 8 * gq + 4 * hh;
           uint2 wp, wd;
-          wp.x = (uint32_t)from_f32<bf16_t>(pd[0]) | ((uint32_t)from_f32<bf16_t>(pd[1]) << 16);
-          wp.y = (uint32_t)from_f32<bf16_t>(pd[2]) | ((uint32_t)from_f32<bf16_t>(pd[3]) << 16);
-          wd.x = (uint32_t)from_f32<bf16_t>(ds[0]) | ((uint32_t)from_f32<bf16_t>(ds[1]) << 16);
-          wd.y = (uint32_t)from_f32<bf16_t>(ds[2]) | ((uint32_t)from_f32<bf16_t>(ds[3]) << 16);
+          wp.x = pack2<T>(pd[0], pd[1]);
+          wp.y = pack2<T>(pd[2], pd[3]);
+          wd.x = pack2<T>(ds[0], ds[1]);
+          wd.y = pack2<T>(ds[2], ds[3]);
           if (!(MSU_EXP & 16) || pd[0] == 1.2345e-30f) {
             *reinterpret_cast<uint2*>(L.P + i * LDP + j0) = wp;
             *reinterpret_cast<uint2*>(L.dS + i * LDP + j0) = wd;
@@ -563,9 +566,9 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
         if constexpr (MSU_EXP & 8) {
           av[ks / 16] += (float)bdo[0] * (float)bq[1] * (float)bk[2];
         } else {
-          av = mfma32(frag_tr_q4(L.P, LDP, ks, mt * 32, lane), bdo, av);
-          ak = mfma32(frag_tr_q4(L.dS, LDP, ks, mt * 32, lane), bq, ak);
-          aq = mfma32(frag_rows(L.dS, LDP, mt * 32, ks, lane), bk, aq);
+          av = mfma32<T>(frag_tr_q4(L.P, LDP, ks, mt * 32, lane), bdo, av);
+          ak = mfma32<T>(frag_tr_q4(L.dS, LDP, ks, mt * 32, lane), bq, ak);
+          aq = mfma32<T>(frag_rows(L.dS, LDP, mt * 32, ks, lane), bk, aq);
         }
       }
       const int d = lane & 31;
@@ -575,9 +578,9 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
         const int tok = sTok[t];
         if (tok >= 0 && (!(MSU_EXP & 1) || aq[r] == 1.2345e-30f)) {
           bf16_t* row = dqkv + (long)tok * C3 + h * HD + d;
-          row[0] = from_f32<bf16_t>(aq[r] * scale);
-          row[g.C] = from_f32<bf16_t>(ak[r] * scale);
-          row[2 * g.C] = from_f32<bf16_t>(av[r]);
+          row[0] = (bf16_t)Fmt16<T>::bits(aq[r] * scale);
+          row[g.C] = (bf16_t)Fmt16<T>::bits(ak[r] * scale);
+          row[2 * g.C] = (bf16_t)Fmt16<T>::bits(av[r]);
         } else if (tok == TOK_PAD) {
           padacc[0] += aq[r] * scale;
           padacc[1] += ak[r] * scale;
@@ -620,12 +623,13 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
 
 // bias image [nh][4 tiles (jt*2+it)][64 lanes][16 regs] = table[idx(i,j)][h] / scale
 // (i, j < 49), -inf for padded keys j >= 49, 0 for padded queries i >= 49.  Block 0 also
-// writes the bf16 qkv-bias row and the zero row.
+// writes the 16-bit qkv-bias row and the zero row.
+template <typename T>
 __global__ void __launch_bounds__(256) aux_kernel(const float* table, const float* qkv_bias, int nh, int C3,
                                                   float inv_scale, float* img, bf16_t* biasrow, bf16_t* zrow) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (blockIdx.x == 0) {
-    for (int c = threadIdx.x; c < C3; c += 256) biasrow[c] = from_f32<bf16_t>(qkv_bias[c]);
+    for (int c = threadIdx.x; c < C3; c += 256) biasrow[c] = (bf16_t)Fmt16<T>::bits(qkv_bias[c]);
     for (int c = threadIdx.x; c < C3; c += 256) zrow[c] = 0;
   }
   if (e >= nh * 4096) return;
@@ -701,7 +705,7 @@ int bwd_blocks(long nwin, int nh) {
 
 }  // namespace
 
-// entry points used by window_attention.hip for dtype == bf16
+// entry points used by window_attention.hip for the 16-bit dtypes
 long msu_attn_mfma_fwd_workspace(int C, int nh) { return aux_floats(C, nh); }
 
 long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh) {
@@ -709,7 +713,7 @@ long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh) {
   return aux_floats(C, nh) + parts * nh * 4096 + (long)nh * 4096 + parts * 3L * C;
 }
 
-int msu_attn_mfma_fwd(const void* qkv, const float* qkv_bias, const float* table, void* out, int B,
+int msu_attn_mfma_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, void* out, int B,
                       int H, int W, int C, int nh, int shift, float p_drop, unsigned long long seed,
                       float* ws, hipStream_t st) {
   const Geom g = make_geom(B, H, W, C, nh, shift);
@@ -718,18 +722,19 @@ int msu_attn_mfma_fwd(const void* qkv, const float* qkv_bias, const float* table
   const float scale = 1.0f / sqrtf((float)HD);
   float* img; bf16_t* brow; bf16_t* zrow;
   const Aux aux = carve_aux(ws, C, nh, &img, &brow, &zrow);
-  hipLaunchKernelGGL(aux_kernel, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
-                     1.0f / scale, img, brow, zrow);
   // persistent: about two 4-wave workgroups per CU, split over the heads
   long nb = (g.nwin + FWD_WAVES - 1) / FWD_WAVES;
   const long cap = 512 / nh > 0 ? 512 / nh : 1;
   if (nb > cap) nb = cap;
-  hipLaunchKernelGGL(attn_fwd_mfma<FWD_WAVES>, dim3((unsigned)nb, (unsigned)nh), dim3(64 * FWD_WAVES), 0, st,
-                     (const bf16_t*)qkv, aux, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed);
+  MSU_DISPATCH16(dtype, T,
+    hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
+                       1.0f / scale, img, brow, zrow);
+    hipLaunchKernelGGL((attn_fwd_mfma<T, FWD_WAVES>), dim3((unsigned)nb, (unsigned)nh), dim3(64 * FWD_WAVES), 0, st,
+                       (const bf16_t*)qkv, aux, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed));
   return MSU_CHECK_LAUNCH();
 }
 
-int msu_attn_mfma_bwd(const void* qkv, const float* qkv_bias, const float* table, const void* dout,
+int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, const void* dout,
                       void* dqkv, float* dtable, float* dqkv_bias_pad, float* ws, int B, int H, int W,
                       int C, int nh, int shift, float p_drop, unsigned long long seed, hipStream_t st,
                       hipStream_t pst) {
@@ -743,11 +748,12 @@ int msu_attn_mfma_bwd(const void* qkv, const float* qkv_bias, const float* table
   float* dB_part = ws + aux_floats(C, nh);
   float* dimg = dB_part + parts * nh * 4096;
   float* qb_part = dimg + (long)nh * 4096;
-  hipLaunchKernelGGL(aux_kernel, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
-                     1.0f / scale, img, brow, zrow);
-  hipLaunchKernelGGL(attn_bwd_mfma<BWD_WAVES>, dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
-                     (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
-                     p_drop, (uint64_t)seed, nblk);
+  MSU_DISPATCH16(dtype, T,
+    hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
+                       1.0f / scale, img, brow, zrow);
+    hipLaunchKernelGGL((attn_bwd_mfma<T, BWD_WAVES>), dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
+                       (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
+                       p_drop, (uint64_t)seed, nblk));
   // parameter-gradient reductions: on pst (after the backward kernel) when given
   const int rc = attn_param_stream(st, pst);
   if (rc) return rc;

@@ -1,20 +1,31 @@
-"""Autograd wrappers over the HIP C-ABI (``include/msunet_hip.h``).
+"""The MS-UNet hot-path operators, registered as ``torch.library`` custom ops.
 
-Every op here launches hand-written gfx950 kernels from ``libmsunet_hip.so`` on the
-current HIP stream of its input's device.  There is no CPU / eager fallback: a CPU tensor
-or a missing library raises.  Activations are float32 (parity mode) or bfloat16 (training
-mode, chosen by ``torch.autocast``); statistics, parameters and parameter gradients are
-float32.
+Every operator is ``torch.ops.msunet.<name>``: a schema, a CUDA (HIP) kernel that launches
+hand-written gfx950 kernels from ``libmsunet_hip.so`` through the C-ABI
+(``include/msunet_hip.h``) on the current HIP stream, a fake (meta) kernel for shape
+propagation, and an autograd formula attached with ``torch.library.register_autograd``.
+There is no CPU / eager fallback: a CPU tensor has no kernel (the dispatcher raises) and a
+missing library raises ``_lib.HipLibraryError``.
+
+Activations are float32 (parity mode), bfloat16 (training mode) or float16 (the reference's
+``torch.amp.autocast('cuda', dtype=torch.float16)`` step, trainer.py:308), chosen by the
+autocast state of the caller; statistics, parameters and parameter gradients are float32.
+
+The public functions below (``layer_norm``, ``linear``, ``window_attention`` ...) are what the
+modules in ``network/`` call.  They cast the activation to the autocast dtype and invoke the
+registered op.  ``set_dispatch("fast")`` routes the same implementations through a plain
+``autograd.Function`` built from the very same forward / setup / backward functions (no
+dispatcher round trip: ~15 us less host time per call), for launch-bound eager loops; the
+numerics are identical by construction.
 """
-import math
-
 import os
 
 import torch
 
 from . import _lib
 
-_DT = {torch.float32: 0, torch.bfloat16: 1}
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+_LOW = (torch.bfloat16, torch.float16)
 
 
 # ----------------------------------------------------------------------------- helpers
@@ -22,7 +33,7 @@ def _dt(t):
     try:
         return _DT[t.dtype]
     except KeyError:
-        raise TypeError(f"unsupported activation dtype {t.dtype} (float32 / bfloat16)") from None
+        raise TypeError(f"unsupported activation dtype {t.dtype} (float32 / bfloat16 / float16)") from None
 
 
 def _need_cuda(*ts):
@@ -40,7 +51,7 @@ _raw_stream = torch._C._cuda_getCurrentRawStream
 
 def _s(t):
     """hipStream_t (as int) of the current stream on t's device.  The raw getter skips the
-    Python Stream object torch.cuda.current_stream builds: a few µs per launch of host time,
+    Python Stream object torch.cuda.current_stream builds: a few us per launch of host time,
     which is what bounds the short stage-2/3 kernels."""
     return _raw_stream(t.get_device())
 
@@ -59,6 +70,62 @@ def _f32(t):
 def _as(t, dtype):
     t = t if t.dtype == dtype else t.to(dtype)
     return t.contiguous()
+
+
+# ----------------------------------------------------------------------------- registration
+_LIB = torch.library.Library("msunet", "DEF")
+_DISPATCH = os.environ.get("MSU_DISPATCH", "torch_ops")  # "torch_ops" | "fast"
+_OPS = {}
+
+
+class _Op:
+    """One registered operator: the ``torch.ops.msunet`` overload and the equivalent direct
+    autograd.Function built from the same forward / setup_context / backward."""
+
+    __slots__ = ("op", "fast")
+
+    def __call__(self, *args):
+        return (self.op if _DISPATCH == "torch_ops" else self.fast)(*args)
+
+
+def set_dispatch(mode):
+    """'torch_ops': call through torch.ops.msunet (dispatcher + register_autograd);
+    'fast': the same implementation as a plain autograd.Function."""
+    global _DISPATCH
+    if mode not in ("torch_ops", "fast"):
+        raise ValueError(mode)
+    _DISPATCH = mode
+
+
+def _fast_function(name, impl, setup, backward):
+    def fwd(ctx, *args):
+        out = impl(*args)
+        setup(ctx, args, out)
+        return out
+
+    def bwd(ctx, *grads):
+        return backward(ctx, *grads)
+
+    return type("_" + name, (torch.autograd.Function,), {"forward": staticmethod(fwd),
+                                                          "backward": staticmethod(bwd)}).apply
+
+
+def _define(name, schema, impl, fake, setup=None, backward=None):
+    _LIB.define(name + schema)
+    _LIB.impl(name, impl, "CUDA")
+    torch.library.register_fake("msunet::" + name, fake, lib=_LIB)
+    if backward is not None:
+        torch.library.register_autograd("msunet::" + name, backward, setup_context=setup, lib=_LIB)
+    o = _Op()
+    o.op = getattr(torch.ops.msunet, name).default
+    o.fast = _fast_function(name, impl, setup, backward) if backward is not None else o.op
+    _OPS[name] = o
+    return o
+
+
+def registered_ops():
+    """Names of the torch.ops.msunet operators."""
+    return sorted(_OPS)
 
 
 # ----------------------------------------------------------------------------- direct grads
@@ -181,233 +248,298 @@ def _ln_parts(rows, C, device):
 IN_PLAIN, IN_ADD, IN_MERGE, IN_D2S2 = 0, 1, 2, 3
 
 
-# ----------------------------------------------------------------------------- LayerNorm
-class _LayerNorm(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w, b, eps):
-        _need_cuda(x)
-        x = x.contiguous()
-        C = x.shape[-1]
-        rows = x.numel() // C
-        y = torch.empty_like(x)
-        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
-        rstd = torch.empty_like(mean)
-        _lib.call("msu_layernorm_fwd", _dt(x), IN_PLAIN, _p(x), None, None, 1, None, _p(w), _p(b),
-                  _p(y), _p(mean), _p(rstd), rows, C, 0, 0, 0, eps, _s(x))
-        ctx.save_for_backward(x, w, mean, rstd)
-        ctx.affine = (w, b)
-        return y
+def _stats(x, rows):
+    return (torch.empty(rows, device=x.device, dtype=torch.float32),
+            torch.empty(rows, device=x.device, dtype=torch.float32))
 
-    @staticmethod
-    def backward(ctx, dy):
-        x, w, mean, rstd = ctx.saved_tensors
-        dy = _as(dy, x.dtype)
-        C = x.shape[-1]
-        rows = x.numel() // C
-        dx = torch.empty_like(x)
-        dw, db, acc, direct = _ln_grads(ctx, C, x.device)
-        n, part = _ln_parts(rows, C, x.device)
-        _lib.call("msu_layernorm_bwd", _dt(x), IN_PLAIN, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, C, 0, 0, 0, acc, _s(x))
-        if direct:
-            _notify(*ctx.affine)
-            return dx, None, None, None
-        return dx, dw, db, None
+
+# ----------------------------------------------------------------------------- LayerNorm
+def _ln_impl(x, w, b, eps):
+    _need_cuda(x)
+    x = x.contiguous()
+    C = x.shape[-1]
+    rows = x.numel() // C
+    y = torch.empty_like(x)
+    mean, rstd = _stats(x, rows)
+    _lib.call("msu_layernorm_fwd", _dt(x), IN_PLAIN, _p(x), None, None, 1, None, _p(w), _p(b),
+              _p(y), _p(mean), _p(rstd), rows, C, 0, 0, 0, eps, _s(x))
+    return y, mean, rstd
+
+
+def _ln_fake(x, w, b, eps):
+    rows = x.numel() // x.shape[-1]
+    return torch.empty_like(x), x.new_empty(rows, dtype=torch.float32), x.new_empty(rows, dtype=torch.float32)
+
+
+def _ln_setup(ctx, inputs, output):
+    x, w, b, eps = inputs
+    ctx.save_for_backward(x.contiguous(), w, output[1], output[2])
+    ctx.affine = (w, b)
+    ctx.set_materialize_grads(False)
+
+
+def _ln_backward(ctx, dy, _dm, _dr):
+    x, w, mean, rstd = ctx.saved_tensors
+    if dy is None:
+        return None, None, None, None
+    dy = _as(dy, x.dtype)
+    C = x.shape[-1]
+    rows = x.numel() // C
+    dx = torch.empty_like(x)
+    dw, db, acc, direct = _ln_grads(ctx, C, x.device)
+    n, part = _ln_parts(rows, C, x.device)
+    _lib.call("msu_layernorm_bwd", _dt(x), IN_PLAIN, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
+              _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, C, 0, 0, 0, acc, _s(x))
+    if direct:
+        _notify(*ctx.affine)
+        return dx, None, None, None
+    return dx, dw, db, None
+
+
+_layer_norm = _define("layer_norm", "(Tensor x, Tensor weight, Tensor bias, float eps) -> (Tensor, Tensor, Tensor)",
+                      _ln_impl, _ln_fake, _ln_setup, _ln_backward)
 
 
 def layer_norm(x, weight, bias, eps=1e-5):
-    """nn.LayerNorm(C) over the last dim; x keeps its dtype."""
-    return _LayerNorm.apply(_as(x, act_dtype()), _f32(weight), _f32(bias), eps)
+    """nn.LayerNorm(C) over the last dim; x keeps its (autocast) dtype."""
+    return _layer_norm(_as(x, act_dtype()), _f32(weight), _f32(bias), float(eps))[0]
 
 
-class _AddLayerNorm(torch.autograd.Function):
-    """s = a + scale[b] * branch ; y = LN(s).  Returns (s, y)."""
+def _add_ln_impl(a, branch, scale, w, b, eps):
+    """s = a + scale[sample] * branch ; y = LN(s)."""
+    _need_cuda(a, branch)
+    a, branch = a.contiguous(), branch.contiguous()
+    C = a.shape[-1]
+    rows = a.numel() // C
+    rps = rows // a.shape[0]
+    s = torch.empty_like(a)
+    y = torch.empty_like(a)
+    mean, rstd = _stats(a, rows)
+    _lib.call("msu_layernorm_fwd", _dt(a), IN_ADD, _p(a), _p(branch), _p(scale), rps, _p(s), _p(w),
+              _p(b), _p(y), _p(mean), _p(rstd), rows, C, 0, 0, 0, eps, _s(a))
+    return s, y, mean, rstd
 
-    @staticmethod
-    def forward(ctx, a, branch, scale, w, b, eps):
-        _need_cuda(a, branch)
-        a, branch = a.contiguous(), branch.contiguous()
-        C = a.shape[-1]
-        rows = a.numel() // C
-        rps = rows // a.shape[0]
-        s = torch.empty_like(a)
-        y = torch.empty_like(a)
-        mean = torch.empty(rows, device=a.device, dtype=torch.float32)
-        rstd = torch.empty_like(mean)
-        _lib.call("msu_layernorm_fwd", _dt(a), IN_ADD, _p(a), _p(branch), _p(scale), rps, _p(s), _p(w),
-                  _p(b), _p(y), _p(mean), _p(rstd), rows, C, 0, 0, 0, eps, _s(a))
-        ctx.save_for_backward(s, w, mean, rstd, scale)
-        ctx.rps = rps
-        ctx.affine = (w, b)
-        ctx.set_materialize_grads(False)
-        return s, y
 
-    @staticmethod
-    def backward(ctx, ds, dy):
-        s, w, mean, rstd, scale = ctx.saved_tensors
-        C = s.shape[-1]
-        rows = s.numel() // C
-        if dy is None:
-            dy = torch.zeros_like(s)
-        dy = _as(dy, s.dtype)
-        ds = None if ds is None else _as(ds, s.dtype)
-        da = torch.empty_like(s)
-        dbr = torch.empty_like(s) if scale is not None else None
-        dw, dbb, acc, direct = _ln_grads(ctx, C, s.device)
-        n, part = _ln_parts(rows, C, s.device)
-        _lib.call("msu_layernorm_bwd", _dt(s), IN_ADD, _p(dy), _p(s), _p(ds), _p(w), _p(mean), _p(rstd),
-                  _p(da), _p(dbr), _p(scale), ctx.rps, _p(part), n, _p(dw), _p(dbb), rows, C, 0, 0, 0, acc,
-                  _s(s))
-        if direct:
-            _notify(*ctx.affine)
-            dw = dbb = None
-        return da, (dbr if dbr is not None else da), None, dw, dbb, None
+def _add_ln_fake(a, branch, scale, w, b, eps):
+    rows = a.numel() // a.shape[-1]
+    return (torch.empty_like(a), torch.empty_like(a), a.new_empty(rows, dtype=torch.float32),
+            a.new_empty(rows, dtype=torch.float32))
+
+
+def _add_ln_setup(ctx, inputs, output):
+    a, branch, scale, w, b, eps = inputs
+    s, y, mean, rstd = output
+    ctx.save_for_backward(s, w, mean, rstd, scale)
+    ctx.rps = (a.numel() // a.shape[-1]) // a.shape[0]
+    ctx.affine = (w, b)
+    ctx.set_materialize_grads(False)
+
+
+def _add_ln_backward(ctx, ds, dy, _dm, _dr):
+    s, w, mean, rstd, scale = ctx.saved_tensors
+    C = s.shape[-1]
+    rows = s.numel() // C
+    if dy is None:
+        dy = torch.zeros_like(s)
+    dy = _as(dy, s.dtype)
+    ds = None if ds is None else _as(ds, s.dtype)
+    da = torch.empty_like(s)
+    dbr = torch.empty_like(s) if scale is not None else None
+    dw, dbb, acc, direct = _ln_grads(ctx, C, s.device)
+    n, part = _ln_parts(rows, C, s.device)
+    _lib.call("msu_layernorm_bwd", _dt(s), IN_ADD, _p(dy), _p(s), _p(ds), _p(w), _p(mean), _p(rstd),
+              _p(da), _p(dbr), _p(scale), ctx.rps, _p(part), n, _p(dw), _p(dbb), rows, C, 0, 0, 0, acc,
+              _s(s))
+    if direct:
+        _notify(*ctx.affine)
+        dw = dbb = None
+    return da, (dbr if dbr is not None else da), None, dw, dbb, None
+
+
+_add_layer_norm = _define(
+    "add_layer_norm",
+    "(Tensor a, Tensor branch, Tensor? scale, Tensor weight, Tensor bias, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
+    _add_ln_impl, _add_ln_fake, _add_ln_setup, _add_ln_backward)
 
 
 def add_layer_norm(a, branch, scale, weight, bias, eps=1e-5):
+    """(s, LN(s)) with s = a + scale[sample] * branch (torchvision block residual with
+    StochasticDepth 'row', fused with the next norm)."""
     dt = act_dtype()
     sc = None if scale is None else _f32(scale)
-    return _AddLayerNorm.apply(_as(a, dt), _as(branch, dt), sc, _f32(weight), _f32(bias), eps)
+    s, y, _, _ = _add_layer_norm(_as(a, dt), _as(branch, dt), sc, _f32(weight), _f32(bias), float(eps))
+    return s, y
 
 
-class _MergeLayerNorm(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w, b, eps):
-        _need_cuda(x)
-        x = x.contiguous()
-        B, H, W, C = x.shape
-        rows = B * (H // 2) * (W // 2)
-        y = torch.empty(B, rows // B, 4 * C, device=x.device, dtype=x.dtype)
-        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
-        rstd = torch.empty_like(mean)
-        _lib.call("msu_layernorm_fwd", _dt(x), IN_MERGE, _p(x), None, None, 1, None, _p(w), _p(b),
-                  _p(y), _p(mean), _p(rstd), rows, 4 * C, H, W, C, eps, _s(x))
-        ctx.save_for_backward(x, w, mean, rstd)
-        ctx.affine = (w, b)
-        return y
+def _merge_ln_impl(x, w, b, eps):
+    _need_cuda(x)
+    x = x.contiguous()
+    B, H, W, C = x.shape
+    rows = B * (H // 2) * (W // 2)
+    y = torch.empty(B, rows // B, 4 * C, device=x.device, dtype=x.dtype)
+    mean, rstd = _stats(x, rows)
+    _lib.call("msu_layernorm_fwd", _dt(x), IN_MERGE, _p(x), None, None, 1, None, _p(w), _p(b),
+              _p(y), _p(mean), _p(rstd), rows, 4 * C, H, W, C, eps, _s(x))
+    return y, mean, rstd
 
-    @staticmethod
-    def backward(ctx, dy):
-        x, w, mean, rstd = ctx.saved_tensors
-        B, H, W, C = x.shape
-        rows = B * (H // 2) * (W // 2)
-        dy = _as(dy, x.dtype)
-        dx = torch.empty_like(x)
-        dw, db, acc, direct = _ln_grads(ctx, 4 * C, x.device)
-        n, part = _ln_parts(rows, 4 * C, x.device)
-        _lib.call("msu_layernorm_bwd", _dt(x), IN_MERGE, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, 4 * C, H, W, C, acc, _s(x))
-        if direct:
-            _notify(*ctx.affine)
-            return dx, None, None, None
-        return dx, dw, db, None
+
+def _merge_ln_fake(x, w, b, eps):
+    B, H, W, C = x.shape
+    rows = B * (H // 2) * (W // 2)
+    return (x.new_empty(B, rows // B, 4 * C), x.new_empty(rows, dtype=torch.float32),
+            x.new_empty(rows, dtype=torch.float32))
+
+
+def _merge_ln_backward(ctx, dy, _dm, _dr):
+    x, w, mean, rstd = ctx.saved_tensors
+    if dy is None:
+        return None, None, None, None
+    B, H, W, C = x.shape
+    rows = B * (H // 2) * (W // 2)
+    dy = _as(dy, x.dtype)
+    dx = torch.empty_like(x)
+    dw, db, acc, direct = _ln_grads(ctx, 4 * C, x.device)
+    n, part = _ln_parts(rows, 4 * C, x.device)
+    _lib.call("msu_layernorm_bwd", _dt(x), IN_MERGE, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
+              _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, 4 * C, H, W, C, acc, _s(x))
+    if direct:
+        _notify(*ctx.affine)
+        return dx, None, None, None
+    return dx, dw, db, None
+
+
+_merge_layer_norm = _define("merge_layer_norm",
+                            "(Tensor x, Tensor weight, Tensor bias, float eps) -> (Tensor, Tensor, Tensor)",
+                            _merge_ln_impl, _merge_ln_fake, _ln_setup, _merge_ln_backward)
 
 
 def merge_layer_norm(x, weight, bias, eps=1e-5):
     """PatchMerging gather (x0,x1,x2,x3 order) + LayerNorm(4C): [B,H,W,C] -> [B,HW/4,4C]."""
-    return _MergeLayerNorm.apply(_as(x, act_dtype()), _f32(weight), _f32(bias), eps)
+    return _merge_layer_norm(_as(x, act_dtype()), _f32(weight), _f32(bias), float(eps))[0]
 
 
-class _D2SLayerNorm(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w, b, eps):
-        _need_cuda(x)
-        x = x.contiguous()
-        B, H, W, C4 = x.shape
-        c = C4 // 4
-        rows = B * 4 * H * W
-        y = torch.empty(B, 4 * H * W, c, device=x.device, dtype=x.dtype)
-        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
-        rstd = torch.empty_like(mean)
-        _lib.call("msu_layernorm_fwd", _dt(x), IN_D2S2, _p(x), None, None, 1, None, _p(w), _p(b),
-                  _p(y), _p(mean), _p(rstd), rows, c, H, W, 0, eps, _s(x))
-        ctx.save_for_backward(x, w, mean, rstd)
-        ctx.affine = (w, b)
-        return y
+def _d2s_ln_impl(x, w, b, eps):
+    _need_cuda(x)
+    x = x.contiguous()
+    B, H, W, C4 = x.shape
+    c = C4 // 4
+    rows = B * 4 * H * W
+    y = torch.empty(B, 4 * H * W, c, device=x.device, dtype=x.dtype)
+    mean, rstd = _stats(x, rows)
+    _lib.call("msu_layernorm_fwd", _dt(x), IN_D2S2, _p(x), None, None, 1, None, _p(w), _p(b),
+              _p(y), _p(mean), _p(rstd), rows, c, H, W, 0, eps, _s(x))
+    return y, mean, rstd
 
-    @staticmethod
-    def backward(ctx, dy):
-        x, w, mean, rstd = ctx.saved_tensors
-        B, H, W, C4 = x.shape
-        c = C4 // 4
-        rows = B * 4 * H * W
-        dy = _as(dy, x.dtype)
-        dx = torch.empty_like(x)
-        dw, db, acc, direct = _ln_grads(ctx, c, x.device)
-        n, part = _ln_parts(rows, c, x.device)
-        _lib.call("msu_layernorm_bwd", _dt(x), IN_D2S2, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, c, H, W, 0, acc, _s(x))
-        if direct:
-            _notify(*ctx.affine)
-            return dx, None, None, None
-        return dx, dw, db, None
+
+def _d2s_ln_fake(x, w, b, eps):
+    B, H, W, C4 = x.shape
+    rows = B * 4 * H * W
+    return (x.new_empty(B, 4 * H * W, C4 // 4), x.new_empty(rows, dtype=torch.float32),
+            x.new_empty(rows, dtype=torch.float32))
+
+
+def _d2s_ln_backward(ctx, dy, _dm, _dr):
+    x, w, mean, rstd = ctx.saved_tensors
+    if dy is None:
+        return None, None, None, None
+    B, H, W, C4 = x.shape
+    c = C4 // 4
+    rows = B * 4 * H * W
+    dy = _as(dy, x.dtype)
+    dx = torch.empty_like(x)
+    dw, db, acc, direct = _ln_grads(ctx, c, x.device)
+    n, part = _ln_parts(rows, c, x.device)
+    _lib.call("msu_layernorm_bwd", _dt(x), IN_D2S2, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
+              _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, c, H, W, 0, acc, _s(x))
+    if direct:
+        _notify(*ctx.affine)
+        return dx, None, None, None
+    return dx, dw, db, None
+
+
+_d2s_layer_norm = _define("d2s_layer_norm",
+                          "(Tensor x, Tensor weight, Tensor bias, float eps) -> (Tensor, Tensor, Tensor)",
+                          _d2s_ln_impl, _d2s_ln_fake, _ln_setup, _d2s_ln_backward)
 
 
 def d2s_layer_norm(x, weight, bias, eps=1e-5):
     """PatchExpand rearrange 'b h w (p1 p2 c) -> b (h p1) (w p2) c' (p=2) + LayerNorm(c)."""
-    return _D2SLayerNorm.apply(_as(x, act_dtype()), _f32(weight), _f32(bias), eps)
+    return _d2s_layer_norm(_as(x, act_dtype()), _f32(weight), _f32(bias), float(eps))[0]
 
 
 # ----------------------------------------------------------------------------- attention
-class _WindowAttention(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, qkv, qkv_bias, table, num_heads, shift, p_drop, seed):
-        _need_cuda(qkv)
-        qkv = qkv.contiguous()
-        B, H, W, C3 = qkv.shape
-        C = C3 // 3
-        out = torch.empty(B, H, W, C, device=qkv.device, dtype=qkv.dtype)
-        ws = torch.empty(_lib.lib().msu_win_attn_fwd_workspace(_dt(qkv), C, num_heads), device=qkv.device,
-                         dtype=torch.float32)
-        _lib.call("msu_win_attn_fwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(out), _p(ws), B, H, W,
-                  C, num_heads, shift, float(p_drop), seed, _s(qkv))
-        ctx.save_for_backward(qkv, qkv_bias, table)
-        # the parameter itself when it reached us uncast (trainer flat buffers: direct .grad)
-        ctx.bias_param = qkv_bias if isinstance(qkv_bias, torch.nn.Parameter) else None
-        ctx.table_param = table if isinstance(table, torch.nn.Parameter) else None
-        ctx.cfg = (num_heads, shift, float(p_drop), seed)
-        return out
+def _attn_impl(qkv, qkv_bias, table, num_heads, shift, p_drop, seed):
+    _need_cuda(qkv)
+    qkv = qkv.contiguous()
+    B, H, W, C3 = qkv.shape
+    C = C3 // 3
+    out = torch.empty(B, H, W, C, device=qkv.device, dtype=qkv.dtype)
+    ws = torch.empty(_lib.lib().msu_win_attn_fwd_workspace(_dt(qkv), C, num_heads), device=qkv.device,
+                     dtype=torch.float32)
+    _lib.call("msu_win_attn_fwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(out), _p(ws), B, H, W,
+              C, num_heads, shift, float(p_drop), seed, _s(qkv))
+    return out
 
-    @staticmethod
-    def backward(ctx, dout):
-        qkv, qkv_bias, table = ctx.saved_tensors
-        nh, shift, p_drop, seed = ctx.cfg
-        B, H, W, C3 = qkv.shape
-        C = C3 // 3
-        dout = _as(dout, qkv.dtype)
-        L = _lib.lib()
-        ws = torch.empty(L.msu_win_attn_bwd_workspace(_dt(qkv), B, H, W, C, nh), device=qkv.device,
-                         dtype=torch.float32)
-        dqkv = torch.empty_like(qkv)
-        bp, tp = ctx.bias_param, ctx.table_param
-        if bp is not None and tp is not None and _side_enabled and _direct(bp, tp):
-            # parameter-gradient tail on the side stream: the relative-table / qkv-bias
-            # reductions and their .grad adds (the qkv bias also receives its Linear's db
-            # there, so every write to its .grad is ordered on one stream)
-            main = torch.cuda.current_stream(qkv.device)
-            side = _side_stream_for(qkv.device)
-            with torch.cuda.stream(side):
-                dtable = torch.empty_like(table)
-                dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
-            _lib.call("msu_win_attn_bwd2", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
-                      _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, main.cuda_stream,
-                      side.cuda_stream)
-            ws.record_stream(side)
-            with torch.cuda.stream(side):
-                bp.grad.add_(dbias)
-                tp.grad.add_(dtable)
-            ev = torch.cuda.Event()
-            ev.record(side)
-            _guard_side_write(bp, ev)
-            _guard_side_write(tp, ev)
-            _join_at_end_of_backward()
-            _notify(bp, tp)
-            return dqkv, None, None, None, None, None, None
-        dtable = torch.empty_like(table)
-        dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
-        _lib.call("msu_win_attn_bwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
-                  _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _s(qkv))
-        return dqkv, dbias, dtable, None, None, None, None
+
+def _attn_fake(qkv, qkv_bias, table, num_heads, shift, p_drop, seed):
+    B, H, W, C3 = qkv.shape
+    return qkv.new_empty(B, H, W, C3 // 3)
+
+
+def _attn_setup(ctx, inputs, output):
+    qkv, qkv_bias, table, num_heads, shift, p_drop, seed = inputs
+    ctx.save_for_backward(qkv.contiguous(), qkv_bias, table)
+    # the parameter itself when it reached us uncast (trainer flat buffers: direct .grad)
+    ctx.bias_param = qkv_bias if isinstance(qkv_bias, torch.nn.Parameter) else None
+    ctx.table_param = table if isinstance(table, torch.nn.Parameter) else None
+    ctx.cfg = (num_heads, shift, float(p_drop), seed)
+
+
+def _attn_backward(ctx, dout):
+    qkv, qkv_bias, table = ctx.saved_tensors
+    nh, shift, p_drop, seed = ctx.cfg
+    B, H, W, C3 = qkv.shape
+    C = C3 // 3
+    dout = _as(dout, qkv.dtype)
+    L = _lib.lib()
+    ws = torch.empty(L.msu_win_attn_bwd_workspace(_dt(qkv), B, H, W, C, nh), device=qkv.device,
+                     dtype=torch.float32)
+    dqkv = torch.empty_like(qkv)
+    bp, tp = ctx.bias_param, ctx.table_param
+    if bp is not None and tp is not None and _side_enabled and _direct(bp, tp):
+        # parameter-gradient tail on the side stream: the relative-table / qkv-bias
+        # reductions and their .grad adds (the qkv bias also receives its Linear's db
+        # there, so every write to its .grad is ordered on one stream)
+        main = torch.cuda.current_stream(qkv.device)
+        side = _side_stream_for(qkv.device)
+        with torch.cuda.stream(side):
+            dtable = torch.empty_like(table)
+            dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
+        _lib.call("msu_win_attn_bwd2", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
+                  _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, main.cuda_stream,
+                  side.cuda_stream)
+        ws.record_stream(side)
+        with torch.cuda.stream(side):
+            bp.grad.add_(dbias)
+            tp.grad.add_(dtable)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        _guard_side_write(bp, ev)
+        _guard_side_write(tp, ev)
+        _join_at_end_of_backward()
+        _notify(bp, tp)
+        return dqkv, None, None, None, None, None, None
+    dtable = torch.empty_like(table)
+    dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
+    _lib.call("msu_win_attn_bwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
+              _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _s(qkv))
+    return dqkv, dbias, dtable, None, None, None, None
+
+
+_window_attention = _define(
+    "window_attention",
+    "(Tensor qkv, Tensor qkv_bias, Tensor table, int num_heads, int shift, float p_drop, int seed) -> Tensor",
+    _attn_impl, _attn_fake, _attn_setup, _attn_backward)
 
 
 def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0):
@@ -416,8 +548,8 @@ def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0)
     C3 = qkv.shape[-1]
     if C3 % 3 or (C3 // 3) != num_heads * 32:
         raise ValueError(f"head_dim must be 32 (C={C3 // 3}, heads={num_heads})")
-    return _WindowAttention.apply(_as(qkv, act_dtype()), _f32(qkv_bias), _f32(table), int(num_heads),
-                                  int(shift), float(p_drop), int(seed) & ((1 << 63) - 1))
+    return _window_attention(_as(qkv, act_dtype()), _f32(qkv_bias), _f32(table), int(num_heads),
+                             int(shift), float(p_drop), int(seed) & ((1 << 63) - 1))
 
 
 # ----------------------------------------------------------------------------- token GEMM
@@ -426,7 +558,7 @@ _tok_cache = {}
 
 
 def tok_supported(M, N, K):
-    """Whether the HIP token GEMM (csrc/gemm_tok.h) covers this bf16 Linear shape."""
+    """Whether the HIP token GEMM (csrc/gemm_tok.h) covers this 16-bit Linear shape."""
     key = (int(M), int(N), int(K))
     r = _tok_cache.get(key)
     if r is None:
@@ -456,21 +588,21 @@ def tok_preferred(M, N, K):
 
 
 def tok_gemm(a, w, bias=None, epi=TOK_PLAIN, h=None, a2=None):
-    """bf16 Y = epi(A . W^T + bias) on the token GEMM kernel.  a: [..., K1] (+ a2: [..., K-K1]),
-    w: [N, K] bf16, bias: [N] f32.  Returns Y (and GELU(Y) for TOK_GELU_DUAL)."""
+    """16-bit Y = epi(A . W^T + bias) on the token GEMM kernel.  a: [..., K1] (+ a2: [..., K-K1]),
+    w: [N, K] (a's dtype), bias: [N] f32.  Returns Y (and GELU(Y) for TOK_GELU_DUAL)."""
     N, K = w.shape
     K1 = a.shape[-1]
     M = a.numel() // K1
     a = a.contiguous()
-    y = torch.empty(*a.shape[:-1], N, device=a.device, dtype=torch.bfloat16)
+    y = torch.empty(*a.shape[:-1], N, device=a.device, dtype=a.dtype)
     y2 = torch.empty_like(y) if epi == TOK_GELU_DUAL else None
-    _lib.call("msu_tok_gemm", _p(a), _p(None if a2 is None else a2.contiguous()), K1 if a2 is not None else 0,
-              _p(w), _p(bias), _p(y), _p(y2), _p(h), M, N, K, epi, _s(a))
+    _lib.call("msu_tok_gemm", _dt(a), _p(a), _p(None if a2 is None else a2.contiguous()),
+              K1 if a2 is not None else 0, _p(w), _p(bias), _p(y), _p(y2), _p(h), M, N, K, epi, _s(a))
     return (y, y2) if epi == TOK_GELU_DUAL else y
 
 
 def _wt(w):
-    """[N, K] bf16 weight -> contiguous W^T [K, N] for the input-gradient GEMM."""
+    """[N, K] 16-bit weight -> contiguous W^T [K, N] for the input-gradient GEMM."""
     return w.t().contiguous()
 
 
@@ -510,96 +642,99 @@ def _wgrad(dy, x, weight, bias, M, N, K):
     return dw, db
 
 
+def _shadow(param, dt):
+    """16-bit copy of an f32 master parameter: the trainer's per-step shadow buffer when it
+    keeps one (``_msu_shadow``, the trainer's compute dtype), else a cast."""
+    sh = getattr(param, "_msu_shadow", None)
+    if sh is not None and sh.dtype == dt and getattr(param, "_msu_shadow_ver", -1) == param._version:
+        return sh
+    return param.to(dt)
+
+
+def _mm(a, w, bias=None):
+    """16-bit a . w^T (+ bias) on the token GEMM where preferred, else the library GEMM."""
+    N, K = w.shape
+    M = a.numel() // K
+    if tok_preferred(M, N, K):
+        return tok_gemm(a, w, bias)
+    with torch.autocast("cuda", enabled=False):
+        return torch.nn.functional.linear(a, w, None if bias is None else bias.to(a.dtype))
+
+
 # ----------------------------------------------------------------------------- Linear
+def _linear_impl(x, weight, bias):
+    """Y = x . W^T + b in x's dtype; the f32 master weight / bias are cast inside the op so
+    that the parameter gradients are the f32 ones of the weight-gradient kernel."""
+    _need_cuda(x)
+    dt = x.dtype
+    w = _shadow(weight, dt)
+    N, K = w.shape
+    M = x.numel() // K
+    if dt in _LOW and tok_preferred(M, N, K):
+        return tok_gemm(x, w, None if bias is None else _f32(bias))
+    b = None if bias is None else _shadow(bias, dt)
+    with torch.autocast("cuda", enabled=False):
+        return torch.nn.functional.linear(x, w, b)
+
+
+def _linear_fake(x, weight, bias):
+    return x.new_empty(*x.shape[:-1], weight.shape[0])
+
+
+def _linear_setup(ctx, inputs, output):
+    x, weight, bias = inputs
+    ctx.save_for_backward(x)
+    ctx.params = (weight, bias)
+
+
+def _linear_backward(ctx, dy):
+    (x,) = ctx.saved_tensors
+    weight, bias = ctx.params
+    w = _shadow(weight, x.dtype)
+    dy = _as(dy, x.dtype)
+    N, K = w.shape
+    M = dy.numel() // N
+    dx = None
+    if ctx.needs_input_grad[0]:
+        if x.dtype in _LOW and tok_preferred(M, K, N):
+            dx = tok_gemm(dy, _wt(w))
+        else:
+            with torch.autocast("cuda", enabled=False):
+                dx = dy.matmul(w)
+    dw, db = _wgrad(dy, x, weight, bias, M, N, K)
+    return dx, dw, db
+
+
+_linear = _define("linear", "(Tensor x, Tensor weight, Tensor? bias) -> Tensor",
+                  _linear_impl, _linear_fake, _linear_setup, _linear_backward)
+
+
 def linear(x, weight, bias=None):
     """nn.functional.linear with the HIP weight-gradient kernel (activation dtype per autocast);
-    bf16 forward / input-gradient GEMMs on the token GEMM where it covers the shape."""
+    16-bit forward / input-gradient GEMMs on the token GEMM where it covers the shape."""
     _need_cuda(x)
     dt = act_dtype()
     x = _as(x, dt)
     N, K = weight.shape
     if K % 8 or N % 8:
         return torch.nn.functional.linear(x, weight.to(dt), None if bias is None else bias.to(dt))
-    return _LinearParams.apply(x, weight, bias, dt)
-
-
-class _LinearParams(torch.autograd.Function):
-    """Casts the f32 master weight/bias to the activation dtype inside the op so that the
-    returned parameter gradients are the f32 ones computed by the wgrad kernel."""
-
-    @staticmethod
-    def forward(ctx, x, weight, bias, dt):
-        w = _shadow(weight, dt)
-        N, K = w.shape
-        M = x.numel() // K
-        if dt == torch.bfloat16 and tok_preferred(M, N, K):
-            y = tok_gemm(x, w, None if bias is None else _f32(bias))
-        else:
-            b = None if bias is None else _shadow(bias, dt)
-            with torch.autocast("cuda", enabled=False):
-                y = torch.nn.functional.linear(x, w, b)
-        ctx.save_for_backward(x, w)
-        ctx.has_bias = bias is not None
-        ctx.params = (weight, bias)
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, w = ctx.saved_tensors
-        weight, bias = ctx.params
-        dy = _as(dy, x.dtype)
-        N, K = w.shape
-        M = dy.numel() // N
-        dx = None
-        if ctx.needs_input_grad[0]:
-            if x.dtype == torch.bfloat16 and tok_preferred(M, K, N):
-                dx = tok_gemm(dy, _wt(w))
-            else:
-                with torch.autocast("cuda", enabled=False):
-                    dx = dy.matmul(w)
-        dw, db = _wgrad(dy, x, weight, bias if ctx.has_bias else None, M, N, K)
-        return dx, dw, db, None
+    return _linear(x, weight, bias)
 
 
 # ----------------------------------------------------------------------------- skip fusion
-class _LinearCat(torch.autograd.Function):
-    """Linear(cat([x, skip], -1)) with the concatenation folded into the token GEMM's A
-    loads (forward) and split back out of the input gradient (two GEMMs over W's halves)."""
+def _linear_cat_impl(x, skip, weight, bias):
+    W = _shadow(weight, x.dtype)
+    return tok_gemm(x, W, _f32(bias), a2=skip)
 
-    @staticmethod
-    def forward(ctx, x, skip, weight, bias):
-        W = _shadow(weight, torch.bfloat16)
-        y = tok_gemm(x, W, _f32(bias), a2=skip)
-        ctx.save_for_backward(x, skip, W)
-        ctx.params = (weight, bias)
-        return y
 
-    @staticmethod
-    def backward(ctx, dy):
-        x, skip, W = ctx.saved_tensors
-        weight, bias = ctx.params
-        dy = _as(dy, torch.bfloat16)
-        N = W.shape[0]
-        C1, C2 = x.shape[-1], skip.shape[-1]
-        M = dy.numel() // N
-        outs = []
-        for part, (lo, hi) in ((x, (0, C1)), (skip, (C1, C1 + C2))):
-            wt = W[:, lo:hi].t().contiguous()
-            if tok_preferred(M, hi - lo, N):
-                outs.append(tok_gemm(dy, wt))
-            else:
-                with torch.autocast("cuda", enabled=False):
-                    outs.append(dy.matmul(wt.t()))
-        # weight gradient per half into temporaries ([N, C1], [N, C2]), bias with the first
-        dw1, db = _wgrad_tmp(dy, x, N, C1, M, with_bias=True)
-        dw2, _ = _wgrad_tmp(dy, skip, N, C2, M, with_bias=False)
-        if _direct(weight, bias):
-            weight.grad[:, :C1] += dw1
-            weight.grad[:, C1:] += dw2
-            bias.grad += db
-            _notify(weight, bias)
-            return outs[0], outs[1], None, None
-        return outs[0], outs[1], torch.cat([dw1, dw2], 1), db
+def _linear_cat_fake(x, skip, weight, bias):
+    return x.new_empty(*x.shape[:-1], weight.shape[0])
+
+
+def _linear_cat_setup(ctx, inputs, output):
+    x, skip, weight, bias = inputs
+    ctx.save_for_backward(x, skip)
+    ctx.params = (weight, bias)
 
 
 def _wgrad_tmp(dy, x, N, K, M, with_bias):
@@ -611,25 +746,58 @@ def _wgrad_tmp(dy, x, N, K, M, with_bias):
     return dw, db
 
 
+def _linear_cat_backward(ctx, dy):
+    x, skip = ctx.saved_tensors
+    weight, bias = ctx.params
+    W = _shadow(weight, x.dtype)
+    dy = _as(dy, x.dtype)
+    N = W.shape[0]
+    C1, C2 = x.shape[-1], skip.shape[-1]
+    M = dy.numel() // N
+    outs = []
+    for lo, hi in ((0, C1), (C1, C1 + C2)):
+        wt = W[:, lo:hi].t().contiguous()
+        if tok_preferred(M, hi - lo, N):
+            outs.append(tok_gemm(dy, wt))
+        else:
+            with torch.autocast("cuda", enabled=False):
+                outs.append(dy.matmul(wt.t()))
+    # weight gradient per half into temporaries ([N, C1], [N, C2]), bias with the first
+    dw1, db = _wgrad_tmp(dy, x, N, C1, M, with_bias=True)
+    dw2, _ = _wgrad_tmp(dy, skip, N, C2, M, with_bias=False)
+    if _direct(weight, bias):
+        weight.grad[:, :C1] += dw1
+        weight.grad[:, C1:] += dw2
+        bias.grad += db
+        _notify(weight, bias)
+        return outs[0], outs[1], None, None
+    return outs[0], outs[1], torch.cat([dw1, dw2], 1), db
+
+
+_linear_cat = _define("linear_cat", "(Tensor x, Tensor skip, Tensor weight, Tensor bias) -> Tensor",
+                      _linear_cat_impl, _linear_cat_fake, _linear_cat_setup, _linear_cat_backward)
+
+
 def linear_cat(x, skip, weight, bias):
     """``F.linear(torch.cat([x, skip], -1), weight, bias)`` (skip fusion, model_parts.py:792-794,
-    :804-806, :823-824); x / skip: [..., C1] / [..., C2] with equal leading dims."""
+    :804-806, :823-824); x / skip: [..., C1] / [..., C2] with equal leading dims.  16-bit: the
+    concatenation is folded into the token GEMM's A loads (no concatenated copy) and split back
+    out of the input gradient (two GEMMs over W's halves)."""
     _need_cuda(x)
     dt = act_dtype()
     x, skip = _as(x, dt), _as(skip, dt)
     N, K = weight.shape
     C1, C2 = x.shape[-1], skip.shape[-1]
     M = x.numel() // C1
-    if (dt == torch.bfloat16 and bias is not None and C1 + C2 == K and C1 % 8 == 0 and
-            tok_preferred(M, N, K)):
-        return _LinearCat.apply(x, skip, weight, bias)
+    if dt in _LOW and bias is not None and C1 + C2 == K and C1 % 8 == 0 and tok_preferred(M, N, K):
+        return _linear_cat(x, skip, weight, bias)
     return linear(torch.cat([x, skip], -1), weight, bias)
 
 
 # ----------------------------------------------------------------------------- fused MLP
 def mlp_fusable(x, fc1_weight, fc2_weight):
-    """torchvision MLP (mlp.0 -> GELU -> mlp.3) fusable on the token GEMM in bf16?"""
-    if act_dtype() != torch.bfloat16:
+    """torchvision MLP (mlp.0 -> GELU -> mlp.3) fusable on the token GEMM in 16-bit?"""
+    if act_dtype() not in _LOW:
         return False
     Hd, C = fc1_weight.shape
     M = x.numel() // C
@@ -643,79 +811,82 @@ def mlp_fusable(x, fc1_weight, fc2_weight):
             tok_supported_epi(M, Hd, C, TOK_GELU_GRAD))
 
 
-def _mm(a, w, bias=None):
-    """bf16 a . w^T (+ bias) on the token GEMM where preferred, else hipBLASLt."""
-    N, K = w.shape
-    M = a.numel() // K
-    if tok_preferred(M, N, K):
-        return tok_gemm(a, w, bias)
-    with torch.autocast("cuda", enabled=False):
-        return torch.nn.functional.linear(a, w, None if bias is None else bias.to(torch.bfloat16))
-
-
-class _Mlp(torch.autograd.Function):
+def _mlp_impl(x, w1, b1, w2, b2):
     """y = mlp.3(GELU(mlp.0(x))) (torchvision ops.misc.MLP without dropout): mlp.0's epilogue
-    stores H and GELU(H); mlp.3's input gradient applies GELU'(H) in its epilogue."""
+    stores H and GELU(H) (returned for backward); mlp.3's input gradient applies GELU'(H) in
+    its epilogue."""
+    _need_cuda(x)
+    W1 = _shadow(w1, x.dtype)
+    W2 = _shadow(w2, x.dtype)
+    h, g = tok_gemm(x, W1, _f32(b1), TOK_GELU_DUAL)
+    y = _mm(g, W2, _f32(b2))
+    return y, h, g
 
-    @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
-        W1 = _shadow(w1, torch.bfloat16)
-        W2 = _shadow(w2, torch.bfloat16)
-        h, g = tok_gemm(x, W1, _f32(b1), TOK_GELU_DUAL)
-        y = _mm(g, W2, _f32(b2))
-        ctx.save_for_backward(x, h, g, W1, W2)
-        ctx.params = (w1, b1, w2, b2)
-        return y
 
-    @staticmethod
-    def backward(ctx, dy):
-        x, h, g, W1, W2 = ctx.saved_tensors
-        w1, b1, w2, b2 = ctx.params
-        dy = _as(dy, torch.bfloat16)
-        Hd, C = W1.shape
-        M = x.numel() // C
-        dw2, db2 = _wgrad(dy, g, w2, b2, M, C, Hd)
-        dh = tok_gemm(dy, _wt(W2), None, TOK_GELU_GRAD, h=h)
-        dw1, db1 = _wgrad(dh, x, w1, b1, M, Hd, C)
-        dx = _mm(dh, _wt(W1)) if ctx.needs_input_grad[0] else None
-        return dx, dw1, db1, dw2, db2
+def _mlp_fake(x, w1, b1, w2, b2):
+    hid = x.new_empty(*x.shape[:-1], w1.shape[0])
+    return x.new_empty(*x.shape[:-1], w2.shape[0]), hid, torch.empty_like(hid)
+
+
+def _mlp_setup(ctx, inputs, output):
+    x, w1, b1, w2, b2 = inputs
+    y, h, g = output
+    ctx.save_for_backward(x, h, g)
+    ctx.params = (w1, b1, w2, b2)
+    ctx.mark_non_differentiable(h, g)
+    ctx.set_materialize_grads(False)
+
+
+def _mlp_backward(ctx, dy, _dh, _dg):
+    x, h, g = ctx.saved_tensors
+    w1, b1, w2, b2 = ctx.params
+    W1 = _shadow(w1, x.dtype)
+    W2 = _shadow(w2, x.dtype)
+    dy = _as(dy, x.dtype)
+    Hd, C = W1.shape
+    M = x.numel() // C
+    dw2, db2 = _wgrad(dy, g, w2, b2, M, C, Hd)
+    dh = tok_gemm(dy, _wt(W2), None, TOK_GELU_GRAD, h=h)
+    dw1, db1 = _wgrad(dh, x, w1, b1, M, Hd, C)
+    dx = _mm(dh, _wt(W1)) if ctx.needs_input_grad[0] else None
+    return dx, dw1, db1, dw2, db2
+
+
+_mlp = _define("mlp", "(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2) -> (Tensor, Tensor, Tensor)",
+               _mlp_impl, _mlp_fake, _mlp_setup, _mlp_backward)
 
 
 def mlp(x, fc1_weight, fc1_bias, fc2_weight, fc2_bias):
-    """Fused torchvision MLP forward/backward (bf16; see ``mlp_fusable``)."""
+    """Fused torchvision MLP forward/backward (16-bit; see ``mlp_fusable``)."""
     _need_cuda(x)
-    return _Mlp.apply(_as(x, torch.bfloat16), fc1_weight, fc1_bias, fc2_weight, fc2_bias)
-
-
-def _shadow(param, dt):
-    """bf16 copy of an f32 master parameter: the trainer's per-step shadow buffer when it
-    keeps one (``_msu_shadow``), else a cast."""
-    sh = getattr(param, "_msu_shadow", None)
-    if sh is not None and sh.dtype == dt and getattr(param, "_msu_shadow_ver", -1) == param._version:
-        return sh
-    return param.to(dt)
+    return _mlp(_as(x, act_dtype()), fc1_weight, fc1_bias, fc2_weight, fc2_bias)[0]
 
 
 # ----------------------------------------------------------------------------- residual
-class _Residual(torch.autograd.Function):
-    """x + br * scale[sample] in one pass (StochasticDepth 'row' scale); backward: dx = dy,
-    dbr = dy * scale[sample]."""
+def _residual_impl(x, br, scale):
+    """x + br * scale[sample] in one pass (StochasticDepth 'row' scale)."""
+    _need_cuda(x, br)
+    x, br = x.contiguous(), br.contiguous()
+    out = torch.empty_like(x)
+    _lib.call("msu_residual", _dt(x), _p(x), _p(br), _p(scale), _p(out), x.numel(), x[0].numel(), _s(x))
+    return out
 
-    @staticmethod
-    def forward(ctx, x, br, scale):
-        _need_cuda(x, br)
-        out = torch.empty_like(x)
-        _lib.call("msu_residual", _dt(x), _p(x), _p(br), _p(scale), _p(out), x.numel(), x[0].numel(), _s(x))
-        ctx.save_for_backward(scale)
-        return out
 
-    @staticmethod
-    def backward(ctx, dy):
-        (scale,) = ctx.saved_tensors
-        dy = dy.contiguous()
-        dbr = torch.empty_like(dy)
-        _lib.call("msu_residual", _dt(dy), None, _p(dy), _p(scale), _p(dbr), dy.numel(), dy[0].numel(), _s(dy))
-        return dy, dbr, None
+def _residual_setup(ctx, inputs, output):
+    ctx.save_for_backward(inputs[2])
+
+
+def _residual_backward(ctx, dy):
+    """dx = dy, dbr = dy * scale[sample]."""
+    (scale,) = ctx.saved_tensors
+    dy = dy.contiguous()
+    dbr = torch.empty_like(dy)
+    _lib.call("msu_residual", _dt(dy), None, _p(dy), _p(scale), _p(dbr), dy.numel(), dy[0].numel(), _s(dy))
+    return dy, dbr, None
+
+
+_residual = _define("residual", "(Tensor x, Tensor br, Tensor scale) -> Tensor",
+                    _residual_impl, lambda x, br, scale: torch.empty_like(x), _residual_setup, _residual_backward)
 
 
 def residual_add(x, br, scale):
@@ -723,62 +894,83 @@ def residual_add(x, br, scale):
     dt = act_dtype()
     if scale is None:
         return x + br.to(x.dtype)
-    return _Residual.apply(_as(x, dt), _as(br, dt), _f32(scale))
+    return _residual(_as(x, dt), _as(br, dt), _f32(scale))
 
 
 # ----------------------------------------------------------------------------- GELU
-class _Gelu(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x):
-        _need_cuda(x)
-        x = x.contiguous()
-        y = torch.empty_like(x)
-        _lib.call("msu_gelu_fwd", _dt(x), _p(x), _p(y), x.numel(), _s(x))
-        ctx.save_for_backward(x)
-        return y
+def _gelu_impl(x):
+    _need_cuda(x)
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    _lib.call("msu_gelu_fwd", _dt(x), _p(x), _p(y), x.numel(), _s(x))
+    return y
 
-    @staticmethod
-    def backward(ctx, dy):
-        (x,) = ctx.saved_tensors
-        dy = _as(dy, x.dtype)
-        dx = torch.empty_like(x)
-        _lib.call("msu_gelu_bwd", _dt(x), _p(x), _p(dy), _p(dx), x.numel(), _s(x))
-        return dx
+
+def _gelu_setup(ctx, inputs, output):
+    ctx.save_for_backward(inputs[0].contiguous())
+
+
+def _gelu_backward(ctx, dy):
+    (x,) = ctx.saved_tensors
+    dy = _as(dy, x.dtype)
+    dx = torch.empty_like(x)
+    _lib.call("msu_gelu_bwd", _dt(x), _p(x), _p(dy), _p(dx), x.numel(), _s(x))
+    return dx
+
+
+_gelu = _define("gelu", "(Tensor x) -> Tensor", _gelu_impl, lambda x: torch.empty_like(x), _gelu_setup,
+                _gelu_backward)
 
 
 def gelu(x):
     """Exact (erf) GELU, nn.GELU()."""
-    return _Gelu.apply(_as(x, act_dtype()))
+    return _gelu(_as(x, act_dtype()))
 
 
 # ----------------------------------------------------------------------------- head
-class _HeadNormOut(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, z, gamma, beta, w, eps):
-        _need_cuda(z)
-        z = z.contiguous()
-        B, H, W, C = z.shape
-        rows = B * H * W
-        logit = torch.empty(B, 1, H, W, device=z.device, dtype=torch.float32)
-        mean = torch.empty(rows, device=z.device, dtype=torch.float32)
-        rstd = torch.empty_like(mean)
-        _lib.call("msu_head_fwd", _dt(z), _p(z), _p(gamma), _p(beta), _p(w), _p(logit), _p(mean),
-                  _p(rstd), rows, C, eps, _s(z))
-        ctx.save_for_backward(z, gamma, beta, w, mean, rstd)
-        return logit
+def _head_impl(z, gamma, beta, w, eps):
+    _need_cuda(z)
+    z = z.contiguous()
+    B, H, W, C = z.shape
+    rows = B * H * W
+    logit = torch.empty(B, 1, H, W, device=z.device, dtype=torch.float32)
+    mean, rstd = _stats(z, rows)
+    _lib.call("msu_head_fwd", _dt(z), _p(z), _p(gamma), _p(beta), _p(w), _p(logit), _p(mean),
+              _p(rstd), rows, C, eps, _s(z))
+    return logit, mean, rstd
 
-    @staticmethod
-    def backward(ctx, dlogit):
-        z, gamma, beta, w, mean, rstd = ctx.saved_tensors
-        B, H, W, C = z.shape
-        rows = B * H * W
-        dlogit = _f32(dlogit)
-        dz = torch.empty_like(z)
-        dg, db, dw = torch.empty(3, C, device=z.device, dtype=torch.float32)  # contiguous: one reduction
-        n, part = _ln_parts(rows, C, z.device)
-        _lib.call("msu_head_bwd", _dt(z), _p(dlogit), _p(z), _p(gamma), _p(beta), _p(w), _p(mean),
-                  _p(rstd), _p(dz), _p(part), n, _p(dg), _p(db), _p(dw), rows, C, _s(z))
-        return dz, dg, db, dw, None
+
+def _head_fake(z, gamma, beta, w, eps):
+    B, H, W, C = z.shape
+    rows = B * H * W
+    return (z.new_empty(B, 1, H, W, dtype=torch.float32), z.new_empty(rows, dtype=torch.float32),
+            z.new_empty(rows, dtype=torch.float32))
+
+
+def _head_setup(ctx, inputs, output):
+    z, gamma, beta, w, eps = inputs
+    ctx.save_for_backward(z.contiguous(), gamma, beta, w, output[1], output[2])
+    ctx.set_materialize_grads(False)
+
+
+def _head_backward(ctx, dlogit, _dm, _dr):
+    z, gamma, beta, w, mean, rstd = ctx.saved_tensors
+    if dlogit is None:
+        return None, None, None, None, None
+    B, H, W, C = z.shape
+    rows = B * H * W
+    dlogit = _f32(dlogit)
+    dz = torch.empty_like(z)
+    dg, db, dw = torch.empty(3, C, device=z.device, dtype=torch.float32)  # contiguous: one reduction
+    n, part = _ln_parts(rows, C, z.device)
+    _lib.call("msu_head_bwd", _dt(z), _p(dlogit), _p(z), _p(gamma), _p(beta), _p(w), _p(mean),
+              _p(rstd), _p(dz), _p(part), n, _p(dg), _p(db), _p(dw), rows, C, _s(z))
+    return dz, dg, db, dw, None
+
+
+_head = _define("head_norm_output",
+                "(Tensor z, Tensor gamma, Tensor beta, Tensor w, float eps) -> (Tensor, Tensor, Tensor)",
+                _head_impl, _head_fake, _head_setup, _head_backward)
 
 
 def head_norm_output(z, gamma, beta, out_weight, eps=1e-5):
@@ -788,7 +980,7 @@ def head_norm_output(z, gamma, beta, out_weight, eps=1e-5):
         raise ValueError("fused head supports num_classes == 1")
     C = z.shape[-1]
     w = _f32(out_weight.reshape(C))
-    return _HeadNormOut.apply(_as(z, act_dtype()), _f32(gamma), _f32(beta), w, eps)
+    return _head(_as(z, act_dtype()), _f32(gamma), _f32(beta), w, float(eps))[0]
 
 
 # ----------------------------------------------------------------------------- conv 3x3
@@ -802,206 +994,267 @@ def _pad_to(t, dim, mult):
     return torch.cat([t, t.new_zeros(shape)], dim)
 
 
-class _RefineConv(torch.autograd.Function):
+def _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout):
+    L = _lib.lib()
+    nchunk = 256
+    ws = torch.empty(L.msu_conv3x3_wgrad_workspace(nchunk, Cin, Cout, 0, 0), device=a.device, dtype=torch.float32)
+    dw = torch.empty(Cout, Cin, 3, 3, device=a.device, dtype=torch.float32)
+    db = torch.empty(Cout, device=a.device, dtype=torch.float32)
+    _lib.call("msu_conv3x3_wgrad", _dt(a), mode, _p(a), _p(dz), _p(dw), _p(db), _p(ws), None, nchunk,
+              B, H, W, Cin, Cout, _s(a))
+    return dw, db
+
+
+def _refine_impl(x, weight, bias, d2s, H, W):
     """z = conv3x3(GELU(map(x)), W) + b, NHWC; map = identity or the 4x4 depth-to-space of
     FinalPatchExpand_X4_V2 (x: [B, H/4, W/4, 16*Cin])."""
+    _need_cuda(x)
+    x = x.contiguous()
+    Cout, Cin = weight.shape[0], weight.shape[1]
+    B = x.shape[0]
+    dt = x.dtype
+    wt = _pad_to(weight.permute(2, 3, 0, 1).reshape(9, Cout, Cin), 2, 32).to(dt).contiguous()
+    z = torch.empty(B, H, W, Cout, device=x.device, dtype=dt)
+    _lib.call("msu_conv3x3_fwd", _dt(x), 1 | (2 if d2s else 0), _p(x), _p(wt), _p(bias), _p(z),
+              B, H, W, Cin, Cout, _s(x))
+    return z
 
-    @staticmethod
-    def forward(ctx, x, weight, bias, d2s, out_hw):
-        _need_cuda(x)
-        x = x.contiguous()
-        Cout, Cin = weight.shape[0], weight.shape[1]
-        B = x.shape[0]
-        H, W = out_hw
-        dt = x.dtype
-        wt = _pad_to(weight.permute(2, 3, 0, 1).reshape(9, Cout, Cin), 2, 32).to(dt).contiguous()
-        z = torch.empty(B, H, W, Cout, device=x.device, dtype=dt)
-        _lib.call("msu_conv3x3_fwd", _dt(x), 1 | (2 if d2s else 0), _p(x), _p(wt), _p(bias), _p(z),
-                  B, H, W, Cin, Cout, _s(x))
-        ctx.save_for_backward(x, weight)
-        ctx.cfg = (d2s, H, W)
-        return z
 
-    @staticmethod
-    def backward(ctx, dz):
-        x, weight = ctx.saved_tensors
-        d2s, H, W = ctx.cfg
-        Cout, Cin = weight.shape[0], weight.shape[1]
-        B = x.shape[0]
-        dz = _as(dz, x.dtype)
-        mode = 1 | (2 if d2s else 0)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            wf = _pad_to(weight.flip(2, 3).permute(2, 3, 1, 0).reshape(9, Cin, Cout), 2, 32)
-            wf = wf.to(x.dtype).contiguous()
-            dx = torch.empty_like(x)
-            _lib.call("msu_conv3x3_dgrad", _dt(x), mode, _p(dz), _p(wf), _p(x), _p(dx), B, H, W, Cin, Cout, _s(x))
-        L = _lib.lib()
-        nchunk = 256
-        ws = torch.empty(L.msu_conv3x3_wgrad_workspace(nchunk, Cin, Cout, 0, 0), device=x.device,
-                         dtype=torch.float32)
-        dw = torch.empty(Cout, Cin, 3, 3, device=x.device, dtype=torch.float32)
-        db = torch.empty(Cout, device=x.device, dtype=torch.float32)
-        _lib.call("msu_conv3x3_wgrad", _dt(x), mode, _p(x), _p(dz), _p(dw), _p(db), _p(ws), None, nchunk,
-                  B, H, W, Cin, Cout, _s(x))
-        return dx, dw, db, None, None
+def _refine_setup(ctx, inputs, output):
+    x, weight, bias, d2s, H, W = inputs
+    ctx.save_for_backward(x.contiguous(), weight)
+    ctx.cfg = (d2s, H, W)
+
+
+def _refine_backward(ctx, dz):
+    x, weight = ctx.saved_tensors
+    d2s, H, W = ctx.cfg
+    Cout, Cin = weight.shape[0], weight.shape[1]
+    B = x.shape[0]
+    dz = _as(dz, x.dtype)
+    mode = 1 | (2 if d2s else 0)
+    dx = None
+    if ctx.needs_input_grad[0]:
+        wf = _pad_to(weight.flip(2, 3).permute(2, 3, 1, 0).reshape(9, Cin, Cout), 2, 32)
+        wf = wf.to(x.dtype).contiguous()
+        dx = torch.empty_like(x)
+        _lib.call("msu_conv3x3_dgrad", _dt(x), mode, _p(dz), _p(wf), _p(x), _p(dx), B, H, W, Cin, Cout, _s(x))
+    dw, db = _conv_wgrad(x, dz, mode, B, H, W, Cin, Cout)
+    return dx, dw, db, None, None, None
+
+
+_refine_conv = _define(
+    "refine_conv", "(Tensor x, Tensor weight, Tensor bias, bool d2s, int H, int W) -> Tensor",
+    _refine_impl, lambda x, weight, bias, d2s, H, W: x.new_empty(x.shape[0], H, W, weight.shape[0]),
+    _refine_setup, _refine_backward)
 
 
 def refine_conv(x, weight, bias, d2s, out_hw):
-    return _RefineConv.apply(_as(x, act_dtype()), _f32(weight), _f32(bias), bool(d2s), tuple(out_hw))
+    H, W = out_hw
+    return _refine_conv(_as(x, act_dtype()), _f32(weight), _f32(bias), bool(d2s), int(H), int(W))
 
 
-class _RefineConvAct(torch.autograd.Function):
-    """z = conv3x3(a, W) + b with a = GELU(map(x)) already materialised by the producer
-    (x: the differentiable pre-activation, a: its activation, non-differentiable).  The
-    conv loads a as is (no GELU on its halo); the input gradient still applies GELU'(x)
-    in the dgrad epilogue, the weight gradient reads a.  dual: also returns GELU(z) from
-    the same epilogue (the next refine conv's input)."""
+def _refine_act_impl(x, a, weight, bias, d2s, H, W, dual):
+    """z = conv3x3(a, W) + b with a = GELU(map(x)) already materialised by the producer (x: the
+    differentiable pre-activation, a: its activation, non-differentiable).  The conv loads a as
+    is; the input gradient applies GELU'(x) in the dgrad epilogue, the weight gradient reads
+    a.  dual: the second output is GELU(z) from the same epilogue (the next refine conv's
+    input); otherwise an empty placeholder."""
+    _need_cuda(x, a)
+    a = a.contiguous()
+    Cout, Cin = weight.shape[0], weight.shape[1]
+    B = a.shape[0]
+    dt = a.dtype
+    wt = _pad_to(weight.permute(2, 3, 0, 1).reshape(9, Cout, Cin), 2, 32).to(dt).contiguous()
+    z = torch.empty(B, H, W, Cout, device=a.device, dtype=dt)
+    z2 = torch.empty_like(z) if dual else z.new_empty(0)
+    _lib.call("msu_conv3x3_fwd2", _dt(a), 2 if d2s else 0, _p(a), _p(wt), _p(bias), _p(z), _p(z2) if dual else None,
+              B, H, W, Cin, Cout, _s(a))
+    return z, z2
 
-    @staticmethod
-    def forward(ctx, x, a, weight, bias, d2s, out_hw, dual):
-        _need_cuda(x, a)
-        a = a.contiguous()
-        Cout, Cin = weight.shape[0], weight.shape[1]
-        B = a.shape[0]
-        H, W = out_hw
-        dt = a.dtype
-        wt = _pad_to(weight.permute(2, 3, 0, 1).reshape(9, Cout, Cin), 2, 32).to(dt).contiguous()
-        z = torch.empty(B, H, W, Cout, device=a.device, dtype=dt)
-        z2 = torch.empty_like(z) if dual else None
-        _lib.call("msu_conv3x3_fwd2", _dt(a), 2 if d2s else 0, _p(a), _p(wt), _p(bias), _p(z), _p(z2),
+
+def _refine_act_fake(x, a, weight, bias, d2s, H, W, dual):
+    z = a.new_empty(a.shape[0], H, W, weight.shape[0])
+    return z, (torch.empty_like(z) if dual else z.new_empty(0))
+
+
+def _refine_act_setup(ctx, inputs, output):
+    x, a, weight, bias, d2s, H, W, dual = inputs
+    ctx.save_for_backward(x, a.contiguous(), weight)
+    ctx.cfg = (d2s, H, W)
+    ctx.mark_non_differentiable(output[1])
+    ctx.set_materialize_grads(False)  # no zero-filled gradient for GELU(z)
+
+
+def _refine_act_backward(ctx, dz, _dz2):
+    x, a, weight = ctx.saved_tensors
+    d2s, H, W = ctx.cfg
+    if dz is None:
+        return (None,) * 8
+    Cout, Cin = weight.shape[0], weight.shape[1]
+    B = a.shape[0]
+    dz = _as(dz, a.dtype)
+    dx = None
+    if ctx.needs_input_grad[0]:
+        wf = _pad_to(weight.flip(2, 3).permute(2, 3, 1, 0).reshape(9, Cin, Cout), 2, 32)
+        wf = wf.to(a.dtype).contiguous()
+        dx = torch.empty_like(x)
+        _lib.call("msu_conv3x3_dgrad", _dt(a), 1 | (2 if d2s else 0), _p(dz), _p(wf), _p(x), _p(dx),
                   B, H, W, Cin, Cout, _s(a))
-        ctx.save_for_backward(x, a, weight)
-        ctx.cfg = (d2s, H, W)
-        ctx.set_materialize_grads(False)  # no zero-filled gradient for GELU(z)
-        if dual:
-            ctx.mark_non_differentiable(z2)
-            return z, z2
-        return z
+    dw, db = _conv_wgrad(a, dz, 2 if d2s else 0, B, H, W, Cin, Cout)
+    return dx, None, dw, db, None, None, None, None
 
-    @staticmethod
-    def backward(ctx, dz, *unused):
-        x, a, weight = ctx.saved_tensors
-        d2s, H, W = ctx.cfg
-        Cout, Cin = weight.shape[0], weight.shape[1]
-        B = a.shape[0]
-        dz = _as(dz, a.dtype)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            wf = _pad_to(weight.flip(2, 3).permute(2, 3, 1, 0).reshape(9, Cin, Cout), 2, 32)
-            wf = wf.to(a.dtype).contiguous()
-            dx = torch.empty_like(x)
-            _lib.call("msu_conv3x3_dgrad", _dt(a), 1 | (2 if d2s else 0), _p(dz), _p(wf), _p(x), _p(dx),
-                      B, H, W, Cin, Cout, _s(a))
-        L = _lib.lib()
-        nchunk = 256
-        ws = torch.empty(L.msu_conv3x3_wgrad_workspace(nchunk, Cin, Cout, 0, 0), device=a.device,
-                         dtype=torch.float32)
-        dw = torch.empty(Cout, Cin, 3, 3, device=a.device, dtype=torch.float32)
-        db = torch.empty(Cout, device=a.device, dtype=torch.float32)
-        _lib.call("msu_conv3x3_wgrad", _dt(a), 2 if d2s else 0, _p(a), _p(dz), _p(dw), _p(db), _p(ws), None,
-                  nchunk, B, H, W, Cin, Cout, _s(a))
-        return dx, None, dw, db, None, None, None
+
+_refine_conv_act = _define(
+    "refine_conv_act",
+    "(Tensor x, Tensor a, Tensor weight, Tensor bias, bool d2s, int H, int W, bool dual) -> (Tensor, Tensor)",
+    _refine_act_impl, _refine_act_fake, _refine_act_setup, _refine_act_backward)
 
 
 def refine_conv_act(x, a, weight, bias, d2s, out_hw, dual=False):
     """``conv(GELU(map(x)))`` of FinalPatchExpand_X4_V2 with a = GELU(x) supplied by the
     producer's epilogue; returns z (and GELU(z), non-differentiable, when dual)."""
     dt = act_dtype()
-    return _RefineConvAct.apply(_as(x, dt), _as(a, dt), _f32(weight), _f32(bias), bool(d2s), tuple(out_hw),
-                                bool(dual))
+    H, W = out_hw
+    z, z2 = _refine_conv_act(_as(x, dt), _as(a, dt), _f32(weight), _f32(bias), bool(d2s), int(H), int(W),
+                             bool(dual))
+    return (z, z2) if dual else z
 
 
-class _LinearGelu(torch.autograd.Function):
-    """y = x . W^T (no bias) returning y and the non-differentiable GELU(y) from the same
-    epilogue (FinalPatchExpand_X4_V2.expand -> act, model_parts.py:458-460); the activation
-    gradient is applied by the consumer (refine_conv_act's dgrad epilogue)."""
+def _linear_gelu_impl(x, weight):
+    """y = x . W^T (no bias) and the non-differentiable GELU(y) from the same epilogue
+    (FinalPatchExpand_X4_V2.expand -> act, model_parts.py:458-460); the activation gradient is
+    applied by the consumer (refine_conv_act's dgrad epilogue)."""
+    _need_cuda(x)
+    dt = x.dtype
+    w = _shadow(weight, dt)
+    N, K = w.shape
+    M = x.numel() // K
+    if dt in _LOW and tok_supported(M, N, K):
+        return tok_gemm(x, w, torch.zeros(N, device=x.device, dtype=torch.float32), TOK_GELU_DUAL)
+    with torch.autocast("cuda", enabled=False):
+        y = torch.nn.functional.linear(x, w)
+    g = torch.empty_like(y)
+    _lib.call("msu_gelu_fwd", _dt(y), _p(y), _p(g), y.numel(), _s(y))
+    return y, g
 
-    @staticmethod
-    def forward(ctx, x, weight, dt):
-        w = _shadow(weight, dt)
-        N, K = w.shape
-        M = x.numel() // K
-        if dt == torch.bfloat16 and tok_supported(M, N, K):
-            y, g = tok_gemm(x, w, torch.zeros(N, device=x.device, dtype=torch.float32), TOK_GELU_DUAL)
+
+def _linear_gelu_fake(x, weight):
+    y = x.new_empty(*x.shape[:-1], weight.shape[0])
+    return y, torch.empty_like(y)
+
+
+def _linear_gelu_setup(ctx, inputs, output):
+    x, weight = inputs
+    ctx.save_for_backward(x)
+    ctx.params = (weight,)
+    ctx.mark_non_differentiable(output[1])
+    ctx.set_materialize_grads(False)  # no zero-filled gradient for GELU(y)
+
+
+def _linear_gelu_backward(ctx, dy, _dg):
+    (x,) = ctx.saved_tensors
+    (weight,) = ctx.params
+    if dy is None:
+        return None, None
+    w = _shadow(weight, x.dtype)
+    dy = _as(dy, x.dtype)
+    N, K = w.shape
+    M = dy.numel() // N
+    dx = None
+    if ctx.needs_input_grad[0]:
+        if x.dtype in _LOW and tok_preferred(M, K, N):
+            dx = tok_gemm(dy, _wt(w))
         else:
             with torch.autocast("cuda", enabled=False):
-                y = torch.nn.functional.linear(x, w)
-            g = torch.empty_like(y)
-            _lib.call("msu_gelu_fwd", _dt(y), _p(y), _p(g), y.numel(), _s(y))
-        ctx.save_for_backward(x, w)
-        ctx.params = (weight,)
-        ctx.set_materialize_grads(False)  # no zero-filled gradient for GELU(y)
-        ctx.mark_non_differentiable(g)
-        return y, g
+                dx = dy.matmul(w)
+    dw, _ = _wgrad(dy, x, weight, None, M, N, K)
+    return dx, dw
 
-    @staticmethod
-    def backward(ctx, dy, unused):
-        x, w = ctx.saved_tensors
-        (weight,) = ctx.params
-        dy = _as(dy, x.dtype)
-        N, K = w.shape
-        M = dy.numel() // N
-        dx = None
-        if ctx.needs_input_grad[0]:
-            if x.dtype == torch.bfloat16 and tok_preferred(M, K, N):
-                dx = tok_gemm(dy, _wt(w))
-            else:
-                with torch.autocast("cuda", enabled=False):
-                    dx = dy.matmul(w)
-        dw, _ = _wgrad(dy, x, weight, None, M, N, K)
-        return dx, dw, None
+
+_linear_gelu = _define("linear_gelu", "(Tensor x, Tensor weight) -> (Tensor, Tensor)",
+                       _linear_gelu_impl, _linear_gelu_fake, _linear_gelu_setup, _linear_gelu_backward)
 
 
 def linear_gelu(x, weight):
-    """(x . W^T, GELU(x . W^T)): the second output is not differentiable (see _LinearGelu)."""
+    """(x . W^T, GELU(x . W^T)): the second output is not differentiable."""
     _need_cuda(x)
-    dt = act_dtype()
-    return _LinearGelu.apply(_as(x, dt), weight, dt)
+    return _linear_gelu(_as(x, act_dtype()), weight)
 
 
 # ----------------------------------------------------------------------------- patch embed
-def patchify(img, patch, dtype):
-    """[B, Cin, H, W] f32 image -> [B*(H/p)*(W/p), Cin*p*p] im2col rows (no grad)."""
+def _patchify_impl(img, patch, dtype_code):
     _need_cuda(img)
     img = _f32(img)
     B, Cin, H, W = img.shape
+    dtype = {v: k for k, v in _DT.items()}[dtype_code]
     out = torch.empty(B * (H // patch) * (W // patch), Cin * patch * patch, device=img.device, dtype=dtype)
-    _lib.call("msu_patchify", _DT[dtype], _p(img), _p(out), B, Cin, H, W, patch, _s(img))
+    _lib.call("msu_patchify", dtype_code, _p(img), _p(out), B, Cin, H, W, patch, _s(img))
     return out
 
 
-# ----------------------------------------------------------------------------- loss
-class _DynamicLoss(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, logits, target, alpha, beta, mix):
-        _need_cuda(logits, target)
-        logits = logits.contiguous()
-        target = _f32(target)
-        B = logits.shape[0]
-        N = logits[0].numel()
-        L = _lib.lib()
-        nblk = L.msu_dynloss_nblk(N)
-        part = torch.empty(B * nblk * 12, device=logits.device, dtype=torch.float32)
-        out = torch.empty(2, device=logits.device, dtype=torch.float32)
-        coef = torch.empty(B * 4, device=logits.device, dtype=torch.float32)
-        _lib.call("msu_dynloss_fwd", _dt(logits), _p(logits), _p(target), B, N, alpha, beta, mix,
-                  _p(part), nblk, _p(out), _p(coef), _s(logits))
-        ctx.save_for_backward(logits, target, coef, out)
-        ctx.cfg = (alpha, beta, mix)
-        return out[0]
+def _patchify_fake(img, patch, dtype_code):
+    B, Cin, H, W = img.shape
+    dtype = {v: k for k, v in _DT.items()}[dtype_code]
+    return img.new_empty(B * (H // patch) * (W // patch), Cin * patch * patch, dtype=dtype)
 
-    @staticmethod
-    def backward(ctx, g):
-        logits, target, coef, out = ctx.saved_tensors
-        alpha, beta, mix = ctx.cfg
-        B = logits.shape[0]
-        N = logits[0].numel()
-        g = _f32(g.reshape(1))
-        dl = torch.empty(logits.shape, device=logits.device, dtype=torch.float32)
-        _lib.call("msu_dynloss_bwd", _dt(logits), _p(logits), _p(target), _p(coef), _p(out), _p(g), B, N,
-                  alpha, beta, mix, _p(dl), _s(logits))
-        return dl.to(logits.dtype), None, None, None, None
+
+_patchify = _define("patchify", "(Tensor img, int patch, int dtype) -> Tensor", _patchify_impl, _patchify_fake)
+
+
+def patchify(img, patch, dtype):
+    """[B, Cin, H, W] f32 image -> [B*(H/p)*(W/p), Cin*p*p] im2col rows (no grad)."""
+    _need_cuda(img)
+    return _patchify(img, int(patch), _DT[dtype])
+
+
+# ----------------------------------------------------------------------------- loss
+def _dynloss_impl(logits, target, alpha, beta, mix):
+    _need_cuda(logits, target)
+    logits = logits.contiguous()
+    target = _f32(target)
+    B = logits.shape[0]
+    N = logits[0].numel()
+    L = _lib.lib()
+    nblk = L.msu_dynloss_nblk(N)
+    part = torch.empty(B * nblk * 12, device=logits.device, dtype=torch.float32)
+    out = torch.empty(2, device=logits.device, dtype=torch.float32)
+    coef = torch.empty(B * 4, device=logits.device, dtype=torch.float32)
+    _lib.call("msu_dynloss_fwd", _dt(logits), _p(logits), _p(target), B, N, alpha, beta, mix,
+              _p(part), nblk, _p(out), _p(coef), _s(logits))
+    return out, coef
+
+
+def _dynloss_fake(logits, target, alpha, beta, mix):
+    return logits.new_empty(2, dtype=torch.float32), logits.new_empty(logits.shape[0] * 4, dtype=torch.float32)
+
+
+def _dynloss_setup(ctx, inputs, output):
+    logits, target, alpha, beta, mix = inputs
+    out, coef = output
+    ctx.save_for_backward(logits.contiguous(), _f32(target), coef, out)
+    ctx.cfg = (alpha, beta, mix)
+    ctx.mark_non_differentiable(coef)
+    ctx.set_materialize_grads(False)
+
+
+def _dynloss_backward(ctx, g, _gc):
+    logits, target, coef, out = ctx.saved_tensors
+    alpha, beta, mix = ctx.cfg
+    if g is None:
+        return None, None, None, None, None
+    B = logits.shape[0]
+    N = logits[0].numel()
+    g = _f32(g.reshape(-1)[:1])  # d loss_vec: only element 0 (the loss) is used downstream
+    dl = torch.empty(logits.shape, device=logits.device, dtype=torch.float32)
+    _lib.call("msu_dynloss_bwd", _dt(logits), _p(logits), _p(target), _p(coef), _p(out), _p(g), B, N,
+              alpha, beta, mix, _p(dl), _s(logits))
+    return dl.to(logits.dtype), None, None, None, None
+
+
+_dynamic_loss = _define(
+    "dynamic_loss", "(Tensor logits, Tensor target, float alpha, float beta, float mix) -> (Tensor, Tensor)",
+    _dynloss_impl, _dynloss_fake, _dynloss_setup, _dynloss_backward)
 
 
 def dynamic_loss(logits, target, alpha, beta, mix):
@@ -1011,7 +1264,10 @@ def dynamic_loss(logits, target, alpha, beta, mix):
         raise ValueError(f"Batchsize from ouptut {logits.shape[0]} not equal to batchsize target {target.shape[0]}")
     if logits.shape[1:] != target.shape[1:]:
         raise ValueError(f"target shape {tuple(target.shape)} does not match output {tuple(logits.shape)}")
-    return _DynamicLoss.apply(logits, target, float(alpha), float(beta), float(mix))
+    if logits.dtype not in _DT:
+        logits = logits.float()
+    out, _ = _dynamic_loss(logits, target, float(alpha), float(beta), float(mix))
+    return out[0]
 
 
 # ----------------------------------------------------------------------------- optimizer
@@ -1034,7 +1290,7 @@ def nonfinite_(x, flag, x2=None):
 def adamw_dev_(param, grad, exp_avg, exp_avg_sq, hyper, beta1, beta2, eps, weight_decay, inv_scale=None,
                found_inf=None):
     """AdamW over flat f32 buffers with lr and step read from the device tensor
-    ``hyper = [lr, step]``; no update at all when found_inf[0] != 0."""
+    ``hyper = [lr, step]`` (f64); no update at all when found_inf[0] != 0."""
     _need_cuda(param)
     _lib.call("msu_adamw_dev", _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), _p(hyper),
               beta1, beta2, eps, weight_decay, _p(inv_scale), _p(found_inf), _s(param))

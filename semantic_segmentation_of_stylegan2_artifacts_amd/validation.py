@@ -25,14 +25,14 @@ COLS = ("inter", "sum_p2", "sum_g", "sum_p", "soft_fp", "soft_fn", "soft_tn", "t
 
 
 def image_sums(logits, labels, threshold=0.5):
-    """Per-image metric sums on the GPU: logits [B, 1, H, W] (f32 / bf16), labels [B, H, W]
+    """Per-image metric sums on the GPU: logits [B, 1, H, W] (f32 / bf16 / f16), labels [B, H, W]
     or [B, 1, H, W] -> float64 tensor [B, 12] (host)."""
     ops._need_cuda(logits, labels)
     B = logits.shape[0]
     if labels.shape[0] != B:
         raise ValueError(f"batch mismatch: logits {B}, labels {labels.shape[0]}")
     x = logits.contiguous()
-    if x.dtype not in (torch.float32, torch.bfloat16):
+    if x.dtype not in (torch.float32, torch.bfloat16, torch.float16):
         x = x.float()
     lab = ops._f32(labels)
     N = x[0].numel()

@@ -62,3 +62,29 @@ def test_ops_refuse_cpu_tensors():
     x = torch.zeros(4, 32)
     with pytest.raises(RuntimeError):
         ops.layer_norm(x, torch.ones(32), torch.zeros(32))
+
+
+def test_torch_library_ops_registered():
+    """The hot-path ops are torch.library custom ops (torch.ops.msunet.*) with schemas, fake
+    kernels (shape propagation without a device) and autograd formulas."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    expected = {"layer_norm", "add_layer_norm", "merge_layer_norm", "d2s_layer_norm", "window_attention",
+                "linear", "linear_cat", "mlp", "residual", "gelu", "head_norm_output", "refine_conv",
+                "refine_conv_act", "linear_gelu", "patchify", "dynamic_loss"}
+    assert expected <= set(ops.registered_ops())
+    for name in expected:
+        op = getattr(torch.ops.msunet, name).default
+        assert str(op._schema).startswith(f"msunet::{name}(")
+    with FakeTensorMode():
+        qkv = torch.empty(2, 10, 12, 3 * 64, device="cuda", dtype=torch.float16)
+        out = torch.ops.msunet.window_attention(qkv, torch.empty(192, device="cuda"),
+                                                torch.empty(169, 2, device="cuda"), 2, 3, 0.0, 0)
+        assert out.shape == (2, 10, 12, 64) and out.dtype == torch.float16
+        y, mean, rstd = torch.ops.msunet.layer_norm(torch.empty(5, 96, device="cuda"), torch.empty(96, device="cuda"),
+                                                    torch.empty(96, device="cuda"), 1e-5)
+        assert y.shape == (5, 96) and mean.shape == (5,)
+    # a CPU tensor has no kernel (no silent CPU fallback)
+    with pytest.raises(NotImplementedError):
+        torch.ops.msunet.gelu(torch.zeros(8))

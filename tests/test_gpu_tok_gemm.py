@@ -1,9 +1,10 @@
 """GPU: the token GEMM (csrc/gemm_tok.h) and the fused MLP against plain fp32 PyTorch.
 
-Reference: fp32 matmul of the same bf16-rounded operands, then the epilogue in fp32.
-Tolerance: the kernel rounds its f32 accumulator to bf16 once (<= 2^-8 relative) and sums in a
-different order, so |y - ref| <= 1e-2 * |ref| + 4e-3 * max|ref| (bf16 storage, 8 significant
-bits); GELU uses the A&S 7.1.26 erf (|err| <= 1.5e-7, below bf16 rounding).
+Reference: fp32 matmul of the same 16-bit-rounded operands, then the epilogue in fp32.
+Tolerance: the kernel rounds its f32 accumulator to bf16 / f16 once (<= 2^-8 relative) and sums
+in a different order, so |y - ref| <= 1e-2 * |ref| + 4e-3 * max|ref| (bf16 storage, 8 significant
+bits; f16's 11 bits sit well inside); GELU uses the A&S 7.1.26 erf (|err| <= 1.5e-7).
+Every test runs for both 16-bit formats (bf16 training mode, f16 = the reference's autocast).
 """
 import pytest
 import torch
@@ -26,10 +27,15 @@ def _check(y, ref, what):
     assert err.max().item() <= 4e-3 * scale, f"{what}: excess err {err.max().item():.3e} vs scale {scale:.3e}"
 
 
-def _inputs(M, N, K, seed):
+@pytest.fixture(params=[torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+def low(request):
+    return request.param
+
+
+def _inputs(M, N, K, seed, low=torch.bfloat16):
     g = torch.Generator().manual_seed(seed)
-    a = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
-    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, torch.bfloat16)
+    a = torch.randn(M, K, generator=g).to(DEV, low)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, low)
     b = torch.randn(N, generator=g).to(DEV)
     return a, w, b
 
@@ -42,11 +48,11 @@ SHAPES = [(1000, 288, 96), (4096, 384, 96), (4096, 96, 384), (2048, 192, 768), (
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("bias", [False, True])
-def test_tok_gemm_plain(M, N, K, bias):
+def test_tok_gemm_plain(M, N, K, bias, low):
     ops = _ops()
     if not ops.tok_supported(M, N, K):
         pytest.skip("shape not covered by the token GEMM plan")
-    a, w, b = _inputs(M, N, K, M + N + K)
+    a, w, b = _inputs(M, N, K, M + N + K, low)
     y = ops.tok_gemm(a, w, b if bias else None)
     ref = a.float() @ w.float().t() + (b if bias else 0)
     _check(y, ref, f"plain {M}x{N}x{K}")
@@ -65,12 +71,12 @@ def test_tok_gemm_plan_covers_stage0():
 
 
 @pytest.mark.parametrize("M,C,K1", [(1000, 96, 96), (2048, 192, 192), (333, 128, 128)])
-def test_tok_gemm_concat(M, C, K1):
+def test_tok_gemm_concat(M, C, K1, low):
     """torch.cat([x, skip], -1) -> Linear(2C, C) without the cat (model_parts.py:792-794)."""
     ops = _ops()
     if not ops.tok_supported(M, C, 2 * K1):
         pytest.skip("shape not covered by the token GEMM plan")
-    a, w, b = _inputs(M, C, 2 * K1, 7)
+    a, w, b = _inputs(M, C, 2 * K1, 7, low)
     x, skip = a[:, :K1].contiguous(), a[:, K1:].contiguous()
     y = ops.tok_gemm(x, w, b, a2=skip)
     ref = a.float() @ w.float().t() + b
@@ -78,19 +84,19 @@ def test_tok_gemm_concat(M, C, K1):
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 384, 96), (4096, 768, 192), (555, 1536, 384)])
-def test_tok_gemm_gelu_dual_and_grad(M, N, K):
+def test_tok_gemm_gelu_dual_and_grad(M, N, K, low):
     ops = _ops()
     if not ops.tok_supported(M, N, K):
         pytest.skip("shape not covered by the token GEMM plan")
-    a, w, b = _inputs(M, N, K, 11)
+    a, w, b = _inputs(M, N, K, 11, low)
     h, g = ops.tok_gemm(a, w, b, ops.TOK_GELU_DUAL)
     ref_h = a.float() @ w.float().t() + b
     _check(h, ref_h, "H")
     _check(g, F.gelu(h.float()), "GELU(H)")
     # epi 2: (dY . W2) * GELU'(H) with dY [M, K'] and W2^T [N, K']
     g2 = torch.Generator().manual_seed(5)
-    dy = torch.randn(M, K, generator=g2).to(DEV, torch.bfloat16)
-    w2t = (torch.randn(N, K, generator=g2) / K ** 0.5).to(DEV, torch.bfloat16)
+    dy = torch.randn(M, K, generator=g2).to(DEV, low)
+    w2t = (torch.randn(N, K, generator=g2) / K ** 0.5).to(DEV, low)
     dh = ops.tok_gemm(dy, w2t, None, ops.TOK_GELU_GRAD, h=h)
     hf = h.float().requires_grad_(True)
     F.gelu(hf).backward(torch.ones_like(hf))
@@ -99,7 +105,7 @@ def test_tok_gemm_gelu_dual_and_grad(M, N, K):
 
 
 @pytest.mark.parametrize("M,C", [(4096, 96), (1000, 96), (512, 128)])
-def test_fused_mlp_matches_fp32(M, C):
+def test_fused_mlp_matches_fp32(M, C, low):
     """ops.mlp (mlp.0 -> GELU -> mlp.3) forward and all gradients vs fp32 autograd."""
     ops = _ops()
     g = torch.Generator().manual_seed(M + C)
@@ -109,17 +115,17 @@ def test_fused_mlp_matches_fp32(M, C):
     w2 = torch.randn(C, 4 * C, generator=g) / (4 * C) ** 0.5
     b2 = 0.1 * torch.randn(C, generator=g)
     dy = torch.randn(M, C, generator=g)
-    # fp32 reference on the bf16-rounded input
-    xr = x.bfloat16().float().requires_grad_(True)
+    # fp32 reference on the 16-bit-rounded input
+    xr = x.to(low).float().requires_grad_(True)
     pr = [t.clone().requires_grad_(True) for t in (w1, b1, w2, b2)]
     yr = F.linear(F.gelu(F.linear(xr, pr[0], pr[1])), pr[2], pr[3])
-    yr.backward(dy.bfloat16().float())
-    xg = x.to(DEV, torch.bfloat16).requires_grad_(True)
+    yr.backward(dy.to(low).float())
+    xg = x.to(DEV, low).requires_grad_(True)
     pg = [t.to(DEV).requires_grad_(True) for t in (w1, b1, w2, b2)]
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.autocast("cuda", dtype=low):
         assert ops.mlp_fusable(xg, pg[0], pg[2])
         y = ops.mlp(xg, *pg)
-    y.backward(dy.to(DEV, torch.bfloat16))
+    y.backward(dy.to(DEV, low))
     _check(y, yr.to(DEV), "y")
     # gradients: bf16 intermediates (H, G, dH) -> 3e-2 of the largest entry
     for name, a, r in [("dx", xg.grad, xr.grad), ("dw1", pg[0].grad, pr[0].grad), ("db1", pg[1].grad, pr[1].grad),
@@ -129,16 +135,16 @@ def test_fused_mlp_matches_fp32(M, C):
 
 
 @pytest.mark.parametrize("M,C", [(1024, 384), (2048, 192)])
-def test_fused_mlp_mixed_routing(M, C, monkeypatch):
+def test_fused_mlp_mixed_routing(M, C, monkeypatch, low):
     """Stage-1/2 widths: the GELU-epilogue GEMMs on the token GEMM, mlp.3 forward and mlp.0's
     input gradient on hipBLASLt (ops._mm) -- same numerics bar as the all-token-GEMM MLP."""
     ops = _ops()
     monkeypatch.setattr(ops, "_MLP_TOK_MIN_M", 0)
     assert not (ops.tok_preferred(M, 4 * C, C) and ops.tok_preferred(M, C, 4 * C))
-    test_fused_mlp_matches_fp32(M, C)
+    test_fused_mlp_matches_fp32(M, C, low)
 
 
-def test_linear_uses_tok_gemm_and_matches():
+def test_linear_uses_tok_gemm_and_matches(low):
     """ops.linear in bf16 routes through the token GEMM for covered shapes (fwd + dgrad)."""
     ops = _ops()
     M, N, K = 2048, 288, 96
@@ -148,21 +154,21 @@ def test_linear_uses_tok_gemm_and_matches():
     w = torch.randn(N, K, generator=g) / K ** 0.5
     b = torch.randn(N, generator=g)
     dy = torch.randn(M, N, generator=g)
-    xr = x.bfloat16().float().requires_grad_(True)
-    yr = F.linear(xr, w.bfloat16().float(), b)
-    yr.backward(dy.bfloat16().float())
-    xg = x.to(DEV, torch.bfloat16).requires_grad_(True)
+    xr = x.to(low).float().requires_grad_(True)
+    yr = F.linear(xr, w.to(low).float(), b)
+    yr.backward(dy.to(low).float())
+    xg = x.to(DEV, low).requires_grad_(True)
     wg = w.to(DEV).requires_grad_(True)
     bg = b.to(DEV).requires_grad_(True)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.autocast("cuda", dtype=low):
         y = ops.linear(xg, wg, bg)
-    y.backward(dy.to(DEV, torch.bfloat16))
+    y.backward(dy.to(DEV, low))
     _check(y, yr.to(DEV), "y")
     _check(xg.grad, xr.grad.to(DEV), "dx")
 
 
 @pytest.mark.parametrize("M,C", [(4096, 96), (1000, 192)])
-def test_linear_cat_matches_cat_then_linear(M, C):
+def test_linear_cat_matches_cat_then_linear(M, C, low):
     """ops.linear_cat (skip fusion without the concatenated copy) == Linear(cat([x, skip])):
     forward and all gradients, bf16 (model_parts.py:792-794)."""
     ops = _ops()
@@ -172,16 +178,16 @@ def test_linear_cat_matches_cat_then_linear(M, C):
     w = torch.randn(C, 2 * C, generator=g) / (2 * C) ** 0.5
     b = torch.randn(C, generator=g)
     dy = torch.randn(M, C, generator=g)
-    xr, sr = x.bfloat16().float().requires_grad_(True), sk.bfloat16().float().requires_grad_(True)
+    xr, sr = x.to(low).float().requires_grad_(True), sk.to(low).float().requires_grad_(True)
     wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
-    yr = F.linear(torch.cat([xr, sr], -1), wr.bfloat16().float(), br)
-    yr.backward(dy.bfloat16().float())
-    xg = x.to(DEV, torch.bfloat16).requires_grad_(True)
-    sg = sk.to(DEV, torch.bfloat16).requires_grad_(True)
+    yr = F.linear(torch.cat([xr, sr], -1), wr.to(low).float(), br)
+    yr.backward(dy.to(low).float())
+    xg = x.to(DEV, low).requires_grad_(True)
+    sg = sk.to(DEV, low).requires_grad_(True)
     wg, bg = w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.autocast("cuda", dtype=low):
         y = ops.linear_cat(xg, sg, wg, bg)
-    y.backward(dy.to(DEV, torch.bfloat16))
+    y.backward(dy.to(DEV, low))
     _check(y, yr.to(DEV), "y")
     _check(xg.grad, xr.grad.to(DEV), "dx")
     _check(sg.grad, sr.grad.to(DEV), "dskip")
