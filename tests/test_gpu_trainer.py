@@ -162,5 +162,5 @@ def test_adamw_dev_skip_matches_torch_adamw():
     assert hyper[1].item() == 2.0
     # same scalars and operation order as torch: a few ulp at most (CPU vs GPU rounding)
     torch.testing.assert_close(p.cpu(), ref.detach(), rtol=4e-7, atol=1e-8)
-    torch.testing.assert_close(m.cpu(), opt.state[ref]["exp_avg"], rtol=4e-7, atol=1e-9)
+    torch.testing.assert_close(m.cpu(), opt.state[ref]["exp_avg"], rtol=4e-7, atol=2e-8)
     torch.testing.assert_close(v.cpu(), opt.state[ref]["exp_avg_sq"], rtol=4e-7, atol=1e-12)
