@@ -68,27 +68,31 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
  * model_parts.py:170 / :538): pad to 7 -> roll(-shift) -> 7x7 windows -> softmax(q k^T *
  * 32^-0.5 + B_rel + shift mask(-100)) -> dropout(p) -> @v -> reverse.  qkv: [B,H,W,3C]
  * (q|k|v, heads contiguous, head_dim 32), out: [B,H,W,C]; table [169, nh] f32 is
- * relative_position_bias_table; qkv_bias [3C] f32 supplies padded tokens' q,k,v. */
+ * relative_position_bias_table; qkv_bias [3C] f32 supplies padded tokens' q,k,v.
+ * Dropout masks are a counter hash of (seed, window, head, i, j); seed_dev (may be null) points
+ * at a device u64 mixed into the seed, so a replayed HIP graph draws new masks per step and the
+ * backward regenerates the forward's mask from the same pair. */
 long msu_win_count(int B, int H, int W);
 /* f32 workspace elements (bf16: the per-head relative-bias image in MFMA C layout). */
 long msu_win_attn_fwd_workspace(int dtype, int C, int nh);
 int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                      void* out, float* workspace, int B, int H, int W, int C, int nh, int shift,
-                     float p_drop, unsigned long long seed, void* stream);
+                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream);
 long msu_win_attn_bwd_workspace(int dtype, int B, int H, int W, int C, int nh);
 /* dqkv [B,H,W,3C]; dtable [169,nh] (overwritten); dqkv_bias_pad [3C]: padded tokens'
  * contribution to the qkv-bias gradient (overwritten). */
 int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                      const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                      float* workspace, int B, int H, int W, int C, int nh, int shift,
-                     float p_drop, unsigned long long seed, void* stream);
+                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream);
 /* As msu_win_attn_bwd; the parameter-gradient tail (relative-table and qkv-bias reductions)
  * runs on param_stream, ordered after the backward kernel by an event (null: on stream).
  * dqkv is complete when `stream` is; dtable / dqkv_bias_pad when `param_stream` is. */
 int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                       const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                       float* workspace, int B, int H, int W, int C, int nh, int shift,
-                      float p_drop, unsigned long long seed, void* stream, void* param_stream);
+                      float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream,
+                      void* param_stream);
 
 /* ---------------------------------------------------------------- refine convs
  * FinalPatchExpand_X4_V2.refine1 / refine2 (model_parts.py:447-448, :468-471): 3x3, pad 1,

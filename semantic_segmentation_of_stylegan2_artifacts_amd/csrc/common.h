@@ -165,6 +165,15 @@ MSU_DEV float hash_uniform(uint64_t seed, uint64_t idx) {
   return (float)(uint32_t)(z >> 40) * (1.0f / 16777216.0f);
 }
 
+// Dropout seed of a launch: the host seed, mixed with a device-resident per-step counter when
+// one is given (seed_dev: a HIP-graph replay draws fresh masks without a host round trip).
+MSU_DEV uint64_t launch_seed(uint64_t seed, const unsigned long long* seed_dev) {
+  if (seed_dev == nullptr) return seed;
+  uint64_t z = seed ^ ((uint64_t)seed_dev[0] * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 31)) * 0xBF58476D1CE4E5B9ull;
+  return z ^ (z >> 29);
+}
+
 // Cheap 32-bit counter hash (murmur3 fmix32 of idx*golden + seed): uniform in [0, 1).
 // Used for dropout masks that forward and backward regenerate identically.
 MSU_DEV float hash_uniform32(uint32_t seed, uint32_t idx) {

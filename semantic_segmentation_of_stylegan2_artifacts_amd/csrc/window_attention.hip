@@ -175,7 +175,9 @@ MSU_DEV float drop_keep(uint64_t seed, long win, int h, int nh, int i, int j, fl
 template <typename T>
 __global__ void __launch_bounds__(64, 4) win_attn_fwd_kernel(const T* qkv, const float* qkv_bias,
                                                           const float* table, T* out, WinGeom g,
-                                                          float scale, float p_drop, uint64_t seed) {
+                                                          float scale, float p_drop, uint64_t seed0,
+                                                          const unsigned long long* seed_dev) {
+  const uint64_t seed = launch_seed(seed0, seed_dev);
   constexpr int LD = HD + row_pad<T>();   // [64 x 32] row images
   constexpr int LDP = 64 + row_pad<T>();  // [64 x 64] P
   __shared__ __attribute__((aligned(16))) T sQ[64 * LD];
@@ -240,7 +242,8 @@ template <typename T>
 __global__ void __launch_bounds__(64, 2) win_attn_bwd_kernel(
     const T* qkv, const float* qkv_bias, const float* table, const T* dout, T* dqkv,
     float* dbias_part /* [nblk, nh, 49*49] */, float* dqkvb_part /* [nblk, 3C] */,
-    WinGeom g, float scale, float p_drop, uint64_t seed, int nblk) {
+    WinGeom g, float scale, float p_drop, uint64_t seed0, const unsigned long long* seed_dev, int nblk) {
+  const uint64_t seed = launch_seed(seed0, seed_dev);
   constexpr int LD = HD + row_pad<T>();
   constexpr int LDP = 64 + row_pad<T>();
   __shared__ __attribute__((aligned(16))) T sQ[64 * LD];
@@ -397,11 +400,11 @@ WinGeom make_geom(int B, int H, int W, int C, int nh, int shift) {
 // bf16 training path: window_attention_mfma.hip
 int msu_attn_mfma_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, void* out, int B,
                       int H, int W, int C, int nh, int shift, float p_drop, unsigned long long seed,
-                      float* bias_img, hipStream_t st);
+                      const unsigned long long* seed_dev, float* bias_img, hipStream_t st);
 int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, const void* dout,
                       void* dqkv, float* dtable, float* dqkv_bias_pad, float* ws, int B, int H, int W,
-                      int C, int nh, int shift, float p_drop, unsigned long long seed, hipStream_t st,
-                      hipStream_t pst);
+                      int C, int nh, int shift, float p_drop, unsigned long long seed,
+                      const unsigned long long* seed_dev, hipStream_t st, hipStream_t pst);
 long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh);
 long msu_attn_mfma_fwd_workspace(int C, int nh);
 
@@ -424,7 +427,7 @@ long msu_win_attn_fwd_workspace(int dtype, int C, int nh) {
 
 int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                      void* out, float* workspace, int B, int H, int W, int C, int nh, int shift,
-                     float p_drop, unsigned long long seed, void* stream) {
+                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream) {
   if (C != nh * HD) return -2;
   const WinGeom g = make_geom(B, H, W, C, nh, shift);
   // the MFMA kernels address qkv / dqkv rows with 32-bit products tok * 3C
@@ -433,11 +436,12 @@ int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const fl
   if (items == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (msu_is16(dtype))
-    return msu_attn_mfma_fwd(dtype, qkv, qkv_bias, table, out, B, H, W, C, nh, shift, p_drop, seed, workspace, st);
+    return msu_attn_mfma_fwd(dtype, qkv, qkv_bias, table, out, B, H, W, C, nh, shift, p_drop, seed, seed_dev,
+                             workspace, st);
   const float scale = 1.0f / sqrtf((float)HD);
   const long nb = items < 262144 ? items : 262144;
   hipLaunchKernelGGL(win_attn_fwd_kernel<float>, dim3((unsigned)nb), dim3(64), 0, st,
-                     (const float*)qkv, qkv_bias, table, (float*)out, g, scale, p_drop, (uint64_t)seed);
+                     (const float*)qkv, qkv_bias, table, (float*)out, g, scale, p_drop, (uint64_t)seed, seed_dev);
   return MSU_CHECK_LAUNCH();
 }
 
@@ -451,7 +455,8 @@ long msu_win_attn_bwd_workspace(int dtype, int B, int H, int W, int C, int nh) {
 int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                       const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                       float* workspace, int B, int H, int W, int C, int nh, int shift,
-                      float p_drop, unsigned long long seed, void* stream, void* param_stream) {
+                      float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream,
+                      void* param_stream) {
   if (C != nh * HD) return -2;
   // the MFMA kernels address qkv / dqkv rows with 32-bit products tok * 3C
   if ((long)B * H * W * 3 * C >= (1L << 32)) return -2;
@@ -461,7 +466,7 @@ int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const f
   if (g.nwin == 0) return 0;
   if (msu_is16(dtype))
     return msu_attn_mfma_bwd(dtype, qkv, qkv_bias, table, dout, dqkv, dtable, dqkv_bias_pad, workspace, B, H, W,
-                             C, nh, shift, p_drop, seed, st, pst);
+                             C, nh, shift, p_drop, seed, seed_dev, st, pst);
   const int nblk = f32_bwd_blocks(g.nwin, nh);
   const float scale = 1.0f / sqrtf((float)HD);
   float* dB_part = workspace;
@@ -469,7 +474,7 @@ int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const f
   float* qb_part = dB + (long)nh * NT * NT;
   hipLaunchKernelGGL(win_attn_bwd_kernel<float>, dim3(nblk, nh), dim3(64), 0, st,
                      (const float*)qkv, qkv_bias, table, (const float*)dout, (float*)dqkv,
-                     dB_part, qb_part, g, scale, p_drop, (uint64_t)seed, nblk);
+                     dB_part, qb_part, g, scale, p_drop, (uint64_t)seed, seed_dev, nblk);
   const int rc = attn_param_stream(st, pst);
   if (rc) return rc;
   const long nB = (long)nh * NT * NT;
@@ -483,9 +488,9 @@ int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const f
 int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                      const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                      float* workspace, int B, int H, int W, int C, int nh, int shift,
-                     float p_drop, unsigned long long seed, void* stream) {
+                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream) {
   return msu_win_attn_bwd2(dtype, qkv, qkv_bias, table, dout, dqkv, dtable, dqkv_bias_pad, workspace, B, H, W,
-                           C, nh, shift, p_drop, seed, stream, nullptr);
+                           C, nh, shift, p_drop, seed, seed_dev, stream, nullptr);
 }
 
 }  // extern "C"

@@ -275,7 +275,9 @@ struct FwdLds {
 template <typename T, int WAVES>
 __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __restrict__ qkv, Aux aux,
                                                                bf16_t* __restrict__ out, Geom g, float scale,
-                                                               float p_drop, uint64_t seed) {
+                                                               float p_drop, uint64_t seed0,
+                                                               const unsigned long long* seed_dev) {
+  const uint64_t seed = launch_seed(seed0, seed_dev);
   __shared__ __attribute__((aligned(16))) float4 sBimg[4 * 4 * 64];
   __shared__ __attribute__((aligned(16))) FwdLds lds_all[WAVES];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -415,7 +417,8 @@ template <typename T, int WAVES>
 __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
     const bf16_t* __restrict__ qkv, Aux aux, const bf16_t* __restrict__ dout, bf16_t* __restrict__ dqkv,
     float* __restrict__ dB_part, float* __restrict__ qb_part, Geom g, float scale, float p_drop,
-    uint64_t seed, int nblk) {
+    uint64_t seed0, const unsigned long long* seed_dev, int nblk) {
+  const uint64_t seed = launch_seed(seed0, seed_dev);
   // grid (nblk, nh): block owns head h, waves walk windows win = (blk*WAVES + wave) + k*nblk*WAVES
   __shared__ __attribute__((aligned(16))) BwdLds lds_all[WAVES];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -715,7 +718,7 @@ long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh) {
 
 int msu_attn_mfma_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, void* out, int B,
                       int H, int W, int C, int nh, int shift, float p_drop, unsigned long long seed,
-                      float* ws, hipStream_t st) {
+                      const unsigned long long* seed_dev, float* ws, hipStream_t st) {
   const Geom g = make_geom(B, H, W, C, nh, shift);
   const long items = g.nwin * nh;
   if (items == 0) return 0;
@@ -730,14 +733,14 @@ int msu_attn_mfma_fwd(int dtype, const void* qkv, const float* qkv_bias, const f
     hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
                        1.0f / scale, img, brow, zrow);
     hipLaunchKernelGGL((attn_fwd_mfma<T, FWD_WAVES>), dim3((unsigned)nb, (unsigned)nh), dim3(64 * FWD_WAVES), 0, st,
-                       (const bf16_t*)qkv, aux, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed));
+                       (const bf16_t*)qkv, aux, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev));
   return MSU_CHECK_LAUNCH();
 }
 
 int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, const void* dout,
                       void* dqkv, float* dtable, float* dqkv_bias_pad, float* ws, int B, int H, int W,
-                      int C, int nh, int shift, float p_drop, unsigned long long seed, hipStream_t st,
-                      hipStream_t pst) {
+                      int C, int nh, int shift, float p_drop, unsigned long long seed,
+                      const unsigned long long* seed_dev, hipStream_t st, hipStream_t pst) {
   const Geom g = make_geom(B, H, W, C, nh, shift);
   if (g.nwin == 0) return 0;
   const float scale = 1.0f / sqrtf((float)HD);
@@ -753,7 +756,7 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
                        1.0f / scale, img, brow, zrow);
     hipLaunchKernelGGL((attn_bwd_mfma<T, BWD_WAVES>), dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
                        (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
-                       p_drop, (uint64_t)seed, nblk));
+                       p_drop, (uint64_t)seed, seed_dev, nblk));
   // parameter-gradient reductions: on pst (after the backward kernel) when given
   const int rc = attn_param_stream(st, pst);
   if (rc) return rc;

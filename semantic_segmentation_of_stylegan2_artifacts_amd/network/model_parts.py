@@ -13,8 +13,11 @@ reference (``structure_of_MSUNet.txt``), so reference checkpoints load with
 * FinalPatchExpand_X4_V2 runs expand -> [d2s + GELU fused into conv1's loads] -> conv1+bias
   -> [GELU fused into conv2's loads] -> conv2+bias -> LayerNorm fused with the 1x1 head.
 
-Dense GEMMs (qkv / proj / MLP / merge reduction / expand / skip fusion / patch embed) run
-through ``torch.nn.functional.linear`` (hipBLASLt) under ``torch.autocast``.
+Dense GEMMs (qkv / proj / MLP / merge reduction / expand / skip fusion / patch embed) are the
+``torch.ops.msunet`` linear family (ops.py): the HIP token GEMM (gemm_tok.h) for the
+HBM-bound stage-0/1 shapes and every fused epilogue (bias, GELU, GELU', skip concat), the HIP
+weight-gradient kernel for every weight gradient, and the library GEMM (hipBLASLt) for the
+remaining MFMA-bound stage-2/3 forward / input-gradient products.
 """
 import math
 import random
@@ -57,6 +60,29 @@ def reseed(seed):
     the pooled stochastic-depth draws made under the previous seed."""
     _seed_rng.seed(int(seed) ^ 0x5EED)
     _SCALE_POOL.clear()
+
+
+# Device-resident dropout counter (int64 [1]) mixed into every attention-dropout seed when set:
+# a trainer that replays its step from a HIP graph advances it inside the graph, so each replay
+# draws new attention-dropout masks although the host-side seeds were fixed at capture.
+_dev_seed = None
+
+
+def set_device_seed(t):
+    global _dev_seed
+    _dev_seed = t
+
+
+def refresh_drop_pools():
+    """Redraw every stochastic-depth pool in place and restart its row cursor.  Called at the
+    start of a captured training step: the draws become part of the graph (torch's generator is
+    graph-safe), so every replay reads fresh scales from the same rows."""
+    for (p, _, _, _), pool in _SCALE_POOL.items():
+        survival = 1.0 - p
+        pool[0].bernoulli_(survival)
+        if survival > 0.0:
+            pool[0].div_(survival)
+        pool[1] = 0
 
 
 _SCALE_POOL = {}
@@ -121,7 +147,8 @@ class ShiftedWindowAttention(nn.Module):
             3 * x.shape[-1], device=x.device, dtype=torch.float32)
         p = self.attention_dropout if self.training else 0.0
         o = ops.window_attention(qkv, qb, self.relative_position_bias_table, self.num_heads,
-                                 self.shift_size[0], p, _next_seed() if p > 0 else 0)
+                                 self.shift_size[0], p, _next_seed() if p > 0 else 0,
+                                 _dev_seed if p > 0 else None)
         o = ops.linear(o, self.proj.weight, self.proj.bias)
         if self.dropout > 0 and self.training:
             o = F.dropout(o, self.dropout, True)

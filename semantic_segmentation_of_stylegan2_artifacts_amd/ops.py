@@ -468,7 +468,7 @@ def d2s_layer_norm(x, weight, bias, eps=1e-5):
 
 
 # ----------------------------------------------------------------------------- attention
-def _attn_impl(qkv, qkv_bias, table, num_heads, shift, p_drop, seed):
+def _attn_impl(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
     _need_cuda(qkv)
     qkv = qkv.contiguous()
     B, H, W, C3 = qkv.shape
@@ -477,18 +477,18 @@ def _attn_impl(qkv, qkv_bias, table, num_heads, shift, p_drop, seed):
     ws = torch.empty(_lib.lib().msu_win_attn_fwd_workspace(_dt(qkv), C, num_heads), device=qkv.device,
                      dtype=torch.float32)
     _lib.call("msu_win_attn_fwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(out), _p(ws), B, H, W,
-              C, num_heads, shift, float(p_drop), seed, _s(qkv))
+              C, num_heads, shift, float(p_drop), seed, _p(seed_dev), _s(qkv))
     return out
 
 
-def _attn_fake(qkv, qkv_bias, table, num_heads, shift, p_drop, seed):
+def _attn_fake(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
     B, H, W, C3 = qkv.shape
     return qkv.new_empty(B, H, W, C3 // 3)
 
 
 def _attn_setup(ctx, inputs, output):
-    qkv, qkv_bias, table, num_heads, shift, p_drop, seed = inputs
-    ctx.save_for_backward(qkv.contiguous(), qkv_bias, table)
+    qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev = inputs
+    ctx.save_for_backward(qkv.contiguous(), qkv_bias, table, seed_dev)
     # the parameter itself when it reached us uncast (trainer flat buffers: direct .grad)
     ctx.bias_param = qkv_bias if isinstance(qkv_bias, torch.nn.Parameter) else None
     ctx.table_param = table if isinstance(table, torch.nn.Parameter) else None
@@ -496,7 +496,7 @@ def _attn_setup(ctx, inputs, output):
 
 
 def _attn_backward(ctx, dout):
-    qkv, qkv_bias, table = ctx.saved_tensors
+    qkv, qkv_bias, table, seed_dev = ctx.saved_tensors
     nh, shift, p_drop, seed = ctx.cfg
     B, H, W, C3 = qkv.shape
     C = C3 // 3
@@ -516,8 +516,8 @@ def _attn_backward(ctx, dout):
             dtable = torch.empty_like(table)
             dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
         _lib.call("msu_win_attn_bwd2", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
-                  _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, main.cuda_stream,
-                  side.cuda_stream)
+                  _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _p(seed_dev),
+                  main.cuda_stream, side.cuda_stream)
         ws.record_stream(side)
         with torch.cuda.stream(side):
             bp.grad.add_(dbias)
@@ -528,28 +528,31 @@ def _attn_backward(ctx, dout):
         _guard_side_write(tp, ev)
         _join_at_end_of_backward()
         _notify(bp, tp)
-        return dqkv, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None
     dtable = torch.empty_like(table)
     dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
     _lib.call("msu_win_attn_bwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
-              _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _s(qkv))
-    return dqkv, dbias, dtable, None, None, None, None
+              _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _p(seed_dev), _s(qkv))
+    return dqkv, dbias, dtable, None, None, None, None, None
 
 
 _window_attention = _define(
     "window_attention",
-    "(Tensor qkv, Tensor qkv_bias, Tensor table, int num_heads, int shift, float p_drop, int seed) -> Tensor",
+    "(Tensor qkv, Tensor qkv_bias, Tensor table, int num_heads, int shift, float p_drop, int seed, Tensor? seed_dev)"
+    " -> Tensor",
     _attn_impl, _attn_fake, _attn_setup, _attn_backward)
 
 
-def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0):
+def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0, seed_dev=None):
     """torchvision shifted_window_attention core between the qkv and proj Linears.
-    qkv: [B, H, W, 3C] (unpadded tokens) -> [B, H, W, C]."""
+    qkv: [B, H, W, 3C] (unpadded tokens) -> [B, H, W, C].  Dropout masks hash (seed, window,
+    head, i, j); seed_dev: optional device int64 [1] mixed into the seed (per-step counter of a
+    replayed HIP graph)."""
     C3 = qkv.shape[-1]
     if C3 % 3 or (C3 // 3) != num_heads * 32:
         raise ValueError(f"head_dim must be 32 (C={C3 // 3}, heads={num_heads})")
     return _window_attention(_as(qkv, act_dtype()), _f32(qkv_bias), _f32(table), int(num_heads),
-                             int(shift), float(p_drop), int(seed) & ((1 << 63) - 1))
+                             int(shift), float(p_drop), int(seed) & ((1 << 63) - 1), seed_dev)
 
 
 # ----------------------------------------------------------------------------- token GEMM

@@ -15,7 +15,10 @@ Here:
   bucket has accumulated its gradient (post-accumulate hooks) the bucket is all-reduced
   (RCCL over xGMI, ``async_op``) while backward continues; the 1/world average is folded
   into the fused AdamW kernel;
-* AdamW = one fused HIP launch per group over the flat buffer;
+* AdamW = one fused HIP launch per group over the flat buffer, lr / step read from device
+  memory, skipped (GradScaler semantics) when a gradient is non-finite;
+* after two eager steps the device side of the step is captured into a HIP graph and
+  replayed (``Trainer.step``): the host issues one launch per step;
 * parameters whose outputs the reference discards (dead central-decoder branches) never
   receive gradients there; they are excluded here, matching torch AdamW's skip of
   ``grad is None``.
@@ -28,6 +31,7 @@ import torch.distributed as dist
 
 from . import ops
 from .loss import DynamicLoss
+from .network import model_parts
 
 # A/B switch: mark the bf16 shadow's parameter versions before AdamW (host-only work while
 # the GPU is still busy) instead of after the step's last launch
@@ -186,7 +190,8 @@ def reseed(seed, rank=0):
 
 class Trainer:
     def __init__(self, model, config, device, lr=None, amp_dtype=torch.bfloat16, bucket_mb=32,
-                 world_size=1, process_group=None, rank=0, seed=None, skip_nonfinite=True):
+                 world_size=1, process_group=None, rank=0, seed=None, skip_nonfinite=True, use_graph=None,
+                 graph_warmup=2):
         self.model = model
         self.device = device
         self.amp_dtype = amp_dtype
@@ -226,6 +231,17 @@ class Trainer:
         self.inv_world = torch.full((1,), 1.0 / world_size, device=device, dtype=torch.float32)
         self.reducer = (GradBucketer(self.groups, int(bucket_mb * (1 << 20)), process_group)
                         if world_size > 1 else None)
+        # HIP-graph replay of the step (see step()); MSU_GRAPH=0 keeps every step eager
+        on_gpu = torch.device(device).type == "cuda"
+        self.use_graph = on_gpu and (use_graph if use_graph is not None else os.environ.get("MSU_GRAPH", "1") != "0")
+        if self.use_graph and world_size > 1 and dist.get_backend(process_group) != "nccl":
+            self.use_graph = False  # gloo collectives run on the host: not capturable
+        self.graph_warmup = graph_warmup
+        self._graph = None
+        self._graph_failed = False
+        self.dev_seed = torch.zeros(1, device=device, dtype=torch.int64)
+        if self.use_graph:
+            model_parts.set_device_seed(self.dev_seed)
 
     @property
     def lr(self):
@@ -254,22 +270,38 @@ class Trainer:
             return self.loss_fn(out, labels)
 
     def step(self, images, labels):
-        """One training step; returns the (device) loss of this rank's batch."""
+        """One training step; returns the (device) loss of this rank's batch.
+
+        After ``graph_warmup`` eager steps (lazy library / kernel-attribute initialisation,
+        the all-reduce accumulation counts of step 0), the whole device side of the step --
+        forward, DynamicLoss, backward with its side-stream work, the bucketed all-reduce,
+        the non-finite check, AdamW, the gradient reset and the bf16 shadow refresh -- is
+        captured once into a HIP graph and replayed: one launch per step instead of ~1300.
+        Inputs are copied into the graph's static buffers; dropout keeps drawing fresh masks
+        (device-side seed counter, drop-path pools redrawn inside the graph)."""
         if not self.model.training:  # Module.train() walks all ~400 modules: ~1 ms of host time
             self.model.train()
+        if self.use_graph and self.step_count >= self.graph_warmup:
+            if self._graph is None and not self._graph_failed:
+                self._capture(images, labels)
+            if self._graph is not None:
+                return self._replay(images, labels)
+        return self._eager_step(images, labels)
+
+    # ------------------------------------------------------------------ eager / captured body
+    def _device_step(self, images, labels):
+        """Everything the step enqueues on the GPU (the body that is captured)."""
+        if self.use_graph:
+            self.dev_seed.add_(1)  # new attention-dropout masks per step / replay
+            model_parts.refresh_drop_pools()
         ops.set_grad_ready_callback(self.reducer._hook if self.reducer is not None else None)
         if self.reducer is not None and torch.device(self.device).type == "cuda":
             self.reducer.main_stream = torch.cuda.current_stream(self.device)
-        if self.amp_dtype == torch.bfloat16 and not self._shadow_fresh:
-            for g in self.groups:
-                g.refresh_shadow()
-        self._shadow_fresh = False
         loss = self.forward_loss(images, labels)
         loss.backward()
         if self.reducer is not None:
             self.reducer.finish()
         ops.join_side_streams()  # weight gradients issued on the side stream
-        self.step_count += 1
         inv = self.inv_world if self.world_size > 1 else None
         bf16 = self.amp_dtype == torch.bfloat16
         if bf16 and _EARLY_MARK:
@@ -294,7 +326,63 @@ class Trainer:
                     g.copy_shadow()
                 else:
                     g.refresh_shadow()
+        return loss.detach()
+
+    def _eager_step(self, images, labels):
+        if self.amp_dtype == torch.bfloat16 and not self._shadow_fresh:
+            for g in self.groups:
+                g.refresh_shadow()
+        self._shadow_fresh = False
+        loss = self._device_step(images, labels)
+        self.step_count += 1
         # the next step's refresh is skipped; a write through a parameter in between bumps its
         # version and the Linear ops cast that weight themselves (ops._shadow)
         self._shadow_fresh = self.amp_dtype == torch.bfloat16
-        return loss.detach()
+        return loss
+
+    def _param_versions(self):
+        return sum(p._version for g in self.groups for p in g.params)
+
+    def _capture(self, images, labels):
+        """Capture _device_step into a HIP graph (nothing executes during capture)."""
+        if self.amp_dtype == torch.bfloat16 and not self._shadow_fresh:
+            for g in self.groups:
+                g.refresh_shadow()
+        self._sx = images.detach().clone()
+        self._sy = labels.detach().clone()
+        torch.cuda.synchronize(self.device)
+        graph = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(graph):
+                loss = self._device_step(self._sx, self._sy)
+        except Exception as e:  # noqa: BLE001 -- any capture failure: stay eager, loudly
+            import warnings
+            warnings.warn(f"HIP graph capture of the training step failed ({e!r}); continuing eagerly")
+            self._graph_failed = True
+            self._sx = self._sy = None
+            torch.cuda.synchronize(self.device)
+            return
+        self._graph = graph
+        self._sloss = loss
+        self._versions = self._param_versions()
+
+    def _replay(self, images, labels):
+        v = self._param_versions()
+        if v != self._versions:
+            # a write through a parameter (load_state_dict, p.copy_) since the last step: the
+            # captured forward reads the bf16 shadow, so re-derive it before replaying
+            if self.amp_dtype == torch.bfloat16:
+                for g in self.groups:
+                    g.refresh_shadow()
+            self._versions = v
+        self._sx.copy_(images)
+        self._sy.copy_(labels)
+        self._graph.replay()
+        self.step_count += 1
+        return self._sloss.clone()
+
+    def invalidate_graph(self):
+        """Drop the captured step (e.g. after changing the model's structure or freezing
+        parameters); the next step captures again."""
+        self._graph = None
+        self._graph_failed = False

@@ -80,7 +80,7 @@ def test_torch_library_ops_registered():
     with FakeTensorMode():
         qkv = torch.empty(2, 10, 12, 3 * 64, device="cuda", dtype=torch.float16)
         out = torch.ops.msunet.window_attention(qkv, torch.empty(192, device="cuda"),
-                                                torch.empty(169, 2, device="cuda"), 2, 3, 0.0, 0)
+                                                torch.empty(169, 2, device="cuda"), 2, 3, 0.0, 0, None)
         assert out.shape == (2, 10, 12, 64) and out.dtype == torch.float16
         y, mean, rstd = torch.ops.msunet.layer_norm(torch.empty(5, 96, device="cuda"), torch.empty(96, device="cuda"),
                                                     torch.empty(96, device="cuda"), 1e-5)
