@@ -5,11 +5,16 @@
 
 A step = one full training step of the reference's trainer.py:308-316 on one batch per
 rank: bf16-autocast forward of MS-UNet -> DynamicLoss -> backward -> bucketed RCCL
-gradient all-reduce (N > 1) -> fused AdamW.  Synthetic StyleGAN2-shaped inputs are
-generated in HBM before timing.  Rank 0 prints ONE JSON line.
+gradient all-reduce (N > 1) -> non-finite check -> fused AdamW.  The Trainer runs its first
+two steps eagerly and then replays the captured step as a HIP graph (both inside the
+warmup when W >= 3).  Synthetic StyleGAN2-shaped inputs are generated in HBM before timing
+and copied into the graph's input buffers inside every timed step.  Rank 0 prints ONE
+JSON line.
 
 Extra objects: ``roofline`` for the dominant kernel (timed live with HIP events on its
-stream) and ``cpu_baseline`` (the CPU oracle's training step on a bounded sample).
+stream), ``roofline_attention`` (window attention), ``roofline_decoder`` (the decoder head
+stack fwd+bwd against the HBM roofline) and ``cpu_baseline`` (the CPU oracle's training step,
+Swin-T and Swin-B, on the box's host cores).
 """
 import argparse
 import json
@@ -23,6 +28,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+BACKBONE_NAME = {"swin_t": "Swin-T", "swin_s": "Swin-S", "swin_b": "Swin-B"}
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
@@ -126,26 +132,34 @@ def attention_roofline(device, batch, img, C, heads):
             "bytes_per_launch": byts, "flops_per_launch": flops, "ms_per_launch": round(ms, 4)}
 
 
-def cpu_baseline(seconds_budget=25.0):
-    """The CPU oracle (pure PyTorch fp32 restatement of the reference path) timing one
-    training step (fwd + DynamicLoss + bwd + AdamW) of Swin-T MS-UNet on 4 x 256^2
-    (BASELINE config 1); bounded to a few steps."""
-    from oracle.msunet import make_cfg, init_params, msunet_forward
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _cpu_train_steps(backbone, steps=10, first=2):
+    """The CPU oracle's fp32 training step (fwd + DynamicLoss + bwd + AdamW) of one backbone
+    on 4 x 256^2 (BASELINE config 1); returns (images/s averaged over steps first..steps-1,
+    s/step, list of step times)."""
+    from oracle.msunet import make_cfg, init_params, msunet_forward, SWIN_T, SWIN_B
     from oracle.dynamic_loss import dynamic_loss
     from semantic_segmentation_of_stylegan2_artifacts_amd.data import synthetic_batch
-    cores = len(os.sched_getaffinity(0))
-    cores = max(1, min(cores, 16))
-    torch.set_num_threads(cores)
-    cfg = make_cfg(img_size=256, embed_dim=96, depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24],
-                   drop_path_rate=0.0)
+    arch = {"swin_t": SWIN_T, "swin_b": SWIN_B}[backbone]
+    cfg = make_cfg(img_size=256, drop_path_rate=0.0, **arch)
     p = init_params(cfg, seed=0)
     params = {k: v.requires_grad_(True) for k, v in p.items() if v.is_floating_point()}
     p.update(params)
     opt = torch.optim.AdamW(list(params.values()), lr=1e-5, weight_decay=1e-3)
     x, y = synthetic_batch(4, 256, "cpu", 120)
     times = []
-    t_start = time.perf_counter()
-    for i in range(6):
+    for _ in range(steps):
         t0 = time.perf_counter()
         out = msunet_forward(p, cfg, x)
         loss = dynamic_loss(out, y, 0.2, 0.8, 0.45)
@@ -153,13 +167,94 @@ def cpu_baseline(seconds_budget=25.0):
         loss.backward()
         opt.step()
         times.append(time.perf_counter() - t0)
-        if time.perf_counter() - t_start > seconds_budget and i >= 1:
-            break
-    steady = times[1:] if len(times) > 1 else times
+    steady = times[first:]
     sps = sum(steady) / len(steady)
-    return {"value": round(4 / sps, 4), "unit": "images/s", "cores": cores, "kind": "port",
-            "sample": f"CPU oracle (torch fp32) Swin-T MS-UNet train step, 4x256^2 (config 1), "
-                      f"{len(steady)} steady steps of {len(times)}, {sps:.2f} s/step"}
+    return 4 / sps, sps, times
+
+
+def cpu_baseline():
+    """the CPU oracle (pure PyTorch fp32 restatement of the reference step,
+    validated against the imported reference in the dev container) on the host cores of this
+    box, config 1 shapes (4 x 256^2), Swin-T (the bench backbone: ``value``) and Swin-B
+    (config.yaml's default backbone), 10 steps each, steps 2-9 averaged.  Threads: the
+    process's CPU share (OMP_NUM_THREADS when the scheduler sets it, else the affinity mask)."""
+    affinity = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get("OMP_NUM_THREADS") or affinity)
+    threads = max(1, min(threads, affinity))
+    torch.set_num_threads(threads)
+    t_ips, t_sps, t_times = _cpu_train_steps("swin_t")
+    b_ips, b_sps, b_times = _cpu_train_steps("swin_b")
+    return {"value": round(t_ips, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "cpus_in_affinity_mask": affinity,
+            "sample": f"CPU oracle (torch fp32) MS-UNet train step, 4x256^2 (config 1), 10 steps, "
+                      f"steps 2-9 averaged: Swin-T {t_sps:.2f} s/step",
+            "swin_b": {"value": round(b_ips, 4), "unit": "images/s", "s_per_step": round(b_sps, 3)},
+            "step_times_s": {"swin_t": [round(v, 3) for v in t_times], "swin_b": [round(v, 3) for v in b_times]}}
+
+
+def decoder_roofline(device, batch, img, C):
+    """North-star figure for the decoder head stack (SURVEY 8a rows 15 + 16): expand Linear
+    (+GELU) -> refine1 (4x4 d2s on load) -> GELU -> refine2 -> LayerNorm + 1x1 head, forward
+    AND backward, timed with HIP events around whole fwd+bwd passes of the model's own modules
+    at the bench shape.  Algorithmic work per op = its FLOPs and the bytes of its inputs read
+    once and outputs written once (bf16 activations, f32 logits / statistics); the roofline time
+    is sum_op max(flops / MFMA peak, bytes / HBM peak).  Reported: HBM GB/s over the measured
+    time (the north star's '>= 40 % HBM on the decoder conv stack') and roofline time /
+    measured time."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd.network.model_parts import FinalPatchExpand_X4_V2
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    h = img // 4
+    head = FinalPatchExpand_X4_V2((h, h), dim=C, dim_scale=4).to(device)
+    out_w = (torch.randn(1, C, 1, 1, device=device) / C ** 0.5).requires_grad_(True)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = (torch.randn(batch, h * h, C, generator=g)).to(device, torch.bfloat16).requires_grad_(True)
+    dl = torch.randn(batch, 1, img, img, generator=g).to(device)
+
+    def run():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            z2 = head.pre_norm(x)
+            logit = ops.head_norm_output(z2, head.norm.weight, head.norm.bias, out_w, head.norm.eps)
+        logit.backward(dl)
+
+    for _ in range(2):
+        run()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream(device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 5
+    e0.record(s)
+    for _ in range(n):
+        run()
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    M, P, E = batch * h * h, batch * img * img, 16 * C
+    a16, f32 = 2, 4
+    act = P * C * a16                      # one full-resolution bf16 activation
+    conv_f = 2.0 * P * C * C * 9
+    lin_f = 2.0 * M * C * E
+    ops_ = {  # op: (flops, bytes)
+        "expand_fwd": (lin_f, M * C * a16 + 2 * M * E * a16),
+        "refine1_fwd": (conv_f, act + 2 * act),
+        "refine2_fwd": (conv_f, act + act),
+        "head_fwd": (8.0 * P * C, act + 3 * P * f32),
+        "head_bwd": (10.0 * P * C, act + 3 * P * f32 + act),
+        "refine2_dgrad": (conv_f, 3 * act),
+        "refine2_wgrad": (conv_f, 2 * act),
+        "refine1_dgrad": (conv_f, 3 * act),
+        "refine1_wgrad": (conv_f, 2 * act),
+        "expand_dgrad": (lin_f, M * E * a16 + M * C * a16),
+        "expand_wgrad": (lin_f, M * E * a16 + M * C * a16),
+    }
+    flops = sum(f for f, _ in ops_.values())
+    byts = sum(b for _, b in ops_.values())
+    t_roof = sum(max(f / (MFMA_BF16_PEAK_TFLOPS * 1e12), b / (HBM_PEAK_GBS * 1e9)) for f, b in ops_.values())
+    gbs = byts / (ms * 1e-3) / 1e9
+    return {"stack": "FinalPatchExpand_X4_V2 + LN/1x1 head, fwd+bwd (rows 15+16)", "bound": "hbm",
+            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "ms_per_pass": round(ms, 3), "bytes_per_pass": byts, "flops_per_pass": flops,
+            "mfma_tflops": round(flops / (ms * 1e-3) / 1e12, 1),
+            "roofline_ms": round(t_roof * 1e3, 3), "roofline_frac": round(t_roof * 1e3 / ms, 4)}
 
 
 def dice_vs_reference(device):
@@ -248,7 +343,8 @@ def main():
     if rank == 0:
         imgs = args.batch * world * args.steps
         res = {
-            "metric": "training images/sec at 1024^2 bs=8 per GPU (MS-UNet Swin-T, fwd+DynamicLoss+bwd+AdamW)",
+            "metric": f"training images/sec at {args.img}^2 bs={args.batch} per GPU "
+                      f"(MS-UNet {BACKBONE_NAME[args.backbone]}, fwd+DynamicLoss+bwd+AdamW)",
             "value": round(imgs / elapsed, 3),
             "unit": "images/s",
             "n_gpus": world,
@@ -261,17 +357,21 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (uniform RGB /255 + ellipse artifact masks, 60% fake), random-init weights",
-            "config": {"workload": f"1xMI355X {args.img}x{args.img} bs={args.batch} Swin-T MS-UNet train step"
-                       if world == 1 else f"{world}xMI355X DP {args.img}x{args.img} global bs={args.batch * world}",
+            "config": {"workload": f"1xMI355X {args.img}x{args.img} bs={args.batch} {BACKBONE_NAME[args.backbone]} "
+                                   f"MS-UNet train step" if world == 1 else
+                                   f"{world}xMI355X DP {args.img}x{args.img} global bs={args.batch * world} "
+                                   f"{BACKBONE_NAME[args.backbone]} MS-UNet train step",
                        "model": f"MS-UNet {args.backbone}", "global_batch": args.batch * world,
                        "img_size": args.img, "parallelism": f"dp{world}",
                        "dead_branches": "skipped" if args.skip_dead else "executed (no grad)",
+                       "step_execution": "hip_graph_replay" if trainer._graph is not None else "eager",
                        "params": trainer.num_params(), "final_loss": round(loss_val, 6)},
         }
         if not args.no_roofline:
             res["roofline"] = conv_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM)
             res["roofline_attention"] = attention_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM,
                                                            cfg.MODEL.SWIN.NUM_HEADS[0])
+            res["roofline_decoder"] = decoder_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline()
             res["dice_vs_ref"] = dice_vs_reference(device)
