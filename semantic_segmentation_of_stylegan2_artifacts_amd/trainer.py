@@ -282,6 +282,8 @@ class Trainer:
         if not self.model.training:  # Module.train() walks all ~400 modules: ~1 ms of host time
             self.model.train()
         if self.use_graph and self.step_count >= self.graph_warmup:
+            if self._graph is not None and self.loss_fn is not self._graph_loss_fn:
+                self.invalidate_graph()  # the captured step holds the old loss module
             if self._graph is None and not self._graph_failed:
                 self._capture(images, labels)
             if self._graph is not None:
@@ -363,6 +365,7 @@ class Trainer:
             torch.cuda.synchronize(self.device)
             return
         self._graph = graph
+        self._graph_loss_fn = self.loss_fn
         self._sloss = loss
         self._versions = self._param_versions()
 
@@ -382,7 +385,9 @@ class Trainer:
         return self._sloss.clone()
 
     def invalidate_graph(self):
-        """Drop the captured step (e.g. after changing the model's structure or freezing
-        parameters); the next step captures again."""
+        """Drop the captured step; the next step captures again.  The replay repeats the
+        captured kernels with the captured Python decisions: call this after changing the
+        model's structure, its train/eval-dependent settings or frozen parameters (a new
+        loss_fn and writes through parameters are detected by step() itself)."""
         self._graph = None
         self._graph_failed = False

@@ -97,7 +97,7 @@ def test_nonfinite_gradient_skips_the_step():
     from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import Trainer
     model, x, target, conf = _setup()
     ref = copy.deepcopy(model)
-    tr = Trainer(model, conf, DEV)
+    tr = Trainer(model, conf, DEV, use_graph=False)  # swaps loss_fn between steps (eager semantics)
     tr.step(x, target)
     snap = [(g.data.clone(), g.exp_avg.clone(), g.exp_avg_sq.clone()) for g in tr.groups]
     bad = x.clone()
@@ -131,6 +131,28 @@ def test_nonfinite_gradient_skips_the_step():
     assert tr.optimizer_steps() == 1
     tr.step(x, target)
     assert tr.optimizer_steps() == 2
+
+
+def test_nonfinite_input_skips_replayed_step():
+    """The same GradScaler rule inside the HIP-graph replay: a NaN image in the replayed
+    step's input buffer skips the captured AdamW, a finite one applies it."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import Trainer
+    model, x, target, conf = _setup()
+    tr = Trainer(model, conf, DEV, use_graph=True, graph_warmup=2)
+    for _ in range(3):
+        tr.step(x, target)
+    assert tr._graph is not None and tr.optimizer_steps() == 3
+    snap = [g.data.clone() for g in tr.groups]
+    bad = x.clone()
+    bad[0, 1, 3, 3] = float("inf")
+    tr.step(bad, target)
+    torch.cuda.synchronize()
+    assert tr.found_inf.item() == 1.0 and tr.optimizer_steps() == 3
+    for g, d in zip(tr.groups, snap):
+        assert torch.equal(g.data, d)
+    tr.step(x, target)
+    assert tr.optimizer_steps() == 4
+    assert not torch.equal(tr.groups[0].data, snap[0])
 
 
 def test_adamw_dev_skip_matches_torch_adamw():
