@@ -6,8 +6,9 @@
 A step = one full training step of the reference's trainer.py:308-316 on one batch per
 rank: bf16-autocast forward of MS-UNet -> DynamicLoss -> backward -> bucketed RCCL
 gradient all-reduce (N > 1) -> non-finite check -> fused AdamW.  The Trainer runs its first
-two steps eagerly and then replays the captured step as a HIP graph (both inside the
-warmup when W >= 3).  Synthetic StyleGAN2-shaped inputs are generated in HBM before timing
+two steps eagerly, times the second, and replays the captured step as a HIP graph from then
+on when that step was launch-bound (host issue time >= 0.9 x GPU time), else stays eager
+(MSU_GRAPH=1/0 forces either; the decision falls inside the warmup when W >= 3).  Synthetic StyleGAN2-shaped inputs are generated in HBM before timing
 and copied into the graph's input buffers inside every timed step.  Rank 0 prints ONE
 JSON line.
 
@@ -365,6 +366,7 @@ def main():
                        "img_size": args.img, "parallelism": f"dp{world}",
                        "dead_branches": "skipped" if args.skip_dead else "executed (no grad)",
                        "step_execution": "hip_graph_replay" if trainer._graph is not None else "eager",
+                       "graph_probe": getattr(trainer, "graph_probe", None),
                        "params": trainer.num_params(), "final_loss": round(loss_val, 6)},
         }
         if not args.no_roofline:

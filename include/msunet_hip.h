@@ -87,12 +87,18 @@ int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const fl
                      float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream);
 /* As msu_win_attn_bwd; the parameter-gradient tail (relative-table and qkv-bias reductions)
  * runs on param_stream, ordered after the backward kernel by an event (null: on stream).
- * dqkv is complete when `stream` is; dtable / dqkv_bias_pad when `param_stream` is. */
+ * dqkv is complete when `stream` is; dtable / dqkv_bias_pad when `param_stream` is.
+ * param_stream == (void*)-1: only the backward kernel is launched; the caller orders its own
+ * stream after `stream` and issues msu_win_attn_bwd_tail (the HIP-graph-safe split). */
 int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                       const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                       float* workspace, int B, int H, int W, int C, int nh, int shift,
                       float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream,
                       void* param_stream);
+/* The parameter-gradient tail of msu_win_attn_bwd2 (dtable, dqkv_bias_pad) from the
+ * workspace partials its backward kernel left, on `stream`. */
+int msu_win_attn_bwd_tail(int dtype, float* workspace, float* dtable, float* dqkv_bias_pad, int B, int H, int W,
+                          int C, int nh, void* stream);
 
 /* ---------------------------------------------------------------- refine convs
  * FinalPatchExpand_X4_V2.refine1 / refine2 (model_parts.py:447-448, :468-471): 3x3, pad 1,

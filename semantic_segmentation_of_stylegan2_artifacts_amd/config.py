@@ -46,6 +46,9 @@ _DEFAULTS = {
     "MODEL": {
         "TYPE": "swin", "NAME": "swin_b", "NUM_CLASSES": 1, "DROP_RATE": 0.0,
         "DROP_PATH_RATE": 0.1, "ATTN_DROP_RATE": 0.05, "FREEZE_ENCODER": False,
+        "PRETRAIN_WEIGHTS": "segface",
+        "PRETRAIN_SEGFACE": "./network/pretrained_weights/SegFace_swin_celaba_512.pt",
+        "PRETRAIN_IMAGENET1K": "./network/pretrained_weights/swin_b-68c6b09e.pth",
         "SWIN": {"PATCH_SIZE": 4, "IN_CHANS": 3, "EMBED_DIM": 128, "DEPTHS": [2, 2, 18, 2],
                  "DECODER_DEPTHS": [2, 2, 6, 2], "NUM_HEADS": [4, 8, 16, 32], "WINDOW_SIZE": 7,
                  "MLP_RATIO": 4.0, "QKV_BIAS": True, "QK_SCALE": None, "APE": False,
@@ -63,6 +66,8 @@ _DEFAULTS = {
     "SEED": 120,
     "DETERMINISTIC": True,
     "OUTPUT_DIR": "./model_out",
+    "SAVE_BEST_RUN": False,
+    "SAVE_LAST_RUN": False,
 }
 
 BACKBONES = {

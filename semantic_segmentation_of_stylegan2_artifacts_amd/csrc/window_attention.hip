@@ -406,6 +406,8 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
                       int C, int nh, int shift, float p_drop, unsigned long long seed,
                       const unsigned long long* seed_dev, hipStream_t st, hipStream_t pst);
 long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh);
+int msu_attn_mfma_bwd_tail(float* ws, float* dtable, float* dqkv_bias_pad, long nwin, int C, int nh,
+                           hipStream_t st);
 long msu_attn_mfma_fwd_workspace(int C, int nh);
 
 namespace {
@@ -452,6 +454,9 @@ long msu_win_attn_bwd_workspace(int dtype, int B, int H, int W, int C, int nh) {
   return nblk * nh * NT * NT + (long)nh * NT * NT + nblk * 3 * C;
 }
 
+int msu_win_attn_bwd_tail(int dtype, float* workspace, float* dtable, float* dqkv_bias_pad, int B, int H, int W,
+                          int C, int nh, void* stream);
+
 int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                       const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                       float* workspace, int B, int H, int W, int C, int nh, int shift,
@@ -475,13 +480,27 @@ int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const f
   hipLaunchKernelGGL(win_attn_bwd_kernel<float>, dim3(nblk, nh), dim3(64), 0, st,
                      (const float*)qkv, qkv_bias, table, (const float*)dout, (float*)dqkv,
                      dB_part, qb_part, g, scale, p_drop, (uint64_t)seed, seed_dev, nblk);
+  if (pst == (hipStream_t)(intptr_t)-1) return MSU_CHECK_LAUNCH();  // tail issued by the caller
   const int rc = attn_param_stream(st, pst);
   if (rc) return rc;
+  return msu_win_attn_bwd_tail(dtype, workspace, dtable, dqkv_bias_pad, B, H, W, C, nh, pst);
+}
+
+int msu_win_attn_bwd_tail(int dtype, float* workspace, float* dtable, float* dqkv_bias_pad, int B, int H, int W,
+                          int C, int nh, void* stream) {
+  if (C != nh * HD) return -2;
+  const WinGeom g = make_geom(B, H, W, C, nh, 0);
+  hipStream_t st = (hipStream_t)stream;
+  if (g.nwin == 0) return 0;
+  if (msu_is16(dtype)) return msu_attn_mfma_bwd_tail(workspace, dtable, dqkv_bias_pad, g.nwin, C, nh, st);
+  const int nblk = f32_bwd_blocks(g.nwin, nh);
+  float* dB_part = workspace;
+  float* dB = dB_part + (long)nblk * nh * NT * NT;
+  float* qb_part = dB + (long)nh * NT * NT;
   const long nB = (long)nh * NT * NT;
-  colsum(dB_part, nblk, nB, nB, dB, 0, pst);
-  hipLaunchKernelGGL(rel_table_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, pst,
-                     dB, nh, dtable);
-  colsum(qb_part, nblk, 3L * C, 3L * C, dqkv_bias_pad, 0, pst);
+  colsum(dB_part, nblk, nB, nB, dB, 0, st);
+  hipLaunchKernelGGL(rel_table_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, st, dB, nh, dtable);
+  colsum(qb_part, nblk, 3L * C, 3L * C, dqkv_bias_pad, 0, st);
   return MSU_CHECK_LAUNCH();
 }
 

@@ -709,6 +709,8 @@ int bwd_blocks(long nwin, int nh) {
 }  // namespace
 
 // entry points used by window_attention.hip for the 16-bit dtypes
+int msu_attn_mfma_bwd_tail(float* ws, float* dtable, float* dqkv_bias_pad, long nwin, int C, int nh,
+                           hipStream_t st);
 long msu_attn_mfma_fwd_workspace(int C, int nh) { return aux_floats(C, nh); }
 
 long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh) {
@@ -757,11 +759,23 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
     hipLaunchKernelGGL((attn_bwd_mfma<T, BWD_WAVES>), dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
                        (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
                        p_drop, (uint64_t)seed, seed_dev, nblk));
+  if (pst == (hipStream_t)(intptr_t)-1) return MSU_CHECK_LAUNCH();  // tail issued by the caller
   // parameter-gradient reductions: on pst (after the backward kernel) when given
   const int rc = attn_param_stream(st, pst);
   if (rc) return rc;
+  return msu_attn_mfma_bwd_tail(ws, dtable, dqkv_bias_pad, g.nwin, C, nh, pst);
+}
+
+// the parameter-gradient reductions of msu_attn_mfma_bwd from its workspace partials
+int msu_attn_mfma_bwd_tail(float* ws, float* dtable, float* dqkv_bias_pad, long nwin, int C, int nh,
+                           hipStream_t st) {
+  if (nwin == 0) return 0;
+  const long parts = (long)bwd_blocks(nwin, nh) * BWD_WAVES;
+  float* dB_part = ws + aux_floats(C, nh);
+  float* dimg = dB_part + parts * nh * 4096;
+  float* qb_part = dimg + (long)nh * 4096;
   const ColSeg segs[2] = {{dB_part, (long)nh * 4096, (long)nh * 4096, dimg}, {qb_part, 3L * C, 3L * C, dqkv_bias_pad}};
-  colsum_multi(segs, 2, (int)parts, 0, pst);
-  hipLaunchKernelGGL(bias_image_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, pst, dimg, nh, dtable);
+  colsum_multi(segs, 2, (int)parts, 0, st);
+  hipLaunchKernelGGL(bias_image_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, st, dimg, nh, dtable);
   return MSU_CHECK_LAUNCH();
 }

@@ -35,3 +35,20 @@ class MSUNet(nn.Module):
 
     def unfreeze_encoder(self, layer_num):
         self.ms_unet.unfreeze_encoder(layer_num)
+
+    def load_segface_weight(self, config, logging):
+        """``MSUNet.py:61-148``: SegFace backbone -> encoder (checkpoint.remap_segface)."""
+        from .. import checkpoint
+        msg = checkpoint.load_pretrained_file(self.ms_unet, config.MODEL.PRETRAIN_SEGFACE, "segface", logging)
+        if msg is not None:
+            logging.info("End of the Segface pretrained copying process")
+        return msg
+
+    def load_IMAGENET1K_weight(self, config, logging):
+        """``MSUNet.py:150-229``: torchvision swin_b IMAGENET1K -> encoder
+        (checkpoint.remap_imagenet1k)."""
+        from .. import checkpoint
+        msg = checkpoint.load_pretrained_file(self.ms_unet, config.MODEL.PRETRAIN_IMAGENET1K, "imagenet1k", logging)
+        if msg is not None:
+            logging.info("End of MAGENET1K the pretrained copying process")
+        return msg

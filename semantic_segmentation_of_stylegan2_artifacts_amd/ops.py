@@ -510,16 +510,21 @@ def _attn_backward(ctx, dout):
         # parameter-gradient tail on the side stream: the relative-table / qkv-bias
         # reductions and their .grad adds (the qkv bias also receives its Linear's db
         # there, so every write to its .grad is ordered on one stream)
+        # (the fork is a fresh torch event per call: a HIP graph capture of the step turns
+        # every record / wait pair into its own edge)
         main = torch.cuda.current_stream(qkv.device)
         side = _side_stream_for(qkv.device)
+        _lib.call("msu_win_attn_bwd2", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
+                  None, None, _p(ws), B, H, W, C, nh, shift, p_drop, seed, _p(seed_dev),
+                  main.cuda_stream, -1)
+        side.wait_stream(main)
+        ws.record_stream(side)
+        _side_keep.append(ws)
         with torch.cuda.stream(side):
             dtable = torch.empty_like(table)
             dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
-        _lib.call("msu_win_attn_bwd2", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
-                  _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _p(seed_dev),
-                  main.cuda_stream, side.cuda_stream)
-        ws.record_stream(side)
-        with torch.cuda.stream(side):
+            _lib.call("msu_win_attn_bwd_tail", _dt(qkv), _p(ws), _p(dtable), _p(dbias), B, H, W, C, nh,
+                      side.cuda_stream)
             bp.grad.add_(dbias)
             tp.grad.add_(dtable)
         ev = torch.cuda.Event()

@@ -25,6 +25,7 @@ Here:
 """
 import math
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -231,11 +232,19 @@ class Trainer:
         self.inv_world = torch.full((1,), 1.0 / world_size, device=device, dtype=torch.float32)
         self.reducer = (GradBucketer(self.groups, int(bucket_mb * (1 << 20)), process_group)
                         if world_size > 1 else None)
-        # HIP-graph replay of the step (see step()); MSU_GRAPH=0 keeps every step eager
+        # HIP-graph replay of the step (see step()).  use_graph: True / False, or None = the
+        # MSU_GRAPH environment switch: "1" always, "0" never, "auto" (default) = capture only
+        # when the eager step is launch-bound (host issue time >= GRAPH_HOST_FRACTION of the
+        # GPU time, measured on the last warmup step): the replay removes the host from the
+        # critical path, but costs ~1-2 % of GPU time where the host is not on it
         on_gpu = torch.device(device).type == "cuda"
-        self.use_graph = on_gpu and (use_graph if use_graph is not None else os.environ.get("MSU_GRAPH", "1") != "0")
-        if self.use_graph and world_size > 1 and dist.get_backend(process_group) != "nccl":
-            self.use_graph = False  # gloo collectives run on the host: not capturable
+        mode = use_graph if use_graph is not None else os.environ.get("MSU_GRAPH", "auto")
+        mode = {True: "1", False: "0"}.get(mode, str(mode))
+        self.graph_mode = mode if on_gpu else "0"
+        if self.graph_mode != "0" and world_size > 1 and dist.get_backend(process_group) != "nccl":
+            self.graph_mode = "0"  # gloo collectives run on the host: not capturable
+        self.use_graph = self.graph_mode != "0"
+        self._probe = None  # (host seconds, start event, end event) of the auto-mode probe step
         self.graph_warmup = graph_warmup
         self._graph = None
         self._graph_failed = False
@@ -255,6 +264,64 @@ class Trainer:
     def optimizer_steps(self):
         """AdamW steps actually applied (skipped non-finite steps excluded); syncs."""
         return int(self.hyper[1].item())
+
+    def _reference_param_order(self):
+        """The parameter list of the reference optimizer (trainer.py:130-152): every trainable
+        parameter in named_parameters() order, the decay group first -- dead-branch
+        parameters included (they are in the reference's groups, they just never get grads)."""
+        decay, no_decay = [], []
+        for name, p in self.model.named_parameters():
+            if p.requires_grad:
+                (no_decay if is_no_decay(name, p) else decay).append(p)
+        return decay, no_decay
+
+    def optimizer_state_dict(self):
+        """This trainer's AdamW state in ``torch.optim.AdamW.state_dict()`` format, parameter
+        indices in the reference's group order (what trainer.py:408 saves)."""
+        decay, no_decay = self._reference_param_order()
+        where = {}
+        for g in self.groups:
+            for p, off in zip(g.params, g.offsets):
+                where[id(p)] = (g, off)
+        step = torch.tensor(float(self.optimizer_steps()))
+        state = {}
+        for i, p in enumerate(decay + no_decay):
+            if id(p) not in where:
+                continue
+            g, off = where[id(p)]
+            n = p.numel()
+            state[i] = {"step": step.clone(),
+                        "exp_avg": g.exp_avg[off:off + n].view_as(p).detach().cpu().clone(),
+                        "exp_avg_sq": g.exp_avg_sq[off:off + n].view_as(p).detach().cpu().clone()}
+        common = {"lr": self.lr, "betas": self.betas, "eps": self.eps, "amsgrad": False, "foreach": None,
+                  "maximize": False, "capturable": False, "differentiable": False, "fused": None}
+        groups = [dict(common, weight_decay=self.groups[0].weight_decay, params=list(range(len(decay)))),
+                  dict(common, weight_decay=0.0, params=list(range(len(decay), len(decay) + len(no_decay))))]
+        return {"state": state, "param_groups": groups}
+
+    def load_optimizer_state_dict(self, sd):
+        """Inverse of optimizer_state_dict (e.g. from a reference ``epoch_<n>.pth``)."""
+        decay, no_decay = self._reference_param_order()
+        where = {}
+        for g in self.groups:
+            for p, off in zip(g.params, g.offsets):
+                where[id(p)] = (g, off)
+        steps = set()
+        with torch.no_grad():
+            for i, p in enumerate(decay + no_decay):
+                st = sd["state"].get(i, sd["state"].get(str(i)))
+                if st is None or id(p) not in where:
+                    continue
+                g, off = where[id(p)]
+                n = p.numel()
+                g.exp_avg[off:off + n].copy_(st["exp_avg"].reshape(-1))
+                g.exp_avg_sq[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.add(float(st["step"]))
+        if len(steps) > 1:
+            raise ValueError(f"per-parameter AdamW steps differ: {sorted(steps)}")
+        if steps:
+            self.hyper[1:2].fill_(steps.pop())
+        self.lr = sd["param_groups"][0]["lr"]
 
     def num_params(self):
         return sum(g.count for g in self.groups)
@@ -281,6 +348,8 @@ class Trainer:
         (device-side seed counter, drop-path pools redrawn inside the graph)."""
         if not self.model.training:  # Module.train() walks all ~400 modules: ~1 ms of host time
             self.model.train()
+        if self.graph_mode == "auto" and self.step_count >= self.graph_warmup and self._graph is None:
+            self._decide_graph()
         if self.use_graph and self.step_count >= self.graph_warmup:
             if self._graph is not None and self.loss_fn is not self._graph_loss_fn:
                 self.invalidate_graph()  # the captured step holds the old loss module
@@ -330,12 +399,35 @@ class Trainer:
                     g.refresh_shadow()
         return loss.detach()
 
+    GRAPH_HOST_FRACTION = 0.9
+
+    def _decide_graph(self):
+        """auto mode: graph replay iff the probed eager step was launch-bound."""
+        if self._probe is None:
+            self.use_graph = False
+            return
+        host_s, e0, e1 = self._probe
+        e1.synchronize()
+        gpu_s = e0.elapsed_time(e1) * 1e-3
+        self.graph_probe = {"host_ms": round(host_s * 1e3, 3), "gpu_ms": round(gpu_s * 1e3, 3)}
+        self.use_graph = host_s >= self.GRAPH_HOST_FRACTION * gpu_s
+        self.graph_mode = "1" if self.use_graph else "0"
+
     def _eager_step(self, images, labels):
         if self.amp_dtype == torch.bfloat16 and not self._shadow_fresh:
             for g in self.groups:
                 g.refresh_shadow()
         self._shadow_fresh = False
+        probe = self.graph_mode == "auto" and self.step_count == self.graph_warmup - 1
+        if probe:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            t0 = time.perf_counter()
         loss = self._device_step(images, labels)
+        if probe:
+            host = time.perf_counter() - t0
+            e1.record()
+            self._probe = (host, e0, e1)
         self.step_count += 1
         # the next step's refresh is skipped; a write through a parameter in between bumps its
         # version and the Linear ops cast that weight themselves (ops._shadow)

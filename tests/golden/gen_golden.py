@@ -195,11 +195,35 @@ def gen_state_dict_contract():
     print("state dict contract:", len(sd), "entries; structure dump:", len(dump))
 
 
+def gen_pretrained_layouts():
+    """Key / shape lists of the two pretrained checkpoints the reference remaps
+    (network/pretrained_weights/structure_of_SegFace.txt, IMAGENET1K_structure.txt): data
+    files of the reference, kept as JSON fixtures for the key-remap tests."""
+    out = {}
+    for name, fname in (("segface", "structure_of_SegFace.txt"), ("imagenet1k", "IMAGENET1K_structure.txt")):
+        rows = []
+        with open(os.path.join(REF, "network/pretrained_weights", fname)) as f:
+            for line in f:
+                line = line.strip()
+                if not line:
+                    continue
+                _, rest = line.split(":", 1)
+                key, shape = rest.split("torch.Size(")
+                rows.append([key.strip(), json.loads(shape.split(")")[0])])
+        out[name] = rows
+    with open(os.path.join(HERE, "pretrained_layouts.json"), "w") as f:
+        json.dump(out, f)
+    print("pretrained layouts:", {k: len(v) for k, v in out.items()})
+
+
 if __name__ == "__main__":
     sys.path.insert(0, REF)
     install_shims()
     torch.set_num_threads(8)
     only = sys.argv[1:]  # model case names: regenerate just those fixtures
+    if only == ["layouts"]:
+        gen_pretrained_layouts()
+        sys.exit(0)
     if only:
         gen_msunet(only)
         sys.exit(0)
