@@ -534,7 +534,7 @@ class MSUNetSys(nn.Module):
         nothing reads its output, so it overlaps the rest of the forward pass."""
         if self.skip_dead_branches:
             return
-        if not x.is_cuda:
+        if not x.is_cuda or not ops._side_enabled:
             with torch.no_grad():
                 mod(x)
             return

@@ -446,16 +446,27 @@ class Trainer:
         self._sy = labels.detach().clone()
         torch.cuda.synchronize(self.device)
         graph = torch.cuda.CUDAGraph()
+        # The captured step is single-stream: with the weight-gradient / dead-branch side
+        # stream forked into the capture, the ROCm 7.2 graph executor's parallel branches gave
+        # run-to-run different gradients (tests/test_gpu_graph.py, tools/determinism_check.py;
+        # deterministic again with DEBUG_HIP_FORCE_GRAPH_QUEUES=1).  Replay is only chosen
+        # when the step is launch-bound, where the side-stream overlap matters least.
+        # MSU_GRAPH_SIDE=1 keeps the side stream (A/B switch).
+        side_prev = ops._side_enabled
+        if os.environ.get("MSU_GRAPH_SIDE", "0") != "1":
+            ops._side_enabled = False
         try:
             with torch.cuda.graph(graph):
                 loss = self._device_step(self._sx, self._sy)
         except Exception as e:  # noqa: BLE001 -- any capture failure: stay eager, loudly
+            ops._side_enabled = side_prev
             import warnings
             warnings.warn(f"HIP graph capture of the training step failed ({e!r}); continuing eagerly")
             self._graph_failed = True
             self._sx = self._sy = None
             torch.cuda.synchronize(self.device)
             return
+        ops._side_enabled = side_prev
         self._graph = graph
         self._graph_loss_fn = self.loss_fn
         self._sloss = loss
