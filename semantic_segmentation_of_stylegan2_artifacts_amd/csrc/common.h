@@ -174,14 +174,23 @@ MSU_DEV uint64_t launch_seed(uint64_t seed, const unsigned long long* seed_dev) 
   return z ^ (z >> 29);
 }
 
-// Cheap 32-bit counter hash (murmur3 fmix32 of idx*golden + seed): uniform in [0, 1).
-// Used for dropout masks that forward and backward regenerate identically.
-MSU_DEV float hash_uniform32(uint32_t seed, uint32_t idx) {
+// Dropout masks of window attention, regenerated identically by forward and backward: one
+// murmur3 fmix32 hash per key pair (j, j+1), j even, of a query row i of item (window, head);
+// its two 16-bit halves are compared with ceil(p 2^16), so the keep probability is
+// 1 - ceil(p 2^16) / 2^16 (within 2^-16 of 1 - p).  Two decisions per hash: the mask costs half
+// the multiplies of a hash per element.
+MSU_DEV uint32_t fmix32_hash(uint32_t seed, uint32_t idx) {
   uint32_t x = idx * 0x9E3779B9u + seed;
   x ^= x >> 16; x *= 0x85EBCA6Bu;
   x ^= x >> 13; x *= 0xC2B2AE35u;
-  x ^= x >> 16;
-  return (float)(x >> 8) * (1.0f / 16777216.0f);
+  return x ^ (x >> 16);
+}
+MSU_DEV uint32_t drop_thresh16(float p) { return (uint32_t)ceilf(p * 65536.0f); }
+MSU_DEV uint32_t drop_seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32); }
+// keep bits of keys j0 (bit 0) and j0 + 1 (bit 1) for query i; item = window * nh + head
+MSU_DEV uint32_t drop_pair(uint32_t seed, uint32_t item, int i, int j0, uint32_t thr) {
+  const uint32_t x = fmix32_hash(seed, (item * 64u + (uint32_t)i) * 32u + ((uint32_t)j0 >> 1));
+  return (uint32_t)((x & 0xFFFFu) >= thr) | ((uint32_t)((x >> 16) >= thr) << 1);
 }
 
 // XCD-aware bijective block remap: blocks b and b+8 share an XCD under round-robin

@@ -166,10 +166,10 @@ MSU_DEV void softmax_block(f32x4 (&S)[4]) {
   }
 }
 
+// the 16-bit kernels' mask (common.h drop_pair), one element at a time
 MSU_DEV float drop_keep(uint64_t seed, long win, int h, int nh, int i, int j, float p) {
-  const uint64_t idx = ((((uint64_t)win * nh + h) * 64 + i) * 64 + j);
-  const uint32_t s = (uint32_t)seed ^ (uint32_t)(seed >> 32);
-  return hash_uniform32(s, (uint32_t)idx) >= p ? 1.0f / (1.0f - p) : 0.0f;
+  const uint32_t bits = drop_pair(drop_seed32(seed), (uint32_t)(win * nh + h), i, j & ~1, drop_thresh16(p));
+  return (bits >> (j & 1)) & 1u ? 1.0f / (1.0f - p) : 0.0f;
 }
 
 template <typename T>

@@ -17,18 +17,15 @@
 // All global loads of an item are issued together before first use (the HBM latency is
 // paid once per item, not once per row).
 // Backward recomputes S^T / P^T, forms dP^T = V dO^T, dS^T = P^T (dP^T - delta), stores
-// Pd and dS once as [i][j] LDS images (8-byte stores) and runs dV = Pd^T dO,
-// dQ = dS K, dK = dS^T Q with tr-read operands; relative-bias gradients accumulate in
-// registers in the bias-image layout; padded tokens' dq/dk/dv go to the qkv-bias partial.
+// Pd and dS once as [i][j] LDS images (8-byte stores) and runs dV^T = dO^T Pd,
+// dQ^T = K^T dS^T, dK^T = Q^T dS with tr-read operands, the token index on the accumulator
+// columns so that every lane stores whole 16-B pieces of its token's rows; relative-bias
+// gradients accumulate in registers in the bias-image layout; padded tokens' dq/dk/dv go
+// to the qkv-bias partial.
 #include <utility>
 
 #include "common.h"
 #include "reduce.h"
-
-// MSU_EXP: ablation bits for timing experiments only (tools/build_exp.sh); 0 in every real build
-#ifndef MSU_EXP
-#define MSU_EXP 0
-#endif
 
 namespace {
 
@@ -164,10 +161,15 @@ MSU_DEV void stage_rows(const int* sTok, const bf16_t* const (&base)[NS], const 
   }
 }
 
-MSU_DEV float drop_keep(uint64_t seed, long win, int h, int nh, int i, int j, float p) {
-  const uint32_t idx = ((((uint32_t)win * nh + h) * 64 + i) * 64 + j);
-  const uint32_t s = (uint32_t)seed ^ (uint32_t)(seed >> 32);
-  return hash_uniform32(s, idx) >= p ? 1.0f / (1.0f - p) : 0.0f;
+// keep bits of the lane's 32 keys of query column tile it: bit jt*16 + r <-> key
+// jt*32 + crow(r, hh) (registers 2k, 2k+1 are keys j0, j0+1 of one hash)
+MSU_DEV uint32_t drop_bits(uint32_t seed, uint32_t item, int i, int hh, uint32_t thr) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m |= drop_pair(seed, item, i, jt * 32 + crow(2 * k, hh), thr) << (jt * 16 + 2 * k);
+  return m;
 }
 
 MSU_DEV void lds_sync() {
@@ -272,7 +274,7 @@ struct FwdLds {
 // win + stride, ...; the HBM loads of window i+1 (token table, K / Q fragments, V rows) are
 // issued before window i is computed, so their latency hides under window i's MFMAs and
 // softmax instead of being paid per item.
-template <typename T, int WAVES>
+template <typename T, int WAVES, bool DROP>
 __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __restrict__ qkv, Aux aux,
                                                                bf16_t* __restrict__ out, Geom g, float scale,
                                                                float p_drop, uint64_t seed0,
@@ -348,14 +350,19 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
       }
     f32x16 P[2][2];
     probs_T<T, true>(P, ka, qb, reinterpret_cast<const float*>(sBimg), L.reg[buf], bnd[buf], scale, lane);
-    if (p_drop > 0.f) {
+    if constexpr (DROP) {
+      const float kscale = 1.0f / (1.0f - p_drop);
+      const uint32_t thr = drop_thresh16(p_drop), ds = drop_seed32(seed), item = (uint32_t)win * g.nh + h;
 #pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
+      for (int it = 0; it < 2; ++it)
 #pragma unroll
-        for (int it = 0; it < 2; ++it)
+        for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            P[jt][it][r] *= drop_keep(seed, win, h, g.nh, it * 32 + (lane & 31), jt * 32 + crow(r, hh), p_drop);
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t b = drop_pair(ds, item, it * 32 + (lane & 31), jt * 32 + crow(2 * k, hh), thr);
+            P[jt][it][2 * k] = b & 1u ? P[jt][it][2 * k] * kscale : 0.f;
+            P[jt][it][2 * k + 1] = b & 2u ? P[jt][it][2 * k + 1] * kscale : 0.f;
+          }
     }
     // O^T[d][i] = sum_j V[j][d] P^T[j][i]
     f32x16 O[2];
@@ -413,7 +420,38 @@ struct BwdLds {
   int tok[2][64], reg[2][64];          // current / prefetched window
 };
 
-template <typename T, int WAVES>
+// Store one 32-d head slice of a lane-major accumulator (lane = token, registers 4q..4q+3 =
+// d 8q + 4hh .. +3) as two 16-B stores per lane: a permlane32 swap pairs each half's 4-d
+// groups into 8 consecutive d (half 0 ends with d 16p..16p+7, half 1 with 16p+8..+15).
+// Every lane must execute it (the swap reads the partner half); `row` is used when ok.
+template <typename T>
+MSU_DEV void store_slice(bf16_t* row, const f32x16& a, float s, int hh, bool ok) {
+  uint32_t w[8];
+#pragma unroll
+  for (int g = 0; g < 8; ++g) w[g] = pack2<T>(a[2 * g] * s, a[2 * g + 1] * s);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const auto s0 = __builtin_amdgcn_permlane32_swap(w[4 * p], w[4 * p + 2], false, false);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(w[4 * p + 1], w[4 * p + 3], false, false);
+    const u32x4 v = {s0[0], s1[0], s0[1], s1[1]};
+    if (ok) *reinterpret_cast<u32x4*>(row + 16 * p + 8 * hh) = v;
+  }
+}
+
+// Padded tokens' rows of a lane-major accumulator, summed over the tile's lanes into
+// acc (lane d = lane&31 of half hh holds d's sum when bit 2 of d is hh; the other half 0).
+MSU_DEV void pad_accumulate(float& acc, const f32x16& a, float s, bool pad, int lane) {
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v = pad ? a[r] * s : 0.f;
+#pragma unroll
+    for (int m = 1; m < 32; m <<= 1) v += __shfl_xor(v, m, 64);
+    if ((lane & 31) == crow(r, hh)) acc += v;
+  }
+}
+
+template <typename T, int WAVES, bool DROP>
 __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
     const bf16_t* __restrict__ qkv, Aux aux, const bf16_t* __restrict__ dout, bf16_t* __restrict__ dqkv,
     float* __restrict__ dB_part, float* __restrict__ qb_part, Geom g, float scale, float p_drop,
@@ -470,63 +508,96 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
     }, std::make_integer_sequence<int, 4>{});
     const long nxt = win + stride;
     const bool more = nxt < g.nwin;
-    if (more && !(MSU_EXP & 32)) prep(nxt, std::integral_constant<int, buf ^ 1>{});
+    if (more) prep(nxt, std::integral_constant<int, buf ^ 1>{});
     const bool boundary = bnd[buf];
     const int* sTok = L.tok[buf];
     const int* sReg = L.reg[buf];
+    // dropout keep bits of the lane's (i, j) pairs, bit jt*16+r of kmasks[it], drawn before
+    // the score tiles are live
+    const float kscale = 1.0f / (1.0f - p_drop);  // the forward's kept-value factor
+    uint32_t kmasks[2] = {~0u, ~0u};
+    if constexpr (DROP) {
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+        kmasks[it] = drop_bits(drop_seed32(seed), (uint32_t)win * g.nh + h, it * 32 + (lane & 31), hh,
+                               drop_thresh16(p_drop));
+    }
     lds_sync();
-    bf16x8 va[2][2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) va[t][ks] = frag_rows(L.v, LD, 32 * t, 16 * ks, lane);
-    bf16x8 ka[2][2], qb[2][2];
+    bf16x8 va[2][2], ka[2][2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
+        va[t][ks] = frag_rows(L.v, LD, 32 * t, 16 * ks, lane);
         ka[t][ks] = frag_rows(L.k, LD, 32 * t, 16 * ks, lane);
-        qb[t][ks] = frag_rows(L.q, LD, 32 * t, 16 * ks, lane);
       }
-    f32x16 P[2][2];
-    bias_init(P, bimg, lane);
-    if constexpr (MSU_EXP & 2) {
-      for (int a = 0; a < 2; ++a)
-        for (int b = 0; b < 2; ++b) P[a][b][0] += (float)ka[a][b][0] * (float)qb[b][a][1];
-    } else {
-      probs_T_from<T>(P, ka, qb, sReg, boundary, scale, lane);
-    }
-    // dPd^T[j][i] = sum_d V[j][d] dO[i][d]
-    f32x16 D[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) D[a][b] = f32x16{0};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 b[2];
-#pragma unroll
-      for (int it = 0; it < 2; ++it) b[it] = frag_rows(L.dO, LD, it * 32, 16 * ks, lane);
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
-          if constexpr (MSU_EXP & 4) D[jt][it][ks] += (float)va[jt][ks][0] * (float)b[it][1];
-          else D[jt][it] = mfma32<T>(va[jt][ks], b[it], D[jt][it]);
-        }
-    }
+    // one query column tile (it) at a time: P^T / dP^T of 32 queries x 64 keys live at once
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int i = it * 32 + (lane & 31);
-      float keep[2][16];
+      f32x16 P[2], D[2];
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        const float4* bp = reinterpret_cast<const float4*>(bimg + ((jt * 2 + it) * 64 + lane) * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = bp[q];
+          P[jt][4 * q] = v.x; P[jt][4 * q + 1] = v.y; P[jt][4 * q + 2] = v.z; P[jt][4 * q + 3] = v.w;
+        }
+        D[jt] = f32x16{0};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 qf = frag_rows(L.q, LD, 32 * it, 16 * ks, lane);
+        const bf16x8 df = frag_rows(L.dO, LD, 32 * it, 16 * ks, lane);
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+          P[jt] = mfma32<T>(ka[jt][ks], qf, P[jt]);   // S^T = K Q^T (+ bias)
+          D[jt] = mfma32<T>(va[jt][ks], df, D[jt]);   // dPd^T = V dO^T
+        }
+      }
+      if (boundary) {
+        const float mval = -100.0f / scale;
+        const int ri = sReg[i];
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (sReg[jt * 32 + crow(r, hh)] != ri) P[jt][r] += mval;
+      }
+      {  // softmax over j (the accumulator rows of this lane's column + the other half)
+        float m = -INFINITY;
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) m = fmaxf(m, P[jt][r]);
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        const float c = scale * 1.44269504088896341f;
+        const float mc = m * c;
+        float sum = 0.f;
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            P[jt][r] = __builtin_amdgcn_exp2f(fmaf(P[jt][r], c, -mc));
+            sum += P[jt][r];
+          }
+        sum += __shfl_xor(sum, 32, 64);
+        const float inv = 1.0f / sum;
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) P[jt][r] *= inv;
+      }
+      const uint32_t kmask = kmasks[it];
       float delta = 0.f;
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          keep[jt][r] = p_drop > 0.f ? drop_keep(seed, win, h, g.nh, i, jt * 32 + crow(r, hh), p_drop) : 1.f;
-          D[jt][it][r] *= keep[jt][r];  // dP = dPd * keep/(1-p)
-          delta += P[jt][it][r] * D[jt][it][r];
+          if constexpr (DROP)  // dP = dPd * keep/(1-p)
+            D[jt][r] = (kmask >> (jt * 16 + r)) & 1u ? D[jt][r] * kscale : 0.f;
+          delta += P[jt][r] * D[jt][r];
         }
       delta += __shfl_xor(delta, 32, 64);
       // Pd and dS images [i][j], 4 consecutive j per 8-byte store
@@ -538,9 +609,9 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * gq + e;
-            const float p = P[jt][it][r];
-            ds[e] = p * (D[jt][it][r] - delta);
-            pd[e] = p * keep[jt][r];
+            const float p = P[jt][r];
+            ds[e] = p * (D[jt][r] - delta);
+            pd[e] = DROP ? ((kmask >> (jt * 16 + r)) & 1u ? p * kscale : 0.f) : p;
             dB[jt][it][r] += ds[e];
           }
           const int j0 = jt * 32 + 8 * gq + 4 * hh;
@@ -549,15 +620,14 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
           wp.y = pack2<T>(pd[2], pd[3]);
           wd.x = pack2<T>(ds[0], ds[1]);
           wd.y = pack2<T>(ds[2], ds[3]);
-          if (!(MSU_EXP & 16) || pd[0] == 1.2345e-30f) {
-            *reinterpret_cast<uint2*>(L.P + i * LDP + j0) = wp;
-            *reinterpret_cast<uint2*>(L.dS + i * LDP + j0) = wd;
-          }
+          *reinterpret_cast<uint2*>(L.P + i * LDP + j0) = wp;
+          *reinterpret_cast<uint2*>(L.dS + i * LDP + j0) = wd;
         }
     }
     lds_sync();
-    // dV[j][d] = sum_i Pd[i][j] dO[i][d]; dK[j][d] = scale sum_i dS[i][j] Q[i][d];
-    // dQ[i][d] = scale sum_j dS[i][j] K[j][d]   (scores = scale * q k^T)
+    // dV^T[d][j] = sum_i dO[i][d] Pd[i][j]; dK^T[d][j] = scale sum_i Q[i][d] dS[i][j];
+    // dQ^T[d][i] = scale sum_j K[j][d] dS[i][j]   (scores = scale * q k^T).  The token index
+    // is the accumulator column (lane), so each lane writes whole 16-B pieces of one row.
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       f32x16 av = f32x16{0}, ak = f32x16{0}, aq = f32x16{0};
@@ -566,29 +636,20 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
         const bf16x8 bdo = frag_tr_q4(L.dO, LD, ks, 0, lane);
         const bf16x8 bq = frag_tr_q4(L.q, LD, ks, 0, lane);
         const bf16x8 bk = frag_tr(L.k, LD, ks, 0, lane);
-        if constexpr (MSU_EXP & 8) {
-          av[ks / 16] += (float)bdo[0] * (float)bq[1] * (float)bk[2];
-        } else {
-          av = mfma32<T>(frag_tr_q4(L.P, LDP, ks, mt * 32, lane), bdo, av);
-          ak = mfma32<T>(frag_tr_q4(L.dS, LDP, ks, mt * 32, lane), bq, ak);
-          aq = mfma32<T>(frag_rows(L.dS, LDP, mt * 32, ks, lane), bk, aq);
-        }
+        av = mfma32<T>(bdo, frag_tr_q4(L.P, LDP, ks, mt * 32, lane), av);
+        ak = mfma32<T>(bq, frag_tr_q4(L.dS, LDP, ks, mt * 32, lane), ak);
+        aq = mfma32<T>(bk, frag_rows(L.dS, LDP, mt * 32, ks, lane), aq);
       }
-      const int d = lane & 31;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int t = mt * 32 + crow(r, hh);
-        const int tok = sTok[t];
-        if (tok >= 0 && (!(MSU_EXP & 1) || aq[r] == 1.2345e-30f)) {
-          bf16_t* row = dqkv + (long)tok * C3 + h * HD + d;
-          row[0] = (bf16_t)Fmt16<T>::bits(aq[r] * scale);
-          row[g.C] = (bf16_t)Fmt16<T>::bits(ak[r] * scale);
-          row[2 * g.C] = (bf16_t)Fmt16<T>::bits(av[r]);
-        } else if (tok == TOK_PAD) {
-          padacc[0] += aq[r] * scale;
-          padacc[1] += ak[r] * scale;
-          padacc[2] += av[r];
-        }
+      const int tok = sTok[mt * 32 + (lane & 31)];
+      bf16_t* row = dqkv + (size_t)((unsigned)(tok >= 0 ? tok : 0) * (unsigned)C3) + h * HD;
+      store_slice<T>(row, aq, scale, hh, tok >= 0);
+      store_slice<T>(row + g.C, ak, scale, hh, tok >= 0);
+      store_slice<T>(row + 2 * g.C, av, 1.0f, hh, tok >= 0);
+      const bool pad = tok == TOK_PAD;
+      if (__ballot(pad) != 0) {  // wave-uniform: only windows over the padded border
+        pad_accumulate(padacc[0], aq, scale, pad, lane);
+        pad_accumulate(padacc[1], ak, scale, pad, lane);
+        pad_accumulate(padacc[2], av, 1.0f, pad, lane);
       }
     }
     lds_sync();  // this window's LDS reads are done before the next window's rows land
@@ -734,8 +795,12 @@ int msu_attn_mfma_fwd(int dtype, const void* qkv, const float* qkv_bias, const f
   MSU_DISPATCH16(dtype, T,
     hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
                        1.0f / scale, img, brow, zrow);
-    hipLaunchKernelGGL((attn_fwd_mfma<T, FWD_WAVES>), dim3((unsigned)nb, (unsigned)nh), dim3(64 * FWD_WAVES), 0, st,
-                       (const bf16_t*)qkv, aux, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev));
+    if (p_drop > 0.f)
+      hipLaunchKernelGGL((attn_fwd_mfma<T, FWD_WAVES, true>), dim3((unsigned)nb, (unsigned)nh), dim3(64 * FWD_WAVES),
+                         0, st, (const bf16_t*)qkv, aux, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev);
+    else
+      hipLaunchKernelGGL((attn_fwd_mfma<T, FWD_WAVES, false>), dim3((unsigned)nb, (unsigned)nh), dim3(64 * FWD_WAVES),
+                         0, st, (const bf16_t*)qkv, aux, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev));
   return MSU_CHECK_LAUNCH();
 }
 
@@ -756,9 +821,14 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
   MSU_DISPATCH16(dtype, T,
     hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
                        1.0f / scale, img, brow, zrow);
-    hipLaunchKernelGGL((attn_bwd_mfma<T, BWD_WAVES>), dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
-                       (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
-                       p_drop, (uint64_t)seed, seed_dev, nblk));
+    if (p_drop > 0.f)
+      hipLaunchKernelGGL((attn_bwd_mfma<T, BWD_WAVES, true>), dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
+                         (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
+                         p_drop, (uint64_t)seed, seed_dev, nblk);
+    else
+      hipLaunchKernelGGL((attn_bwd_mfma<T, BWD_WAVES, false>), dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
+                         (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
+                         p_drop, (uint64_t)seed, seed_dev, nblk));
   if (pst == (hipStream_t)(intptr_t)-1) return MSU_CHECK_LAUNCH();  // tail issued by the caller
   // parameter-gradient reductions: on pst (after the backward kernel) when given
   const int rc = attn_param_stream(st, pst);

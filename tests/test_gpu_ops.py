@@ -527,13 +527,10 @@ def test_window_attention_bf16_dropout_consistency():
     lhs = terms.sum().item()
     rhs = (q.grad[..., 2 * C:].float() * q[..., 2 * C:].float()).sum().item()
     assert abs(lhs - rhs) <= 4e-3 * terms.abs().sum().item(), (lhs, rhs)
-    # a wrong mask (another seed) breaks the identity by far more than that noise
-    q2 = qkv.clone().requires_grad_(True)
+    # the masks are live: another seed gives another output, by O(1)
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        y2 = ops.window_attention(q2, qb, table, nh, 3, 0.5, 4321)
-    y2.backward(dy)
-    rhs_wrong = (q2.grad[..., 2 * C:].float() * q2[..., 2 * C:].float()).sum().item()
-    assert abs(lhs - rhs_wrong) > 4e-3 * terms.abs().sum().item()
+        y2 = ops.window_attention(qkv, qb, table, nh, 3, 0.5, 4321)
+    assert ((y2.float() - y.float()).norm() / y.float().norm()).item() > 0.3
 
 
 @pytest.mark.parametrize("dtype", ALL)
