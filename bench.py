@@ -92,45 +92,71 @@ def conv_roofline(device, batch, img, C):
             "flops_per_launch": flops, "ms_per_launch": round(ms, 4)}
 
 
-def attention_roofline(device, batch, img, C, heads):
+def attention_roofline(device, batch, img, C, heads, p_drop):
     """Window attention (the north star's second named kernel): the stage-0 shifted block's
-    msu_win_attn_fwd launch at the bench shape, timed with HIP events on the launching
-    (current) stream.  Algorithmic work per window x head: 4*49*49*32 FLOP (QK^T and PV) and
-    q, k, v in + o out; the padded grid (ceil(H/7)^2 windows per image) is what the kernel
-    computes.  The timed call includes the tiny aux kernel (bias image, scaled qkv bias) that
-    precedes every attention launch.  HBM-bound (AI ~ 25 FLOP/B); both fractions are reported."""
+    msu_win_attn_fwd and msu_win_attn_bwd launches at the bench shape with the training
+    attention dropout, each timed with HIP events on the launching (current) stream.
+    Algorithmic work per window x head: forward 4*49*49*32 FLOP (QK^T, PV), backward 2.5x that
+    (QK^T and dO V^T recomputed, dV, dK, dQ); bytes: forward q, k, v in + o out, backward
+    q, k, v, dO in + dq, dk, dv out (the forward's dropout keep bits, 128 B per window x head
+    each way, are not counted).  The padded grid (ceil(H/7)^2 windows per image) is what the
+    kernels compute.  Each timed call includes the tiny aux kernel (bias image, 16-bit qkv
+    bias) that precedes every attention launch; the backward's parameter-gradient tail
+    (reductions over workgroup partials) is included.  HBM-bound (AI ~ 25 FLOP/B)."""
     from semantic_segmentation_of_stylegan2_artifacts_amd import ops
     res = img // 4
     g = torch.Generator(device="cpu").manual_seed(2)
     qkv = torch.randn(batch, res, res, 3 * C, generator=g).to(device, torch.bfloat16)
     qb = torch.zeros(3 * C, device=device)
     tb = (0.02 * torch.randn(169, heads, generator=g)).to(device)
+    dout = torch.randn(batch, res, res, C, generator=g).to(device, torch.bfloat16)
     s = torch.cuda.current_stream(device)
 
-    def launch():
+    def fwd():
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-            ops.window_attention(qkv, qb, tb, heads, 3, 0.0, 1)
+            return ops.window_attention(qkv, qb, tb, heads, 3, p_drop, 1)
 
-    for _ in range(3):
-        launch()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    def graph_for_bwd():
+        x = qkv.detach().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            return ops.window_attention(x, qb, tb, heads, 3, p_drop, 1)
+
+    def timed(run, args):
+        # back-to-back launches between two events: the GPU never waits on the host
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for a in args:
+            run(a)
+        e1.record(s)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / len(args)
+
     n = 10
-    e0.record(s)
-    for _ in range(n):
-        launch()
-    e1.record(s)
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / n
+    timed(lambda _: fwd(), range(3))
+    ms_f = timed(lambda _: fwd(), range(n))
+    timed(lambda y: y.backward(dout), [graph_for_bwd() for _ in range(3)])
+    ms_b = timed(lambda y: y.backward(dout), [graph_for_bwd() for _ in range(n)])
     nwin = batch * ((res + 6) // 7) ** 2
     flops = 4.0 * 49 * 49 * 32 * nwin * heads
-    byts = batch * res * res * 4 * C * 2
-    return {"kernel": "attn_fwd_mfma (stage-0 shifted window attention fwd, bf16 MFMA)", "bound": "hbm",
-            "achieved": round(byts / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "mfma_tflops": round(flops / (ms * 1e-3) / 1e12, 1),
-            "mfma_frac": round(flops / (ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
-            "bytes_per_launch": byts, "flops_per_launch": flops, "ms_per_launch": round(ms, 4)}
+    tok = batch * res * res
+    byts, byts_b = tok * 4 * C * 2, tok * 7 * C * 2
+
+    def rate(b, ms):
+        return b / (ms * 1e-3) / 1e9
+
+    return {"kernel": "attn_fwd_mfma (stage-0 shifted window attention fwd, bf16 MFMA, dropout %g)" % p_drop,
+            "bound": "hbm", "achieved": round(rate(byts, ms_f), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(rate(byts, ms_f) / HBM_PEAK_GBS, 4),
+            "mfma_tflops": round(flops / (ms_f * 1e-3) / 1e12, 1),
+            "mfma_frac": round(flops / (ms_f * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+            "bytes_per_launch": byts, "flops_per_launch": flops, "ms_per_launch": round(ms_f, 4),
+            "backward": {"kernel": "attn_bwd_mfma (+ aux, partial reductions)", "bound": "hbm",
+                         "achieved": round(rate(byts_b, ms_b), 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(rate(byts_b, ms_b) / HBM_PEAK_GBS, 4),
+                         "mfma_tflops": round(2.5 * flops / (ms_b * 1e-3) / 1e12, 1),
+                         "bytes_per_launch": byts_b, "flops_per_launch": 2.5 * flops,
+                         "ms_per_launch": round(ms_b, 4)}}
 
 
 def _cpu_model():
@@ -372,7 +398,7 @@ def main():
         if not args.no_roofline:
             res["roofline"] = conv_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM)
             res["roofline_attention"] = attention_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM,
-                                                           cfg.MODEL.SWIN.NUM_HEADS[0])
+                                                           cfg.MODEL.SWIN.NUM_HEADS[0], cfg.MODEL.ATTN_DROP_RATE)
             res["roofline_decoder"] = decoder_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline()

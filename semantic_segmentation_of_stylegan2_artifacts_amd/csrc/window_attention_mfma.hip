@@ -125,42 +125,6 @@ MSU_DEV bool window_tokens(const Geom& g, long win_l, int* sTok, int* sReg, int 
   return (g.sh + g.sw) > 0 && (wy == g.nWy - 1 || wx == g.nWx - 1);
 }
 
-MSU_DEV const bf16_t* row_ptr(int tok, const bf16_t* base, long stride, const bf16_t* padrow,
-                              const bf16_t* zrow) {
-  return tok >= 0 ? base + (long)tok * stride : (tok == TOK_PAD ? padrow : zrow);
-}
-
-// fragment straight from HBM: lane l -> window row row0 + (l&31), k = k0 + 8(l>>5) .. +7
-MSU_DEV bf16x8 frag_global(const int* sTok, int row0, const bf16_t* base, long stride,
-                           const bf16_t* padrow, const bf16_t* zrow, int k0, int lane) {
-  const bf16_t* p = row_ptr(sTok[row0 + (lane & 31)], base, stride, padrow, zrow);
-  return *reinterpret_cast<const bf16x8*>(p + k0 + 8 * (lane >> 5));
-}
-
-// Stage NS head slices (rows t = 0..63, 32 bf16 each) into LDS; all 4*NS loads issued first.
-template <int NS>
-MSU_DEV void stage_rows(const int* sTok, const bf16_t* const (&base)[NS], const long (&stride)[NS],
-                        const bf16_t* const (&padrow)[NS], const bf16_t* zrow,
-                        bf16_t* const (&dst)[NS], int lane) {
-  uint4 raw[NS][4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int idx = lane + 64 * c;
-    const int t = idx >> 2, q = idx & 3;
-    const int tok = sTok[t];
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      raw[s][c] = *reinterpret_cast<const uint4*>(row_ptr(tok, base[s], stride[s], padrow[s], zrow) + q * 8);
-  }
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int idx = lane + 64 * c;
-    const int t = idx >> 2, q = idx & 3;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) *reinterpret_cast<uint4*>(dst[s] + t * LD + q * 8) = raw[s][c];
-  }
-}
-
 // keep bits of the lane's 32 keys of query column tile it: bit jt*16 + r <-> key
 // jt*32 + crow(r, hh) (registers 2k, 2k+1 are keys j0, j0+1 of one hash)
 MSU_DEV uint32_t drop_bits(uint32_t seed, uint32_t item, int i, int hh, uint32_t thr) {
@@ -177,81 +141,42 @@ MSU_DEV void lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// S^T tiles (jt, it): bias image init + K Q^T from fragments ka[jt][ks], qb[it][ks];
-// mask; softmax over j with exp(scale * (s - max)) -> P^T
-// bimg: the head's bias image, lane-major ([tile][lane][16], global) or, LANE_INNER,
-// [tile][q][lane][4] (an LDS copy: consecutive lanes read consecutive 16 B, conflict-free)
-template <bool LANE_INNER = false>
-MSU_DEV void bias_init(f32x16 (&P)[2][2], const float* bimg, int lane) {
+// Softmax over keys j of one query-column tile (it): the lane's column of both key tiles
+// (accumulator rows) + the other half-wave (xor-32).  exp(scale (s - max)) as 2^(c s - c max).
+MSU_DEV void softmax_col(f32x16 (&P)[2], float scale) {
+  float m = -INFINITY;
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const float4* bp = LANE_INNER ? reinterpret_cast<const float4*>(bimg) + (jt * 2 + it) * 256 + lane
-                                    : reinterpret_cast<const float4*>(bimg + ((jt * 2 + it) * 64 + lane) * 16);
+    for (int r = 0; r < 16; ++r) m = fmaxf(m, P[jt][r]);
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  const float c = scale * 1.44269504088896341f;
+  const float mc = m * c;
+  float sum = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = bp[LANE_INNER ? 64 * q : q];
-        P[jt][it][4 * q] = v.x; P[jt][it][4 * q + 1] = v.y; P[jt][it][4 * q + 2] = v.z; P[jt][it][4 * q + 3] = v.w;
-      }
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      P[jt][r] = __builtin_amdgcn_exp2f(fmaf(P[jt][r], c, -mc));
+      sum += P[jt][r];
     }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.0f / sum;
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) P[jt][r] *= inv;
 }
 
-// P: the bias image (bias_init); + K Q^T, mask, softmax over j
-template <typename T>
-MSU_DEV void probs_T_from(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (&qb)[2][2],
-                          const int* sReg, bool boundary, float scale, int lane) {
+// shifted-window mask of one query-column tile: -100/scale where query and key regions differ
+MSU_DEV void mask_col(f32x16 (&P)[2], const int* sReg, int it, float scale, int lane) {
+  const float mval = -100.0f / scale;
+  const int ri = sReg[it * 32 + (lane & 31)], hh = lane >> 5;
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
+  for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int it = 0; it < 2; ++it) P[jt][it] = mfma32<T>(ka[jt][ks], qb[it][ks], P[jt][it]);
-  const int h = lane >> 5;
-  if (boundary) {
-    const float mval = -100.0f / scale;
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int ri = sReg[it * 32 + (lane & 31)];
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (sReg[jt * 32 + crow(r, h)] != ri) P[jt][it][r] += mval;
-    }
-  }
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    float m = -INFINITY;
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) m = fmaxf(m, P[jt][it][r]);
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    const float ms = m * scale;
-    float s = 0.f;
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float e = __expf(fmaf(P[jt][it][r], scale, -ms));
-        P[jt][it][r] = e;
-        s += e;
-      }
-    s += __shfl_xor(s, 32, 64);
-    const float inv = 1.0f / s;
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) P[jt][it][r] *= inv;
-  }
-}
-
-template <typename T, bool LANE_INNER = false>
-MSU_DEV void probs_T(f32x16 (&P)[2][2], const bf16x8 (&ka)[2][2], const bf16x8 (&qb)[2][2],
-                     const float* bimg, const int* sReg, bool boundary, float scale, int lane) {
-  bias_init<LANE_INNER>(P, bimg, lane);
-  probs_T_from<T>(P, ka, qb, sReg, boundary, scale, lane);
+    for (int r = 0; r < 16; ++r)
+      if (sReg[jt * 32 + crow(r, hh)] != ri) P[jt][r] += mval;
 }
 
 struct Aux {
@@ -336,55 +261,67 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
       *reinterpret_cast<u32x4*>(L.q + o) = qr[buf][c];
       *reinterpret_cast<u32x4*>(L.v + o) = vr[buf][c];
     }, std::make_integer_sequence<int, 4>{});
+    // dropout keep bits (bit jt*16 + r of kmasks[it], the backward's layout), drawn while
+    // the fewest registers are live: this window's rows are in LDS, the next one's not issued
+    uint32_t kmasks[2] = {~0u, ~0u};
+    if constexpr (DROP) {
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+        kmasks[it] = drop_bits(drop_seed32(seed), (uint32_t)win * g.nh + h, it * 32 + (lane & 31), hh,
+                               drop_thresh16(p_drop));
+    }
     const long nxt = it_cur + stride;
     const bool more = nxt < nitems;
     if (more) prep(nxt, std::integral_constant<int, buf ^ 1>{});
     lds_sync();
-    bf16x8 ka[2][2], qb[2][2];
+    bf16x8 ka[2][2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        ka[t][ks] = frag_rows(L.k, LD, 32 * t, 16 * ks, lane);
-        qb[t][ks] = frag_rows(L.q, LD, 32 * t, 16 * ks, lane);
-      }
-    f32x16 P[2][2];
-    probs_T<T, true>(P, ka, qb, reinterpret_cast<const float*>(sBimg), L.reg[buf], bnd[buf], scale, lane);
-    if constexpr (DROP) {
-      const float kscale = 1.0f / (1.0f - p_drop);
-      const uint32_t thr = drop_thresh16(p_drop), ds = drop_seed32(seed), item = (uint32_t)win * g.nh + h;
+      for (int ks = 0; ks < 2; ++ks) ka[t][ks] = frag_rows(L.k, LD, 32 * t, 16 * ks, lane);
+    // one query column tile (it) at a time: 32 queries x 64 keys of scores live at once
 #pragma unroll
-      for (int it = 0; it < 2; ++it)
+    for (int it = 0; it < 2; ++it) {
+      f32x16 P[2];
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {  // bias image tiles (jt, it) from the LDS copy
+        const float4* bp = sBimg + (jt * 2 + it) * 256 + lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = bp[64 * q];
+          P[jt][4 * q] = v.x; P[jt][4 * q + 1] = v.y; P[jt][4 * q + 2] = v.z; P[jt][4 * q + 3] = v.w;
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 qf = frag_rows(L.q, LD, 32 * it, 16 * ks, lane);
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) P[jt] = mfma32<T>(ka[jt][ks], qf, P[jt]);  // S^T = K Q^T (+ bias)
+      }
+      if (bnd[buf]) mask_col(P, L.reg[buf], it, scale, lane);
+      softmax_col(P, scale);
+      if constexpr (DROP) {
+        const float kscale = 1.0f / (1.0f - p_drop);
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const uint32_t b = drop_pair(ds, item, it * 32 + (lane & 31), jt * 32 + crow(2 * k, hh), thr);
-            P[jt][it][2 * k] = b & 1u ? P[jt][it][2 * k] * kscale : 0.f;
-            P[jt][it][2 * k + 1] = b & 2u ? P[jt][it][2 * k + 1] * kscale : 0.f;
-          }
-    }
-    // O^T[d][i] = sum_j V[j][d] P^T[j][i]
-    f32x16 O[2];
-    O[0] = f32x16{0}; O[1] = f32x16{0};
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 a = frag_tr_perm(L.v, LD, jt * 32 + 16 * s, 0, lane);
-#pragma unroll
-        for (int it = 0; it < 2; ++it) O[it] = mfma32<T>(a, pack8<T>(P[jt][it], s), O[it]);
+          for (int r = 0; r < 16; ++r) P[jt][r] = (kmasks[it] >> (jt * 16 + r)) & 1u ? P[jt][r] * kscale : 0.f;
       }
-    // output through the q image (its fragments are consumed): lane -> query i, registers
-    // 4gq..4gq+3 -> d = 8gq + 4hh .. +3; then 4 lanes per token store its 64-B slice
+      // O^T[d][i] = sum_j V[j][d] P^T[j][i]: P^T is the B operand straight from the registers
+      f32x16 O = f32x16{0};
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb)
+          O = mfma32<T>(frag_tr_perm(L.v, LD, jt * 32 + 16 * sb, 0, lane), pack8<T>(P[jt], sb), O);
+      // output through the q image (rows of this tile, whose fragments are consumed): lane ->
+      // query i, registers 4gq..4gq+3 -> d = 8gq + 4hh .. +3
       const int i = it * 32 + (lane & 31);
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
         uint2 w;
-        w.x = pack2<T>(O[it][4 * gq], O[it][4 * gq + 1]);
-        w.y = pack2<T>(O[it][4 * gq + 2], O[it][4 * gq + 3]);
+        w.x = pack2<T>(O[4 * gq], O[4 * gq + 1]);
+        w.y = pack2<T>(O[4 * gq + 2], O[4 * gq + 3]);
         *reinterpret_cast<uint2*>(L.q + i * LD + 8 * gq + 4 * hh) = w;
       }
     }
@@ -413,12 +350,6 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
     item += stride;
   }
 }
-
-struct BwdLds {
-  bf16_t q[64 * LD], k[64 * LD], v[64 * LD], dO[64 * LD];
-  bf16_t P[64 * LDP], dS[64 * LDP];  // [i][j] images
-  int tok[2][64], reg[2][64];          // current / prefetched window
-};
 
 // Store one 32-d head slice of a lane-major accumulator (lane = token, registers 4q..4q+3 =
 // d 8q + 4hh .. +3) as two 16-B stores per lane: a permlane32 swap pairs each half's 4-d
@@ -451,237 +382,260 @@ MSU_DEV void pad_accumulate(float& acc, const f32x16& a, float s, bool pad, int 
   }
 }
 
-template <typename T, int WAVES, bool DROP>
-__global__ void __launch_bounds__(64 * WAVES) attn_bwd_mfma(
+// source token and mask region of window token t (window_tokens, one entry per call)
+MSU_DEV int token_of(const Geom& g, int win, int t, int* reg) {
+  const int nw = g.nWy * g.nWx;
+  const int b = win / nw;
+  const int wr = win - b * nw;
+  const int wy = wr / g.nWx, wx = wr - wy * g.nWx;
+  if (t >= NT) {
+    *reg = 0;
+    return TOK_ZERO;
+  }
+  const int py = wy * WS + t / WS, px = wx * WS + t % WS;
+  int sy = py + g.sh; if (sy >= g.Hp) sy -= g.Hp;
+  int sx = px + g.sw; if (sx >= g.Wp) sx -= g.Wp;
+  *reg = region(py, g.Hp, g.sh) * 3 + region(px, g.Wp, g.sw);
+  return (sy < g.H && sx < g.W) ? (b * g.H + sy) * g.W + sx : TOK_PAD;
+}
+
+MSU_DEV bool window_boundary(const Geom& g, int win) {
+  const int wr = win % (g.nWy * g.nWx);
+  return (g.sh + g.sw) > 0 && (wr / g.nWx == g.nWy - 1 || wr % g.nWx == g.nWx - 1);
+}
+
+struct BwdLds {
+  bf16_t q[64 * LD], k[64 * LD], v[64 * LD], dO[64 * LD];  // the window's head slices [t][d]
+  bf16_t P[64 * LDP], dS[64 * LDP];                          // [i][j] images (Pd and dS)
+  int tok[2][64], reg[2][64];                                // current / next window's token table
+};
+
+// Backward: a 2-wave workgroup per (window, head) item -- wave w owns query tile it = w in the
+// score pass and key tile mt = w in the gradient pass, so each wave carries half the item's
+// state (registers ~190, LDS ~20 KB) and two workgroups share a SIMD pair: one item's
+// latency chain (LDS round trips, MFMA dependencies, softmax) hides under the other's.
+//   score pass (it = w):  S^T[:, it] = K Q_it^T + bias, P^T by softmax over j (the lane's
+//     column, + one xor-32 shuffle), dPd^T = V dO_it^T, delta, dS^T = P^T (dP^T - delta);
+//     Pd and dS written as rows i of the [i][j] images; dS^T summed into dB (this wave's
+//     bias-image column tiles).
+//   gradient pass (mt = w): dV^T = dO^T Pd, dK^T = Q^T dS for keys j in tile mt and
+//     dQ^T = K^T dS^T for queries i in tile mt -- the token index on the accumulator columns,
+//     so every lane stores whole 16-B pieces of its token's rows.
+// Blocks walk windows blk, blk + nblk, ...; window k+1's rows are loaded into registers (each
+// wave its 32 rows) while window k is computed.
+template <typename T, bool DROP>
+__global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     const bf16_t* __restrict__ qkv, Aux aux, const bf16_t* __restrict__ dout, bf16_t* __restrict__ dqkv,
     float* __restrict__ dB_part, float* __restrict__ qb_part, Geom g, float scale, float p_drop,
     uint64_t seed0, const unsigned long long* seed_dev, int nblk) {
   const uint64_t seed = launch_seed(seed0, seed_dev);
-  // grid (nblk, nh): block owns head h, waves walk windows win = (blk*WAVES + wave) + k*nblk*WAVES
-  __shared__ __attribute__((aligned(16))) BwdLds lds_all[WAVES];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  BwdLds& L = lds_all[wave];
+  __shared__ __attribute__((aligned(16))) BwdLds L;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;  // w: this wave's query / key tile
   const int h = blockIdx.y;
   const long C3 = 3L * g.C;
   const int hh = lane >> 5;
   const float* bimg = aux.bimg + (long)h * 4096;
   const int cq = h * HD, ck = g.C + h * HD, cv = 2 * g.C + h * HD;
-  f32x16 dB[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) dB[a][b] = f32x16{0};
+  const float kscale = 1.0f / (1.0f - p_drop);  // the forward's kept-value factor
+  f32x16 dB[2];  // dS^T tiles (jt, it = w) summed over this block's windows
+  dB[0] = f32x16{0};
+  dB[1] = f32x16{0};
   float padacc[3] = {0.f, 0.f, 0.f};  // column d = lane&31 of padded tokens' dq, dk, dv (per half)
-  const long stride = (long)nblk * WAVES;
-  // The window's q / k / v / dO head slices (4 lanes per 64-B slice) are loaded into
-  // registers one window ahead: window i+1's HBM latency hides under window i's math.
-  u32x4 rq[2][4], rk[2][4], rv[2][4], rd[2][4];
+  u32x4 rq[2][2], rk[2][2], rv[2][2], rd[2][2];  // [buf][c]: rows 32w + (lane>>2) + 16c
   bool bnd[2] = {false, false};
   auto rowbase = [&](int tok) -> const bf16_t* {
     return tok >= 0 ? qkv + (size_t)((unsigned)tok * (unsigned)C3) : (tok == TOK_PAD ? aux.biasrow : aux.zrow);
   };
-  auto prep = [&](long w, auto BUF) __attribute__((always_inline)) {
+  // window win's token-table entries 32w + (lane&31) and this wave's rows -> registers
+  auto prep = [&](long win_l, auto BUF) __attribute__((always_inline)) {
     constexpr int buf = decltype(BUF)::value;
-    bnd[buf] = window_tokens(g, w, L.tok[buf], L.reg[buf], lane);
-    lds_sync();
+    const int win = (int)win_l;  // < 2^31 windows (checked on the host)
+    bnd[buf] = window_boundary(g, win);
+    int reg;
+    const int tt = 32 * w + (lane & 31);
+    const int tokt = token_of(g, win, tt, &reg);
+    if (lane < 32) {
+      L.tok[buf][tt] = tokt;
+      L.reg[buf][tt] = reg;
+    }
     const int o = 8 * (lane & 3);
     static_for([&](auto CI) {
       constexpr int c = decltype(CI)::value;
-      const int tok = L.tok[buf][(lane >> 2) + 16 * c];
+      int rg;
+      const int tok = token_of(g, win, 32 * w + (lane >> 2) + 16 * c, &rg);
       const bf16_t* rb = rowbase(tok);
       rq[buf][c] = *reinterpret_cast<const u32x4*>(rb + cq + o);
       rk[buf][c] = *reinterpret_cast<const u32x4*>(rb + ck + o);
       rv[buf][c] = *reinterpret_cast<const u32x4*>(rb + cv + o);
       const bf16_t* db = tok >= 0 ? dout + (size_t)((unsigned)tok * (unsigned)g.C) + h * HD : aux.zrow;
       rd[buf][c] = *reinterpret_cast<const u32x4*>(db + o);
-    }, std::make_integer_sequence<int, 4>{});
+    }, std::make_integer_sequence<int, 2>{});
   };
   auto step = [&](auto BUF, long win) __attribute__((always_inline)) -> bool {
     constexpr int buf = decltype(BUF)::value;
     static_for([&](auto CI) {
       constexpr int c = decltype(CI)::value;
-      const int off = ((lane >> 2) + 16 * c) * LD + 8 * (lane & 3);
+      const int off = (32 * w + (lane >> 2) + 16 * c) * LD + 8 * (lane & 3);
       *reinterpret_cast<u32x4*>(L.q + off) = rq[buf][c];
       *reinterpret_cast<u32x4*>(L.k + off) = rk[buf][c];
       *reinterpret_cast<u32x4*>(L.v + off) = rv[buf][c];
       *reinterpret_cast<u32x4*>(L.dO + off) = rd[buf][c];
-    }, std::make_integer_sequence<int, 4>{});
-    const long nxt = win + stride;
+    }, std::make_integer_sequence<int, 2>{});
+    __syncthreads();  // rows + this window's token table visible to both waves
+    const long nxt = win + nblk;
     const bool more = nxt < g.nwin;
     if (more) prep(nxt, std::integral_constant<int, buf ^ 1>{});
     const bool boundary = bnd[buf];
     const int* sTok = L.tok[buf];
     const int* sReg = L.reg[buf];
-    // dropout keep bits of the lane's (i, j) pairs, bit jt*16+r of kmasks[it], drawn before
-    // the score tiles are live
-    const float kscale = 1.0f / (1.0f - p_drop);  // the forward's kept-value factor
-    uint32_t kmasks[2] = {~0u, ~0u};
-    if constexpr (DROP) {
+    // ---- score pass: query tile it = w
+    const int it = w;
+    const int i = it * 32 + (lane & 31);
+    uint32_t kmask = ~0u;  // bit jt*16+r: (i, key jt*32 + crow(r, hh)) kept by the dropout
+    if constexpr (DROP)  // the forward's mask, regenerated from the seed
+      kmask = drop_bits(drop_seed32(seed), (uint32_t)win * g.nh + h, i, hh, drop_thresh16(p_drop));
+    f32x16 P[2], D[2];
 #pragma unroll
-      for (int it = 0; it < 2; ++it)
-        kmasks[it] = drop_bits(drop_seed32(seed), (uint32_t)win * g.nh + h, it * 32 + (lane & 31), hh,
-                               drop_thresh16(p_drop));
-    }
-    lds_sync();
-    bf16x8 va[2][2], ka[2][2];
+    for (int jt = 0; jt < 2; ++jt) {
+      const float4* bp = reinterpret_cast<const float4*>(bimg + ((jt * 2 + it) * 64 + lane) * 16);
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        va[t][ks] = frag_rows(L.v, LD, 32 * t, 16 * ks, lane);
-        ka[t][ks] = frag_rows(L.k, LD, 32 * t, 16 * ks, lane);
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = bp[q];
+        P[jt][4 * q] = v.x; P[jt][4 * q + 1] = v.y; P[jt][4 * q + 2] = v.z; P[jt][4 * q + 3] = v.w;
       }
-    // one query column tile (it) at a time: P^T / dP^T of 32 queries x 64 keys live at once
+      D[jt] = f32x16{0};
+    }
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int i = it * 32 + (lane & 31);
-      f32x16 P[2], D[2];
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 qf = frag_rows(L.q, LD, 32 * it, 16 * ks, lane);
+      const bf16x8 df = frag_rows(L.dO, LD, 32 * it, 16 * ks, lane);
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt) {
-        const float4* bp = reinterpret_cast<const float4*>(bimg + ((jt * 2 + it) * 64 + lane) * 16);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v = bp[q];
-          P[jt][4 * q] = v.x; P[jt][4 * q + 1] = v.y; P[jt][4 * q + 2] = v.z; P[jt][4 * q + 3] = v.w;
-        }
-        D[jt] = f32x16{0};
+        P[jt] = mfma32<T>(frag_rows(L.k, LD, 32 * jt, 16 * ks, lane), qf, P[jt]);  // S^T = K Q^T (+ bias)
+        D[jt] = mfma32<T>(frag_rows(L.v, LD, 32 * jt, 16 * ks, lane), df, D[jt]);  // dPd^T = V dO^T
       }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 qf = frag_rows(L.q, LD, 32 * it, 16 * ks, lane);
-        const bf16x8 df = frag_rows(L.dO, LD, 32 * it, 16 * ks, lane);
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt) {
-          P[jt] = mfma32<T>(ka[jt][ks], qf, P[jt]);   // S^T = K Q^T (+ bias)
-          D[jt] = mfma32<T>(va[jt][ks], df, D[jt]);   // dPd^T = V dO^T
-        }
-      }
-      if (boundary) {
-        const float mval = -100.0f / scale;
-        const int ri = sReg[i];
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (sReg[jt * 32 + crow(r, hh)] != ri) P[jt][r] += mval;
-      }
-      {  // softmax over j (the accumulator rows of this lane's column + the other half)
-        float m = -INFINITY;
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) m = fmaxf(m, P[jt][r]);
-        m = fmaxf(m, __shfl_xor(m, 32, 64));
-        const float c = scale * 1.44269504088896341f;
-        const float mc = m * c;
-        float sum = 0.f;
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            P[jt][r] = __builtin_amdgcn_exp2f(fmaf(P[jt][r], c, -mc));
-            sum += P[jt][r];
-          }
-        sum += __shfl_xor(sum, 32, 64);
-        const float inv = 1.0f / sum;
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) P[jt][r] *= inv;
-      }
-      const uint32_t kmask = kmasks[it];
-      float delta = 0.f;
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          if constexpr (DROP)  // dP = dPd * keep/(1-p)
-            D[jt][r] = (kmask >> (jt * 16 + r)) & 1u ? D[jt][r] * kscale : 0.f;
-          delta += P[jt][r] * D[jt][r];
-        }
-      delta += __shfl_xor(delta, 32, 64);
-      // Pd and dS images [i][j], 4 consecutive j per 8-byte store
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          float pd[4], ds[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * gq + e;
-            const float p = P[jt][r];
-            ds[e] = p * (D[jt][r] - delta);
-            pd[e] = DROP ? ((kmask >> (jt * 16 + r)) & 1u ? p * kscale : 0.f) : p;
-            dB[jt][it][r] += ds[e];
-          }
-          const int j0 = jt * 32 + 8 * gq + 4 * hh;
-          uint2 wp, wd;
-          wp.x = pack2<T>(pd[0], pd[1]);
-          wp.y = pack2<T>(pd[2], pd[3]);
-          wd.x = pack2<T>(ds[0], ds[1]);
-          wd.y = pack2<T>(ds[2], ds[3]);
-          *reinterpret_cast<uint2*>(L.P + i * LDP + j0) = wp;
-          *reinterpret_cast<uint2*>(L.dS + i * LDP + j0) = wd;
-        }
     }
-    lds_sync();
-    // dV^T[d][j] = sum_i dO[i][d] Pd[i][j]; dK^T[d][j] = scale sum_i Q[i][d] dS[i][j];
-    // dQ^T[d][i] = scale sum_j K[j][d] dS[i][j]   (scores = scale * q k^T).  The token index
-    // is the accumulator column (lane), so each lane writes whole 16-B pieces of one row.
+    if (boundary) mask_col(P, sReg, it, scale, lane);
+    softmax_col(P, scale);
+    float delta = 0.f;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      f32x16 av = f32x16{0}, ak = f32x16{0}, aq = f32x16{0};
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if constexpr (DROP)  // dP = dPd * keep/(1-p)
+          D[jt][r] = (kmask >> (jt * 16 + r)) & 1u ? D[jt][r] * kscale : 0.f;
+        delta += P[jt][r] * D[jt][r];
+      }
+    delta += __shfl_xor(delta, 32, 64);
+    // Pd and dS images [i][j], 4 consecutive j per 8-byte store
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        float pd[4], ds[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * gq + e;
+          const float p = P[jt][r];
+          ds[e] = p * (D[jt][r] - delta);
+          pd[e] = DROP ? ((kmask >> (jt * 16 + r)) & 1u ? p * kscale : 0.f) : p;
+          dB[jt][r] += ds[e];
+        }
+        const int j0 = jt * 32 + 8 * gq + 4 * hh;
+        uint2 wp, wd;
+        wp.x = pack2<T>(pd[0], pd[1]);
+        wp.y = pack2<T>(pd[2], pd[3]);
+        wd.x = pack2<T>(ds[0], ds[1]);
+        wd.y = pack2<T>(ds[2], ds[3]);
+        *reinterpret_cast<uint2*>(L.P + i * LDP + j0) = wp;
+        *reinterpret_cast<uint2*>(L.dS + i * LDP + j0) = wd;
+      }
+    __syncthreads();  // both halves of the images written
+    // ---- gradient pass: key tile mt = w (dV, dK) and query tile mt (dQ)
+    // dV^T[d][j] = sum_i dO[i][d] Pd[i][j]; dK^T[d][j] = scale sum_i Q[i][d] dS[i][j];
+    // dQ^T[d][i] = scale sum_j K[j][d] dS[i][j]   (scores = scale * q k^T)
+    const int mt = w;
+    const int tok = sTok[mt * 32 + (lane & 31)];
+    const bool pad = tok == TOK_PAD;
+    const bool anypad = __ballot(pad) != 0;  // wave-uniform: only windows over the padded border
+    bf16_t* row = dqkv + (size_t)((unsigned)(tok >= 0 ? tok : 0) * (unsigned)C3) + h * HD;
+    {
+      f32x16 av = f32x16{0}, ak = f32x16{0};
 #pragma unroll
       for (int ks = 0; ks < 64; ks += 16) {
-        const bf16x8 bdo = frag_tr_q4(L.dO, LD, ks, 0, lane);
-        const bf16x8 bq = frag_tr_q4(L.q, LD, ks, 0, lane);
-        const bf16x8 bk = frag_tr(L.k, LD, ks, 0, lane);
-        av = mfma32<T>(bdo, frag_tr_q4(L.P, LDP, ks, mt * 32, lane), av);
-        ak = mfma32<T>(bq, frag_tr_q4(L.dS, LDP, ks, mt * 32, lane), ak);
-        aq = mfma32<T>(bk, frag_rows(L.dS, LDP, mt * 32, ks, lane), aq);
+        av = mfma32<T>(frag_tr_q4(L.dO, LD, ks, 0, lane), frag_tr_q4(L.P, LDP, ks, mt * 32, lane), av);
+        ak = mfma32<T>(frag_tr_q4(L.q, LD, ks, 0, lane), frag_tr_q4(L.dS, LDP, ks, mt * 32, lane), ak);
       }
-      const int tok = sTok[mt * 32 + (lane & 31)];
-      bf16_t* row = dqkv + (size_t)((unsigned)(tok >= 0 ? tok : 0) * (unsigned)C3) + h * HD;
-      store_slice<T>(row, aq, scale, hh, tok >= 0);
       store_slice<T>(row + g.C, ak, scale, hh, tok >= 0);
       store_slice<T>(row + 2 * g.C, av, 1.0f, hh, tok >= 0);
-      const bool pad = tok == TOK_PAD;
-      if (__ballot(pad) != 0) {  // wave-uniform: only windows over the padded border
-        pad_accumulate(padacc[0], aq, scale, pad, lane);
+      if (anypad) {
         pad_accumulate(padacc[1], ak, scale, pad, lane);
         pad_accumulate(padacc[2], av, 1.0f, pad, lane);
       }
     }
-    lds_sync();  // this window's LDS reads are done before the next window's rows land
+    {
+      f32x16 aq = f32x16{0};
+#pragma unroll
+      for (int ks = 0; ks < 64; ks += 16)
+        aq = mfma32<T>(frag_tr(L.k, LD, ks, 0, lane), frag_rows(L.dS, LDP, mt * 32, ks, lane), aq);
+      store_slice<T>(row, aq, scale, hh, tok >= 0);
+      if (anypad) pad_accumulate(padacc[0], aq, scale, pad, lane);
+    }
+    __syncthreads();  // this window's LDS reads done before the next window's rows land
     return more;
   };
 
-  long win = (long)blockIdx.x * WAVES + wave;
-  if (win < g.nwin) {
+  const long win0 = blockIdx.x;
+  if (win0 < g.nwin) {  // block-uniform
+    long win = win0;
     prep(win, std::integral_constant<int, 0>{});
     for (;;) {
       if (!step(std::integral_constant<int, 0>{}, win)) break;
-      win += stride;
+      win += nblk;
       if (!step(std::integral_constant<int, 1>{}, win)) break;
-      win += stride;
+      win += nblk;
     }
   }
 
-  const long part = (long)blockIdx.x * WAVES + wave;
-  float* db = dB_part + (part * g.nh + h) * 4096;
+  // dB -> the 169 relative-position entries, once per block: both waves' tiles go to LDS (over
+  // the images) in the bias-image layout [tile jt*2+it][lane][16], then a thread sums a table
+  // entry's <= 49 (i, j) pairs.  Partials [blk][169][nh] reduce over blocks straight into d table.
+  const long part = blockIdx.x;
+  float* img = reinterpret_cast<float*>(L.P);  // 16 KB image + 96 floats of wave 1's pad sums
+  __syncthreads();
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      float4* dst = reinterpret_cast<float4*>(db + ((jt * 2 + it) * 64 + lane) * 16);
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(img + ((jt * 2 + w) * 64 + lane) * 16 + 4 * q) =
+          make_float4(dB[jt][4 * q], dB[jt][4 * q + 1], dB[jt][4 * q + 2], dB[jt][4 * q + 3]);
+  float padv[3];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        dst[q] = make_float4(dB[jt][it][4 * q], dB[jt][it][4 * q + 1], dB[jt][it][4 * q + 2], dB[jt][it][4 * q + 3]);
+  for (int k = 0; k < 3; ++k) padv[k] = padacc[k] + __shfl_xor(padacc[k], 32, 64);
+  if (w == 1 && lane < 32) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) img[4096 + 32 * k + lane] = padv[k];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 169; e += 128) {
+    const int dh = e / 13 - 6, dw = e % 13 - 6;
+    float sum = 0.f;
+    for (int ih = 0; ih < WS; ++ih) {
+      const int jh = ih - dh;
+      if (jh < 0 || jh >= WS) continue;
+      for (int iw = 0; iw < WS; ++iw) {
+        const int jw = iw - dw;
+        if (jw < 0 || jw >= WS) continue;
+        const int ii = ih * WS + iw, j = jh * WS + jw;
+        const int jj = j & 31;
+        sum += img[(((j >> 5) * 2 + (ii >> 5)) * 64 + (ii & 31) + 32 * ((jj >> 2) & 1)) * 16 + (jj & 3) + 4 * (jj >> 3)];
+      }
     }
+    dB_part[(part * 169 + e) * g.nh + h] = sum;
+  }
+  if (w == 0 && lane < 32) {
 #pragma unroll
-  for (int w = 0; w < 3; ++w) {
-    const float v = padacc[w] + __shfl_xor(padacc[w], 32, 64);
-    if (lane < 32) qb_part[part * C3 + w * g.C + h * HD + lane] = v;
+    for (int k = 0; k < 3; ++k) qb_part[part * C3 + k * g.C + h * HD + lane] = padv[k] + img[4096 + 32 * k + lane];
   }
 }
 
@@ -708,29 +662,6 @@ __global__ void __launch_bounds__(256) aux_kernel(const float* table, const floa
   img[e] = v;
 }
 
-// d bias image [nh][4096] (dS, in the image layout) -> d table [169][nh]
-__global__ void __launch_bounds__(256) bias_image_grad_kernel(const float* dimg, int nh, float* dtable) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= 169 * nh) return;
-  const int idx = e / nh, h = e - (e / nh) * nh;
-  const int dh = idx / 13 - 6, dw = idx % 13 - 6;
-  float s = 0.f;
-  for (int ih = 0; ih < WS; ++ih) {
-    const int jh = ih - dh;
-    if (jh < 0 || jh >= WS) continue;
-    for (int iw = 0; iw < WS; ++iw) {
-      const int jw = iw - dw;
-      if (jw < 0 || jw >= WS) continue;
-      const int i = ih * WS + iw, j = jh * WS + jw;
-      const int jt = j >> 5, it = i >> 5, jj = j & 31;
-      const int hh = (jj >> 2) & 1, r = (jj & 3) + 4 * (jj >> 3);
-      const int lane = (i & 31) + 32 * hh;
-      s += dimg[(long)h * 4096 + ((jt * 2 + it) * 64 + lane) * 16 + r];
-    }
-  }
-  dtable[e] = s;
-}
-
 Geom make_geom(int B, int H, int W, int C, int nh, int shift) {
   Geom g;
   g.B = B; g.H = H; g.W = W; g.C = C; g.nh = nh;
@@ -743,7 +674,7 @@ Geom make_geom(int B, int H, int W, int C, int nh, int shift) {
   return g;
 }
 
-constexpr int FWD_WAVES = 4, BWD_WAVES = 2;
+constexpr int FWD_WAVES = 4;
 
 // aux workspace (f32 units): bias image nh*4096, bf16 bias row (3C bf16), zero row (64 bf16)
 long aux_floats(int C, int nh) { return (long)nh * 4096 + (6L * C + 1) / 2 + 4; }
@@ -759,13 +690,19 @@ Aux carve_aux(float* ws, int C, int nh, float** img_out, bf16_t** brow, bf16_t**
   return a;
 }
 
-int bwd_blocks(long nwin, int nh) {
-  long nblk = 1024 / ((long)nh * BWD_WAVES);
-  if (nblk < 1) nblk = 1;
-  const long maxb = (nwin + BWD_WAVES - 1) / BWD_WAVES;
-  if (nblk > maxb) nblk = maxb;
-  return (int)nblk;
+// Workgroups per head (grid (n, nh), head-major dispatch order): min(need, cap), a multiple of
+// 8 so that block (x, h) lands on XCD x % 8 for every head h.  The heads of one window then
+// run on the same XCD at about the same time, and the 128-B lines they share (a head slice
+// is 64 B of a token's q / k / v row) come from that XCD's L2 after the first head's miss.
+long head_blocks(long need, long cap) {
+  cap = cap / 8 * 8;
+  if (cap < 8) cap = 8;
+  if (need > cap) need = cap;
+  return (need + 7) / 8 * 8;
 }
+
+// backward workgroups per head: about four 2-wave workgroups per CU over all heads
+int bwd_blocks(long nwin, int nh) { return (int)head_blocks(nwin, 1024 / nh); }
 
 }  // namespace
 
@@ -775,8 +712,8 @@ int msu_attn_mfma_bwd_tail(float* ws, float* dtable, float* dqkv_bias_pad, long 
 long msu_attn_mfma_fwd_workspace(int C, int nh) { return aux_floats(C, nh); }
 
 long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh) {
-  const long parts = (long)bwd_blocks(nwin, nh) * BWD_WAVES;
-  return aux_floats(C, nh) + parts * nh * 4096 + (long)nh * 4096 + parts * 3L * C;
+  const long parts = (long)bwd_blocks(nwin, nh);
+  return aux_floats(C, nh) + parts * nh * 169 + parts * 3L * C;
 }
 
 int msu_attn_mfma_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, void* out, int B,
@@ -789,18 +726,17 @@ int msu_attn_mfma_fwd(int dtype, const void* qkv, const float* qkv_bias, const f
   float* img; bf16_t* brow; bf16_t* zrow;
   const Aux aux = carve_aux(ws, C, nh, &img, &brow, &zrow);
   // persistent: about two 4-wave workgroups per CU, split over the heads
-  long nb = (g.nwin + FWD_WAVES - 1) / FWD_WAVES;
-  const long cap = 512 / nh > 0 ? 512 / nh : 1;
-  if (nb > cap) nb = cap;
+  const long nb = head_blocks((g.nwin + FWD_WAVES - 1) / FWD_WAVES, 512 / nh);
+  const dim3 grid((unsigned)nb, (unsigned)nh), blk(64 * FWD_WAVES);
   MSU_DISPATCH16(dtype, T,
     hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
                        1.0f / scale, img, brow, zrow);
     if (p_drop > 0.f)
-      hipLaunchKernelGGL((attn_fwd_mfma<T, FWD_WAVES, true>), dim3((unsigned)nb, (unsigned)nh), dim3(64 * FWD_WAVES),
-                         0, st, (const bf16_t*)qkv, aux, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev);
+      hipLaunchKernelGGL((attn_fwd_mfma<T, FWD_WAVES, true>), grid, blk, 0, st, (const bf16_t*)qkv, aux,
+                         (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev);
     else
-      hipLaunchKernelGGL((attn_fwd_mfma<T, FWD_WAVES, false>), dim3((unsigned)nb, (unsigned)nh), dim3(64 * FWD_WAVES),
-                         0, st, (const bf16_t*)qkv, aux, (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev));
+      hipLaunchKernelGGL((attn_fwd_mfma<T, FWD_WAVES, false>), grid, blk, 0, st, (const bf16_t*)qkv, aux,
+                         (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev));
   return MSU_CHECK_LAUNCH();
 }
 
@@ -812,23 +748,23 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
   if (g.nwin == 0) return 0;
   const float scale = 1.0f / sqrtf((float)HD);
   const int nblk = bwd_blocks(g.nwin, nh);
-  const long parts = (long)nblk * BWD_WAVES;
+  const long parts = nblk;
   float* img; bf16_t* brow; bf16_t* zrow;
   const Aux aux = carve_aux(ws, C, nh, &img, &brow, &zrow);
   float* dB_part = ws + aux_floats(C, nh);
-  float* dimg = dB_part + parts * nh * 4096;
-  float* qb_part = dimg + (long)nh * 4096;
+  float* qb_part = dB_part + parts * nh * 169;
+  const dim3 grid(nblk, nh);
   MSU_DISPATCH16(dtype, T,
     hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
                        1.0f / scale, img, brow, zrow);
     if (p_drop > 0.f)
-      hipLaunchKernelGGL((attn_bwd_mfma<T, BWD_WAVES, true>), dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
-                         (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
-                         p_drop, (uint64_t)seed, seed_dev, nblk);
+      hipLaunchKernelGGL((attn_bwd_mfma<T, true>), grid, dim3(128), 0, st, (const bf16_t*)qkv, aux,
+                         (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale, p_drop, (uint64_t)seed,
+                         seed_dev, nblk);
     else
-      hipLaunchKernelGGL((attn_bwd_mfma<T, BWD_WAVES, false>), dim3(nblk, nh), dim3(64 * BWD_WAVES), 0, st,
-                         (const bf16_t*)qkv, aux, (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale,
-                         p_drop, (uint64_t)seed, seed_dev, nblk));
+      hipLaunchKernelGGL((attn_bwd_mfma<T, false>), grid, dim3(128), 0, st, (const bf16_t*)qkv, aux,
+                         (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale, p_drop, (uint64_t)seed,
+                         seed_dev, nblk));
   if (pst == (hipStream_t)(intptr_t)-1) return MSU_CHECK_LAUNCH();  // tail issued by the caller
   // parameter-gradient reductions: on pst (after the backward kernel) when given
   const int rc = attn_param_stream(st, pst);
@@ -840,12 +776,10 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
 int msu_attn_mfma_bwd_tail(float* ws, float* dtable, float* dqkv_bias_pad, long nwin, int C, int nh,
                            hipStream_t st) {
   if (nwin == 0) return 0;
-  const long parts = (long)bwd_blocks(nwin, nh) * BWD_WAVES;
+  const long parts = (long)bwd_blocks(nwin, nh);
   float* dB_part = ws + aux_floats(C, nh);
-  float* dimg = dB_part + parts * nh * 4096;
-  float* qb_part = dimg + (long)nh * 4096;
-  const ColSeg segs[2] = {{dB_part, (long)nh * 4096, (long)nh * 4096, dimg}, {qb_part, 3L * C, 3L * C, dqkv_bias_pad}};
+  float* qb_part = dB_part + parts * nh * 169;
+  const ColSeg segs[2] = {{dB_part, 169L * nh, 169L * nh, dtable}, {qb_part, 3L * C, 3L * C, dqkv_bias_pad}};
   colsum_multi(segs, 2, (int)parts, 0, st);
-  hipLaunchKernelGGL(bias_image_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, st, dimg, nh, dtable);
   return MSU_CHECK_LAUNCH();
 }
