@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--skip-dead", action="store_true", help="skip the reference's discarded branches (exact)")
+    ap.add_argument("--grad-wire", choices=["f32", "bf16", "fp16"], default="f32",
+                    help="DP gradient all-reduce precision (BASELINE config 5: fp16 grads)")
     return ap.parse_args()
 
 
@@ -342,8 +344,10 @@ def main():
     torch.manual_seed(cfg.SEED)
     model = MSUNet(cfg, img_size=args.img, num_classes=1).to(device)
     model.ms_unet.skip_dead_branches = args.skip_dead
+    wire = {"f32": None, "bf16": torch.bfloat16, "fp16": torch.float16}[args.grad_wire]
     trainer = Trainer(model, cfg, device, world_size=world,
-                      process_group=dist.group.WORLD if world > 1 else None, rank=rank, seed=cfg.SEED)
+                      process_group=dist.group.WORLD if world > 1 else None, rank=rank, seed=cfg.SEED,
+                      grad_wire_dtype=wire)
     pool = batch_pool(2, args.batch, args.img, device, cfg.SEED + 1000 * rank)
 
     for i in range(args.warmup):
@@ -389,7 +393,7 @@ def main():
                                    f"{world}xMI355X DP {args.img}x{args.img} global bs={args.batch * world} "
                                    f"{BACKBONE_NAME[args.backbone]} MS-UNet train step",
                        "model": f"MS-UNet {args.backbone}", "global_batch": args.batch * world,
-                       "img_size": args.img, "parallelism": f"dp{world}",
+                       "img_size": args.img, "parallelism": f"dp{world}", "grad_allreduce": args.grad_wire,
                        "dead_branches": "skipped" if args.skip_dead else "executed (no grad)",
                        "step_execution": "hip_graph_replay" if trainer._graph is not None else "eager",
                        "graph_probe": getattr(trainer, "graph_probe", None),

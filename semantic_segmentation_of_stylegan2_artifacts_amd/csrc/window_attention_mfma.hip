@@ -125,14 +125,25 @@ MSU_DEV bool window_tokens(const Geom& g, long win_l, int* sTok, int* sReg, int 
   return (g.sh + g.sw) > 0 && (wy == g.nWy - 1 || wx == g.nWx - 1);
 }
 
+// x where bit n of m is set, else +0 (the bit shifted into the sign, spread, ANDed: no VCC)
+MSU_DEV float keep_sel(uint32_t m, int n, float x) {
+  return __int_as_float(((int)(m << (31 - n)) >> 31) & __float_as_int(x));
+}
+
 // keep bits of the lane's 32 keys of query column tile it: bit jt*16 + r <-> key
 // jt*32 + crow(r, hh) (registers 2k, 2k+1 are keys j0, j0+1 of one hash)
+// SERIAL: one hash in flight (the backward, whose register peak 16 interleaved hashes raise);
+// unrolled, the forward hides the hash latency with them
+template <bool SERIAL>
 MSU_DEV uint32_t drop_bits(uint32_t seed, uint32_t item, int i, int hh, uint32_t thr) {
   uint32_t m = 0;
+  if constexpr (SERIAL) {
+#pragma unroll 1
+    for (int n = 0; n < 16; ++n) m |= drop_pair(seed, item, i, (n >> 3) * 32 + crow(2 * (n & 7), hh), thr) << (2 * n);
+  } else {
 #pragma unroll
-  for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) m |= drop_pair(seed, item, i, jt * 32 + crow(2 * k, hh), thr) << (jt * 16 + 2 * k);
+    for (int n = 0; n < 16; ++n) m |= drop_pair(seed, item, i, (n >> 3) * 32 + crow(2 * (n & 7), hh), thr) << (2 * n);
+  }
   return m;
 }
 
@@ -267,7 +278,7 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
     if constexpr (DROP) {
 #pragma unroll
       for (int it = 0; it < 2; ++it)
-        kmasks[it] = drop_bits(drop_seed32(seed), (uint32_t)win * g.nh + h, it * 32 + (lane & 31), hh,
+        kmasks[it] = drop_bits<false>(drop_seed32(seed), (uint32_t)win * g.nh + h, it * 32 + (lane & 31), hh,
                                drop_thresh16(p_drop));
     }
     const long nxt = it_cur + stride;
@@ -493,7 +504,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     const int i = it * 32 + (lane & 31);
     uint32_t kmask = ~0u;  // bit jt*16+r: (i, key jt*32 + crow(r, hh)) kept by the dropout
     if constexpr (DROP)  // the forward's mask, regenerated from the seed
-      kmask = drop_bits(drop_seed32(seed), (uint32_t)win * g.nh + h, i, hh, drop_thresh16(p_drop));
+      kmask = drop_bits<true>(drop_seed32(seed), (uint32_t)win * g.nh + h, i, hh, drop_thresh16(p_drop));
     f32x16 P[2], D[2];
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
@@ -523,7 +534,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         if constexpr (DROP)  // dP = dPd * keep/(1-p)
-          D[jt][r] = (kmask >> (jt * 16 + r)) & 1u ? D[jt][r] * kscale : 0.f;
+          D[jt][r] = keep_sel(kmask, jt * 16 + r, D[jt][r] * kscale);
         delta += P[jt][r] * D[jt][r];
       }
     delta += __shfl_xor(delta, 32, 64);
@@ -538,7 +549,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
           const int r = 4 * gq + e;
           const float p = P[jt][r];
           ds[e] = p * (D[jt][r] - delta);
-          pd[e] = DROP ? ((kmask >> (jt * 16 + r)) & 1u ? p * kscale : 0.f) : p;
+          pd[e] = DROP ? keep_sel(kmask, jt * 16 + r, p * kscale) : p;
           dB[jt][r] += ds[e];
         }
         const int j0 = jt * 32 + 8 * gq + 4 * hh;

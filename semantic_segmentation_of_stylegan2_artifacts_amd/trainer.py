@@ -14,7 +14,8 @@ Here:
 * DP: the gradient buffers are cut into ~``bucket_mb`` buckets; when every parameter of a
   bucket has accumulated its gradient (post-accumulate hooks) the bucket is all-reduced
   (RCCL over xGMI, ``async_op``) while backward continues; the 1/world average is folded
-  into the fused AdamW kernel;
+  into the fused AdamW kernel; ``grad_wire_dtype`` (bf16 / f16) all-reduces 16-bit casts of
+  the buckets instead (half the bytes; BASELINE config 5's "fp16 grads");
 * AdamW = one fused HIP launch per group over the flat buffer, lr / step read from device
   memory, skipped (GradScaler semantics) when a gradient is non-finite;
 * after two eager steps the device side of the step is captured into a HIP graph and
@@ -118,8 +119,14 @@ class GradBucketer:
     graph is static), which all-reduces every bucket after backward; later steps overlap.
     """
 
-    def __init__(self, groups, bucket_bytes, process_group=None):
+    def __init__(self, groups, bucket_bytes, process_group=None, wire_dtype=None):
         self.pg = process_group
+        # wire_dtype (bf16 / f16): each bucket is cast into a persistent 16-bit buffer, summed
+        # over the ranks in that precision and cast back into the f32 gradients -- half the
+        # xGMI bytes per step (BASELINE config 5: "fp16 grads"), at 16-bit rounding of the
+        # per-rank gradients and of the ring's partial sums.  None: f32 all-reduce.
+        self.wire_dtype = None if wire_dtype in (None, torch.float32) else wire_dtype
+        self.wire = {}  # bucket index -> 16-bit buffer
         self.buckets = []       # (group, start, end)
         self.param_bucket = {}  # id(param) -> bucket index
         for g in groups:
@@ -144,12 +151,22 @@ class GradBucketer:
             for p in g.params:
                 self.handles.append(p.register_post_accumulate_grad_hook(self._hook))
 
+    def _reduce(self, b, g, s, e):
+        """Issue bucket b's all-reduce on the current stream: (work, 16-bit buffer or None)."""
+        if self.wire_dtype is None:
+            return dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True), None
+        buf = self.wire.get(b)
+        if buf is None:
+            buf = self.wire[b] = torch.empty(e - s, device=g.grad.device, dtype=self.wire_dtype)
+        buf.copy_(g.grad[s:e])
+        return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True), buf
+
     def _launch(self, b):
         g, s, e = self.buckets[b]
         self.launched[b] = True
         side = ops.side_stream(g.grad.device)
         if side is None:
-            self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+            self.works.append((b,) + self._reduce(b, g, s, e))
             return
         # the bucket's gradients come from both streams: issue from the side stream after it
         # has caught up with the main stream's work so far (the hook may fire while autograd
@@ -157,7 +174,7 @@ class GradBucketer:
         main = self.main_stream if self.main_stream is not None else torch.cuda.current_stream(g.grad.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            self.works.append(dist.all_reduce(g.grad[s:e], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+            self.works.append((b,) + self._reduce(b, g, s, e))
 
     def _hook(self, p):
         b = self.param_bucket[id(p)]
@@ -171,8 +188,11 @@ class GradBucketer:
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
-        for w in self.works:
+        for b, w, buf in self.works:
             w.wait()
+            if buf is not None:  # back into the f32 gradients, after the sum (stream-ordered)
+                g, s, e = self.buckets[b]
+                g.grad[s:e].copy_(buf)
         self.works = []
         self.pending = [0] * len(self.buckets)
         self.launched = [False] * len(self.buckets)
@@ -192,7 +212,7 @@ def reseed(seed, rank=0):
 class Trainer:
     def __init__(self, model, config, device, lr=None, amp_dtype=torch.bfloat16, bucket_mb=32,
                  world_size=1, process_group=None, rank=0, seed=None, skip_nonfinite=True, use_graph=None,
-                 graph_warmup=2):
+                 graph_warmup=2, grad_wire_dtype=None):
         self.model = model
         self.device = device
         self.amp_dtype = amp_dtype
@@ -230,7 +250,7 @@ class Trainer:
         self.step_count = 0
         self._shadow_fresh = False
         self.inv_world = torch.full((1,), 1.0 / world_size, device=device, dtype=torch.float32)
-        self.reducer = (GradBucketer(self.groups, int(bucket_mb * (1 << 20)), process_group)
+        self.reducer = (GradBucketer(self.groups, int(bucket_mb * (1 << 20)), process_group, grad_wire_dtype)
                         if world_size > 1 else None)
         # HIP-graph replay of the step (see step()).  use_graph: True / False, or None = the
         # MSU_GRAPH environment switch: "1" always, "0" never, "auto" (default) = capture only

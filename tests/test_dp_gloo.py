@@ -49,7 +49,7 @@ def _data(rank, n=6):
     return torch.randn(n, 16, generator=g), torch.randn(n, 8, generator=g)
 
 
-def _worker(rank, world, port, bucket_bytes, out):
+def _worker(rank, world, port, bucket_bytes, out, wire=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     m = _model()
@@ -57,7 +57,7 @@ def _worker(rank, world, port, bucket_bytes, out):
     decay = [(n, p) for n, p in named if not is_no_decay(n, p)][::-1]
     nodecay = [(n, p) for n, p in named if is_no_decay(n, p)][::-1]
     groups = [FlatGroup(decay, 0.01, "cpu"), FlatGroup(nodecay, 0.0, "cpu")]
-    red = GradBucketer(groups, bucket_bytes)
+    red = GradBucketer(groups, bucket_bytes, wire_dtype=wire)
     for step in range(3):  # step 0 learns the accumulation counts, later steps overlap
         x, y = _data(rank + 10 * step)
         loss = ((m(x) - y) ** 2).mean() / world  # each rank's share of the global mean
@@ -75,12 +75,16 @@ def _worker(rank, world, port, bucket_bytes, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket_bytes", [64, 1 << 20])
-def test_bucketed_allreduce_equals_global_batch(bucket_bytes):
+@pytest.mark.parametrize("bucket_bytes,wire", [(64, None), (1 << 20, None), (256, torch.bfloat16),
+                                               (1 << 20, torch.float16)])
+def test_bucketed_allreduce_equals_global_batch(bucket_bytes, wire):
+    """wire: the 16-bit gradient all-reduce (BASELINE config 5 'fp16 grads'): the sum is
+    taken over 16-bit casts of each rank's gradient, so it matches the global-batch gradient
+    to 16-bit rounding; every rank still ends with bitwise-identical gradients."""
     world = 2
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), bucket_bytes, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), bucket_bytes, out, wire), nprocs=world, join=True)
     for step in range(3):
         m = _model()
         named = list(m.named_parameters())
@@ -92,7 +96,12 @@ def test_bucketed_allreduce_equals_global_batch(bucket_bytes):
         ref = torch.cat([p.grad.reshape(-1) for p in decay + nodecay])
         g0, g1 = out[(0, step)], out[(1, step)]
         assert torch.equal(g0, g1), "ranks disagree"
-        torch.testing.assert_close(g0, ref, rtol=1e-5, atol=1e-6)
+        if wire is None:
+            torch.testing.assert_close(g0, ref, rtol=1e-5, atol=1e-6)
+        else:
+            eps = 2.0 ** -8 if wire == torch.bfloat16 else 2.0 ** -11
+            torch.testing.assert_close(g0, ref, rtol=3 * eps, atol=3 * eps * ref.abs().max().item())
+            assert not torch.equal(g0, ref)  # the wire really is 16-bit
 
 
 def test_no_decay_rule_matches_reference():
