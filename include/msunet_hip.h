@@ -150,6 +150,12 @@ int msu_tok_gemm_supported_epi(long M, int N, int K, int epi);
 int msu_tok_gemm(int dtype, const void* A, const void* A2, int K1, const void* W, const float* bias, void* Y,
                  void* Y2, const void* H, long M, int N, int K, int epi, void* stream);
 int msu_tok_gemm_plan(long M, int N, int K, long* out6);
+/* Tiled NT GEMM (128 x 128 tiles, LDS-DMA double buffering) for the stage 1-3 Linears, whose
+ * wide weights do not fit the token GEMM's LDS: same Y / epi semantics as msu_tok_gemm without
+ * the split-A input.  Covered: N % 32 == 0, K % 64 == 0. */
+int msu_nt_gemm_supported(long M, int N, int K);
+int msu_nt_gemm(int dtype, const void* A, const void* W, const float* bias, void* Y, void* Y2, const void* H,
+                long M, int N, int K, int epi, void* stream);
 
 /* ---------------------------------------------------------------- streaming ops
  * nn.GELU() (exact erf): torchvision MLP activation, FinalPatchExpand_X4_V2.act. */

@@ -583,9 +583,6 @@ def tok_supported_epi(M, N, K, epi):
     return r
 
 
-# GELU-epilogue GEMMs of the MLP on the token GEMM from this many tokens up (A/B switch
-# MSU_MLP_TOK_MIN_M): below it hipBLASLt + the standalone GELU kernels.
-_MLP_TOK_MIN_M = int(os.environ.get("MSU_MLP_TOK_MIN_M", "131072"))
 
 
 def tok_preferred(M, N, K):
@@ -606,6 +603,26 @@ def tok_gemm(a, w, bias=None, epi=TOK_PLAIN, h=None, a2=None):
     y2 = torch.empty_like(y) if epi == TOK_GELU_DUAL else None
     _lib.call("msu_tok_gemm", _dt(a), _p(a), _p(None if a2 is None else a2.contiguous()),
               K1 if a2 is not None else 0, _p(w), _p(bias), _p(y), _p(y2), _p(h), M, N, K, epi, _s(a))
+    return (y, y2) if epi == TOK_GELU_DUAL else y
+
+
+def nt_supported(M, N, K):
+    """Whether the tiled NT GEMM (csrc/gemm_nt.hip) covers this 16-bit Linear shape."""
+    key = ("nt", int(M), int(N), int(K))
+    r = _tok_cache.get(key)
+    if r is None:
+        r = _tok_cache[key] = bool(_lib.lib().msu_nt_gemm_supported(*key[1:]))
+    return r
+
+
+def nt_gemm(a, w, bias=None, epi=TOK_PLAIN, h=None):
+    """16-bit Y = epi(A . W^T + bias) on the tiled NT GEMM (tok_gemm's epilogues)."""
+    N, K = w.shape
+    M = a.numel() // K
+    a = a.contiguous()
+    y = torch.empty(*a.shape[:-1], N, device=a.device, dtype=a.dtype)
+    y2 = torch.empty_like(y) if epi == TOK_GELU_DUAL else None
+    _lib.call("msu_nt_gemm", _dt(a), _p(a), _p(w), _p(bias), _p(y), _p(y2), _p(h), M, N, K, epi, _s(a))
     return (y, y2) if epi == TOK_GELU_DUAL else y
 
 
@@ -659,14 +676,54 @@ def _shadow(param, dt):
     return param.to(dt)
 
 
-def _mm(a, w, bias=None):
-    """16-bit a . w^T (+ bias) on the token GEMM where preferred, else the library GEMM."""
+# GEMM routing of the 16-bit Linears (forward and input gradient): the token GEMM (weight in
+# LDS, tokens streamed) for the HBM-bound stage-0 shapes and the narrow-K stage-1 qkv, the
+# library GEMM (hipBLASLt) for the wide-weight stage 1-3 shapes.  The tiled NT GEMM
+# (csrc/gemm_nt.hip, MSU_GEMM_ROUTE=nt) beats hipBLASLt on 17 of the 21 stage 1-3 shapes in
+# isolation (tools/kbench.py nt: 1.0-1.7x) but costs 1-2 % of the overlapped training step
+# (GEMM routing), so it is opt-in.  MSU_GEMM_ROUTE=lib: the library GEMM wherever the
+# epilogue allows it.
+_ROUTE_FORCE = os.environ.get("MSU_GEMM_ROUTE", "")
+
+
+def gemm_route(M, N, K, epi=TOK_PLAIN):
+    """'tok' | 'nt' | 'lib' for a 16-bit Y = epi(A[M,K] . W[N,K]^T + b) (input gradients: W^T)."""
+    key = ("route", int(M), int(N), int(K), int(epi))
+    r = _tok_cache.get(key)
+    if r is None:
+        tok = tok_supported_epi(M, N, K, epi)
+        if _ROUTE_FORCE == "lib" and epi == TOK_PLAIN:
+            r = "lib"
+        elif tok and (M >= 262144 or (epi == TOK_PLAIN and N * K <= 576 * 192 and N >= 3 * K)):
+            r = "tok"
+        elif _ROUTE_FORCE == "nt" and nt_supported(M, N, K):
+            r = "nt"
+        elif tok and (N * K <= 576 * 192 or (epi != TOK_PLAIN and M >= 131072)):
+            r = "tok"
+        else:
+            r = "lib"
+        _tok_cache[key] = r
+    return r
+
+
+def _gemm(a, w, bias=None, epi=TOK_PLAIN, h=None):
+    """16-bit epi(a . w^T + bias) on the routed GEMM (bias: f32 [N] or None)."""
     N, K = w.shape
     M = a.numel() // K
-    if tok_preferred(M, N, K):
-        return tok_gemm(a, w, bias)
+    r = gemm_route(M, N, K, epi)
+    if r == "tok":
+        return tok_gemm(a, w, bias, epi, h)
+    if r == "nt":
+        return nt_gemm(a, w, bias, epi, h)
+    if epi != TOK_PLAIN:
+        raise RuntimeError(f"no HIP GEMM covers the epilogue {epi} at M={M} N={N} K={K}")
     with torch.autocast("cuda", enabled=False):
         return torch.nn.functional.linear(a, w, None if bias is None else bias.to(a.dtype))
+
+
+def _mm(a, w, bias=None):
+    """16-bit a . w^T (+ bias) on the routed GEMM."""
+    return _gemm(a, w, bias)
 
 
 # ----------------------------------------------------------------------------- Linear
@@ -678,8 +735,8 @@ def _linear_impl(x, weight, bias):
     w = _shadow(weight, dt)
     N, K = w.shape
     M = x.numel() // K
-    if dt in _LOW and tok_preferred(M, N, K):
-        return tok_gemm(x, w, None if bias is None else _f32(bias))
+    if dt in _LOW and gemm_route(M, N, K) != "lib":
+        return _gemm(x, w, None if bias is None else _f32(bias))
     b = None if bias is None else _shadow(bias, dt)
     with torch.autocast("cuda", enabled=False):
         return torch.nn.functional.linear(x, w, b)
@@ -704,8 +761,8 @@ def _linear_backward(ctx, dy):
     M = dy.numel() // N
     dx = None
     if ctx.needs_input_grad[0]:
-        if x.dtype in _LOW and tok_preferred(M, K, N):
-            dx = tok_gemm(dy, _wt(w))
+        if x.dtype in _LOW and gemm_route(M, K, N) != "lib":
+            dx = _gemm(dy, _wt(w))
         else:
             with torch.autocast("cuda", enabled=False):
                 dx = dy.matmul(w)
@@ -764,12 +821,7 @@ def _linear_cat_backward(ctx, dy):
     M = dy.numel() // N
     outs = []
     for lo, hi in ((0, C1), (C1, C1 + C2)):
-        wt = W[:, lo:hi].t().contiguous()
-        if tok_preferred(M, hi - lo, N):
-            outs.append(tok_gemm(dy, wt))
-        else:
-            with torch.autocast("cuda", enabled=False):
-                outs.append(dy.matmul(wt.t()))
+        outs.append(_gemm(dy, W[:, lo:hi].t().contiguous()))
     # weight gradient per half into temporaries ([N, C1], [N, C2]), bias with the first
     dw1, db = _wgrad_tmp(dy, x, N, C1, M, with_bias=True)
     dw2, _ = _wgrad_tmp(dy, skip, N, C2, M, with_bias=False)
@@ -804,19 +856,17 @@ def linear_cat(x, skip, weight, bias):
 
 # ----------------------------------------------------------------------------- fused MLP
 def mlp_fusable(x, fc1_weight, fc2_weight):
-    """torchvision MLP (mlp.0 -> GELU -> mlp.3) fusable on the token GEMM in 16-bit?"""
+    """torchvision MLP (mlp.0 -> GELU -> mlp.3) fusable in 16-bit: the two GELU-epilogue GEMMs
+    (mlp.0 forward, mlp.3 input gradient: both [M,C] x [C,Hd]) have a HIP GEMM (token GEMM
+    or tiled NT GEMM), the other two run on whichever GEMM is routed for their shape."""
     if act_dtype() not in _LOW:
         return False
     Hd, C = fc1_weight.shape
     M = x.numel() // C
     if fc2_weight.shape != (C, Hd):
         return False
-    if tok_preferred(M, Hd, C) and tok_preferred(M, C, Hd):
-        return True
-    # the two GELU-epilogue GEMMs (mlp.0 forward, mlp.3 input gradient: both [M,C]x[C,Hd])
-    # on the token GEMM, the other two on whichever GEMM is preferred for their shape
-    return (M >= _MLP_TOK_MIN_M and tok_supported_epi(M, Hd, C, TOK_GELU_DUAL) and
-            tok_supported_epi(M, Hd, C, TOK_GELU_GRAD))
+    return (gemm_route(M, Hd, C, TOK_GELU_DUAL) != "lib" and
+            gemm_route(M, Hd, C, TOK_GELU_GRAD) != "lib")
 
 
 def _mlp_impl(x, w1, b1, w2, b2):
@@ -826,8 +876,8 @@ def _mlp_impl(x, w1, b1, w2, b2):
     _need_cuda(x)
     W1 = _shadow(w1, x.dtype)
     W2 = _shadow(w2, x.dtype)
-    h, g = tok_gemm(x, W1, _f32(b1), TOK_GELU_DUAL)
-    y = _mm(g, W2, _f32(b2))
+    h, g = _gemm(x, W1, _f32(b1), TOK_GELU_DUAL)
+    y = _gemm(g, W2, _f32(b2))
     return y, h, g
 
 
@@ -854,9 +904,9 @@ def _mlp_backward(ctx, dy, _dh, _dg):
     Hd, C = W1.shape
     M = x.numel() // C
     dw2, db2 = _wgrad(dy, g, w2, b2, M, C, Hd)
-    dh = tok_gemm(dy, _wt(W2), None, TOK_GELU_GRAD, h=h)
+    dh = _gemm(dy, _wt(W2), None, TOK_GELU_GRAD, h=h)
     dw1, db1 = _wgrad(dh, x, w1, b1, M, Hd, C)
-    dx = _mm(dh, _wt(W1)) if ctx.needs_input_grad[0] else None
+    dx = _gemm(dh, _wt(W1)) if ctx.needs_input_grad[0] else None
     return dx, dw1, db1, dw2, db2
 
 
@@ -1138,8 +1188,8 @@ def _linear_gelu_impl(x, weight):
     w = _shadow(weight, dt)
     N, K = w.shape
     M = x.numel() // K
-    if dt in _LOW and tok_supported(M, N, K):
-        return tok_gemm(x, w, torch.zeros(N, device=x.device, dtype=torch.float32), TOK_GELU_DUAL)
+    if dt in _LOW and gemm_route(M, N, K, TOK_GELU_DUAL) != "lib":
+        return _gemm(x, w, torch.zeros(N, device=x.device, dtype=torch.float32), TOK_GELU_DUAL)
     with torch.autocast("cuda", enabled=False):
         y = torch.nn.functional.linear(x, w)
     g = torch.empty_like(y)
@@ -1171,8 +1221,8 @@ def _linear_gelu_backward(ctx, dy, _dg):
     M = dy.numel() // N
     dx = None
     if ctx.needs_input_grad[0]:
-        if x.dtype in _LOW and tok_preferred(M, K, N):
-            dx = tok_gemm(dy, _wt(w))
+        if x.dtype in _LOW and gemm_route(M, K, N) != "lib":
+            dx = _gemm(dy, _wt(w))
         else:
             with torch.autocast("cuda", enabled=False):
                 dx = dy.matmul(w)

@@ -1,0 +1,115 @@
+"""GPU: the tiled NT GEMM (csrc/gemm_nt.hip) against plain fp32 PyTorch, and its routing.
+
+Reference: fp32 matmul of the same 16-bit-rounded operands, then the epilogue in fp32 (same
+bar as the token GEMM's tests: one rounding of the f32 accumulator to bf16 / f16 and another
+summation order -> |y - ref| <= 1e-2 |ref| + 4e-3 max|ref|).  Shapes: the Swin-T stage 1-3
+Linears (forward and input gradient) at small M, plus ragged M (not a multiple of the 128-row
+tile), N not a multiple of the 128-column tile (N % 32 == 0) and single-K-step K = 64.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+SHAPES = [(4096, 1152, 384), (4096, 384, 1152), (1000, 384, 384), (2048, 768, 192), (777, 192, 768),
+          (300, 2304, 768), (128, 768, 3072), (513, 96, 64), (64, 160, 128), (1, 32, 64)]
+
+
+def _ops():
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    return ops
+
+
+@pytest.fixture(params=[torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+def low(request):
+    return request.param
+
+
+def _check(y, ref, what):
+    y = y.float()
+    scale = ref.abs().max().item()
+    err = (y - ref).abs() - 1e-2 * ref.abs()
+    assert err.max().item() <= 4e-3 * scale, f"{what}: excess err {err.max().item():.3e} vs scale {scale:.3e}"
+
+
+def _inputs(M, N, K, seed, low):
+    g = torch.Generator().manual_seed(seed)
+    a = torch.randn(M, K, generator=g).to(DEV, low)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV, low)
+    b = torch.randn(N, generator=g).to(DEV)
+    return a, w, b
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("bias", [False, True])
+def test_nt_gemm_plain(M, N, K, bias, low):
+    ops = _ops()
+    assert ops.nt_supported(M, N, K)
+    a, w, b = _inputs(M, N, K, M + N + K, low)
+    y = ops.nt_gemm(a, w, b if bias else None)
+    ref = F.linear(a.float(), w.float(), b if bias else None)
+    assert y.dtype == low and y.shape == (M, N)
+    _check(y, ref, "y")
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 1536, 384), (777, 768, 192), (300, 3072, 768)])
+def test_nt_gemm_gelu_epilogues(M, N, K, low):
+    """EPI 1: (H, GELU(H)) of mlp.0; EPI 2: (dY . W2) * GELU'(H) -- mlp.3's input gradient
+    through the activation (W2^T [N, K'] passed as the weight)."""
+    ops = _ops()
+    a, w, b = _inputs(M, N, K, 7 * M + N, low)
+    h, g = ops.nt_gemm(a, w, b, ops.TOK_GELU_DUAL)
+    href = F.linear(a.float(), w.float(), b)
+    _check(h, href, "h")
+    _check(g, F.gelu(h.float()), "gelu(h)")
+    gen = torch.Generator().manual_seed(M)
+    dy = torch.randn(M, K, generator=gen).to(DEV, low)
+    w2t = (torch.randn(N, K, generator=gen) / K ** 0.5).to(DEV, low)  # [Hd, C] = W2^T
+    dh = ops.nt_gemm(dy, w2t, None, ops.TOK_GELU_GRAD, h=h)
+    hf = h.float().requires_grad_(True)
+    F.gelu(hf).backward(torch.ones_like(hf))
+    ref = F.linear(dy.float(), w2t.float()) * hf.grad
+    _check(dh, ref, "dh")
+
+
+def test_nt_gemm_rejects_uncovered_shapes():
+    ops = _ops()
+    assert not ops.nt_supported(4096, 100, 384)  # N % 32
+    assert not ops.nt_supported(4096, 384, 96)   # K % 64
+    a = torch.zeros(64, 96, device=DEV, dtype=torch.bfloat16)
+    w = torch.zeros(64, 96, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        ops.nt_gemm(a, w)
+
+
+@pytest.mark.parametrize("M,N,K", [(32768, 1152, 384), (8192, 768, 3072), (131072, 192, 384)])
+def test_linear_routes_stage_shapes_to_nt_and_matches(M, N, K, monkeypatch):
+    """ops.linear at stage 1-3 shapes (bf16 autocast) with the NT GEMM routed in
+    (MSU_GEMM_ROUTE=nt): forward and input gradient on the NT GEMM, weight gradient on the HIP
+    wgrad kernel; all against fp32 autograd."""
+    ops = _ops()
+    monkeypatch.setattr(ops, "_ROUTE_FORCE", "nt")
+    monkeypatch.setattr(ops, "_tok_cache", {})
+    assert ops.gemm_route(M, N, K) == "nt" and ops.gemm_route(M, K, N) == "nt"
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    dy = torch.randn(M, N, generator=g)
+    xr = x.bfloat16().float().requires_grad_(True)
+    wr = w.bfloat16().float()
+    yr = F.linear(xr, wr, b)
+    yr.backward(dy.bfloat16().float())
+    xg = x.to(DEV, torch.bfloat16).requires_grad_(True)
+    wg = w.to(DEV).requires_grad_(True)
+    bg = b.to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.linear(xg, wg, bg)
+    y.backward(dy.to(DEV, torch.bfloat16))
+    _check(y, yr.detach().to(DEV), "y")
+    _check(xg.grad, xr.grad.to(DEV), "dx")
+    gw = wg.grad.float().cpu()
+    wref = dy.bfloat16().float().t() @ xr.detach()
+    assert ((gw - wref).norm() / wref.norm()).item() < 1e-2

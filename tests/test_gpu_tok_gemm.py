@@ -134,13 +134,16 @@ def test_fused_mlp_matches_fp32(M, C, low):
         assert err <= 3e-2 * r.abs().max().item(), f"{name}: {err:.3e} vs {r.abs().max().item():.3e}"
 
 
-@pytest.mark.parametrize("M,C", [(1024, 384), (2048, 192)])
+@pytest.mark.parametrize("M,C", [(1024, 384), (2048, 192), (1000, 768)])
 def test_fused_mlp_mixed_routing(M, C, monkeypatch, low):
-    """Stage-1/2 widths: the GELU-epilogue GEMMs on the token GEMM, mlp.3 forward and mlp.0's
-    input gradient on hipBLASLt (ops._mm) -- same numerics bar as the all-token-GEMM MLP."""
+    """Stage-1/2/3 widths with the NT GEMM routed in (MSU_GEMM_ROUTE=nt): the GELU-epilogue
+    GEMMs on the tiled NT GEMM, the other two on whichever GEMM is routed -- same numerics bar
+    as the all-token-GEMM MLP."""
     ops = _ops()
-    monkeypatch.setattr(ops, "_MLP_TOK_MIN_M", 0)
-    assert not (ops.tok_preferred(M, 4 * C, C) and ops.tok_preferred(M, C, 4 * C))
+    monkeypatch.setattr(ops, "_ROUTE_FORCE", "nt")
+    monkeypatch.setattr(ops, "_tok_cache", {})
+    assert ops.gemm_route(M, 4 * C, C, ops.TOK_GELU_DUAL) == "nt"
+    assert ops.gemm_route(M, 4 * C, C, ops.TOK_GELU_GRAD) == "nt"
     test_fused_mlp_matches_fp32(M, C, low)
 
 

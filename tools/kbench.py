@@ -184,8 +184,36 @@ def tok():
         print(line, flush=True)
 
 
+def nt():
+    """Tiled NT GEMM vs hipBLASLt (and the token GEMM) at the stage 1-3 forward and
+    input-gradient shapes (M tokens, N outputs, K inputs)."""
+    shapes = [(B * 16384, 192, 384), (B * 16384, 576, 192), (B * 16384, 192, 192), (B * 16384, 768, 192),
+              (B * 16384, 192, 768), (B * 16384, 192, 576), (B * 16384, 384, 192),
+              (B * 4096, 1152, 384), (B * 4096, 384, 1152), (B * 4096, 384, 384), (B * 4096, 1536, 384),
+              (B * 4096, 384, 1536), (B * 4096, 384, 768), (B * 4096, 768, 384),
+              (B * 1024, 2304, 768), (B * 1024, 768, 2304), (B * 1024, 768, 768), (B * 1024, 3072, 768),
+              (B * 1024, 768, 3072), (B * 1024, 768, 1536), (B * 1024, 1536, 768)]
+    for M, N, K in shapes:
+        a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+        w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+        bias = torch.randn(N, device=DEV)
+        bb = bias.bfloat16()
+        fl = 2.0 * M * N * K
+        mt = timeit(lambda: torch.nn.functional.linear(a, w, bb))
+        line = f"nt M={M:7d} N={N:5d} K={K:5d}: hipBLASLt {mt*1e3:6.1f} us ({fl/mt/1e9:6.1f} TF/s)"
+        if ops.nt_supported(M, N, K):
+            ms = timeit(lambda: ops.nt_gemm(a, w, bias))
+            ref = torch.nn.functional.linear(a.float(), w.float(), bias)
+            err = ((ops.nt_gemm(a, w, bias).float() - ref).norm() / ref.norm()).item()
+            line += f"  nt {ms*1e3:6.1f} us ({fl/ms/1e9:6.1f} TF/s, rel err {err:.1e})"
+        if ops.tok_supported(M, N, K):
+            mk = timeit(lambda: ops.tok_gemm(a, w, bias))
+            line += f"  tok {mk*1e3:6.1f} us"
+        print(line, flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
-    for name, fn in (("attn", attn), ("wgrad", wgrad), ("conv", conv), ("ln", ln), ("lnadd", lnadd), ("tok", tok), ("stream", stream)):
+    for name, fn in (("attn", attn), ("wgrad", wgrad), ("conv", conv), ("ln", ln), ("lnadd", lnadd), ("tok", tok), ("nt", nt), ("stream", stream)):
         if what in (name, "all"):
             fn()
