@@ -215,6 +215,19 @@ int msu_nonfinite(const float* x, long n, float* flag, void* stream);
 int msu_nonfinite2(const float* x0, long n0, const float* x1, long n1, float* flag, void* stream);
 int msu_cast(int dtype, const float* x, void* y, long n, void* stream);
 
+/* ---------------------------------------------------------------- input pipeline
+ * The per-sample CPU transform of the reference's DataLoader workers (dataset/dataset.py:20-95
+ * RandomGenerator: albumentations ToGray / RandomBrightnessContrast / HueSaturationValue /
+ * OneOf(RandomGamma, GaussianBlur), random_flip, /255 and label > 127; :97-119 DataPrepartion)
+ * as one pass over a decoded uint8 batch.  img [B, H, W, 3] u8 (PIL RGB), label [B, H, W] u8
+ * (PIL "L") or null; ops [B][2] i32 = (bits: 1 gray, 2 brightness/contrast, 4 HSV, 8 gamma,
+ * 16 hflip; blur ksize 0/3/5) and luts [B][5][256] u8 (brightness/contrast, hue, saturation,
+ * value, gamma; built on the host as albumentations builds them), both null for normalisation
+ * only; out [B, 3, H, W] f32 = u8/255, out_label [B, H, W] f32 in {0, 1}. */
+int msu_augment_batch(const unsigned char* img, const unsigned char* label, const int* ops,
+                      const unsigned char* luts, float* out, float* out_label, int B, int H, int W,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -212,8 +212,29 @@ def nt():
         print(line, flush=True)
 
 
+def aug():
+    """msu_augment_batch at the bench batch (8 x 1024^2): 4 B read + 16 B written per pixel."""
+    import random
+    import numpy as np
+    from semantic_segmentation_of_stylegan2_artifacts_amd.dataset import augment as A
+    from semantic_segmentation_of_stylegan2_artifacts_amd.dataset.dataset import augment_batch
+    H = W = 1024
+    img = torch.randint(0, 256, (B, H, W, 3), device=DEV, dtype=torch.uint8)
+    lbl = torch.randint(0, 256, (B, H, W), device=DEV, dtype=torch.uint8)
+    byts = B * H * W * 20
+    for name, draw in (("none", lambda i: (0, 0, A.identity_luts())),
+                       ("drawn", lambda i: A.draw(A.sample_rng(1, 0, i), True, True)),
+                       ("hsv+blur5", lambda i: (A.BC | A.HSV | A.FLIP, 5, A.identity_luts())),
+                       ("hsv", lambda i: (A.BC | A.HSV, 0, A.identity_luts()))):
+        d = [draw(i) for i in range(B)]
+        ops_t = torch.tensor([[o, k] for o, k, _ in d], dtype=torch.int32, device=DEV)
+        luts = torch.from_numpy(np.stack([l for _, _, l in d])).to(DEV)
+        ms = timeit(lambda: augment_batch(img, lbl, ops_t, luts))
+        print(f"augment {name:10s} {ms*1e3:7.1f} us  {byts/ms/1e6:7.1f} GB/s", flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
-    for name, fn in (("attn", attn), ("wgrad", wgrad), ("conv", conv), ("ln", ln), ("lnadd", lnadd), ("tok", tok), ("nt", nt), ("stream", stream)):
+    for name, fn in (("attn", attn), ("wgrad", wgrad), ("conv", conv), ("ln", ln), ("lnadd", lnadd), ("tok", tok), ("nt", nt), ("stream", stream), ("aug", aug)):
         if what in (name, "all"):
             fn()
