@@ -15,7 +15,9 @@ JSON line.
 Extra objects: ``roofline`` for the dominant kernel (timed live with HIP events on its
 stream), ``roofline_attention`` (window attention), ``roofline_decoder`` (the decoder head
 stack fwd+bwd against the HBM roofline) and ``cpu_baseline`` (the CPU oracle's training step,
-Swin-T and Swin-B, on the box's host cores).
+Swin-T and Swin-B, on the box's host cores) and ``input_pipeline`` (the augmentation kernel's
+HBM roofline, and training steps fed from PNG files through the GPU input pipeline: the
+decode- and PCIe-inclusive rate next to the resident one).
 """
 import argparse
 import json
@@ -44,6 +46,8 @@ def parse():
     ap.add_argument("--backbone", default="swin_t")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-input-pipeline", action="store_true",
+                    help="skip the PNG -> GpuBatchLoader -> train-step leg (runs after the timed region)")
     ap.add_argument("--skip-dead", action="store_true", help="skip the reference's discarded branches (exact)")
     ap.add_argument("--grad-wire", choices=["f32", "bf16", "fp16"], default="f32",
                     help="DP gradient all-reduce precision (BASELINE config 5: fp16 grads)")
@@ -325,6 +329,115 @@ def dice_vs_reference(device):
     return out
 
 
+def _write_png_set(root, n_fake, n_real, img, seed, unique=4):
+    """Synthetic StyleGAN2-shaped PNG files in the reference's layout (dataset.py:141-144):
+    smooth colour fields + noise (compressible like a photo) and the synthetic artifact masks;
+    ``unique`` distinct files per kind, the rest hard links (every file is decoded anyway)."""
+    import numpy as np
+    from PIL import Image
+    from semantic_segmentation_of_stylegan2_artifacts_amd.data import synthetic_batch
+    g = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:img, 0:img].astype(np.float32) / img
+    for kind, n in (("fake", n_fake), ("real", n_real)):
+        os.makedirs(os.path.join(root, kind + "_images"), exist_ok=True)
+        os.makedirs(os.path.join(root, kind + "_labels"), exist_ok=True)
+        names = [f"{kind}{i:04d}" for i in range(n)]
+        with open(os.path.join(root, kind + ".txt"), "w") as f:
+            f.write("\n".join(names) + "\n")
+        u = min(unique, n)
+        _, masks = synthetic_batch(u, img, "cpu", seed + (kind == "real"), fake_ratio=1.0 if kind == "fake" else 0.0)
+        for i, name in enumerate(names):
+            ip = os.path.join(root, kind + "_images", name + ".png")
+            lp = os.path.join(root, kind + "_labels", name + "_mask.png")
+            if i >= u:
+                os.link(os.path.join(root, kind + "_images", names[i % u] + ".png"), ip)
+                os.link(os.path.join(root, kind + "_labels", names[i % u] + "_mask.png"), lp)
+                continue
+            a, b, c = g.random(3) * 6
+            base = np.stack([np.sin(a * xx + b * yy), np.cos(b * xx - c * yy), np.sin(c * (xx + yy))], -1)
+            im = np.clip((base * 0.4 + 0.5) * 255 + g.normal(0, 6, (img, img, 3)), 0, 255).astype(np.uint8)
+            Image.fromarray(im).save(ip, compress_level=1)
+            lab = masks[i].numpy() if kind == "fake" else np.zeros((img, img), np.float32)
+            Image.fromarray((lab > 0).astype(np.uint8) * 255).save(lp, compress_level=1)
+
+
+def input_pipeline_leg(device, trainer, batch, img, seed, resident_ms):
+    """The reference's input path (PNG decode, augmentation, /255, H2D: trainer.py:239-245,
+    :299-300) in front of the same training step: ``augment_kernel`` = msu_augment_batch at the
+    bench batch against the HBM roofline (20 B / pixel); ``loader_fed`` = training steps fed by
+    GpuBatchLoader from PNG files on the box's disk (decode on host threads, pinned uint8
+    upload, GPU augmentation), i.e. the PCIe- and decode-inclusive rate next to the resident one."""
+    import shutil
+    import tempfile
+    import numpy as np
+    from semantic_segmentation_of_stylegan2_artifacts_amd.dataset import (GpuBatchLoader, RandomGenerator,
+                                                                          SegArtifact_dataset, epoch_plan)
+    from semantic_segmentation_of_stylegan2_artifacts_amd.dataset import augment as A
+    from semantic_segmentation_of_stylegan2_artifacts_amd.dataset.dataset import augment_batch
+    out = {}
+    imgs = torch.randint(0, 256, (batch, img, img, 3), device=device, dtype=torch.uint8)
+    lbls = torch.randint(0, 256, (batch, img, img), device=device, dtype=torch.uint8)
+    draws = [A.draw(A.sample_rng(seed, 0, i), True, True) for i in range(batch)]
+    ops_t = torch.tensor([[o, k] for o, k, _ in draws], dtype=torch.int32, device=device)
+    luts = torch.from_numpy(np.stack([l for _, _, l in draws])).to(device)
+    for _ in range(2):
+        augment_batch(imgs, lbls, ops_t, luts)
+    torch.cuda.synchronize()
+    n = 20
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        augment_batch(imgs, lbls, ops_t, luts)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    byts = batch * img * img * 20
+    out["augment_kernel"] = {"kernel": "augment_kernel (msu_augment_batch, drawn ops)", "bound": "hbm",
+                             "achieved": round(byts / ms / 1e6, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(byts / ms / 1e6 / HBM_PEAK_GBS, 4), "bytes_per_launch": byts,
+                             "ms_per_launch": round(ms, 4),
+                             "ops": [[int(o), int(k)] for o, k, _ in draws]}
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    root = tempfile.mkdtemp(prefix="msu_png_")
+    try:
+        n_fake, n_real = 6 * batch, 4 * batch
+        _write_png_set(root, n_fake, n_real, img, seed)
+        tf = RandomGenerator(output_size=[img, img], random_flip_flag=True, transform=True)
+        db_fake = SegArtifact_dataset(root, root, "fake", transform=tf)
+        db_real = SegArtifact_dataset(root, root, "real", transform=tf)
+        t = time.perf_counter()
+        for i in range(4):
+            db_fake.read_raw(i)
+        decode_ms = (time.perf_counter() - t) / 4 * 1e3
+        mixed, sampler, _, _ = epoch_plan(db_fake, db_real, epoch_num=0, seed=seed)
+        loader = GpuBatchLoader(mixed, sampler, device=device, num_threads=threads, slots=3, seed=seed,
+                                epoch=0, batches_per_step=batch // 2)
+        it = iter(loader)
+        warm = 2
+        for _ in range(warm):
+            b = next(it)
+            trainer.step(b["image"], b["label"])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        k = 0
+        for b in it:
+            last = trainer.step(b["image"], b["label"])
+            k += 1
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        out["loader_fed"] = {
+            "value": round(k * batch / el, 3), "unit": "images/s", "steps": k, "warmup": warm,
+            "ms_per_step": round(el / k * 1e3, 3), "resident_ms_per_step": round(resident_ms, 3),
+            "decode_threads": threads, "png_decode_ms_per_image": round(decode_ms, 2),
+            "final_loss": round(last.item(), 6),
+            "sample": f"{n_fake} fake + {n_real} real synthetic {img}^2 PNGs (compress_level 1), epoch plan "
+                      f"real ratio 0.4, BatchPatternSampler pairs x {batch // 2} per step, RandomGenerator "
+                      f"(transform + flip) on the GPU"}
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -404,6 +517,9 @@ def main():
             res["roofline_attention"] = attention_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM,
                                                            cfg.MODEL.SWIN.NUM_HEADS[0], cfg.MODEL.ATTN_DROP_RATE)
             res["roofline_decoder"] = decoder_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM)
+        if not args.no_input_pipeline and world == 1:
+            res["input_pipeline"] = input_pipeline_leg(device, trainer, args.batch, args.img, cfg.SEED,
+                                                       elapsed / args.steps * 1e3)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline()
             res["dice_vs_ref"] = dice_vs_reference(device)

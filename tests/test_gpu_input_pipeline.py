@@ -157,7 +157,10 @@ def test_loader_end_to_end(tmp_path):
     mixed, sampler, _, _ = epoch_plan(db_fake, db_real, epoch_num=2, seed=120)
     ld = GpuBatchLoader(mixed, sampler, device=DEV, num_threads=4, slots=2, seed=120, epoch=2, batches_per_step=2)
     from semantic_segmentation_of_stylegan2_artifacts_amd.dataset.loader import resolve
-    steps = list(ld.steps())
+    # the expected index lists from a second plan of the same epoch (a sampler pass reshuffles
+    # its pattern in place, so a pass over ld's own sampler here would change ld's batches)
+    _, sampler2, _, _ = epoch_plan(db_fake, db_real, epoch_num=2, seed=120)
+    steps = list(GpuBatchLoader(mixed, sampler2, device=DEV, batches_per_step=2).steps())
     seen = 0
     for k, batch in enumerate(ld):
         idx = steps[k]
