@@ -27,6 +27,10 @@
 #include "common.h"
 #include "reduce.h"
 
+#ifndef MSU_EXP
+#define MSU_EXP 0
+#endif
+
 namespace {
 
 template <typename F, int... Is>
@@ -472,7 +476,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     const int o = 8 * (lane & 3);
     static_for([&](auto CI) {
       constexpr int c = decltype(CI)::value;
-      int rg;
+      int rg;  // (a __shfl of tokt from lane (lane>>2) + 16c measured no faster)
       const int tok = token_of(g, win, 32 * w + (lane >> 2) + 16 * c, &rg);
       const bf16_t* rb = rowbase(tok);
       rq[buf][c] = *reinterpret_cast<const u32x4*>(rb + cq + o);
@@ -484,6 +488,9 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
   };
   auto step = [&](auto BUF, long win) __attribute__((always_inline)) -> bool {
     constexpr int buf = decltype(BUF)::value;
+#if (MSU_EXP & 2)
+    prep(win, BUF);
+#endif
     static_for([&](auto CI) {
       constexpr int c = decltype(CI)::value;
       const int off = (32 * w + (lane >> 2) + 16 * c) * LD + 8 * (lane & 3);
@@ -492,20 +499,11 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
       *reinterpret_cast<u32x4*>(L.v + off) = rv[buf][c];
       *reinterpret_cast<u32x4*>(L.dO + off) = rd[buf][c];
     }, std::make_integer_sequence<int, 2>{});
-    __syncthreads();  // rows + this window's token table visible to both waves
-    const long nxt = win + nblk;
-    const bool more = nxt < g.nwin;
-    if (more) prep(nxt, std::integral_constant<int, buf ^ 1>{});
-    const bool boundary = bnd[buf];
-    const int* sTok = L.tok[buf];
-    const int* sReg = L.reg[buf];
-    // ---- score pass: query tile it = w
     const int it = w;
-    const int i = it * 32 + (lane & 31);
-    uint32_t kmask = ~0u;  // bit jt*16+r: (i, key jt*32 + crow(r, hh)) kept by the dropout
-    if constexpr (DROP)  // the forward's mask, regenerated from the seed
-      kmask = drop_bits<true>(drop_seed32(seed), (uint32_t)win * g.nh + h, i, hh, drop_thresh16(p_drop));
     f32x16 P[2], D[2];
+    // the bias-image loads go out BEFORE the next window's prefetch: vmcnt retires in order, so
+    // a load issued after the prefetch would wait for the prefetch's HBM latency here
+#if !(MSU_EXP & 1)
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
       const float4* bp = reinterpret_cast<const float4*>(bimg + ((jt * 2 + it) * 64 + lane) * 16);
@@ -516,6 +514,33 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
       }
       D[jt] = f32x16{0};
     }
+#endif
+    __syncthreads();  // rows + this window's token table visible to both waves
+    const long nxt = win + nblk;
+    const bool more = nxt < g.nwin;
+#if !(MSU_EXP & 2)
+    if (more) prep(nxt, std::integral_constant<int, buf ^ 1>{});
+#endif
+#if (MSU_EXP & 1)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      const float4* bp = reinterpret_cast<const float4*>(bimg + ((jt * 2 + it) * 64 + lane) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = bp[q];
+        P[jt][4 * q] = v.x; P[jt][4 * q + 1] = v.y; P[jt][4 * q + 2] = v.z; P[jt][4 * q + 3] = v.w;
+      }
+      D[jt] = f32x16{0};
+    }
+#endif
+    const bool boundary = bnd[buf];
+    const int* sTok = L.tok[buf];
+    const int* sReg = L.reg[buf];
+    // ---- score pass: query tile it = w
+    const int i = it * 32 + (lane & 31);
+    uint32_t kmask = ~0u;  // bit jt*16+r: (i, key jt*32 + crow(r, hh)) kept by the dropout
+    if constexpr (DROP)  // the forward's mask, regenerated from the seed
+      kmask = drop_bits<true>(drop_seed32(seed), (uint32_t)win * g.nh + h, i, hh, drop_thresh16(p_drop));
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 qf = frag_rows(L.q, LD, 32 * it, 16 * ks, lane);
@@ -572,7 +597,11 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     bf16_t* row = dqkv + (size_t)((unsigned)(tok >= 0 ? tok : 0) * (unsigned)C3) + h * HD;
     {
       f32x16 av = f32x16{0}, ak = f32x16{0};
+#if (MSU_EXP & 4)
 #pragma unroll
+#else
+#pragma unroll 1  // unrolled, the fragment reads of all four k steps were hoisted: 17 VGPRs spilled
+#endif
       for (int ks = 0; ks < 64; ks += 16) {
         av = mfma32<T>(frag_tr_q4(L.dO, LD, ks, 0, lane), frag_tr_q4(L.P, LDP, ks, mt * 32, lane), av);
         ak = mfma32<T>(frag_tr_q4(L.q, LD, ks, 0, lane), frag_tr_q4(L.dS, LDP, ks, mt * 32, lane), ak);
@@ -586,7 +615,11 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     }
     {
       f32x16 aq = f32x16{0};
+#if (MSU_EXP & 4)
 #pragma unroll
+#else
+#pragma unroll 1  // unrolled, the fragment reads of all four k steps were hoisted: 17 VGPRs spilled
+#endif
       for (int ks = 0; ks < 64; ks += 16)
         aq = mfma32<T>(frag_tr(L.k, LD, ks, 0, lane), frag_rows(L.dS, LDP, mt * 32, ks, lane), aq);
       store_slice<T>(row, aq, scale, hh, tok >= 0);
@@ -599,7 +632,9 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
   const long win0 = blockIdx.x;
   if (win0 < g.nwin) {  // block-uniform
     long win = win0;
+#if !(MSU_EXP & 2)
     prep(win, std::integral_constant<int, 0>{});
+#endif
     for (;;) {
       if (!step(std::integral_constant<int, 0>{}, win)) break;
       win += nblk;

@@ -16,6 +16,6 @@ for m in $2; do
 done
 if [ "$3" = "bench" ]; then
   echo "== bench"
-  timeout -k 10 300 python -u $R/bench.py --no-cpu-baseline > $O/iter_bench.json 2> $O/iter_bench.err || { tail -30 $O/iter_bench.err; exit 1; }
+  timeout -k 10 300 python -u $R/bench.py --no-cpu-baseline --no-input-pipeline > $O/iter_bench.json 2> $O/iter_bench.err || { tail -30 $O/iter_bench.err; exit 1; }
   cat $O/iter_bench.json
 fi

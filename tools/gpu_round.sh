@@ -16,7 +16,7 @@ cat $O/bench_$TAG.json
 echo "== rocprof kernel trace"
 # eager (the bench's own choice at 1024^2; under the profiler the auto policy would capture)
 MSU_GRAPH=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o run --output-format csv -- \
-    python3 $R/bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-roofline > $O/prof_$TAG.log 2>&1 || { tail -30 $O/prof_$TAG.log; exit 1; }
+    python3 $R/bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-roofline --no-input-pipeline > $O/prof_$TAG.log 2>&1 || { tail -30 $O/prof_$TAG.log; exit 1; }
 python3 $R/tools/stream_summary.py $O/prof_$TAG/run_kernel_trace.csv > $O/streams_$TAG.txt
 echo "== HBM counters (conv fwd)"
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_$TAG -o fetch --output-format csv -- \
