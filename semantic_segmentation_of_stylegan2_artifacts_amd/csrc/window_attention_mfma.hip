@@ -27,10 +27,6 @@
 #include "common.h"
 #include "reduce.h"
 
-#ifndef MSU_EXP
-#define MSU_EXP 0
-#endif
-
 namespace {
 
 template <typename F, int... Is>
@@ -488,9 +484,6 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
   };
   auto step = [&](auto BUF, long win) __attribute__((always_inline)) -> bool {
     constexpr int buf = decltype(BUF)::value;
-#if (MSU_EXP & 2)
-    prep(win, BUF);
-#endif
     static_for([&](auto CI) {
       constexpr int c = decltype(CI)::value;
       const int off = (32 * w + (lane >> 2) + 16 * c) * LD + 8 * (lane & 3);
@@ -503,7 +496,6 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     f32x16 P[2], D[2];
     // the bias-image loads go out BEFORE the next window's prefetch: vmcnt retires in order, so
     // a load issued after the prefetch would wait for the prefetch's HBM latency here
-#if !(MSU_EXP & 1)
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt) {
       const float4* bp = reinterpret_cast<const float4*>(bimg + ((jt * 2 + it) * 64 + lane) * 16);
@@ -514,25 +506,10 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
       }
       D[jt] = f32x16{0};
     }
-#endif
     __syncthreads();  // rows + this window's token table visible to both waves
     const long nxt = win + nblk;
     const bool more = nxt < g.nwin;
-#if !(MSU_EXP & 2)
     if (more) prep(nxt, std::integral_constant<int, buf ^ 1>{});
-#endif
-#if (MSU_EXP & 1)
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      const float4* bp = reinterpret_cast<const float4*>(bimg + ((jt * 2 + it) * 64 + lane) * 16);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = bp[q];
-        P[jt][4 * q] = v.x; P[jt][4 * q + 1] = v.y; P[jt][4 * q + 2] = v.z; P[jt][4 * q + 3] = v.w;
-      }
-      D[jt] = f32x16{0};
-    }
-#endif
     const bool boundary = bnd[buf];
     const int* sTok = L.tok[buf];
     const int* sReg = L.reg[buf];
@@ -597,11 +574,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     bf16_t* row = dqkv + (size_t)((unsigned)(tok >= 0 ? tok : 0) * (unsigned)C3) + h * HD;
     {
       f32x16 av = f32x16{0}, ak = f32x16{0};
-#if (MSU_EXP & 4)
-#pragma unroll
-#else
 #pragma unroll 1  // unrolled, the fragment reads of all four k steps were hoisted: 17 VGPRs spilled
-#endif
       for (int ks = 0; ks < 64; ks += 16) {
         av = mfma32<T>(frag_tr_q4(L.dO, LD, ks, 0, lane), frag_tr_q4(L.P, LDP, ks, mt * 32, lane), av);
         ak = mfma32<T>(frag_tr_q4(L.q, LD, ks, 0, lane), frag_tr_q4(L.dS, LDP, ks, mt * 32, lane), ak);
@@ -615,11 +588,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     }
     {
       f32x16 aq = f32x16{0};
-#if (MSU_EXP & 4)
-#pragma unroll
-#else
-#pragma unroll 1  // unrolled, the fragment reads of all four k steps were hoisted: 17 VGPRs spilled
-#endif
+#pragma unroll 1
       for (int ks = 0; ks < 64; ks += 16)
         aq = mfma32<T>(frag_tr(L.k, LD, ks, 0, lane), frag_rows(L.dS, LDP, mt * 32, ks, lane), aq);
       store_slice<T>(row, aq, scale, hh, tok >= 0);
@@ -632,9 +601,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
   const long win0 = blockIdx.x;
   if (win0 < g.nwin) {  // block-uniform
     long win = win0;
-#if !(MSU_EXP & 2)
     prep(win, std::integral_constant<int, 0>{});
-#endif
     for (;;) {
       if (!step(std::integral_constant<int, 0>{}, win)) break;
       win += nblk;
