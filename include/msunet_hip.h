@@ -156,6 +156,12 @@ int msu_tok_gemm_plan(long M, int N, int K, long* out6);
 int msu_nt_gemm_supported(long M, int N, int K);
 int msu_nt_gemm(int dtype, const void* A, const void* W, const float* bias, void* Y, void* Y2, const void* H,
                 long M, int N, int K, int epi, void* stream);
+/* The same with the weight given as Wk[K][N]: Y = epi(A . Wk + bias).  The input gradient of a
+ * Linear, dX = dY . W with the forward weight W[N_fwd][K_fwd] (K = N_fwd, N = K_fwd) read in place
+ * (transposed LDS fragment reads) instead of a W^T copy per call (torch F.linear backward,
+ * replaced for the stage 1-3 Linears of model_parts.py:143-151, :72, :379, :639-641). */
+int msu_nt_gemm_kn(int dtype, const void* A, const void* Wk, const float* bias, void* Y, void* Y2, const void* H,
+                   long M, int N, int K, int epi, void* stream);
 
 /* ---------------------------------------------------------------- streaming ops
  * nn.GELU() (exact erf): torchvision MLP activation, FinalPatchExpand_X4_V2.act. */

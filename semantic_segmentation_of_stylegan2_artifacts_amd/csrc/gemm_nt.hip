@@ -22,6 +22,8 @@
 // reduction, PatchExpand expand, concat_back_dim (via ops.linear / ops.mlp) when routed in
 // (ops.gemm_route, MSU_GEMM_ROUTE=nt): alone it beats hipBLASLt on most stage 1-3 shapes, inside
 // the overlapped training step it has not (GEMM routing).
+#include <cstring>
+
 #include "common.h"
 
 namespace {
@@ -70,10 +72,56 @@ struct NtTile {
   }
 };
 
-template <typename T, int EPI, int BK>
+// W given as [K][N] (N-contiguous: the forward weight [N_fwd][K_fwd] of an input-gradient GEMM,
+// dX = dY . W, read without a transposed copy).  Its BK x 128 tile is staged as a [k][n] image
+// (256-B rows); 16-B chunk c of row r sits at chunk c ^ 4(r & 3), so the four rows a half-wave's
+// transposed read covers fall on four different 64-B bank groups.
+struct KnTile {
+  static MSU_DEV int off(int row, int col) { return row * BN + ((((col >> 3) ^ (4 * (row & 3)))) << 3) + (col & 7); }
+  // 64 x 128 tile: 1024 16-B slots, 4 per thread; columns past N re-read column n0
+  static MSU_DEV void stage(const bf16_t* __restrict__ W, int n0, int N, int k0, bf16_t* tile, int tid) {
+    const int wave = tid >> 6;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int p = c * 256 + tid;
+      const int row = p >> 4, lc = (p & 15) ^ (4 * (row & 3));
+      int n = n0 + 8 * lc;
+      if (n >= N) n = n0;
+      glds16(W + (size_t)(k0 + row) * N + n, tile + (c * 256 + wave * 64) * 8);
+    }
+  }
+  // 32-column fragment (the MFMA A operand): lane l -> column col0 + (l & 31), element e -> k =
+  // 16 ks + 8 (l >> 5) + e, as two ds_read_b64_tr_b16 (4 k rows x 4 columns per lane group)
+  static MSU_DEV bf16x8 frag(const bf16_t* tile, int col0, int ks, int lane) {
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4s lds_v4s;
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
+    const int col = col0 + 16 * (g & 1) + 4 * p;
+    const int row = 16 * ks + 8 * h + q;
+    v4s both[2] = {__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(tile + off(row, col))),
+                   __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(tile + off(row + 4, col)))};
+    return *reinterpret_cast<bf16x8*>(both);
+  }
+};
+
+// Runtime-selected s_waitcnt vmcnt(n * PER), n in [0, 2] (DMA steps allowed to stay in flight)
+template <int PER>
+MSU_DEV void wait_steps(int n) {
+  if (n >= 2) wait_vmcnt<2 * PER>();
+  else if (n == 1) wait_vmcnt<PER>();
+  else wait_vmcnt<0>();
+}
+
+// NST-stage LDS ring of K steps (prefetch distance NST - 1, one barrier per K step): the
+// short-K stage 1-3 shapes (K = 192..768: 3-24 steps) otherwise wait out a DMA round trip per
+// step.  Fragments of k-slice ks + 1 are read before the MFMAs of ks.
+template <typename T, int EPI, int BK, int NST, bool WKN>
 __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs a) {
   typedef NtTile<BK> Tl;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2][2][BM * BK];  // [buffer][A | W]
+  static_assert(NST >= 2 && NST <= 4, "ring depth");
+  static_assert(!WKN || BK == 64, "[K][N] weights: 64-deep K steps");
+  constexpr int KSL = BK / 16;  // 16-wide k slices per step
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NST][2][BM * BK];  // [stage][A | W]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;  // this wave's 64 x 64 quarter (tokens, columns)
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -87,33 +135,49 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
 
-  Tl::stage(a.A, m0, a.M, a.K, 0, lds[0][0], tid);
-  Tl::stage(a.W, n0, a.N, a.K, 0, lds[0][1], tid);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {  // next K step in flight while this one computes
-      Tl::stage(a.A, m0, a.M, a.K, (kt + 1) * BK, lds[cur ^ 1][0], tid);
-      Tl::stage(a.W, n0, a.N, a.K, (kt + 1) * BK, lds[cur ^ 1][1], tid);
-      wait_vmcnt<Tl::CH>();  // this step's CH DMAs (2 tiles x CH/2) done, the next step's in flight
-    } else {
-      wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_s_barrier();  // every wave's DMA of step kt has landed
-    asm volatile("" ::: "memory");
-    const bf16_t* ta = lds[cur][0];
-    const bf16_t* tw = lds[cur][1];
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      const bf16x8 w0 = Tl::frag(tw, 64 * wn, ks, lane), w1 = Tl::frag(tw, 64 * wn + 32, ks, lane);
-      const bf16x8 x0 = Tl::frag(ta, 64 * wm, ks, lane), x1 = Tl::frag(ta, 64 * wm + 32, ks, lane);
-      acc[0][0] = Fmt16<T>::mma32(w0, x0, acc[0][0]);
-      acc[0][1] = Fmt16<T>::mma32(w0, x1, acc[0][1]);
-      acc[1][0] = Fmt16<T>::mma32(w1, x0, acc[1][0]);
-      acc[1][1] = Fmt16<T>::mma32(w1, x1, acc[1][1]);
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) {
+      Tl::stage(a.A, m0, a.M, a.K, s * BK, lds[s][0], tid);
+      if constexpr (WKN) KnTile::stage(a.W, n0, a.N, s * BK, lds[s][1], tid);
+      else Tl::stage(a.W, n0, a.N, a.K, s * BK, lds[s][1], tid);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // all reads of buffer cur done before it is restaged
-    asm volatile("" ::: "memory");
+  for (int kt = 0; kt < nk; ++kt) {
+    // this step's DMAs done; those of steps kt+1 .. kt+NST-2 may stay in flight
+    wait_steps<Tl::CH>(min(NST - 2, nk - 1 - kt));
+    __builtin_amdgcn_s_barrier();  // every wave's DMA of step kt has landed, and every wave is
+    asm volatile("" ::: "memory");  // done reading step kt-1's stage (refilled below)
+    if (kt + NST - 1 < nk) {
+      const int sn = (kt + NST - 1) % NST;
+      Tl::stage(a.A, m0, a.M, a.K, (kt + NST - 1) * BK, lds[sn][0], tid);
+      if constexpr (WKN) KnTile::stage(a.W, n0, a.N, (kt + NST - 1) * BK, lds[sn][1], tid);
+      else Tl::stage(a.W, n0, a.N, a.K, (kt + NST - 1) * BK, lds[sn][1], tid);
+    }
+    const bf16_t* ta = lds[kt % NST][0];
+    const bf16_t* tw = lds[kt % NST][1];
+    bf16x8 fw[2][2], fx[2][2];
+    auto rd = [&](int ks, int set) {
+      if constexpr (WKN) {
+        fw[set][0] = KnTile::frag(tw, 64 * wn, ks, lane);
+        fw[set][1] = KnTile::frag(tw, 64 * wn + 32, ks, lane);
+      } else {
+        fw[set][0] = Tl::frag(tw, 64 * wn, ks, lane);
+        fw[set][1] = Tl::frag(tw, 64 * wn + 32, ks, lane);
+      }
+      fx[set][0] = Tl::frag(ta, 64 * wm, ks, lane);
+      fx[set][1] = Tl::frag(ta, 64 * wm + 32, ks, lane);
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < KSL; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < KSL) rd(ks + 1, cur ^ 1);
+      acc[0][0] = Fmt16<T>::mma32(fw[cur][0], fx[cur][0], acc[0][0]);
+      acc[0][1] = Fmt16<T>::mma32(fw[cur][0], fx[cur][1], acc[0][1]);
+      acc[1][0] = Fmt16<T>::mma32(fw[cur][1], fx[cur][0], acc[1][0]);
+      acc[1][1] = Fmt16<T>::mma32(fw[cur][1], fx[cur][1], acc[1][1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 
   // epilogue: lane (l & 31) is token m; after the swap, 8 consecutive columns per store
@@ -170,35 +234,31 @@ bool nt_shape_ok(long M, int N, int K) {
   return M > 0 && M < (1L << 31) && N > 0 && N % 32 == 0 && K > 0 && K % 64 == 0 && (long)M * N < (1L << 40);
 }
 
-// K step: 64 (faster alone, tools/kbench.py nt) or 32 (32 KB of LDS per workgroup instead of
-// 64: more room for the weight-gradient kernels beside it on the side stream; A/B switch
-// MSU_NT_BK=32, no step-level gain measured)
-int nt_bk() {
-  static const int bk = getenv("MSU_NT_BK") ? atoi(getenv("MSU_NT_BK")) : 64;
-  return bk == 32 ? 32 : 64;
+// Ring configuration (A/B switch MSU_NT_CFG = BKxNST): 64x2 (default: 64 KB of LDS, one K step
+// in flight), 32x4 (64 KB, three steps in flight), 32x3 (48 KB: three workgroups per CU).  The
+// deeper rings measured 2-15 % slower alone (tools/nt_cfg_ab.sh): the per-step DMA latency is
+// not what bounds these tiles.
+int nt_cfg() {
+  static const int cfg = [] {
+    const char* e = getenv("MSU_NT_CFG");
+    if (e && !strcmp(e, "32x4")) return 324;
+    if (e && !strcmp(e, "32x3")) return 323;
+    return 642;
+  }();
+  return cfg;
 }
 
-template <typename T, int BK>
+template <typename T, int BK, int NST, bool WKN>
 void launch_nt(int epi, long tiles, const NtArgs& a, hipStream_t st) {
   switch (epi) {
-    case EPI_PLAIN: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_PLAIN, BK>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
-    case EPI_GELU_DUAL: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_DUAL, BK>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_GRAD, BK>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
+    case EPI_PLAIN: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_PLAIN, BK, NST, WKN>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
+    case EPI_GELU_DUAL: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_DUAL, BK, NST, WKN>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_GRAD, BK, NST, WKN>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
   }
 }
 
-}  // namespace
-
-extern "C" {
-
-// Whether msu_nt_gemm covers this shape (K % 64, N % 32).
-int msu_nt_gemm_supported(long M, int N, int K) { return nt_shape_ok(M, N, K) ? 1 : 0; }
-
-// Y[M][N] = epi(A . W^T + bias), 16-bit in / out (dtype 1 bf16, 2 f16), f32 accumulation.
-// epi 0: plain (+ bias when given); 1: Y = H and Y2 = GELU(H) (needs bias); 2: Y = (A . W^T) *
-// GELU'(H) (no bias).  Same semantics as msu_tok_gemm without the split-A input.
-int msu_nt_gemm(int dtype, const void* A, const void* W, const float* bias, void* Y, void* Y2, const void* H,
-                long M, int N, int K, int epi, void* stream) {
+int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* Y, void* Y2, const void* H, long M,
+              int N, int K, int epi, void* stream, bool wkn) {
   if (!msu_is16(dtype)) return -3;
   if (!nt_shape_ok(M, N, K)) return -2;
   if (epi == EPI_GELU_DUAL && (Y2 == nullptr || bias == nullptr)) return -3;
@@ -218,9 +278,33 @@ int msu_nt_gemm(int dtype, const void* A, const void* W, const float* bias, void
   const long tiles = (long)((M + BM - 1) / BM) * a.tiles_n;
   hipStream_t st = (hipStream_t)stream;
   MSU_DISPATCH16(dtype, T,
-    if (nt_bk() == 64) launch_nt<T, 64>(epi, tiles, a, st);
-    else launch_nt<T, 32>(epi, tiles, a, st));
+    if (wkn) launch_nt<T, 64, 2, true>(epi, tiles, a, st);
+    else if (nt_cfg() == 642) launch_nt<T, 64, 2, false>(epi, tiles, a, st);
+    else if (nt_cfg() == 323) launch_nt<T, 32, 3, false>(epi, tiles, a, st);
+    else launch_nt<T, 32, 4, false>(epi, tiles, a, st));
   return MSU_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Whether msu_nt_gemm covers this shape (K % 64, N % 32).
+int msu_nt_gemm_supported(long M, int N, int K) { return nt_shape_ok(M, N, K) ? 1 : 0; }
+
+// Y[M][N] = epi(A . W^T + bias), 16-bit in / out (dtype 1 bf16, 2 f16), f32 accumulation.
+// epi 0: plain (+ bias when given); 1: Y = H and Y2 = GELU(H) (needs bias); 2: Y = (A . W^T) *
+// GELU'(H) (no bias).  Same semantics as msu_tok_gemm without the split-A input.
+int msu_nt_gemm(int dtype, const void* A, const void* W, const float* bias, void* Y, void* Y2, const void* H,
+                long M, int N, int K, int epi, void* stream) {
+  return nt_launch(dtype, A, W, bias, Y, Y2, H, M, N, K, epi, stream, false);
+}
+
+// Same with the weight given as Wk[K][N] (Y = epi(A . Wk + bias)): the input gradient of a Linear,
+// dX[M][K_fwd] = dY[M][N_fwd] . W[N_fwd][K_fwd], straight from the forward weight (no W^T copy).
+int msu_nt_gemm_kn(int dtype, const void* A, const void* Wk, const float* bias, void* Y, void* Y2, const void* H,
+                   long M, int N, int K, int epi, void* stream) {
+  return nt_launch(dtype, A, Wk, bias, Y, Y2, H, M, N, K, epi, stream, true);
 }
 
 }  // extern "C"

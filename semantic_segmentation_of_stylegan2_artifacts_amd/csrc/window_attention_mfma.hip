@@ -27,6 +27,11 @@
 #include "common.h"
 #include "reduce.h"
 
+// MSU_EXP: ablation bits for timing experiments only (tools/build_exp.sh); 0 in every real build
+#ifndef MSU_EXP
+#define MSU_EXP 0
+#endif
+
 namespace {
 
 template <typename F, int... Is>
@@ -501,7 +506,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
       const float4* bp = reinterpret_cast<const float4*>(bimg + ((jt * 2 + it) * 64 + lane) * 16);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float4 v = bp[q];
+        const float4 v = (MSU_EXP & 1) ? make_float4(0.f, 0.f, 0.f, 0.f) : bp[q];
         P[jt][4 * q] = v.x; P[jt][4 * q + 1] = v.y; P[jt][4 * q + 2] = v.z; P[jt][4 * q + 3] = v.w;
       }
       D[jt] = f32x16{0};
@@ -509,14 +514,14 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     __syncthreads();  // rows + this window's token table visible to both waves
     const long nxt = win + nblk;
     const bool more = nxt < g.nwin;
-    if (more) prep(nxt, std::integral_constant<int, buf ^ 1>{});
+    if (more && !(MSU_EXP & 4)) prep(nxt, std::integral_constant<int, buf ^ 1>{});
     const bool boundary = bnd[buf];
     const int* sTok = L.tok[buf];
     const int* sReg = L.reg[buf];
     // ---- score pass: query tile it = w
     const int i = it * 32 + (lane & 31);
     uint32_t kmask = ~0u;  // bit jt*16+r: (i, key jt*32 + crow(r, hh)) kept by the dropout
-    if constexpr (DROP)  // the forward's mask, regenerated from the seed
+    if constexpr (DROP && !(MSU_EXP & 8))  // the forward's mask, regenerated from the seed
       kmask = drop_bits<true>(drop_seed32(seed), (uint32_t)win * g.nh + h, i, hh, drop_thresh16(p_drop));
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -572,6 +577,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     const bool pad = tok == TOK_PAD;
     const bool anypad = __ballot(pad) != 0;  // wave-uniform: only windows over the padded border
     bf16_t* row = dqkv + (size_t)((unsigned)(tok >= 0 ? tok : 0) * (unsigned)C3) + h * HD;
+    const bool st_ok = tok >= 0 && (!(MSU_EXP & 2) || scale == 1.2345e-30f);
     {
       f32x16 av = f32x16{0}, ak = f32x16{0};
 #pragma unroll 1  // unrolled, the fragment reads of all four k steps were hoisted: 17 VGPRs spilled
@@ -579,8 +585,8 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
         av = mfma32<T>(frag_tr_q4(L.dO, LD, ks, 0, lane), frag_tr_q4(L.P, LDP, ks, mt * 32, lane), av);
         ak = mfma32<T>(frag_tr_q4(L.q, LD, ks, 0, lane), frag_tr_q4(L.dS, LDP, ks, mt * 32, lane), ak);
       }
-      store_slice<T>(row + g.C, ak, scale, hh, tok >= 0);
-      store_slice<T>(row + 2 * g.C, av, 1.0f, hh, tok >= 0);
+      store_slice<T>(row + g.C, ak, scale, hh, st_ok);
+      store_slice<T>(row + 2 * g.C, av, 1.0f, hh, st_ok);
       if (anypad) {
         pad_accumulate(padacc[1], ak, scale, pad, lane);
         pad_accumulate(padacc[2], av, 1.0f, pad, lane);
@@ -591,7 +597,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
 #pragma unroll 1
       for (int ks = 0; ks < 64; ks += 16)
         aq = mfma32<T>(frag_tr(L.k, LD, ks, 0, lane), frag_rows(L.dS, LDP, mt * 32, ks, lane), aq);
-      store_slice<T>(row, aq, scale, hh, tok >= 0);
+      store_slice<T>(row, aq, scale, hh, st_ok);
       if (anypad) pad_accumulate(padacc[0], aq, scale, pad, lane);
     }
     __syncthreads();  // this window's LDS reads done before the next window's rows land

@@ -626,9 +626,29 @@ def nt_gemm(a, w, bias=None, epi=TOK_PLAIN, h=None):
     return (y, y2) if epi == TOK_GELU_DUAL else y
 
 
+def nt_gemm_kn(a, wk, epi=TOK_PLAIN, h=None):
+    """16-bit Y = epi(A . Wk) on the tiled NT GEMM with Wk [K, N] read in place (no bias)."""
+    K, N = wk.shape
+    M = a.numel() // K
+    a = a.contiguous()
+    y = torch.empty(*a.shape[:-1], N, device=a.device, dtype=a.dtype)
+    _lib.call("msu_nt_gemm_kn", _dt(a), _p(a), _p(wk), None, _p(y), None, _p(h), M, N, K, epi, _s(a))
+    return y
+
+
 def _wt(w):
     """[N, K] 16-bit weight -> contiguous W^T [K, N] for the input-gradient GEMM."""
     return w.t().contiguous()
+
+
+def _gemm_dx(dy, w, epi=TOK_PLAIN, h=None):
+    """16-bit epi(dy . w): the input gradient of y = x . w^T (w [N, K]) on the routed GEMM; the
+    NT route reads w in place, the token GEMM takes W^T."""
+    N, K = w.shape
+    M = dy.numel() // N
+    if gemm_route(M, K, N, epi) == "nt":
+        return nt_gemm_kn(dy, w, epi, h)
+    return _gemm(dy, _wt(w), None, epi, h)
 
 
 def _wgrad(dy, x, weight, bias, M, N, K):
@@ -700,6 +720,8 @@ def gemm_route(M, N, K, epi=TOK_PLAIN):
             r = "nt"
         elif tok and (N * K <= 576 * 192 or (epi != TOK_PLAIN and M >= 131072)):
             r = "tok"
+        elif _ROUTE_FORCE == "ntlib" and nt_supported(M, N, K):
+            r = "nt"
         else:
             r = "lib"
         _tok_cache[key] = r
@@ -762,7 +784,7 @@ def _linear_backward(ctx, dy):
     dx = None
     if ctx.needs_input_grad[0]:
         if x.dtype in _LOW and gemm_route(M, K, N) != "lib":
-            dx = _gemm(dy, _wt(w))
+            dx = _gemm_dx(dy, w)
         else:
             with torch.autocast("cuda", enabled=False):
                 dx = dy.matmul(w)
@@ -904,9 +926,9 @@ def _mlp_backward(ctx, dy, _dh, _dg):
     Hd, C = W1.shape
     M = x.numel() // C
     dw2, db2 = _wgrad(dy, g, w2, b2, M, C, Hd)
-    dh = _gemm(dy, _wt(W2), None, TOK_GELU_GRAD, h=h)
+    dh = _gemm_dx(dy, W2, TOK_GELU_GRAD, h=h)
     dw1, db1 = _wgrad(dh, x, w1, b1, M, Hd, C)
-    dx = _gemm(dh, _wt(W1)) if ctx.needs_input_grad[0] else None
+    dx = _gemm_dx(dh, W1) if ctx.needs_input_grad[0] else None
     return dx, dw1, db1, dw2, db2
 
 
@@ -1222,7 +1244,7 @@ def _linear_gelu_backward(ctx, dy, _dg):
     dx = None
     if ctx.needs_input_grad[0]:
         if x.dtype in _LOW and gemm_route(M, K, N) != "lib":
-            dx = _gemm(dy, _wt(w))
+            dx = _gemm_dx(dy, w)
         else:
             with torch.autocast("cuda", enabled=False):
                 dx = dy.matmul(w)

@@ -74,6 +74,32 @@ def test_nt_gemm_gelu_epilogues(M, N, K, low):
     _check(dh, ref, "dh")
 
 
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_nt_gemm_kn_plain(M, N, K, low):
+    """msu_nt_gemm_kn: Y = A . Wk with Wk [K, N] read in place (a Linear's input gradient dX = dY . W
+    with its forward weight W); same bar as the [N, K] form."""
+    ops = _ops()
+    a, w, _ = _inputs(M, N, K, 3 * M + N + K, low)
+    wk = w.t().contiguous()  # [K, N]
+    y = ops.nt_gemm_kn(a, wk)
+    assert y.dtype == low and y.shape == (M, N)
+    _check(y, a.float() @ wk.float(), "y")
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 1536, 384), (777, 768, 192), (300, 3072, 768)])
+def test_nt_gemm_kn_gelu_grad(M, N, K, low):
+    """EPI 2 with the weight in place: dH = (dY . W2) * GELU'(H), W2 [K, N] = mlp.3's weight."""
+    ops = _ops()
+    gen = torch.Generator().manual_seed(M + 1)
+    dy = torch.randn(M, K, generator=gen).to(DEV, low)
+    w2 = (torch.randn(K, N, generator=gen) / K ** 0.5).to(DEV, low)
+    h = torch.randn(M, N, generator=gen).to(DEV, low)
+    dh = ops.nt_gemm_kn(dy, w2, ops.TOK_GELU_GRAD, h=h)
+    hf = h.float().requires_grad_(True)
+    F.gelu(hf).backward(torch.ones_like(hf))
+    _check(dh, (dy.float() @ w2.float()) * hf.grad, "dh")
+
+
 def test_nt_gemm_rejects_uncovered_shapes():
     ops = _ops()
     assert not ops.nt_supported(4096, 100, 384)  # N % 32
@@ -87,8 +113,9 @@ def test_nt_gemm_rejects_uncovered_shapes():
 @pytest.mark.parametrize("M,N,K", [(32768, 1152, 384), (8192, 768, 3072), (131072, 192, 384)])
 def test_linear_routes_stage_shapes_to_nt_and_matches(M, N, K, monkeypatch):
     """ops.linear at stage 1-3 shapes (bf16 autocast) with the NT GEMM routed in
-    (MSU_GEMM_ROUTE=nt): forward and input gradient on the NT GEMM, weight gradient on the HIP
-    wgrad kernel; all against fp32 autograd."""
+    (MSU_GEMM_ROUTE=nt): forward and input gradient on the NT GEMM (the input gradient reads the
+    weight in place, msu_nt_gemm_kn), weight gradient on the HIP wgrad kernel; all against fp32
+    autograd."""
     ops = _ops()
     monkeypatch.setattr(ops, "_ROUTE_FORCE", "nt")
     monkeypatch.setattr(ops, "_tok_cache", {})
