@@ -75,16 +75,22 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
 long msu_win_count(int B, int H, int W);
 /* f32 workspace elements (bf16: the per-head relative-bias image in MFMA C layout). */
 long msu_win_attn_fwd_workspace(int dtype, int C, int nh);
+/* u32 words of the dropout keep-bit buffer (16-bit dtypes: 128 per window x head, 0 for f32). */
+long msu_win_attn_keep_words(int dtype, int B, int H, int W, int nh);
+/* keep (may be null; 16-bit dtypes with p_drop > 0): the forward writes its dropout keep bits
+ * there, the backward given the same buffer reads them instead of re-hashing. */
 int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                      void* out, float* workspace, int B, int H, int W, int C, int nh, int shift,
-                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream);
+                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* keep,
+                     void* stream);
 long msu_win_attn_bwd_workspace(int dtype, int B, int H, int W, int C, int nh);
 /* dqkv [B,H,W,3C]; dtable [169,nh] (overwritten); dqkv_bias_pad [3C]: padded tokens'
  * contribution to the qkv-bias gradient (overwritten). */
 int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                      const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                      float* workspace, int B, int H, int W, int C, int nh, int shift,
-                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream);
+                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, const void* keep,
+                     void* stream);
 /* As msu_win_attn_bwd; the parameter-gradient tail (relative-table and qkv-bias reductions)
  * runs on param_stream, ordered after the backward kernel by an event (null: on stream).
  * dqkv is complete when `stream` is; dtable / dqkv_bias_pad when `param_stream` is.
@@ -93,8 +99,8 @@ int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const fl
 int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                       const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                       float* workspace, int B, int H, int W, int C, int nh, int shift,
-                      float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream,
-                      void* param_stream);
+                      float p_drop, unsigned long long seed, const unsigned long long* seed_dev, const void* keep,
+                      void* stream, void* param_stream);
 /* The parameter-gradient tail of msu_win_attn_bwd2 (dtable, dqkv_bias_pad) from the
  * workspace partials its backward kernel left, on `stream`. */
 int msu_win_attn_bwd_tail(int dtype, float* workspace, float* dtable, float* dqkv_bias_pad, int B, int H, int W,

@@ -27,10 +27,11 @@ SIGNATURES = {
     "msu_head_bwd": (I, [I, P, P, P, P, P, P, P, P, P, I, P, P, P, L, I, P]),
     "msu_win_count": (L, [I, I, I]),
     "msu_win_attn_fwd_workspace": (L, [I, I, I]),
-    "msu_win_attn_fwd": (I, [I, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P]),
+    "msu_win_attn_keep_words": (L, [I, I, I, I, I]),
+    "msu_win_attn_fwd": (I, [I, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P, P]),
     "msu_win_attn_bwd_workspace": (L, [I, I, I, I, I, I]),
-    "msu_win_attn_bwd": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P]),
-    "msu_win_attn_bwd2": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P, P]),
+    "msu_win_attn_bwd": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P, P]),
+    "msu_win_attn_bwd2": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P, P, P]),
     "msu_win_attn_bwd_tail": (I, [I, P, P, P, I, I, I, I, I, P]),
     "msu_gelu_fwd": (I, [I, P, P, L, P]),
     "msu_gelu_bwd": (I, [I, P, P, P, L, P]),

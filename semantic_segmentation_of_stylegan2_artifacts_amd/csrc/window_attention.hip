@@ -400,11 +400,11 @@ WinGeom make_geom(int B, int H, int W, int C, int nh, int shift) {
 // bf16 training path: window_attention_mfma.hip
 int msu_attn_mfma_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, void* out, int B,
                       int H, int W, int C, int nh, int shift, float p_drop, unsigned long long seed,
-                      const unsigned long long* seed_dev, float* bias_img, hipStream_t st);
+                      const unsigned long long* seed_dev, void* keep, float* bias_img, hipStream_t st);
 int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, const void* dout,
                       void* dqkv, float* dtable, float* dqkv_bias_pad, float* ws, int B, int H, int W,
                       int C, int nh, int shift, float p_drop, unsigned long long seed,
-                      const unsigned long long* seed_dev, hipStream_t st, hipStream_t pst);
+                      const unsigned long long* seed_dev, const void* keep, hipStream_t st, hipStream_t pst);
 long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh);
 int msu_attn_mfma_bwd_tail(float* ws, float* dtable, float* dqkv_bias_pad, long nwin, int C, int nh,
                            hipStream_t st);
@@ -427,9 +427,14 @@ long msu_win_attn_fwd_workspace(int dtype, int C, int nh) {
   return msu_is16(dtype) ? msu_attn_mfma_fwd_workspace(C, nh) : 1;
 }
 
+long msu_win_attn_keep_words(int dtype, int B, int H, int W, int nh) {
+  return msu_is16(dtype) ? make_geom(B, H, W, 32 * nh, nh, 0).nwin * nh * 128 : 0;
+}
+
 int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                      void* out, float* workspace, int B, int H, int W, int C, int nh, int shift,
-                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream) {
+                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* keep,
+                     void* stream) {
   if (C != nh * HD) return -2;
   const WinGeom g = make_geom(B, H, W, C, nh, shift);
   // the MFMA kernels address qkv / dqkv rows with 32-bit products tok * 3C
@@ -439,7 +444,7 @@ int msu_win_attn_fwd(int dtype, const void* qkv, const float* qkv_bias, const fl
   hipStream_t st = (hipStream_t)stream;
   if (msu_is16(dtype))
     return msu_attn_mfma_fwd(dtype, qkv, qkv_bias, table, out, B, H, W, C, nh, shift, p_drop, seed, seed_dev,
-                             workspace, st);
+                             keep, workspace, st);
   const float scale = 1.0f / sqrtf((float)HD);
   const long nb = items < 262144 ? items : 262144;
   hipLaunchKernelGGL(win_attn_fwd_kernel<float>, dim3((unsigned)nb), dim3(64), 0, st,
@@ -460,8 +465,8 @@ int msu_win_attn_bwd_tail(int dtype, float* workspace, float* dtable, float* dqk
 int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                       const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                       float* workspace, int B, int H, int W, int C, int nh, int shift,
-                      float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream,
-                      void* param_stream) {
+                      float p_drop, unsigned long long seed, const unsigned long long* seed_dev, const void* keep,
+                      void* stream, void* param_stream) {
   if (C != nh * HD) return -2;
   // the MFMA kernels address qkv / dqkv rows with 32-bit products tok * 3C
   if ((long)B * H * W * 3 * C >= (1L << 32)) return -2;
@@ -471,7 +476,7 @@ int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const f
   if (g.nwin == 0) return 0;
   if (msu_is16(dtype))
     return msu_attn_mfma_bwd(dtype, qkv, qkv_bias, table, dout, dqkv, dtable, dqkv_bias_pad, workspace, B, H, W,
-                             C, nh, shift, p_drop, seed, seed_dev, st, pst);
+                             C, nh, shift, p_drop, seed, seed_dev, keep, st, pst);
   const int nblk = f32_bwd_blocks(g.nwin, nh);
   const float scale = 1.0f / sqrtf((float)HD);
   float* dB_part = workspace;
@@ -507,9 +512,10 @@ int msu_win_attn_bwd_tail(int dtype, float* workspace, float* dtable, float* dqk
 int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                      const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                      float* workspace, int B, int H, int W, int C, int nh, int shift,
-                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* stream) {
+                     float p_drop, unsigned long long seed, const unsigned long long* seed_dev, const void* keep,
+                     void* stream) {
   return msu_win_attn_bwd2(dtype, qkv, qkv_bias, table, dout, dqkv, dtable, dqkv_bias_pad, workspace, B, H, W,
-                           C, nh, shift, p_drop, seed, seed_dev, stream, nullptr);
+                           C, nh, shift, p_drop, seed, seed_dev, keep, stream, nullptr);
 }
 
 }  // extern "C"

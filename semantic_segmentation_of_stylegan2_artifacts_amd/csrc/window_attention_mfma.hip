@@ -219,7 +219,8 @@ template <typename T, int WAVES, bool DROP>
 __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __restrict__ qkv, Aux aux,
                                                                bf16_t* __restrict__ out, Geom g, float scale,
                                                                float p_drop, uint64_t seed0,
-                                                               const unsigned long long* seed_dev) {
+                                                               const unsigned long long* seed_dev,
+                                                               uint32_t* __restrict__ keep_out) {
   const uint64_t seed = launch_seed(seed0, seed_dev);
   __shared__ __attribute__((aligned(16))) float4 sBimg[4 * 4 * 64];
   __shared__ __attribute__((aligned(16))) FwdLds lds_all[WAVES];
@@ -285,6 +286,11 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
       for (int it = 0; it < 2; ++it)
         kmasks[it] = drop_bits<false>(drop_seed32(seed), (uint32_t)win * g.nh + h, it * 32 + (lane & 31), hh,
                                drop_thresh16(p_drop));
+      if (keep_out) {  // for the backward: [item][it][lane] words, two 256-B stores per wave
+        uint32_t* kp = keep_out + ((size_t)win * g.nh + h) * 128 + lane;
+        kp[0] = kmasks[0];
+        kp[64] = kmasks[1];
+      }
     }
     const long nxt = it_cur + stride;
     const bool more = nxt < nitems;
@@ -439,11 +445,14 @@ struct BwdLds {
 //     so every lane stores whole 16-B pieces of its token's rows.
 // Blocks walk windows blk, blk + nblk, ...; window k+1's rows are loaded into registers (each
 // wave its 32 rows) while window k is computed.
-template <typename T, bool DROP>
+// KEPT: the forward's keep bits are read from keep_in ([item][it][lane] words) instead of
+// re-hashed (16 hashes per lane per window were ~15 % of the stage-0 backward).
+template <typename T, bool DROP, bool KEPT>
 __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     const bf16_t* __restrict__ qkv, Aux aux, const bf16_t* __restrict__ dout, bf16_t* __restrict__ dqkv,
     float* __restrict__ dB_part, float* __restrict__ qb_part, Geom g, float scale, float p_drop,
-    uint64_t seed0, const unsigned long long* seed_dev, int nblk) {
+    uint64_t seed0, const unsigned long long* seed_dev, const uint32_t* __restrict__ keep_in, int nblk) {
+  static_assert(DROP || !KEPT, "keep bits only with dropout");
   const uint64_t seed = launch_seed(seed0, seed_dev);
   __shared__ __attribute__((aligned(16))) BwdLds L;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;  // w: this wave's query / key tile
@@ -458,6 +467,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
   dB[1] = f32x16{0};
   float padacc[3] = {0.f, 0.f, 0.f};  // column d = lane&31 of padded tokens' dq, dk, dv (per half)
   u32x4 rq[2][2], rk[2][2], rv[2][2], rd[2][2];  // [buf][c]: rows 32w + (lane>>2) + 16c
+  uint32_t rkeep[2] = {~0u, ~0u};                 // [buf]: the forward's keep bits (KEPT)
   bool bnd[2] = {false, false};
   auto rowbase = [&](int tok) -> const bf16_t* {
     return tok >= 0 ? qkv + (size_t)((unsigned)tok * (unsigned)C3) : (tok == TOK_PAD ? aux.biasrow : aux.zrow);
@@ -475,6 +485,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
       L.reg[buf][tt] = reg;
     }
     const int o = 8 * (lane & 3);
+    if constexpr (KEPT) rkeep[buf] = keep_in[((size_t)win * g.nh + h) * 128 + 64 * w + lane];
     static_for([&](auto CI) {
       constexpr int c = decltype(CI)::value;
       int rg;  // (a __shfl of tokt from lane (lane>>2) + 16c measured no faster)
@@ -521,7 +532,9 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     // ---- score pass: query tile it = w
     const int i = it * 32 + (lane & 31);
     uint32_t kmask = ~0u;  // bit jt*16+r: (i, key jt*32 + crow(r, hh)) kept by the dropout
-    if constexpr (DROP && !(MSU_EXP & 8))  // the forward's mask, regenerated from the seed
+    if constexpr (KEPT)
+      kmask = rkeep[buf];
+    else if constexpr (DROP && !(MSU_EXP & 8))  // the forward's mask, regenerated from the seed
       kmask = drop_bits<true>(drop_seed32(seed), (uint32_t)win * g.nh + h, i, hh, drop_thresh16(p_drop));
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -737,7 +750,7 @@ long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh) {
 
 int msu_attn_mfma_fwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, void* out, int B,
                       int H, int W, int C, int nh, int shift, float p_drop, unsigned long long seed,
-                      const unsigned long long* seed_dev, float* ws, hipStream_t st) {
+                      const unsigned long long* seed_dev, void* keep, float* ws, hipStream_t st) {
   const Geom g = make_geom(B, H, W, C, nh, shift);
   const long items = g.nwin * nh;
   if (items == 0) return 0;
@@ -752,17 +765,17 @@ int msu_attn_mfma_fwd(int dtype, const void* qkv, const float* qkv_bias, const f
                        1.0f / scale, img, brow, zrow);
     if (p_drop > 0.f)
       hipLaunchKernelGGL((attn_fwd_mfma<T, FWD_WAVES, true>), grid, blk, 0, st, (const bf16_t*)qkv, aux,
-                         (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev);
+                         (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev, (uint32_t*)keep);
     else
       hipLaunchKernelGGL((attn_fwd_mfma<T, FWD_WAVES, false>), grid, blk, 0, st, (const bf16_t*)qkv, aux,
-                         (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev));
+                         (bf16_t*)out, g, scale, p_drop, (uint64_t)seed, seed_dev, nullptr));
   return MSU_CHECK_LAUNCH();
 }
 
 int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table, const void* dout,
                       void* dqkv, float* dtable, float* dqkv_bias_pad, float* ws, int B, int H, int W,
                       int C, int nh, int shift, float p_drop, unsigned long long seed,
-                      const unsigned long long* seed_dev, hipStream_t st, hipStream_t pst) {
+                      const unsigned long long* seed_dev, const void* keep, hipStream_t st, hipStream_t pst) {
   const Geom g = make_geom(B, H, W, C, nh, shift);
   if (g.nwin == 0) return 0;
   const float scale = 1.0f / sqrtf((float)HD);
@@ -776,14 +789,18 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
   MSU_DISPATCH16(dtype, T,
     hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
                        1.0f / scale, img, brow, zrow);
-    if (p_drop > 0.f)
-      hipLaunchKernelGGL((attn_bwd_mfma<T, true>), grid, dim3(128), 0, st, (const bf16_t*)qkv, aux,
+    if (p_drop > 0.f && keep)
+      hipLaunchKernelGGL((attn_bwd_mfma<T, true, true>), grid, dim3(128), 0, st, (const bf16_t*)qkv, aux,
                          (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale, p_drop, (uint64_t)seed,
-                         seed_dev, nblk);
+                         seed_dev, (const uint32_t*)keep, nblk);
+    else if (p_drop > 0.f)
+      hipLaunchKernelGGL((attn_bwd_mfma<T, true, false>), grid, dim3(128), 0, st, (const bf16_t*)qkv, aux,
+                         (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale, p_drop, (uint64_t)seed,
+                         seed_dev, nullptr, nblk);
     else
-      hipLaunchKernelGGL((attn_bwd_mfma<T, false>), grid, dim3(128), 0, st, (const bf16_t*)qkv, aux,
+      hipLaunchKernelGGL((attn_bwd_mfma<T, false, false>), grid, dim3(128), 0, st, (const bf16_t*)qkv, aux,
                          (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale, p_drop, (uint64_t)seed,
-                         seed_dev, nblk));
+                         seed_dev, nullptr, nblk));
   if (pst == (hipStream_t)(intptr_t)-1) return MSU_CHECK_LAUNCH();  // tail issued by the caller
   // parameter-gradient reductions: on pst (after the backward kernel) when given
   const int rc = attn_param_stream(st, pst);

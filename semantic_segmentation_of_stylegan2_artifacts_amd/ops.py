@@ -468,35 +468,52 @@ def d2s_layer_norm(x, weight, bias, eps=1e-5):
 
 
 # ----------------------------------------------------------------------------- attention
+# dropout keep bits stored by the forward for the backward (A/B switch MSU_ATTN_KEEP=0: the
+# backward re-hashes the mask from the seed, as the f32 parity kernels always do)
+_ATTN_KEEP = os.environ.get("MSU_ATTN_KEEP", "1") != "0"
+
 def _attn_impl(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
     _need_cuda(qkv)
     qkv = qkv.contiguous()
     B, H, W, C3 = qkv.shape
     C = C3 // 3
     out = torch.empty(B, H, W, C, device=qkv.device, dtype=qkv.dtype)
-    ws = torch.empty(_lib.lib().msu_win_attn_fwd_workspace(_dt(qkv), C, num_heads), device=qkv.device,
+    L = _lib.lib()
+    ws = torch.empty(L.msu_win_attn_fwd_workspace(_dt(qkv), C, num_heads), device=qkv.device,
                      dtype=torch.float32)
+    # the dropout keep bits, written by the forward for the backward (16-bit dtypes)
+    keep = torch.empty(L.msu_win_attn_keep_words(_dt(qkv), B, H, W, num_heads) if p_drop > 0 and _ATTN_KEEP else 0,
+                       device=qkv.device, dtype=torch.int32)
     _lib.call("msu_win_attn_fwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(out), _p(ws), B, H, W,
-              C, num_heads, shift, float(p_drop), seed, _p(seed_dev), _s(qkv))
-    return out
+              C, num_heads, shift, float(p_drop), seed, _p(seed_dev), _p(keep) if keep.numel() else None,
+              _s(qkv))
+    return out, keep
 
 
 def _attn_fake(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
     B, H, W, C3 = qkv.shape
-    return qkv.new_empty(B, H, W, C3 // 3)
+    nwin = B * (-(-H // 7)) * (-(-W // 7))
+    kw = nwin * num_heads * 128 if (p_drop > 0 and _ATTN_KEEP and qkv.dtype in _LOW) else 0
+    return qkv.new_empty(B, H, W, C3 // 3), qkv.new_empty(kw, dtype=torch.int32)
 
 
 def _attn_setup(ctx, inputs, output):
     qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev = inputs
-    ctx.save_for_backward(qkv.contiguous(), qkv_bias, table, seed_dev)
+    keep = output[1]
+    ctx.mark_non_differentiable(keep)
+    ctx.set_materialize_grads(False)
+    ctx.save_for_backward(qkv.contiguous(), qkv_bias, table, seed_dev, keep)
     # the parameter itself when it reached us uncast (trainer flat buffers: direct .grad)
     ctx.bias_param = qkv_bias if isinstance(qkv_bias, torch.nn.Parameter) else None
     ctx.table_param = table if isinstance(table, torch.nn.Parameter) else None
     ctx.cfg = (num_heads, shift, float(p_drop), seed)
 
 
-def _attn_backward(ctx, dout):
-    qkv, qkv_bias, table, seed_dev = ctx.saved_tensors
+def _attn_backward(ctx, dout, _dkeep):
+    qkv, qkv_bias, table, seed_dev, keep = ctx.saved_tensors
+    if dout is None:
+        return None, None, None, None, None, None, None, None
+    kp = _p(keep) if keep.numel() else None
     nh, shift, p_drop, seed = ctx.cfg
     B, H, W, C3 = qkv.shape
     C = C3 // 3
@@ -515,7 +532,7 @@ def _attn_backward(ctx, dout):
         main = torch.cuda.current_stream(qkv.device)
         side = _side_stream_for(qkv.device)
         _lib.call("msu_win_attn_bwd2", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
-                  None, None, _p(ws), B, H, W, C, nh, shift, p_drop, seed, _p(seed_dev),
+                  None, None, _p(ws), B, H, W, C, nh, shift, p_drop, seed, _p(seed_dev), kp,
                   main.cuda_stream, -1)
         side.wait_stream(main)
         ws.record_stream(side)
@@ -537,14 +554,14 @@ def _attn_backward(ctx, dout):
     dtable = torch.empty_like(table)
     dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
     _lib.call("msu_win_attn_bwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
-              _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _p(seed_dev), _s(qkv))
+              _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _p(seed_dev), kp, _s(qkv))
     return dqkv, dbias, dtable, None, None, None, None, None
 
 
 _window_attention = _define(
     "window_attention",
     "(Tensor qkv, Tensor qkv_bias, Tensor table, int num_heads, int shift, float p_drop, int seed, Tensor? seed_dev)"
-    " -> Tensor",
+    " -> (Tensor, Tensor)",
     _attn_impl, _attn_fake, _attn_setup, _attn_backward)
 
 
@@ -557,7 +574,7 @@ def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0,
     if C3 % 3 or (C3 // 3) != num_heads * 32:
         raise ValueError(f"head_dim must be 32 (C={C3 // 3}, heads={num_heads})")
     return _window_attention(_as(qkv, act_dtype()), _f32(qkv_bias), _f32(table), int(num_heads),
-                             int(shift), float(p_drop), int(seed) & ((1 << 63) - 1), seed_dev)
+                             int(shift), float(p_drop), int(seed) & ((1 << 63) - 1), seed_dev)[0]
 
 
 # ----------------------------------------------------------------------------- token GEMM

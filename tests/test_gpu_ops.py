@@ -216,6 +216,58 @@ def test_window_attention_dropout_statistics():
     assert abs(lhs.item() - rhs.item()) <= 1e-3 * abs(lhs.item()) + 1e-3
 
 
+@pytest.mark.parametrize("low", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shift", [0, 3])
+def test_window_attention_keep_bits_equal_rehash(low, shift):
+    """16-bit dropout: the backward reading the forward's stored keep bits (the op's path) gives
+    bit-identical dqkv / dtable / dbias to the backward that re-hashes the mask from the seed
+    (keep = null), and the stored bits have the kept fraction ~1 - p."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
+    ops = _ops()
+    B, H, W, nh = 2, 30, 33, 3
+    C = 32 * nh
+    g = _g(7 + shift)
+    qkv = torch.randn(B, H, W, 3 * C, generator=g).to(DEV, low)
+    qb = (torch.randn(3 * C, generator=g) * 0.1).to(DEV)
+    table = (torch.randn(169, nh, generator=g) * 0.1).to(DEV)
+    dout = torch.randn(B, H, W, C, generator=g).to(DEV, low)
+    p, seed = 0.3, 4321
+    y, keep = torch.ops.msunet.window_attention(qkv, qb, table, nh, shift, p, seed, None)
+    nwin = B * ((H + 6) // 7) * ((W + 6) // 7)
+    assert keep.numel() == nwin * nh * 128
+    # bit b of word [item][it][lane]: query i = 32 it + (lane & 31), key j = 32 (b >> 4) + crow(b & 15)
+    it, lane, b = torch.meshgrid(torch.arange(2), torch.arange(64), torch.arange(32), indexing="ij")
+    r = b & 15
+    i = 32 * it + (lane & 31)
+    j = 32 * (b >> 4) + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+    real = ((i < 49) & (j < 49)).to(DEV)
+    bits = (keep.view(nwin * nh, 2, 64, 1) >> torch.arange(32, device=DEV)) & 1
+    kept = (bits.bool() & real).sum().item() / (real.sum().item() * nwin * nh)
+    assert abs(kept - (1 - p)) < 0.01, kept
+    L = _lib.lib()
+    dt = ops._dt(qkv)
+    outs = []
+    for kp in (keep.data_ptr(), None):
+        ws = torch.empty(L.msu_win_attn_bwd_workspace(dt, B, H, W, C, nh), device=DEV)
+        dqkv = torch.empty_like(qkv)
+        dtab = torch.empty_like(table)
+        dbias = torch.empty(3 * C, device=DEV)
+        _lib.call("msu_win_attn_bwd", dt, qkv.data_ptr(), qb.data_ptr(), table.data_ptr(), dout.data_ptr(),
+                  dqkv.data_ptr(), dtab.data_ptr(), dbias.data_ptr(), ws.data_ptr(), B, H, W, C, nh, shift, p,
+                  seed, None, kp, torch.cuda.current_stream().cuda_stream)
+        outs.append((dqkv, dtab, dbias))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    # and the op's own backward is that result
+    q = qkv.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=low):
+        y2 = ops.window_attention(q, qb, table, nh, shift, p, seed)
+    assert torch.equal(y2, y)
+    y2.backward(dout)
+    assert torch.equal(q.grad, outs[0][0])
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2), (torch.float16, 5e-3)])
 def test_gelu(dtype, tol):
     ops = _ops()
