@@ -739,6 +739,8 @@ def gemm_route(M, N, K, epi=TOK_PLAIN):
             r = "tok"
         elif _ROUTE_FORCE == "ntlib" and nt_supported(M, N, K):
             r = "nt"
+        elif _ROUTE_FORCE == "ntmlp" and epi != TOK_PLAIN and nt_supported(M, N, K):
+            r = "nt"
         else:
             r = "lib"
         _tok_cache[key] = r
