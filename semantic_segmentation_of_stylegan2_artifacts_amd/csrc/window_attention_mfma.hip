@@ -286,11 +286,6 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
       for (int it = 0; it < 2; ++it)
         kmasks[it] = drop_bits<false>(drop_seed32(seed), (uint32_t)win * g.nh + h, it * 32 + (lane & 31), hh,
                                drop_thresh16(p_drop));
-      if (keep_out) {  // for the backward: [item][it][lane] words, two 256-B stores per wave
-        uint32_t* kp = keep_out + ((size_t)win * g.nh + h) * 128 + lane;
-        kp[0] = kmasks[0];
-        kp[64] = kmasks[1];
-      }
     }
     const long nxt = it_cur + stride;
     const bool more = nxt < nitems;
@@ -360,6 +355,14 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
     for (int c = 0; c < 4; ++c)
       if (otok[c] >= 0)
         *reinterpret_cast<u32x4*>(out + (size_t)((unsigned)otok[c] * (unsigned)g.C) + h * HD + 8 * (lane & 3)) = ov[c];
+    if (DROP && keep_out) {
+      // keep bits for the backward: [item][it][lane] words, two 256-B stores per wave.  Issued
+      // after the next window's loads: vmcnt retires in order, so a store issued before them
+      // would put its write latency on the next item's operand wait
+      uint32_t* kp = keep_out + ((size_t)win * g.nh + h) * 128 + lane;
+      kp[0] = kmasks[0];
+      kp[64] = kmasks[1];
+    }
     lds_sync();  // LDS reads of this item done before they are overwritten
     return more;
   };
