@@ -1,11 +1,11 @@
 # Counter passes over one window-attention shape (fwd + bwd):
-#   bash tools/pmc_attn.sh TAG res nh shift      (stage 0 of the 1024^2 bench: 256 3 0)
+#   bash tools/pmc_attn.sh TAG res nh shift [p_drop]   (stage 0 of the 1024^2 bench: 256 3 0)
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 TAG=$1; shift
 O=$R/gpurun_out/pmc_attn_$TAG
 mkdir -p $O
-ARGS="$1 $2 $3 1 3"
+ARGS="$1 $2 $3 1 3 ${4:-0.0}"
 run() { timeout -s KILL 60 rocprofv3 --pmc $2 -d $O -o $1 --output-format csv -- python3 $R/tools/attn_one.py $ARGS > $O/$1.log 2>&1 || { tail -5 $O/$1.log; exit 1; }; }
 run fetch FETCH_SIZE
 run write WRITE_SIZE
