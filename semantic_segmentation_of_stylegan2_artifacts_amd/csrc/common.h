@@ -174,11 +174,14 @@ MSU_DEV uint64_t launch_seed(uint64_t seed, const unsigned long long* seed_dev) 
   return z ^ (z >> 29);
 }
 
-// Dropout masks of window attention, regenerated identically by forward and backward: one
-// murmur3 fmix32 hash per key pair (j, j+1), j even, of a query row i of item (window, head);
-// its two 16-bit halves are compared with ceil(p 2^16), so the keep probability is
-// 1 - ceil(p 2^16) / 2^16 (within 2^-16 of 1 - p).  Two decisions per hash: the mask costs half
-// the multiplies of a hash per element.
+// Dropout masks of window attention.  The 64 x 64 keep decisions of an item (window, head) come
+// from 2 x 64 short streams, one per (query row i, key half hh): a murmur3 fmix32 hash of
+// (seed, item, i, hh) seeds a xorshift32 + Weyl generator (xorwow-style, the generator cuRAND
+// long used for dropout) whose 16 words hold the key pairs of that half -- word n covers keys
+// j0, j0 + 1 with j0 = 32 (n >> 3) + crow(2 (n & 7), hh) (crow: the 32x32 MFMA accumulator row
+// order, so a lane's bits line up with its score registers).  Each 16-bit half is compared with
+// ceil(p 2^16): keep probability 1 - ceil(p 2^16) / 2^16, within 2^-16 of 1 - p.  One hash and
+// 16 multiply-free steps per stream instead of a 3-multiply hash per key pair.
 MSU_DEV uint32_t fmix32_hash(uint32_t seed, uint32_t idx) {
   uint32_t x = idx * 0x9E3779B9u + seed;
   x ^= x >> 16; x *= 0x85EBCA6Bu;
@@ -187,10 +190,32 @@ MSU_DEV uint32_t fmix32_hash(uint32_t seed, uint32_t idx) {
 }
 MSU_DEV uint32_t drop_thresh16(float p) { return (uint32_t)ceilf(p * 65536.0f); }
 MSU_DEV uint32_t drop_seed32(uint64_t seed) { return (uint32_t)seed ^ (uint32_t)(seed >> 32); }
-// keep bits of keys j0 (bit 0) and j0 + 1 (bit 1) for query i; item = window * nh + head
-MSU_DEV uint32_t drop_pair(uint32_t seed, uint32_t item, int i, int j0, uint32_t thr) {
-  const uint32_t x = fmix32_hash(seed, (item * 64u + (uint32_t)i) * 32u + ((uint32_t)j0 >> 1));
-  return (uint32_t)((x & 0xFFFFu) >= thr) | ((uint32_t)((x >> 16) >= thr) << 1);
+// stream state of (item = window * nh + head, query i, key half hh); x != 0
+struct DropStream {
+  uint32_t x, d;
+};
+MSU_DEV DropStream drop_stream(uint32_t seed, uint32_t item, int i, int hh) {
+  const uint32_t h = fmix32_hash(seed, (item * 64u + (uint32_t)i) * 2u + (uint32_t)hh);
+  return DropStream{h | 1u, h};
+}
+// next word's keep bits: bit 0 <-> key j0, bit 1 <-> key j0 + 1
+MSU_DEV uint32_t drop_next2(DropStream& s, uint32_t thr) {
+  s.x ^= s.x << 13;
+  s.x ^= s.x >> 17;
+  s.x ^= s.x << 5;
+  s.d += 362437u;
+  const uint32_t w = s.x + s.d;
+  return (uint32_t)((w & 0xFFFFu) >= thr) | ((uint32_t)((w >> 16) >= thr) << 1);
+}
+// keep decision of one (query i, key j) pair of an item (the f32 kernels: one element at a time)
+MSU_DEV bool drop_keep_bit(uint32_t seed, uint32_t item, int i, int j, uint32_t thr) {
+  const int jt = j >> 5, jj = j & 31;
+  const int hh = (jj >> 2) & 1, r = (jj & 3) + 4 * (jj >> 3);  // j = 32 jt + crow(r, hh)
+  const int n = jt * 8 + (r >> 1);
+  DropStream s = drop_stream(seed, item, i, hh);
+  uint32_t b = 0;
+  for (int k = 0; k <= n; ++k) b = drop_next2(s, thr);
+  return (b >> (r & 1)) & 1u;
 }
 
 // XCD-aware bijective block remap: blocks b and b+8 share an XCD under round-robin

@@ -166,10 +166,10 @@ MSU_DEV void softmax_block(f32x4 (&S)[4]) {
   }
 }
 
-// the 16-bit kernels' mask (common.h drop_pair), one element at a time
+// the 16-bit kernels' mask (common.h drop streams), one element at a time
 MSU_DEV float drop_keep(uint64_t seed, long win, int h, int nh, int i, int j, float p) {
-  const uint32_t bits = drop_pair(drop_seed32(seed), (uint32_t)(win * nh + h), i, j & ~1, drop_thresh16(p));
-  return (bits >> (j & 1)) & 1u ? 1.0f / (1.0f - p) : 0.0f;
+  return drop_keep_bit(drop_seed32(seed), (uint32_t)(win * nh + h), i, j, drop_thresh16(p)) ? 1.0f / (1.0f - p)
+                                                                                             : 0.0f;
 }
 
 template <typename T>

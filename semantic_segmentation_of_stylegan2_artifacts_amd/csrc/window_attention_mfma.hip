@@ -136,18 +136,18 @@ MSU_DEV float keep_sel(uint32_t m, int n, float x) {
 }
 
 // keep bits of the lane's 32 keys of query column tile it: bit jt*16 + r <-> key
-// jt*32 + crow(r, hh) (registers 2k, 2k+1 are keys j0, j0+1 of one hash)
-// SERIAL: one hash in flight (the backward, whose register peak 16 interleaved hashes raise);
-// unrolled, the forward hides the hash latency with them
+// jt*32 + crow(r, hh) (word n of the lane's stream holds bits 2n, 2n+1, common.h)
+// SERIAL: not unrolled (the backward's re-hash path, whose register peak an unrolled stream raises)
 template <bool SERIAL>
 MSU_DEV uint32_t drop_bits(uint32_t seed, uint32_t item, int i, int hh, uint32_t thr) {
+  DropStream s = drop_stream(seed, item, i, hh);
   uint32_t m = 0;
   if constexpr (SERIAL) {
 #pragma unroll 1
-    for (int n = 0; n < 16; ++n) m |= drop_pair(seed, item, i, (n >> 3) * 32 + crow(2 * (n & 7), hh), thr) << (2 * n);
+    for (int n = 0; n < 16; ++n) m |= drop_next2(s, thr) << (2 * n);
   } else {
 #pragma unroll
-    for (int n = 0; n < 16; ++n) m |= drop_pair(seed, item, i, (n >> 3) * 32 + crow(2 * (n & 7), hh), thr) << (2 * n);
+    for (int n = 0; n < 16; ++n) m |= drop_next2(s, thr) << (2 * n);
   }
   return m;
 }
@@ -318,6 +318,8 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
       if (bnd[buf]) mask_col(P, L.reg[buf], it, scale, lane);
       softmax_col(P, scale);
       if constexpr (DROP) {
+        // select-and-scale per element: measured 17 % faster here than folding 1/(1-p) into the
+        // normaliser and masking with keep_sel (150 vs 180 us at stage 0)
         const float kscale = 1.0f / (1.0f - p_drop);
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt)

@@ -216,6 +216,26 @@ def test_window_attention_dropout_statistics():
     assert abs(lhs.item() - rhs.item()) <= 1e-3 * abs(lhs.item()) + 1e-3
 
 
+@pytest.mark.parametrize("shift", [0, 3])
+def test_window_attention_dropout_masks_agree_f32_bf16(shift):
+    """The f32 parity kernels draw the same dropout masks as the 16-bit MFMA kernels (one
+    element at a time from the same per-row streams): with p = 0.3 the outputs agree to bf16
+    rounding, which a single differing mask element per row would break."""
+    ops = _ops()
+    B, H, W, nh = 2, 21, 26, 2
+    C = 32 * nh
+    g = _g(31 + shift)
+    qkv = torch.randn(B, H, W, 3 * C, generator=g).to(DEV)
+    qb = (torch.randn(3 * C, generator=g) * 0.1).to(DEV)
+    table = (torch.randn(169, nh, generator=g) * 0.1).to(DEV)
+    q16 = qkv.bfloat16()
+    y32 = ops.window_attention(q16.float(), qb, table, nh, shift, 0.3, 77)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y16 = ops.window_attention(q16, qb, table, nh, shift, 0.3, 77)
+    err = (y16.float() - y32).abs().max().item()
+    assert err <= 3e-2 * y32.abs().max().item(), err
+
+
 @pytest.mark.parametrize("low", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shift", [0, 3])
 def test_window_attention_keep_bits_equal_rehash(low, shift):
