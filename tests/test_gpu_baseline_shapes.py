@@ -108,18 +108,21 @@ def test_swinT_1024_bs1_fp32_forward_matches_oracle():
     assert abs(d_hip - d_ref) <= 1e-3, (d_hip, d_ref)
 
 
-@pytest.mark.parametrize("img", [512, 1024])
-def test_bf16_training_step_at_baseline_config(img):
-    """BASELINE configs 2 (8 x 512^2) and 3 (8 x 1024^2): the benchmarked bf16 training step."""
+@pytest.mark.parametrize("backbone,img,bs", [("swin_t", 512, 8), ("swin_t", 1024, 8), ("swin_s", 1024, 8),
+                                             ("swin_b", 1024, 4)])
+def test_bf16_training_step_at_baseline_config(backbone, img, bs):
+    """BASELINE configs 2 (8 x 512^2) and 3 (8 x 1024^2): the benchmarked bf16 training step;
+    the Swin-S per-GPU shape of configs 4 / 5 and the reference's default Swin-B backbone
+    (config.yaml) at 1024^2 through the same checks."""
     from semantic_segmentation_of_stylegan2_artifacts_amd import load_config, ops, validation
     from semantic_segmentation_of_stylegan2_artifacts_amd.network import MSUNet
     from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import Trainer
     from semantic_segmentation_of_stylegan2_artifacts_amd.data import synthetic_batch
-    cfg = load_config(None, "swin_t", **{"DATA.IMG_SIZE": img, "DATA.BATCH_SIZE": 8})
+    cfg = load_config(None, backbone, **{"DATA.IMG_SIZE": img, "DATA.BATCH_SIZE": bs})
     torch.manual_seed(cfg.SEED)
     model = MSUNet(cfg, img_size=img, num_classes=1).to(DEV)
     tr = Trainer(model, cfg, DEV, lr=1e-4)
-    x, y = synthetic_batch(8, img, DEV, 120)
+    x, y = synthetic_batch(bs, img, DEV, 120)
 
     # forward + backward as Trainer.step runs them; gradients finite and non-zero
     for g in tr.groups:
