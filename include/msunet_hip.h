@@ -69,9 +69,10 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
  * 32^-0.5 + B_rel + shift mask(-100)) -> dropout(p) -> @v -> reverse.  qkv: [B,H,W,3C]
  * (q|k|v, heads contiguous, head_dim 32), out: [B,H,W,C]; table [169, nh] f32 is
  * relative_position_bias_table; qkv_bias [3C] f32 supplies padded tokens' q,k,v.
- * Dropout masks are a counter hash of (seed, window, head, i, j); seed_dev (may be null) points
- * at a device u64 mixed into the seed, so a replayed HIP graph draws new masks per step and the
- * backward regenerates the forward's mask from the same pair. */
+ * Dropout masks: a counter hash of (seed, window, head, query i, key half) seeds a short
+ * xorshift stream per query row (common.h); seed_dev (may be null) points at a device u64
+ * mixed into the seed, so a replayed HIP graph draws new masks per step, and the backward reads
+ * the forward's keep bits (keep buffer) or regenerates them from the same pair. */
 long msu_win_count(int B, int H, int W);
 /* f32 workspace elements (bf16: the per-head relative-bias image in MFMA C layout). */
 long msu_win_attn_fwd_workspace(int dtype, int C, int nh);
