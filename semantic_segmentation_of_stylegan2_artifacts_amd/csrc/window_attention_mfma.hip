@@ -530,7 +530,24 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     __syncthreads();  // rows + this window's token table visible to both waves
     const long nxt = win + nblk;
     const bool more = nxt < g.nwin;
-    if (more && !(MSU_EXP & 4)) prep(nxt, std::integral_constant<int, buf ^ 1>{});
+    if (more) {
+      if constexpr ((MSU_EXP & 4) != 0) {
+        // ablation "no row prefetch": the next window computes on stale rows (results wrong
+        // by design), but its token table must still be written -- the gradient pass forms
+        // store addresses from it (skipping it faulted)
+        constexpr int nb = buf ^ 1;
+        bnd[nb] = window_boundary(g, (int)nxt);
+        int reg;
+        const int tt = 32 * w + (lane & 31);
+        const int tokt = token_of(g, (int)nxt, tt, &reg);
+        if (lane < 32) {
+          L.tok[nb][tt] = tokt;
+          L.reg[nb][tt] = reg;
+        }
+      } else {
+        prep(nxt, std::integral_constant<int, buf ^ 1>{});
+      }
+    }
     const bool boundary = bnd[buf];
     const int* sTok = L.tok[buf];
     const int* sReg = L.reg[buf];

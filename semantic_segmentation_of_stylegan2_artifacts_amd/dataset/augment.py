@@ -62,7 +62,10 @@ def gamma_lut(gamma):
 
 
 def sample_rng(seed, epoch, index):
-    return random.Random((int(seed) & 0xFFFFFFFF) << 40 ^ (int(epoch) & 0xFFFFF) << 20 ^ int(index))
+    """Per-(seed, epoch, sample) draw stream: the three keys sit in disjoint 64-bit fields
+    (random.Random hashes arbitrarily long ints), so no (epoch, index) pair aliases another."""
+    key = ((int(seed) & (2**64 - 1)) << 128) | ((int(epoch) & (2**64 - 1)) << 64) | (int(index) & (2**64 - 1))
+    return random.Random(key)
 
 
 def draw(rng, transform=True, flip=False):

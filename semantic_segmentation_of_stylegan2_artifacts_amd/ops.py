@@ -151,9 +151,10 @@ _side_streams = {}
 
 
 def side_stream(device):
-    """The weight-gradient side stream of a device, or None when disabled / never used."""
+    """The weight-gradient side stream of a device, or None when disabled (also while a
+    single-stream HIP graph capture has switched it off) / never used."""
     device = torch.device(device)
-    if device.type != "cuda" or not _side_streams:
+    if device.type != "cuda" or not _side_enabled or not _side_streams:
         return None
     return _side_streams.get(device.index if device.index is not None else torch.cuda.current_device())
 

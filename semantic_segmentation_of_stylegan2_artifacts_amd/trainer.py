@@ -119,6 +119,9 @@ class GradBucketer:
     graph is static), which all-reduces every bucket after backward; later steps overlap.
     """
 
+    # GradScaler defaults (torch.amp.GradScaler): the fp16 wire's dynamic scale
+    INIT_SCALE, GROWTH_FACTOR, BACKOFF_FACTOR, GROWTH_INTERVAL = 2.0 ** 16, 2.0, 0.5, 2000
+
     def __init__(self, groups, bucket_bytes, process_group=None, wire_dtype=None):
         self.pg = process_group
         # wire_dtype (bf16 / f16): each bucket is cast into a persistent 16-bit buffer, summed
@@ -127,6 +130,22 @@ class GradBucketer:
         # per-rank gradients and of the ring's partial sums.  None: f32 all-reduce.
         self.wire_dtype = None if wire_dtype in (None, torch.float32) else wire_dtype
         self.wire = {}  # bucket index -> 16-bit buffer
+        # f16 has 5 exponent bits: like the reference's GradScaler-scaled fp16 gradients
+        # (trainer.py:182,314-316) the buckets are multiplied by a dynamic scale before the
+        # cast (tiny gradients stay above f16's 6e-8 underflow) and divided by it on the way
+        # back; a sum that overflows comes back inf, the trainer's non-finite check skips the
+        # step on every rank and update_scale() halves the scale (x2 after 2000 clean steps).
+        # bf16 keeps f32's exponent range: no scale.
+        dev = groups[0].grad.device
+        self.scale = self.inv_scale = self.growth_tracker = None
+        if self.wire_dtype == torch.float16:
+            self.scale = torch.full((1,), self.INIT_SCALE, device=dev, dtype=torch.float32)
+            self.inv_scale = torch.full((1,), 1.0 / self.INIT_SCALE, device=dev, dtype=torch.float32)
+            self.growth_tracker = torch.zeros(1, device=dev, dtype=torch.int32)
+        # the collectives' own stream (one per device): each bucket's cast / all-reduce waits
+        # there for both the main and the weight-gradient side stream, so neither stream's
+        # later kernels queue behind a collective that blocks until every rank arrives
+        self.comm = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
         self.buckets = []       # (group, start, end)
         self.param_bucket = {}  # id(param) -> bucket index
         for g in groups:
@@ -158,22 +177,28 @@ class GradBucketer:
         buf = self.wire.get(b)
         if buf is None:
             buf = self.wire[b] = torch.empty(e - s, device=g.grad.device, dtype=self.wire_dtype)
-        buf.copy_(g.grad[s:e])
+        if self.scale is not None:
+            torch.mul(g.grad[s:e], self.scale, out=buf)
+        else:
+            buf.copy_(g.grad[s:e])
         return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True), buf
 
     def _launch(self, b):
         g, s, e = self.buckets[b]
         self.launched[b] = True
-        side = ops.side_stream(g.grad.device)
-        if side is None:
+        if self.comm is None:
             self.works.append((b,) + self._reduce(b, g, s, e))
             return
-        # the bucket's gradients come from both streams: issue from the side stream after it
-        # has caught up with the main stream's work so far (the hook may fire while autograd
-        # runs a side-stream node, so the main stream is named explicitly)
-        main = self.main_stream if self.main_stream is not None else torch.cuda.current_stream(g.grad.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
+        # the bucket's gradients come from both streams: the comm stream catches up with the
+        # work issued so far on the main stream (named explicitly: the hook may fire while
+        # autograd runs a side-stream node) and on the weight-gradient side stream
+        dev = g.grad.device
+        main = self.main_stream if self.main_stream is not None else torch.cuda.current_stream(dev)
+        self.comm.wait_stream(main)
+        side = ops.side_stream(dev)
+        if side is not None:
+            self.comm.wait_stream(side)
+        with torch.cuda.stream(self.comm):
             self.works.append((b,) + self._reduce(b, g, s, e))
 
     def _hook(self, p):
@@ -182,20 +207,54 @@ class GradBucketer:
         if self.expected is not None and self.pending[b] == self.expected[b]:
             self._launch(b)
 
+    def _unwire(self, b, buf):
+        g, s, e = self.buckets[b]
+        if self.scale is not None:
+            torch.mul(buf, self.inv_scale, out=g.grad[s:e])
+        else:
+            g.grad[s:e].copy_(buf)
+
     def finish(self):
+        """Launch what backward did not, wait for every bucket's sum (the current stream waits
+        for the comm stream: AdamW is ordered after the exchange without a host sync)."""
         if self.expected is None:
             self.expected = list(self.pending)
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
-        for b, w, buf in self.works:
-            w.wait()
-            if buf is not None:  # back into the f32 gradients, after the sum (stream-ordered)
-                g, s, e = self.buckets[b]
-                g.grad[s:e].copy_(buf)
+        if self.comm is None:
+            for b, w, buf in self.works:
+                w.wait()
+                if buf is not None:
+                    self._unwire(b, buf)
+        else:
+            with torch.cuda.stream(self.comm):
+                for b, w, buf in self.works:
+                    w.wait()  # the comm stream waits for the collective
+                    if buf is not None:  # back into the f32 gradients, after the sum
+                        self._unwire(b, buf)
+            main = self.main_stream if self.main_stream is not None else torch.cuda.current_stream(self.comm.device)
+            main.wait_stream(self.comm)
         self.works = []
         self.pending = [0] * len(self.buckets)
         self.launched = [False] * len(self.buckets)
+
+    def reset(self):
+        """Forget a step that did not finish (e.g. an aborted HIP-graph capture): no pending
+        accumulation counts, no launched flags, no outstanding work handles."""
+        self.works = []
+        self.pending = [0] * len(self.buckets)
+        self.launched = [False] * len(self.buckets)
+
+    def update_scale(self, found_inf):
+        """GradScaler's dynamic-scale rule for the f16 wire (no-op otherwise), on the device:
+        found_inf (f32 [1], the step's non-finite flag) -> scale x0.5, else x2 after
+        GROWTH_INTERVAL consecutive clean steps."""
+        if self.scale is None:
+            return
+        torch._amp_update_scale_(self.scale, self.growth_tracker, found_inf, self.GROWTH_FACTOR,
+                                 self.BACKOFF_FACTOR, self.GROWTH_INTERVAL)
+        torch.reciprocal(self.scale, out=self.inv_scale)
 
 
 def reseed(seed, rank=0):
@@ -212,7 +271,7 @@ def reseed(seed, rank=0):
 class Trainer:
     def __init__(self, model, config, device, lr=None, amp_dtype=torch.bfloat16, bucket_mb=32,
                  world_size=1, process_group=None, rank=0, seed=None, skip_nonfinite=True, use_graph=None,
-                 graph_warmup=2, grad_wire_dtype=None):
+                 graph_warmup=2, grad_wire_dtype=None, always_reduce=False):
         self.model = model
         self.device = device
         self.amp_dtype = amp_dtype
@@ -248,10 +307,13 @@ class Trainer:
                                    tversky_bce_mix=t.LOSS_TVERSKY_BCE_MIX)
         self.world_size = world_size
         self.step_count = 0
+        self._applied_base = 0  # AdamW step count not taken by this trainer (loaded checkpoints)
         self._shadow_fresh = False
         self.inv_world = torch.full((1,), 1.0 / world_size, device=device, dtype=torch.float32)
+        # always_reduce: the bucketed all-reduce even for one rank (a 1-rank RCCL group exercises
+        # the product DP path on one GPU)
         self.reducer = (GradBucketer(self.groups, int(bucket_mb * (1 << 20)), process_group, grad_wire_dtype)
-                        if world_size > 1 else None)
+                        if world_size > 1 or always_reduce else None)
         # HIP-graph replay of the step (see step()).  use_graph: True / False, or None = the
         # MSU_GRAPH environment switch: "1" always, "0" never, "auto" (default) = capture only
         # when the eager step is launch-bound (host issue time >= GRAPH_HOST_FRACTION of the
@@ -261,8 +323,12 @@ class Trainer:
         mode = use_graph if use_graph is not None else os.environ.get("MSU_GRAPH", "auto")
         mode = {True: "1", False: "0"}.get(mode, str(mode))
         self.graph_mode = mode if on_gpu else "0"
-        if self.graph_mode != "0" and world_size > 1 and dist.get_backend(process_group) != "nccl":
+        if self.graph_mode != "0" and self.reducer is not None and dist.get_backend(process_group) != "nccl":
             self.graph_mode = "0"  # gloo collectives run on the host: not capturable
+        if self.graph_mode == "auto" and world_size > 1:
+            # a captured multi-rank step has only been replayed on a 1-rank RCCL group
+            # (tests/test_gpu_rccl.py): replay under DP only when asked for (MSU_GRAPH=1)
+            self.graph_mode = "0"
         self.use_graph = self.graph_mode != "0"
         self._probe = None  # (host seconds, start event, end event) of the auto-mode probe step
         self.graph_warmup = graph_warmup
@@ -284,6 +350,10 @@ class Trainer:
     def optimizer_steps(self):
         """AdamW steps actually applied (skipped non-finite steps excluded); syncs."""
         return int(self.hyper[1].item())
+
+    def skipped_steps(self):
+        """Training steps whose update was skipped (non-finite gradients); syncs."""
+        return self.step_count - (self.optimizer_steps() - self._applied_base)
 
     def _reference_param_order(self):
         """The parameter list of the reference optimizer (trainer.py:130-152): every trainable
@@ -340,7 +410,9 @@ class Trainer:
         if len(steps) > 1:
             raise ValueError(f"per-parameter AdamW steps differ: {sorted(steps)}")
         if steps:
-            self.hyper[1:2].fill_(steps.pop())
+            st = steps.pop()
+            self._applied_base += int(st) - self.optimizer_steps()
+            self.hyper[1:2].fill_(st)
         self.lr = sd["param_groups"][0]["lr"]
 
     def num_params(self):
@@ -401,12 +473,15 @@ class Trainer:
             for g in self.groups:
                 g.mark_shadow()
         found = None
-        if self.skip_nonfinite:
+        wire_scaled = self.reducer is not None and self.reducer.scale is not None
+        if self.skip_nonfinite or wire_scaled:
             # after the all-reduce: an inf on any rank reaches every rank's sum, so all ranks
-            # skip together
+            # skip together (an f16-wire overflow included: it must never reach AdamW)
             found = self.found_inf
             found.zero_()
             ops.nonfinite_(self.groups[0].grad, found, self.groups[1].grad)
+            if wire_scaled:
+                self.reducer.update_scale(found)
         ops.step_advance_(self.hyper, found)
         for g in self.groups:
             ops.adamw_dev_(g.data, g.grad, g.exp_avg, g.exp_avg_sq, self.hyper, self.betas[0], self.betas[1],
@@ -480,11 +555,20 @@ class Trainer:
                 loss = self._device_step(self._sx, self._sy)
         except Exception as e:  # noqa: BLE001 -- any capture failure: stay eager, loudly
             ops._side_enabled = side_prev
+            # the aborted capture left accumulation counts, launched flags and captured work
+            # handles in the reducer: a later eager step must start from a clean bucket state
+            if self.reducer is not None:
+                self.reducer.reset()
+            ops._side_keep.clear()
+            self._sx = self._sy = None
+            torch.cuda.synchronize(self.device)
+            if self.world_size > 1:
+                # one rank silently falling back to eager while the others replay would
+                # desynchronise the collectives: fail on every rank instead
+                raise RuntimeError(f"HIP graph capture of the data-parallel training step failed: {e!r}") from e
             import warnings
             warnings.warn(f"HIP graph capture of the training step failed ({e!r}); continuing eagerly")
             self._graph_failed = True
-            self._sx = self._sy = None
-            torch.cuda.synchronize(self.device)
             return
         ops._side_enabled = side_prev
         self._graph = graph
@@ -493,6 +577,11 @@ class Trainer:
         self._versions = self._param_versions()
 
     def _replay(self, images, labels):
+        if images.shape != self._sx.shape or labels.shape != self._sy.shape or \
+                images.dtype != self._sx.dtype or labels.dtype != self._sy.dtype:
+            # the graph is specialised to the captured batch: anything else (a short last
+            # batch, another resolution) runs eagerly instead of broadcasting into the buffers
+            return self._eager_step(images, labels)
         v = self._param_versions()
         if v != self._versions:
             # a write through a parameter (load_state_dict, p.copy_) since the last step: the

@@ -104,6 +104,62 @@ def test_bucketed_allreduce_equals_global_batch(bucket_bytes, wire):
             assert not torch.equal(g0, ref)  # the wire really is 16-bit
 
 
+def _small_worker(rank, world, port, out, loss_scale, init_scale):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = _model()
+    named = list(m.named_parameters())
+    groups = [FlatGroup(named[::-1], 0.0, "cpu")]
+    red = GradBucketer(groups, 1 << 20, wire_dtype=torch.float16)
+    if init_scale is not None:
+        red.scale.fill_(init_scale)
+        red.inv_scale.fill_(1.0 / init_scale)
+    x, y = _data(0)  # the same batch on both ranks: the sum has no cancellation
+    (((m(x) - y) ** 2).mean() * loss_scale / world).backward()
+    red.finish()
+    found = torch.zeros(1)
+    found.fill_(float(not torch.isfinite(groups[0].grad).all()))
+    red.update_scale(found)
+    out[rank] = (groups[0].grad.clone(), float(found), float(red.scale))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("loss_scale", [1e-4, 1e-6])
+def test_fp16_wire_keeps_tiny_gradients(loss_scale):
+    """the f16 wire scales the buckets (GradScaler-style, 2^16 to start) before the
+    cast, so gradients of 1e-6 .. 1e-10 survive f16's 6e-8 underflow; unscaled they would
+    flush to zero or lose most of their bits."""
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_small_worker, args=(world, _free_port(), out, loss_scale, None), nprocs=world, join=True)
+    m = _model()
+    named = list(m.named_parameters())
+    x, y = _data(0)
+    (((m(x) - y) ** 2).mean() * loss_scale).backward()
+    ref = torch.cat([p.grad.reshape(-1) for _, p in named[::-1]])
+    got = torch.cat([out[0][0][o:o + p.numel()] for p, o in
+                     zip([p for _, p in named[::-1]], FlatGroup(named[::-1], 0.0, "cpu").offsets)])
+    assert torch.equal(out[0][0], out[1][0])
+    assert out[0][1] == 0.0 and out[0][2] == 2.0 ** 16  # no overflow, scale kept
+    if loss_scale < 1e-5:  # the case needs the scale: many gradients below f16's underflow
+        assert (ref.abs() < 6e-8).float().mean().item() > 0.05
+    # f16 rounding of each rank's scaled share and of the sum; 1e-11 absolute floor
+    # (unscaled, anything below 6e-8 would be lost)
+    excess = ((got - ref).abs() - 4 * 2.0 ** -11 * ref.abs()).max().item()
+    assert excess <= 1e-11, excess
+
+
+def test_fp16_wire_overflow_is_flagged_and_backs_off():
+    """A scale that overflows f16 in the sum: the gradients come back non-finite on every rank
+    (the trainer's non-finite check then skips the step everywhere) and the scale halves."""
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_small_worker, args=(world, _free_port(), out, 1.0, 2.0 ** 40), nprocs=world, join=True)
+    for r in range(world):
+        assert out[r][1] == 1.0
+        assert out[r][2] == 2.0 ** 39
+
+
 def test_no_decay_rule_matches_reference():
     """trainer.py:137: 1-D params, '.bias' names and names containing 'norm' -> no decay."""
     p2 = torch.zeros(3, 3)

@@ -108,6 +108,53 @@ def test_swinT_1024_bs1_fp32_forward_matches_oracle():
     assert abs(d_hip - d_ref) <= 1e-3, (d_hip, d_ref)
 
 
+FULL_GRADS = ("up.refine1.weight", "up.refine2.weight", "layers.0.blocks.1.attn.relative_position_bias_table",
+              "layers.0.blocks.1.attn.qkv.weight", "up.expand.weight")
+
+
+def test_swinT_1024_bs1_fp32_backward_matches_oracle():
+    """Config 3 resolution, forward AND backward vs the oracle (fp32 parity mode): every
+    parameter-gradient norm within 2e-3 relative, and the full gradient tensors of the 1024^2
+    refine convs (conv dgrad / wgrad at 1024^2), the shifted stage-0 block's relative-position
+    table (the 1369-window attention backward) and qkv weight, and the x4 expand within 2e-3
+    of their largest entry (reference model_parts.py:437-476, 775-855)."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd.loss import DynamicLoss
+    from semantic_segmentation_of_stylegan2_artifacts_amd.data import synthetic_batch
+    torch.set_num_threads(16)
+    cfg = make_cfg(img_size=1024, drop_path_rate=0.0, **SWIN_T)
+    params = init_params(cfg, seed=23)
+    x, y = synthetic_batch(1, 1024, "cpu", 123)
+    assert float(y.sum()) > 0  # a fake image: the Tversky term is live
+    ref_p = {k: (v.clone().requires_grad_(True) if v.is_floating_point() else v) for k, v in params.items()}
+    ref = msunet_forward(ref_p, cfg, x)
+    ref_loss = oracle_loss(ref, y, 0.2, 0.8, 0.45)
+    ref_loss.backward()
+
+    model = _model(cfg)
+    model.load_state_dict(params, strict=True)
+    model = model.to(DEV).train()
+    logits = model(x.to(DEV))
+    err = (logits.detach().cpu() - ref.detach()).abs().max().item()
+    assert err <= 1e-3 * ref.detach().abs().max().item(), err
+    loss = DynamicLoss(alpha=0.2, beta=0.8, tversky_bce_mix=0.45)(logits, y.to(DEV))
+    assert abs(loss.item() - ref_loss.item()) <= 1e-4 * max(1.0, abs(ref_loss.item()))
+    loss.backward()
+    n = 0
+    for k, p in model.named_parameters():
+        rg = ref_p[k].grad
+        if rg is None:  # the discarded central-decoder blocks
+            assert p.grad is None, k
+            continue
+        assert p.grad is not None, k
+        gn, rn = p.grad.norm().item(), rg.norm().item()
+        assert abs(gn - rn) <= 2e-3 * rn + 1e-6, (k, gn, rn)
+        n += 1
+        if k in FULL_GRADS:
+            e = (p.grad.detach().cpu() - rg).abs().max().item()
+            assert e <= 2e-3 * rg.abs().max().item(), (k, e, rg.abs().max().item())
+    assert n > 300
+
+
 @pytest.mark.parametrize("backbone,img,bs", [("swin_t", 512, 8), ("swin_t", 1024, 8), ("swin_s", 1024, 8),
                                              ("swin_b", 1024, 4)])
 def test_bf16_training_step_at_baseline_config(backbone, img, bs):

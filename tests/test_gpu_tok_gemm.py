@@ -197,3 +197,67 @@ def test_linear_cat_matches_cat_then_linear(M, C, low):
     for name, a, r in [("dw", wg.grad, wr.grad), ("db", bg.grad, br.grad)]:
         err = (a.float().cpu() - r).abs().max().item()
         assert err <= 2e-2 * r.abs().max().item(), f"{name}: {err:.3e}"
+
+
+# ----------------------------------------------------------------------------- production M
+# The benchmarked step (Swin-T, 8 x 1024^2) runs these GEMMs at M = 8 * 256^2 = 524288 stage-0
+# tokens (131072 at stage 1).  Same fp32 reference and tolerance as above, at full size
+# (the small-M tests alone do not pin the benchmarked path).
+T0 = 8 * 256 ** 2
+PROD = [(T0, 288, 96), (T0, 96, 96), (T0, 384, 96), (T0, 96, 384), (T0, 96, 288), (T0 // 4, 576, 192),
+        (T0 // 4, 192, 576), (T0 // 4, 192, 384), (T0, 96, 48), (T0, 96, 192)]
+
+
+@pytest.fixture(autouse=False)
+def strict_fp32():
+    prev = torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = False
+    yield
+    torch.backends.cuda.matmul.allow_tf32 = prev
+
+
+@pytest.mark.parametrize("M,N,K", PROD)
+def test_tok_gemm_production_M(M, N, K, strict_fp32):
+    """Plain + bias epilogue at the benchmark's token counts (forward shapes and the input
+    gradients' [M, N] x [N, K] shapes: qkv, proj, fc1, fc2, merge reduction, patch embed, skip)."""
+    ops = _ops()
+    assert ops.tok_supported(M, N, K), (M, N, K)
+    a, w, b = _inputs(M, N, K, N + K, torch.bfloat16)
+    y = ops.tok_gemm(a, w, b)
+    ref = torch.addmm(b, a.float(), w.float().t())
+    _check(y, ref, f"plain {M}x{N}x{K}")
+
+
+def test_tok_gemm_gelu_epilogues_production_M(strict_fp32):
+    """mlp.0's GELU dual epilogue (H, GELU(H)) and mlp.3's GELU' input-gradient epilogue at
+    M = 524288 (stage-0 fc1 / fc2, model_parts.py:143-151 via torchvision's MLP)."""
+    ops = _ops()
+    M, N, K = T0, 384, 96
+    a, w, b = _inputs(M, N, K, 31, torch.bfloat16)
+    h, g = ops.tok_gemm(a, w, b, ops.TOK_GELU_DUAL)
+    ref_h = torch.addmm(b, a.float(), w.float().t())
+    _check(h, ref_h, "H")
+    del ref_h
+    _check(g, F.gelu(h.float()), "GELU(H)")
+    g2 = torch.Generator().manual_seed(6)
+    dy = torch.randn(M, K, generator=g2).to(DEV, torch.bfloat16)
+    w2t = (torch.randn(N, K, generator=g2) / K ** 0.5).to(DEV, torch.bfloat16)
+    dh = ops.tok_gemm(dy, w2t, None, ops.TOK_GELU_GRAD, h=h)
+    hf = h.float()
+    # d/dh GELU(h) = Phi(h) + h * phi(h)
+    gp = 0.5 * (1 + torch.erf(hf / 2 ** 0.5)) + hf * torch.exp(-0.5 * hf * hf) / (2 * torch.pi) ** 0.5
+    ref = (dy.float() @ w2t.float().t()) * gp
+    _check(dh, ref, "dH")
+
+
+def test_linear_cat_production_M(strict_fp32):
+    """Skip fusion at stage 0 (concat_back_dim[3]: [x | skip] 2x96 -> 96 over 524288 tokens):
+    forward, both input gradients, weight and bias gradients vs fp32 autograd."""
+    test_linear_cat_matches_cat_then_linear(T0, 96, torch.bfloat16)
+
+
+def test_fused_mlp_production_M(strict_fp32):
+    """The stage-0 fused MLP (fc1 GELU dual -> fc2; backward: fc2 wgrad, GELU' dgrad, fc1 wgrad
+    and dgrad) at M = 524288 and the stage-1 one at 131072 vs fp32 autograd."""
+    test_fused_mlp_matches_fp32(T0, 96, torch.bfloat16)
+    test_fused_mlp_matches_fp32(T0 // 4, 192, torch.bfloat16)

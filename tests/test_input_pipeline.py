@@ -162,6 +162,10 @@ def test_sample_rng_is_keyed():
     assert a[0] == b[0] and a[1] == b[1] and np.array_equal(a[2], b[2])
     ops = {aug.draw(aug.sample_rng(1, 2, i), True, True)[0] for i in range(64)}
     assert len(ops) > 4
+    # indices >= 2^20 must not alias (epoch, index) pairs of other epochs
+    big = 1 << 20
+    sig = lambda e, i: aug.sample_rng(1, e, i).getrandbits(64)  # noqa: E731
+    assert sig(0, big) != sig(1, 0) and sig(0, big + 5) != sig(1, 5) and sig(3, 7) != sig(7, 3)
 
 
 # ------------------------------------------------------------------ oracle known answers (cv2 8U)

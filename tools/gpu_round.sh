@@ -25,5 +25,5 @@ timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_$TAG -o write --output-f
     python3 $R/tools/conv_one.py 0 3 fwd act >> $O/pmc_$TAG.log 2>&1 || { tail -20 $O/pmc_$TAG.log; exit 1; }
 python3 $R/tools/pmc_json.py conv3x3_v2_kernel $O/pmc_$TAG/fetch_counter_collection.csv \
     $O/pmc_$TAG/write_counter_collection.csv $O/conv3x3_fwd_pmc_$TAG.json
-python3 $R/tools_profsum.py $O/prof_$TAG/run_kernel_stats.csv 6 40
+python3 $R/tools/profsum.py $O/prof_$TAG/run_kernel_stats.csv 6 40
 echo done
