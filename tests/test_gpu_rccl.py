@@ -47,7 +47,7 @@ def rccl_group():
     dist.destroy_process_group()
 
 
-def _run(pg, graph, reduce, wire=None, steps=5):
+def _run(pg, graph, reduce, wire=None, steps=5, bucket_mb=1.0):
     from semantic_segmentation_of_stylegan2_artifacts_amd import load_config, ops
     from semantic_segmentation_of_stylegan2_artifacts_amd.network.model_parts import MSUNetSys
     from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import Trainer
@@ -60,7 +60,7 @@ def _run(pg, graph, reduce, wire=None, steps=5):
     x, t = cases.model_inputs(cfg, 2, spec["seed"])
     x, t = x.to(DEV), t.to(DEV)
     tr = Trainer(m, load_config(None, "swin_t", **{"TRAIN.BASE_LR": 1e-3}), DEV, use_graph=graph,
-                 graph_warmup=2, process_group=pg, always_reduce=reduce, bucket_mb=1 / 16,
+                 graph_warmup=2, process_group=pg, always_reduce=reduce, bucket_mb=bucket_mb,
                  grad_wire_dtype=wire)
     losses = []
     for i in range(steps):
@@ -76,16 +76,19 @@ def _run(pg, graph, reduce, wire=None, steps=5):
 
 def test_rccl_bucketer_eager_equals_no_dp(rccl_group):
     l0, s0, _ = _run(None, False, False)
-    l1, s1, info = _run(rccl_group, False, True)
-    assert info["buckets"] > 20 and info["comm"] and info["skipped"] == 0
+    l1, s1, info = _run(rccl_group, False, True, bucket_mb=1 / 16)  # ~2600 buckets
+    assert info["buckets"] > 1000 and info["comm"] and info["skipped"] == 0
     assert l0 == l1
     for a, b in zip(s0, s1):
         assert torch.equal(a, b)
 
 
 def test_rccl_bucketer_graph_replay_equals_eager(rccl_group):
-    le, se, _ = _run(rccl_group, False, True)
-    lg, sg, info = _run(rccl_group, True, True)
+    # 4 MB buckets (~40 all-reduces captured): a graph of ~2600 RCCL nodes (64 KB buckets)
+    # crashed hipStreamEndCapture on ROCm 7.2; the product default is 32 MB
+    le, se, _ = _run(rccl_group, False, True, bucket_mb=4)
+    lg, sg, info = _run(rccl_group, True, True, bucket_mb=4)
+    assert info["buckets"] > 20
     assert info["captured"], "the step with RCCL all-reduces was not captured"
     assert lg == pytest.approx(le, rel=1e-5, abs=1e-6), (le, lg)
     for a, b in zip(se, sg):
