@@ -7,8 +7,9 @@
 //   * 128 x 128 output tile per 4-wave workgroup (waves 2 x 2, 64 x 64 each, four 32 x 32
 //     accumulators), K steps of 64 (or 32);
 //   * A and W tiles go global -> LDS by LDS-DMA (global_load_lds_dwordx4), double-buffered: the
-//     next K step's tiles are in flight while this one's MFMAs run (counted vmcnt + raw
-//     s_barrier, so the barrier does not drain the prefetch);
+//     next K step's tiles are in flight while this one's MFMAs run (raw s_barrier);
+//   * persistent: the workgroups walk their tiles as one flat sequence of K steps (the ring
+//     runs across tile boundaries; see gemm_nt_kernel);
 //   * the LDS image is lane-linear (the DMA's constraint) with the 16-B k-chunks of each row
 //     permuted by the row's position in its 256-B bank row: the fragment reads (16 rows x 16 B
 //     per quarter-wave) then hit every bank group once -- the permutation is applied to the
@@ -19,9 +20,9 @@
 //   * blocks are mapped XCD-contiguously with the N tiles of one M tile adjacent: the A rows of
 //     a tile are fetched from HBM once per XCD and re-read from its L2 by the other N tiles.
 // Model call sites: network/model_parts.py Mlp / WindowAttention qkv / proj, PatchMerging
-// reduction, PatchExpand expand, concat_back_dim (via ops.linear / ops.mlp) when routed in
-// (ops.gemm_route, MSU_GEMM_ROUTE=nt): alone it beats hipBLASLt on most stage 1-3 shapes, inside
-// the overlapped training step it has not (GEMM routing).
+// reduction, PatchExpand expand, concat_back_dim (via ops.linear / ops.mlp), routed by
+// ops.gemm_route for the stage 1-3 shapes the token GEMM does not take.
+#include <cstdlib>
 #include <cstring>
 
 #include "common.h"
@@ -39,7 +40,7 @@ struct NtArgs {
   bf16_t* Y2;          // [M][N] (GELU_DUAL: GELU(Y))
   const bf16_t* H;     // [M][N] (GELU_GRAD: pre-activation)
   int M, N, K;
-  int tiles_n;
+  int tiles_m, tiles_n;
 };
 
 // Tile geometry for a K step of BK: CH = BK / 8 16-B chunks per row; a 256-B LDS bank row
@@ -104,30 +105,42 @@ struct KnTile {
   }
 };
 
-// Runtime-selected s_waitcnt vmcnt(n * PER), n in [0, 2] (DMA steps allowed to stay in flight)
-template <int PER>
-MSU_DEV void wait_steps(int n) {
-  if (n >= 2) wait_vmcnt<2 * PER>();
-  else if (n == 1) wait_vmcnt<PER>();
-  else wait_vmcnt<0>();
-}
-
-// NST-stage LDS ring of K steps (prefetch distance NST - 1, one barrier per K step): the
-// short-K stage 1-3 shapes (K = 192..768: 3-24 steps) otherwise wait out a DMA round trip per
-// step.  Fragments of k-slice ks + 1 are read before the MFMAs of ks.
+// Persistent: a grid of at most NT_WG_PER_CU workgroups per CU walks the output tiles t = L,
+// L + G, L + 2G, ... (L = the XCD-remapped block index, G = grid size) as ONE flat sequence of
+// K steps, so the LDS ring never drains at a tile boundary: the first K step of the next tile
+// is staged while the last one of the current tile is multiplied, and the epilogue's stores
+// leave while that DMA is in flight.  The stage-1..3 shapes have only 3-12 K steps per tile
+// (K = 192..768), so a per-tile prologue / epilogue was a large share of a non-persistent
+// tile's time.  In one round of tiles an XCD takes a contiguous range of tile indices, i.e.
+// the N tiles of a few M tiles: their A rows come from HBM once and from that XCD's L2 after.
+// Ring: NST = 2 stages of BK = 64 (64 KB of LDS: two workgroups per CU); the wait before a
+// step is vmcnt(0), which also retires the previous tile's epilogue stores.
 template <typename T, int EPI, int BK, int NST, bool WKN>
 __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs a) {
   typedef NtTile<BK> Tl;
-  static_assert(NST >= 2 && NST <= 4, "ring depth");
+  static_assert(NST == 2, "the epilogue stores are retired by the per-step vmcnt(0)");
   static_assert(!WKN || BK == 64, "[K][N] weights: 64-deep K steps");
   constexpr int KSL = BK / 16;  // 16-wide k slices per step
   __shared__ __attribute__((aligned(16))) bf16_t lds[NST][2][BM * BK];  // [stage][A | W]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;  // this wave's 64 x 64 quarter (tokens, columns)
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
-  const int m0 = mt * BM, n0 = nt * BN;
+  const int G = gridDim.x;
+  const int L = xcd_remap(blockIdx.x, G);
+  const int ntiles = a.tiles_m * a.tiles_n;
   const int nk = a.K / BK;  // K % 64 == 0 (nt_shape_ok)
+  const int mine = L < ntiles ? (ntiles - 1 - L) / G + 1 : 0;
+  const int nsteps = mine * nk;
+
+  // K step s of this workgroup's sequence -> LDS stage s % NST
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    const int ti = s / nk, kk = s - ti * nk;
+    const int t = L + ti * G;
+    const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
+    bf16_t* dst = lds[s & (NST - 1)][0];
+    Tl::stage(a.A, mt * BM, a.M, a.K, kk * BK, dst, tid);
+    if constexpr (WKN) KnTile::stage(a.W, nt * BN, a.N, kk * BK, dst + BM * BK, tid);
+    else Tl::stage(a.W, nt * BN, a.N, a.K, kk * BK, dst + BM * BK, tid);
+  };
 
   f32x16 acc[2][2];  // [column tile ni][token tile mi]: C^T, W rows on the accumulator rows
 #pragma unroll
@@ -135,26 +148,42 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
 
+  if (nsteps > 0) issue(0);
+  int kk = 0, ti = 0;  // K step within the tile, tile ordinal (within this workgroup)
+  for (int s = 0; s < nsteps; ++s) {
+    wait_vmcnt<0>();                // step s's DMA (and the last epilogue's stores) done
+    __builtin_amdgcn_s_barrier();   // every wave's DMA of step s has landed, and every wave is
+    asm volatile("" ::: "memory");  // done reading step s-1's stage (refilled below)
+    if (s + 1 < nsteps) issue(s + 1);
+    const bool last = kk + 1 == nk;
+    const int t = L + ti * G;
+    const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int hh = lane >> 5;
+    // the epilogue's operands (bias columns, GELU' pre-activations) are loaded before the
+    // tile's last MFMAs, all at once: one wait in the epilogue instead of one per store
+    float4 eb[2][2][2];
+    u32x4 eh[2][2][2];
+    if (last) {
 #pragma unroll
-  for (int s = 0; s < NST - 1; ++s)
-    if (s < nk) {
-      Tl::stage(a.A, m0, a.M, a.K, s * BK, lds[s][0], tid);
-      if constexpr (WKN) KnTile::stage(a.W, n0, a.N, s * BK, lds[s][1], tid);
-      else Tl::stage(a.W, n0, a.N, a.K, s * BK, lds[s][1], tid);
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const int n = min(n0 + 64 * wn + 32 * ni + 16 * g + 8 * hh, a.N - 8);
+          if constexpr (EPI == EPI_GELU_GRAD) {
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) {
+              const int m = min(m0 + 64 * wm + 32 * mi + (lane & 31), a.M - 1);
+              eh[mi][ni][g] = *reinterpret_cast<const u32x4*>(a.H + (size_t)m * a.N + n);
+            }
+          } else if (a.bias) {
+            eb[ni][g][0] = *reinterpret_cast<const float4*>(a.bias + n);
+            eb[ni][g][1] = *reinterpret_cast<const float4*>(a.bias + n + 4);
+          }
+        }
     }
-  for (int kt = 0; kt < nk; ++kt) {
-    // this step's DMAs done; those of steps kt+1 .. kt+NST-2 may stay in flight
-    wait_steps<Tl::CH>(min(NST - 2, nk - 1 - kt));
-    __builtin_amdgcn_s_barrier();  // every wave's DMA of step kt has landed, and every wave is
-    asm volatile("" ::: "memory");  // done reading step kt-1's stage (refilled below)
-    if (kt + NST - 1 < nk) {
-      const int sn = (kt + NST - 1) % NST;
-      Tl::stage(a.A, m0, a.M, a.K, (kt + NST - 1) * BK, lds[sn][0], tid);
-      if constexpr (WKN) KnTile::stage(a.W, n0, a.N, (kt + NST - 1) * BK, lds[sn][1], tid);
-      else Tl::stage(a.W, n0, a.N, a.K, (kt + NST - 1) * BK, lds[sn][1], tid);
-    }
-    const bf16_t* ta = lds[kt % NST][0];
-    const bf16_t* tw = lds[kt % NST][1];
+    const bf16_t* ta = lds[s & (NST - 1)][0];
+    const bf16_t* tw = ta + BM * BK;
     bf16x8 fw[2][2], fx[2][2];
     auto rd = [&](int ks, int set) {
       if constexpr (WKN) {
@@ -178,55 +207,65 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs a) {
       acc[1][1] = Fmt16<T>::mma32(fw[cur][1], fx[cur][1], acc[1][1]);
       __builtin_amdgcn_sched_barrier(0);
     }
-  }
-
-  // epilogue: lane (l & 31) is token m; after the swap, 8 consecutive columns per store
-  const int hh = lane >> 5;
+    if (!last) {
+      ++kk;
+      continue;
+    }
+    kk = 0;
+    ++ti;
+    wait_vmcnt<0>();  // the epilogue operands (and the next step's DMA) have landed: one wait,
+                      // not one per exec-masked store branch
+    // ---- epilogue of tile t: lane (l & 31) is token m; after the swap, 8 consecutive columns
+    // per store
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi) {
-    const int m = m0 + 64 * wm + 32 * mi + (lane & 31);
+    for (int mi = 0; mi < 2; ++mi) {
+      const int m = m0 + 64 * wm + 32 * mi + (lane & 31);
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
+      for (int ni = 0; ni < 2; ++ni) {
 #pragma unroll
-      for (int g0 = 0; g0 < 4; g0 += 2) {
-        float v[8];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[ni][mi][4 * g0 + i]),
-                                                          __float_as_uint(acc[ni][mi][4 * g0 + 4 + i]), false, false);
-          v[i] = __uint_as_float(r[0]);
-          v[4 + i] = __uint_as_float(r[1]);
-        }
-        const int n = n0 + 64 * wn + 32 * ni + 8 * g0 + 8 * hh;
-        if (m >= a.M || n >= a.N) continue;
-        if (a.bias) {
-          const float4 b0 = *reinterpret_cast<const float4*>(a.bias + n);
-          const float4 b1 = *reinterpret_cast<const float4*>(a.bias + n + 4);
-          v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
-          v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-        }
-        const size_t off = (size_t)m * a.N + n;
-        if constexpr (EPI == EPI_GELU_GRAD) {
-          const u32x4 hv = *reinterpret_cast<const u32x4*>(a.H + off);
+        for (int g0 = 0; g0 < 4; g0 += 2) {
+          float v[8];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            v[2 * i] *= gelu_grad_fast(Fmt16<T>::lo(hv[i]));
-            v[2 * i + 1] *= gelu_grad_fast(Fmt16<T>::hi(hv[i]));
+            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[ni][mi][4 * g0 + i]),
+                                                            __float_as_uint(acc[ni][mi][4 * g0 + 4 + i]), false, false);
+            v[i] = __uint_as_float(r[0]);
+            v[4 + i] = __uint_as_float(r[1]);
           }
-        }
-        const u32x4 pk = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
-        *reinterpret_cast<u32x4*>(a.Y + off) = pk;
-        if constexpr (EPI == EPI_GELU_DUAL) {
-          // GELU of the rounded pre-activation, as the unfused GELU kernel would see it
-          float gv[8];
+          const int n = n0 + 64 * wn + 32 * ni + 8 * g0 + 8 * hh;
+          if (m >= a.M || n >= a.N) continue;
+          if (EPI != EPI_GELU_GRAD && a.bias) {
+            const float4 b0 = eb[ni][g0 >> 1][0], b1 = eb[ni][g0 >> 1][1];
+            v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+            v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+          }
+          const size_t off = (size_t)m * a.N + n;
+          if constexpr (EPI == EPI_GELU_GRAD) {
+            const u32x4 hv = eh[mi][ni][g0 >> 1];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) gv[i] = gelu_fast(round16<T>(v[i]));
-          const u32x4 pg = {pack2<T>(gv[0], gv[1]), pack2<T>(gv[2], gv[3]), pack2<T>(gv[4], gv[5]),
-                            pack2<T>(gv[6], gv[7])};
-          *reinterpret_cast<u32x4*>(a.Y2 + off) = pg;
+            for (int i = 0; i < 4; ++i) {
+              v[2 * i] *= gelu_grad_fast(Fmt16<T>::lo(hv[i]));
+              v[2 * i + 1] *= gelu_grad_fast(Fmt16<T>::hi(hv[i]));
+            }
+          }
+          const u32x4 pk = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
+          *reinterpret_cast<u32x4*>(a.Y + off) = pk;
+          if constexpr (EPI == EPI_GELU_DUAL) {
+            // GELU of the rounded pre-activation, as the unfused GELU kernel would see it
+            float gv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) gv[i] = gelu_fast(round16<T>(v[i]));
+            const u32x4 pg = {pack2<T>(gv[0], gv[1]), pack2<T>(gv[2], gv[3]), pack2<T>(gv[4], gv[5]),
+                              pack2<T>(gv[6], gv[7])};
+            *reinterpret_cast<u32x4*>(a.Y2 + off) = pg;
+          }
         }
       }
     }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
   }
 }
 
@@ -234,22 +273,27 @@ bool nt_shape_ok(long M, int N, int K) {
   return M > 0 && M < (1L << 31) && N > 0 && N % 32 == 0 && K > 0 && K % 64 == 0 && (long)M * N < (1L << 40);
 }
 
-// Ring configuration (A/B switch MSU_NT_CFG = BKxNST): 64x2 (default: 64 KB of LDS, one K step
-// in flight), 32x4 (64 KB, three steps in flight), 32x3 (48 KB: three workgroups per CU).  The
-// deeper rings measured 2-15 % slower alone (tools/nt_cfg_ab.sh): the per-step DMA latency is
-// not what bounds these tiles.
-int nt_cfg() {
-  static const int cfg = [] {
-    const char* e = getenv("MSU_NT_CFG");
-    if (e && !strcmp(e, "32x4")) return 324;
-    if (e && !strcmp(e, "32x3")) return 323;
-    return 642;
+// Workgroups per CU of the persistent grid (A/B switch MSU_NT_WG_PER_CU, 1 or 2; default 2:
+// the LDS of two 64 KB rings) and the CU budget (MSU_NT_CUS: leave CUs to the weight-gradient
+// side stream; default all).
+int nt_grid_cap() {
+  static const int cap = [] {
+    int cus = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    const char* e = getenv("MSU_NT_CUS");
+    if (e && atoi(e) > 0 && atoi(e) < cus) cus = atoi(e);
+    const char* w = getenv("MSU_NT_WG_PER_CU");
+    const int per = (w && atoi(w) == 1) ? 1 : 2;
+    return cus * per;
   }();
-  return cfg;
+  return cap;
 }
 
 template <typename T, int BK, int NST, bool WKN>
 void launch_nt(int epi, long tiles, const NtArgs& a, hipStream_t st) {
+  const long cap = nt_grid_cap();
+  if (tiles > cap) tiles = cap;
   switch (epi) {
     case EPI_PLAIN: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_PLAIN, BK, NST, WKN>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
     case EPI_GELU_DUAL: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_DUAL, BK, NST, WKN>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
@@ -275,13 +319,13 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
   a.N = N;
   a.K = K;
   a.tiles_n = (N + BN - 1) / BN;
-  const long tiles = (long)((M + BM - 1) / BM) * a.tiles_n;
+  a.tiles_m = (int)((M + BM - 1) / BM);
+  const long tiles = (long)a.tiles_m * a.tiles_n;
+  if (tiles >= (1L << 31)) return -2;
   hipStream_t st = (hipStream_t)stream;
   MSU_DISPATCH16(dtype, T,
     if (wkn) launch_nt<T, 64, 2, true>(epi, tiles, a, st);
-    else if (nt_cfg() == 642) launch_nt<T, 64, 2, false>(epi, tiles, a, st);
-    else if (nt_cfg() == 323) launch_nt<T, 32, 3, false>(epi, tiles, a, st);
-    else launch_nt<T, 32, 4, false>(epi, tiles, a, st));
+    else launch_nt<T, 64, 2, false>(epi, tiles, a, st));
   return MSU_CHECK_LAUNCH();
 }
 

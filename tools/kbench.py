@@ -206,6 +206,10 @@ def nt():
             ref = torch.nn.functional.linear(a.float(), w.float(), bias)
             err = ((ops.nt_gemm(a, w, bias).float() - ref).norm() / ref.norm()).item()
             line += f"  nt {ms*1e3:6.1f} us ({fl/ms/1e9:6.1f} TF/s, rel err {err:.1e})"
+            wk = w.t().contiguous()  # [K][N]: an input-gradient GEMM's forward weight, read in place
+            mkn = timeit(lambda: ops.nt_gemm_kn(a, wk))
+            mlk = timeit(lambda: a.matmul(wk))
+            line += f"  kn {mkn*1e3:6.1f} us (lib {mlk*1e3:6.1f})"
         if ops.tok_supported(M, N, K):
             mk = timeit(lambda: ops.tok_gemm(a, w, bias))
             line += f"  tok {mk*1e3:6.1f} us"
