@@ -715,12 +715,12 @@ def _shadow(param, dt):
 
 
 # GEMM routing of the 16-bit Linears (forward and input gradient): the token GEMM (weight in
-# LDS, tokens streamed) for the HBM-bound stage-0 shapes and the narrow-K stage-1 qkv, the
-# library GEMM (hipBLASLt) for the wide-weight stage 1-3 shapes.  The tiled NT GEMM
-# (csrc/gemm_nt.hip, MSU_GEMM_ROUTE=nt) beats hipBLASLt on 17 of the 21 stage 1-3 shapes in
-# isolation (tools/kbench.py nt: 1.0-1.7x) but costs 1-2 % of the overlapped training step
-# (GEMM routing), so it is opt-in.  MSU_GEMM_ROUTE=lib: the library GEMM wherever the
-# epilogue allows it.
+# LDS, tokens streamed) for the HBM-bound stage-0 shapes and the narrow-K stage-1 shapes, the
+# persistent tiled NT GEMM (csrc/gemm_nt.hip) for the wide-weight stage 1-3 shapes -- every
+# Linear of the step runs on a hand-written kernel.  A/B switches (MSU_GEMM_ROUTE): "lib" =
+# the library GEMM (hipBLASLt) wherever the epilogue allows it, "ntmlp" = the NT GEMM only for
+# the GELU-epilogue MLP GEMMs (library elsewhere), "nt" = the NT GEMM before the narrow-K token
+# GEMM plans.
 _ROUTE_FORCE = os.environ.get("MSU_GEMM_ROUTE", "")
 
 
@@ -738,7 +738,7 @@ def gemm_route(M, N, K, epi=TOK_PLAIN):
             r = "nt"
         elif tok and (N * K <= 576 * 192 or (epi != TOK_PLAIN and M >= 131072)):
             r = "tok"
-        elif _ROUTE_FORCE == "ntlib" and nt_supported(M, N, K):
+        elif _ROUTE_FORCE in ("", "ntlib") and nt_supported(M, N, K):
             r = "nt"
         elif _ROUTE_FORCE == "ntmlp" and epi != TOK_PLAIN and nt_supported(M, N, K):
             r = "nt"

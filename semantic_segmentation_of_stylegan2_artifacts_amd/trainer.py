@@ -194,6 +194,16 @@ class GradBucketer:
         # autograd runs a side-stream node) and on the weight-gradient side stream
         dev = g.grad.device
         main = self.main_stream if self.main_stream is not None else torch.cuda.current_stream(dev)
+        if torch.cuda.is_current_stream_capturing():
+            # under HIP-graph capture the collective is issued from the capturing main stream
+            # (the graph runs it as a branch of its own anyway): a capture that also forked the
+            # comm stream crashed hipStreamEndCapture on ROCm 7.2 (tests/test_gpu_rccl.py)
+            side = ops.side_stream(dev)
+            if side is not None:
+                main.wait_stream(side)
+            with torch.cuda.stream(main):
+                self.works.append((b,) + self._reduce(b, g, s, e))
+            return
         self.comm.wait_stream(main)
         side = ops.side_stream(dev)
         if side is not None:
@@ -222,8 +232,8 @@ class GradBucketer:
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
-        if self.comm is None:
-            for b, w, buf in self.works:
+        if self.comm is None or torch.cuda.is_current_stream_capturing():
+            for b, w, buf in self.works:  # (the current stream waits for each collective)
                 w.wait()
                 if buf is not None:
                     self._unwire(b, buf)
