@@ -157,12 +157,16 @@ int msu_tok_gemm_supported_epi(long M, int N, int K, int epi);
 int msu_tok_gemm(int dtype, const void* A, const void* A2, int K1, const void* W, const float* bias, void* Y,
                  void* Y2, const void* H, long M, int N, int K, int epi, void* stream);
 int msu_tok_gemm_plan(long M, int N, int K, long* out6);
-/* Tiled NT GEMM (128 x 128 tiles, LDS-DMA double buffering) for the stage 1-3 Linears, whose
- * wide weights do not fit the token GEMM's LDS: same Y / epi semantics as msu_tok_gemm without
- * the split-A input.  Covered: N % 32 == 0, K % 64 == 0. */
+/* Persistent tiled NT GEMM (128 x 128 tiles, LDS-DMA double buffering, one flat K-step sequence per
+ * workgroup) for the stage 1-3 Linears, whose wide weights do not fit the token GEMM's LDS: same
+ * Y / epi semantics as msu_tok_gemm.  Covered: N % 32 == 0, K % 64 == 0. */
 int msu_nt_gemm_supported(long M, int N, int K);
 int msu_nt_gemm(int dtype, const void* A, const void* W, const float* bias, void* Y, void* Y2, const void* H,
                 long M, int N, int K, int epi, void* stream);
+/* Plain epilogue with the split-A input of msu_tok_gemm: A's columns [K1, K) from A2 (K1 % 64 == 0):
+ * the wide skip fusions (concat_back_dim at stages 1-3, model_parts.py:792-794, :804-806, :823-824). */
+int msu_nt_gemm_cat(int dtype, const void* A, const void* A2, int K1, const void* W, const float* bias, void* Y,
+                    long M, int N, int K, void* stream);
 /* The same with the weight given as Wk[K][N]: Y = epi(A . Wk + bias).  The input gradient of a
  * Linear, dX = dY . W with the forward weight W[N_fwd][K_fwd] (K = N_fwd, N = K_fwd) read in place
  * (transposed LDS fragment reads) instead of a W^T copy per call (torch F.linear backward,

@@ -61,6 +61,7 @@ SIGNATURES = {
     "msu_nt_gemm_supported": (I, [L, I, I]),
     "msu_nt_gemm": (I, [I, P, P, P, P, P, P, L, I, I, I, P]),
     "msu_nt_gemm_kn": (I, [I, P, P, P, P, P, P, L, I, I, I, P]),
+    "msu_nt_gemm_cat": (I, [I, P, P, I, P, P, P, L, I, I, P]),
     "msu_metrics_nblk": (I, [L]),
     "msu_seg_metrics": (I, [I, P, P, I, L, F, P, I, P, P]),
     "msu_augment_batch": (I, [P, P, P, P, P, P, I, I, I, P]),

@@ -33,13 +33,14 @@ constexpr int BM = 128, BN = 128;
 enum { EPI_PLAIN = 0, EPI_GELU_DUAL = 1, EPI_GELU_GRAD = 2 };
 
 struct NtArgs {
-  const bf16_t* A;     // [M][K]
+  const bf16_t* A;     // [M][K] (or [M][K1] when A2 is set)
+  const bf16_t* A2;    // null, or A's columns [K1, K): [M][K - K1] (the skip concatenation)
   const bf16_t* W;     // [N][K]
   const float* bias;   // [N] or null
   bf16_t* Y;           // [M][N]
   bf16_t* Y2;          // [M][N] (GELU_DUAL: GELU(Y))
   const bf16_t* H;     // [M][N] (GELU_GRAD: pre-activation)
-  int M, N, K;
+  int M, N, K, K1;
   int tiles_m, tiles_n;
 };
 
@@ -137,7 +138,9 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs a) {
     const int t = L + ti * G;
     const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
     bf16_t* dst = lds[s & (NST - 1)][0];
-    Tl::stage(a.A, mt * BM, a.M, a.K, kk * BK, dst, tid);
+    if (a.A2 == nullptr) Tl::stage(a.A, mt * BM, a.M, a.K, kk * BK, dst, tid);
+    else if (kk * BK < a.K1) Tl::stage(a.A, mt * BM, a.M, a.K1, kk * BK, dst, tid);  // K1 % BK == 0
+    else Tl::stage(a.A2, mt * BM, a.M, a.K - a.K1, kk * BK - a.K1, dst, tid);
     if constexpr (WKN) KnTile::stage(a.W, nt * BN, a.N, kk * BK, dst + BM * BK, tid);
     else Tl::stage(a.W, nt * BN, a.N, a.K, kk * BK, dst + BM * BK, tid);
   };
@@ -302,14 +305,17 @@ void launch_nt(int epi, long tiles, const NtArgs& a, hipStream_t st) {
 }
 
 int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* Y, void* Y2, const void* H, long M,
-              int N, int K, int epi, void* stream, bool wkn) {
+              int N, int K, int epi, void* stream, bool wkn, const void* A2 = nullptr, int K1 = 0) {
   if (!msu_is16(dtype)) return -3;
   if (!nt_shape_ok(M, N, K)) return -2;
   if (epi == EPI_GELU_DUAL && (Y2 == nullptr || bias == nullptr)) return -3;
   if (epi == EPI_GELU_GRAD && (H == nullptr || bias != nullptr)) return -3;
   if (epi < 0 || epi > 2) return -3;
   NtArgs a;
+  if (A2 != nullptr && (wkn || epi != EPI_PLAIN || K1 <= 0 || K1 >= K || K1 % 64)) return -3;
   a.A = (const bf16_t*)A;
+  a.A2 = (const bf16_t*)A2;
+  a.K1 = A2 != nullptr ? K1 : K;
   a.W = (const bf16_t*)W;
   a.bias = bias;
   a.Y = (bf16_t*)Y;
@@ -342,6 +348,14 @@ int msu_nt_gemm_supported(long M, int N, int K) { return nt_shape_ok(M, N, K) ? 
 int msu_nt_gemm(int dtype, const void* A, const void* W, const float* bias, void* Y, void* Y2, const void* H,
                 long M, int N, int K, int epi, void* stream) {
   return nt_launch(dtype, A, W, bias, Y, Y2, H, M, N, K, epi, stream, false);
+}
+
+// Y[M][N] = [A | A2] . W^T + bias (plain epilogue): A [M][K1], A2 [M][K - K1], K1 % 64 == 0 -- the
+// skip fusion torch.cat([x, skip], -1) -> concat_back_dim Linear without the concatenated copy.
+int msu_nt_gemm_cat(int dtype, const void* A, const void* A2, int K1, const void* W, const float* bias, void* Y,
+                    long M, int N, int K, void* stream) {
+  if (A2 == nullptr) return -3;
+  return nt_launch(dtype, A, W, bias, Y, nullptr, nullptr, M, N, K, EPI_PLAIN, stream, false, A2, K1);
 }
 
 // Same with the weight given as Wk[K][N] (Y = epi(A . Wk + bias)): the input gradient of a Linear,

@@ -603,13 +603,6 @@ def tok_supported_epi(M, N, K, epi):
 
 
 
-def tok_preferred(M, N, K):
-    """Token GEMM where it beats hipBLASLt (measured, tools/kbench.py tok): the HBM-bound
-    stage-0 shapes (M >= 256k tokens) and small weights (N*K <= 576*192); wider weights at
-    smaller M are MFMA-heavier and stay on the library GEMM."""
-    return tok_supported(M, N, K) and (M >= 262144 or N * K <= 576 * 192)
-
-
 def tok_gemm(a, w, bias=None, epi=TOK_PLAIN, h=None, a2=None):
     """16-bit Y = epi(A . W^T + bias) on the token GEMM kernel.  a: [..., K1] (+ a2: [..., K-K1]),
     w: [N, K] (a's dtype), bias: [N] f32.  Returns Y (and GELU(Y) for TOK_GELU_DUAL)."""
@@ -829,8 +822,33 @@ def linear(x, weight, bias=None):
 
 
 # ----------------------------------------------------------------------------- skip fusion
+def nt_gemm_cat(x, skip, w, bias):
+    """16-bit Y = [x | skip] . W^T + bias on the NT GEMM (x's width a multiple of 64)."""
+    N, K = w.shape
+    K1 = x.shape[-1]
+    M = x.numel() // K1
+    x, skip = x.contiguous(), skip.contiguous()
+    y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=x.dtype)
+    _lib.call("msu_nt_gemm_cat", _dt(x), _p(x), _p(skip), K1, _p(w), _p(bias), _p(y), M, N, K, _s(x))
+    return y
+
+
+def _cat_route(M, N, K, C1):
+    """The GEMM that takes a skip fusion without the concatenated copy, or None."""
+    r = gemm_route(M, N, K)
+    if r == "tok" and C1 % 8 == 0:
+        return "tok"
+    if r == "nt" and C1 % 64 == 0:
+        return "nt"
+    return None
+
+
 def _linear_cat_impl(x, skip, weight, bias):
     W = _shadow(weight, x.dtype)
+    N, K = W.shape
+    C1 = x.shape[-1]
+    if _cat_route(x.numel() // C1, N, K, C1) == "nt":
+        return nt_gemm_cat(x, skip, W, _f32(bias))
     return tok_gemm(x, W, _f32(bias), a2=skip)
 
 
@@ -883,15 +901,15 @@ _linear_cat = _define("linear_cat", "(Tensor x, Tensor skip, Tensor weight, Tens
 def linear_cat(x, skip, weight, bias):
     """``F.linear(torch.cat([x, skip], -1), weight, bias)`` (skip fusion, model_parts.py:792-794,
     :804-806, :823-824); x / skip: [..., C1] / [..., C2] with equal leading dims.  16-bit: the
-    concatenation is folded into the token GEMM's A loads (no concatenated copy) and split back
-    out of the input gradient (two GEMMs over W's halves)."""
+    concatenation is folded into the A loads of the routed GEMM (token GEMM or NT GEMM: no
+    concatenated copy) and split back out of the input gradient (two GEMMs over W's halves)."""
     _need_cuda(x)
     dt = act_dtype()
     x, skip = _as(x, dt), _as(skip, dt)
     N, K = weight.shape
     C1, C2 = x.shape[-1], skip.shape[-1]
     M = x.numel() // C1
-    if dt in _LOW and bias is not None and C1 + C2 == K and C1 % 8 == 0 and tok_preferred(M, N, K):
+    if dt in _LOW and bias is not None and C1 + C2 == K and _cat_route(M, N, K, C1) is not None:
         return _linear_cat(x, skip, weight, bias)
     return linear(torch.cat([x, skip], -1), weight, bias)
 

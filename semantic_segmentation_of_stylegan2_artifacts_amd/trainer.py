@@ -561,7 +561,10 @@ class Trainer:
         if os.environ.get("MSU_GRAPH_SIDE", "0") != "1":
             ops._side_enabled = False
         try:
-            with torch.cuda.graph(graph):
+            # thread_local: the process group's watchdog thread keeps querying its events while
+            # this thread captures; in the default "global" mode such a query from another
+            # thread fails the capture (hipErrorStreamCaptureUnsupported, tests/test_gpu_rccl.py)
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 loss = self._device_step(self._sx, self._sy)
         except Exception as e:  # noqa: BLE001 -- any capture failure: stay eager, loudly
             ops._side_enabled = side_prev

@@ -170,11 +170,13 @@ def test_linear_uses_tok_gemm_and_matches(low):
     _check(xg.grad, xr.grad.to(DEV), "dx")
 
 
-@pytest.mark.parametrize("M,C", [(4096, 96), (1000, 192)])
+@pytest.mark.parametrize("M,C", [(4096, 96), (1000, 192), (2048, 384), (32768, 384)])
 def test_linear_cat_matches_cat_then_linear(M, C, low):
     """ops.linear_cat (skip fusion without the concatenated copy) == Linear(cat([x, skip])):
-    forward and all gradients, bf16 (model_parts.py:792-794)."""
+    forward and all gradients, bf16 (model_parts.py:792-794).  C = 96 / 192 take the token
+    GEMM's split-A loads, C = 384 (concat_back_dim[1] at stage 2) the NT GEMM's."""
     ops = _ops()
+    assert ops._cat_route(M, C, 2 * C, C) == ("nt" if C == 384 else "tok")
     g = torch.Generator().manual_seed(M + C)
     x = torch.randn(M, C, generator=g)
     sk = torch.randn(M, C, generator=g)
