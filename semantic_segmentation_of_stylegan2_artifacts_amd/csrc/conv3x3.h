@@ -12,6 +12,7 @@
 // weights).  wgrad reads both operands k-strided from natural [pixel][channel] LDS images
 // with ds_read_b64_tr_b16 (bf16) and writes deterministic per-block partials.
 #pragma once
+#include <cstdlib>
 #include <utility>
 
 #include "common.h"
@@ -515,6 +516,281 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_v2_kernel(const bf16_t* __res
   }
 }
 
+// ------------------------------------------------------------------ 16-bit fwd, v3 (C = 96)
+// The v2 kernel (8 waves x one output row) spends as many LDS cycles as MFMA cycles: per tap
+// and wave 24 ds_read_b128 for 18 MFMAs, plus 24 KB of register-staged weight writes per tap.
+// v3 halves both per output pixel:
+//   * a tile is 16 rows x 32 pixels x 96 channels; wave w owns rows 2w, 2w + 1, so each weight
+//     fragment feeds two MFMAs (reads per MFMA 5/6 instead of 4/3);
+//   * the halo [18][34][96] and the weight image of a tap [96][96] are stored UNPADDED with
+//     the 16-B chunk c of row / pixel p at c ^ ((p >> 2) & 3): a half-wave's fragment read
+//     (32 consecutive rows, one chunk) covers all 64 banks, and the 154 KB of LDS fit;
+//   * the weights of tap t + 1 arrive by LDS-DMA (global_load_lds_dwordx4, source addresses
+//     permuted by the same swizzle) into the other of two weight images while tap t runs --
+//     no registers and no ds_write for the weight ring, one barrier per tap;
+//   * the next tile's halo is loaded into registers at tap 1 and written to LDS after tap 8.
+// Epilogue as v2 (bias, DUAL = GELU(Y) as a second output, GELU'(S) for the backward-data
+// launches with S prefetched at tap 7, 16-B stores after a permlane32 swap).
+constexpr int V3_HALO_TAP = 1;
+constexpr int SPRE = 12;  // GELU' operand loads per lane (dgrad), issued at tap 7
+
+MSU_DEV int swz(int p) { return (p >> 2) & 3; }
+
+template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL>
+__global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restrict__ X,
+                                                         const bf16_t* __restrict__ Wt,
+                                                         const float* __restrict__ bias,
+                                                         const bf16_t* __restrict__ S,
+                                                         bf16_t* __restrict__ Y, bf16_t* __restrict__ Y2,
+                                                         ConvGeom g, int ntiles) {
+  constexpr int C = 96, CH = 12, NW = 8, MT = 2, TH = NW * MT, TWV = 32, HWD = TWV + 2;
+  constexpr int HPIX = (TH + 2) * HWD;  // 612 halo pixels
+  constexpr int HCH = HPIX * CH;        // 7344 16-B chunks
+  constexpr int NTHR = 64 * NW;
+  constexpr int NHC = (HCH + NTHR - 1) / NTHR;  // 15 chunks per thread
+  constexpr int WIMG = C * C;                   // elements of one tap's weight image
+  constexpr int WINS = WIMG * 2 / 1024;         // 18 DMA wave-instructions per tap
+  constexpr int WPER = (WINS + NW - 1) / NW;    // <= 3 per wave
+  static_assert(WINS * 1024 == WIMG * 2, "weight image in whole DMA instructions");
+
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  bf16_t* sX = reinterpret_cast<bf16_t*>(smem_raw);
+  bf16_t* sW = sX + HPIX * C;  // [2][96][96]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_x = (g.W + TWV - 1) / TWV, tiles_y = (g.H + TH - 1) / TH;
+  const int per_img = tiles_x * tiles_y;
+
+  auto coords = [&](int tile, int& b, int& y0, int& x0) {
+    b = tile / per_img;
+    const int r = tile - b * per_img;
+    y0 = (r / tiles_x) * TH;
+    x0 = (r - (r / tiles_x) * tiles_x) * TWV;
+  };
+  u32x4 hr[NHC];
+  auto load_halo = [&](int tile) {
+    int b, y0, x0;
+    coords(tile, b, y0, x0);
+    const int t = opaque(tid);
+#pragma unroll
+    for (int c = 0; c < NHC; ++c) {
+      const int i = t + NTHR * c;
+      const int pix = i / CH, ch = i - (i / CH) * CH;
+      const int row = pix / HWD, col = pix - (pix / HWD) * HWD;
+      const int y = y0 - 1 + row, x = x0 - 1 + col;
+      const bool ok = i < HCH && y >= 0 && y < g.H && x >= 0 && x < g.W;
+      // out-of-image chunks read the zero region: no select on the loaded value, so the load
+      // stays in flight until the halo is stored after tap 8 (address select, no branch)
+      const int yc = min(max(y, 0), g.H - 1), xc = min(max(x, 0), g.W - 1);
+      const bf16_t* in = X + pix_off32<IN_D2S>(b, yc, xc, g.H, g.W, C) + ch * 8;
+      const bf16_t* src = ok ? in : reinterpret_cast<const bf16_t*>(zero_src(i));
+      hr[c] = *reinterpret_cast<const u32x4*>(src);
+    }
+  };
+  auto store_halo = [&]() {
+    const int t = opaque(tid);
+#pragma unroll
+    for (int c = 0; c < NHC; ++c) {
+      const int i = t + NTHR * c;
+      if (HCH % NTHR == 0 || c + 1 < NHC || i < HCH) {
+        const int pix = i / CH, ch = i - (i / CH) * CH;
+        *reinterpret_cast<u32x4*>(sX + pix * C + ((ch ^ swz(pix)) << 3)) = hr[c];
+      }
+    }
+  };
+  // this wave's share of the DMA of tap `tap`'s weight image into buffer `buf`
+  auto dma_w = [&](int tap, int buf) {
+    const bf16_t* src = Wt + (long)tap * WIMG;
+    bf16_t* dst = sW + buf * WIMG;
+    const int ln = opaque(lane);
+#pragma unroll
+    for (int r = 0; r < WPER; ++r) {
+      const int k = wave + NW * r;
+      if (WINS % NW == 0 || k < WINS) {
+        const int q = 64 * k + ln;
+        const int row = q / CH, pos = q - (q / CH) * CH;
+        glds16(src + row * C + ((pos ^ swz(row)) << 3), dst + 512 * k);
+      }
+    }
+  };
+  // DMA wave-instructions this wave issues per tap (wave-uniform)
+  const int my_wdma = (WINS - wave + NW - 1) / NW;
+
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  load_halo(tile);
+  store_halo();
+  dma_w(0, 0);
+  int wbuf = 0;
+
+  const int xl = lane & 31, h = lane >> 5;
+  // lane chunk offsets (elements) of k steps with ks even / odd, for row / pixel swizzle sw:
+  // chunk 2ks + h -> 4 (ks >> 1) + ((2 (ks & 1) + h) ^ sw)
+  auto koff = [&](int sw, int odd) { return ((2 * odd + h) ^ sw) << 3; };
+  const int wsw = swz(xl);  // weight rows 32n + xl
+  const int wk0 = xl * C + koff(wsw, 0), wk1 = xl * C + koff(wsw, 1);
+
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int next = tile + gridDim.x;
+    int b, y0, x0;
+    coords(tile, b, y0, x0);
+    const int xo = x0 + xl;
+    f32x16 acc[MT][3];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 3; ++n) acc[m][n] = f32x16{0};
+    u32x4 sp[OUT_GGRAD ? MT : 1][OUT_GGRAD ? 3 : 1][2];
+
+    static_for([&](auto TAP) {
+      constexpr int tap = decltype(TAP)::value;
+      constexpr int dy = tap / 3, dx = tap % 3;
+      // W(tap) landed (this wave's DMAs; the halo loads issued after them may stay in flight),
+      // then the barrier: every wave's DMA landed, every wave done with the other buffer
+      if constexpr (tap == V3_HALO_TAP + 1) {
+        if (next < ntiles) wait_vmcnt<NHC>();
+        else wait_vmcnt<0>();
+      } else if constexpr (OUT_GGRAD && tap == 8) {
+        wait_vmcnt<SPRE>();  // the GELU' operands issued at tap 7 stay in flight
+      } else {
+        wait_vmcnt<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const bf16_t* wcur = sW + wbuf * WIMG;
+      if constexpr (tap < 8) {
+        dma_w(tap + 1, wbuf ^ 1);
+      } else {
+        if (next < ntiles) dma_w(0, wbuf ^ 1);
+      }
+      if constexpr (tap == V3_HALO_TAP) {
+        if (next < ntiles) load_halo(next);
+      }
+      if constexpr (OUT_GGRAD && tap == 7) {
+        // dgrad: the pre-activation S of this tile's outputs for the GELU' epilogue
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int y = min(y0 + 2 * wave + m, g.H - 1), xs = min(xo, g.W - 1);
+#pragma unroll
+          for (int n = 0; n < 3; ++n)
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp)
+              sp[m][n][pp] = *reinterpret_cast<const u32x4*>(S + pix_off32<OUT_D2S>(b, y, xs, g.H, g.W, C) + 32 * n +
+                                                             16 * pp + 8 * h);
+        }
+      }
+      // fragment lane offsets of this tap: X rows 2w + m + dy, pixels dx + xl
+      // (recomputed per tap through opaque(): hoisted, the nine taps' offsets would pin 36 VGPRs)
+      int xo0[MT], xo1[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int p = opaque((2 * wave + m + dy) * HWD + dx) + xl;
+        xo0[m] = p * C + koff(swz(p), 0);
+        xo1[m] = p * C + koff(swz(p), 1);
+      }
+      // X fragments double buffered (k step ks + 1 read before the MFMAs of ks); each weight
+      // fragment is read one co tile ahead of its two MFMAs (registers: the halo prefetch
+      // holds 60 VGPRs across the taps)
+      bf16x8 xa[2][MT], wf[2];
+      auto read_x = [&](auto KSI, int set) __attribute__((always_inline)) {
+        constexpr int ks = decltype(KSI)::value;
+        constexpr int kb = 32 * (ks >> 1);  // elements: 4 chunks per even / odd pair
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          xa[set][m] = *reinterpret_cast<const bf16x8*>(sX + ((ks & 1) ? xo1[m] : xo0[m]) + kb);
+      };
+      auto read_w = [&](auto KSI, int n) __attribute__((always_inline)) -> bf16x8 {
+        constexpr int ks = decltype(KSI)::value;
+        constexpr int kb = 32 * (ks >> 1);
+        return *reinterpret_cast<const bf16x8*>(wcur + 32 * n * C + ((ks & 1) ? wk1 : wk0) + kb);
+      };
+      read_x(IC<0>{}, 0);
+      wf[0] = read_w(IC<0>{}, 0);
+      static_for([&](auto KSI) {
+        constexpr int ks = decltype(KSI)::value;
+        constexpr int cur = ks & 1;
+        if constexpr (ks + 1 < 6) read_x(IC<ks + 1>{}, cur ^ 1);
+        static_for([&](auto NI) {
+          constexpr int n = decltype(NI)::value;
+          if constexpr (n < 2) wf[(n + 1) & 1] = read_w(IC<ks>{}, n + 1);
+          else if constexpr (ks + 1 < 6) wf[(n + 1) & 1] = read_w(IC<ks + 1>{}, 0);
+#pragma unroll
+          for (int m = 0; m < MT; ++m) acc[m][n] = Fmt16<T>::mma32(wf[n & 1], xa[cur][m], acc[m][n]);
+        }, std::make_integer_sequence<int, 3>{});
+        __builtin_amdgcn_sched_barrier(0);
+      }, std::make_integer_sequence<int, 6>{});
+      if constexpr (tap == 8) {
+        if (next < ntiles) {
+          __syncthreads();  // every wave's last halo read done (s_barrier + lgkmcnt)
+          store_halo();
+        }
+      }
+      wbuf ^= 1;
+    }, std::make_integer_sequence<int, 9>{});
+    (void)my_wdma;
+
+    // epilogue: lane holds pixel xo, channels 32n + 8q + 4h + e of rows 2w + m; the
+    // permlane32 swap gives lane l < 32 channels 32n + 16pp + 0..7 and l + 32 the next 8
+    // bias columns of this lane's 6 store groups, loaded together: one wait, not one per
+    // store group behind the previous group's stores
+    float4 bq[3][2][2];
+    if constexpr (BIAS) {
+#pragma unroll
+      for (int n = 0; n < 3; ++n)
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          const int co = 32 * n + 16 * pp + 8 * h;
+          bq[n][pp][0] = *reinterpret_cast<const float4*>(bias + co);
+          bq[n][pp][1] = *reinterpret_cast<const float4*>(bias + co + 4);
+        }
+    }
+    if constexpr (BIAS || OUT_GGRAD) wait_vmcnt<0>();
+    if (xo < g.W) {
+#pragma unroll
+      for (int n = 0; n < 3; ++n)
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          const int co = 32 * n + 16 * pp + 8 * h;
+          float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          if constexpr (BIAS) {
+            const float4 t0 = bq[n][pp][0], t1 = bq[n][pp][1];
+            bv[0] = t0.x; bv[1] = t0.y; bv[2] = t0.z; bv[3] = t0.w;
+            bv[4] = t1.x; bv[5] = t1.y; bv[6] = t1.z; bv[7] = t1.w;
+          }
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            const int y = y0 + 2 * wave + m;
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[m][n][8 * pp + i]),
+                                                              __float_as_uint(acc[m][n][8 * pp + 4 + i]), false, false);
+              v[i] = __uint_as_float(r[0]) + bv[i];
+              v[4 + i] = __uint_as_float(r[1]) + bv[4 + i];
+            }
+            if (y >= g.H) continue;
+            if constexpr (OUT_GGRAD) {
+              const u32x4 t = sp[m][n][pp];
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                v[2 * i] *= gelu_grad_fast(Fmt16<T>::lo(t[i]));
+                v[2 * i + 1] *= gelu_grad_fast(Fmt16<T>::hi(t[i]));
+              }
+            }
+            const u32x4 pk = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
+            const int off = pix_off32<OUT_D2S>(b, y, xo, g.H, g.W, C) + co;
+            *reinterpret_cast<u32x4*>(Y + off) = pk;
+            if constexpr (DUAL) *reinterpret_cast<u32x4*>(Y2 + off) = gelu8<T>(pk);
+          }
+        }
+    }
+    if (next < ntiles) {
+      // the next tile's halo (stored after tap 8) visible to every wave before its tap 0
+      __syncthreads();
+    }
+  }
+}
+
 // ------------------------------------------------------------------ wgrad kernel
 // dW[dy][co][dx][ci] partial per block: sum over the block's pixel tiles of
 //   DY[pixel][co] * Xt[pixel + (dy-1, dx-1)][ci];  one block = one dy, NT waves (one per
@@ -874,10 +1150,43 @@ int launch_v2(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float*
   return MSU_CHECK_LAUNCH();
 }
 
+// v3 forward (A/B switch MSU_CONV_V=2: every launch on v2)
+inline bool conv_v3_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("MSU_CONV_V");
+    return !(e && e[0] == '2');
+  }();
+  return on;
+}
+
+template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL>
+int launch_v3(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S, bf16_t* Y,
+              bf16_t* Y2, hipStream_t st) {
+  constexpr size_t lds = sizeof(bf16_t) * ((size_t)18 * 34 * 96 + 2 * 96 * 96);
+  static_assert(lds <= 160 * 1024, "LDS");
+  auto kern = conv3x3_v3_kernel<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  const long ntiles = (long)g.B * ((g.W + 31) / 32) * ((g.H + 15) / 16);
+  if (ntiles == 0) return 0;
+  if ((long)g.B * g.H * g.W * 96 >= (1L << 31)) return -2;
+  const int grid = (int)(ntiles < num_cus() ? ntiles : num_cus());
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, X, Wt, bias, S, Y, Y2, g, (int)ntiles);
+  return MSU_CHECK_LAUNCH();
+}
+
 template <typename T, bool IN_D2S, bool IN_GELU, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL = false>
 int conv_nt(const ConvGeom& g, const void* X, const void* Wt, const float* bias, const void* S,
             void* Y, void* Y2, hipStream_t st) {
   const T* x = (const T*)X; const T* w = (const T*)Wt; const T* s = (const T*)S; T* y = (T*)Y; T* y2 = (T*)Y2;
+  if constexpr (sizeof(T) == 2 && !IN_GELU) {
+    if (g.Cout == 96 && g.CinP == 96 && g.Cin == 96 && conv_v3_enabled())
+      return launch_v3<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL>(g, (const bf16_t*)x, (const bf16_t*)w, bias,
+                                                                  (const bf16_t*)s, (bf16_t*)y, (bf16_t*)y2, st);
+  }
   if constexpr (sizeof(T) == 2) {
     // the Swin-T/S decoder head width takes the persistent v2 kernel
     if (g.Cout == 96 && g.CinP == 96)

@@ -382,6 +382,33 @@ def test_refine_conv_act(B, H, W, C, d2s, dtype):
     _close(b2.grad, b1.grad, tol, tol, "db")
 
 
+@pytest.mark.parametrize("B,H,W,d2s", [(2, 64, 64, True), (1, 48, 32, False), (1, 40, 56, True),
+                                        (2, 20, 36, False), (1, 16, 32, False), (1, 128, 96, True)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_refine_conv_act_fwd_matches_fp32(B, H, W, d2s, dtype):
+    """The 16-bit C = 96 forward as the model runs it (activation precomputed by the producer:
+    the 16-row x 32-pixel persistent kernel, conv3x3_v3_kernel) against fp32 conv2d of the same
+    16-bit activation -- z and the dual output GELU(z); tiles cut by the image edge included."""
+    ops = _ops()
+    C = 96
+    g = _g(H * W + 11)
+    xs = (B, H // 4, W // 4, 16 * C) if d2s else (B, H, W, C)
+    a = torch.randn(xs, generator=g).to(dtype)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    b = 0.1 * torch.randn(C, generator=g)
+    from einops import rearrange
+    af = a.float()
+    if d2s:
+        af = rearrange(af, "b h w (p1 p2 c) -> b (h p1) (w p2) c", p1=4, p2=4, c=C)
+    zr = F.conv2d(af.permute(0, 3, 1, 2), w, b, padding=1).permute(0, 2, 3, 1)
+    with torch.autocast("cuda", dtype=dtype):
+        ad = a.to(DEV)
+        z, z2 = ops.refine_conv_act(ad, ad, w.to(DEV), b.to(DEV), d2s, (H, W), dual=True)
+    tol = _tol(dtype, 1e-4, 2e-2)
+    _close(z, zr, tol, tol, "z")
+    _close(z2, F.gelu(z.float()), tol, tol, "GELU(z)")
+
+
 @pytest.mark.parametrize("M,N,K", [(4096, 1536, 96), (1000, 256, 16)])
 @pytest.mark.parametrize("dtype", ALL)
 def test_linear_gelu(M, N, K, dtype):
