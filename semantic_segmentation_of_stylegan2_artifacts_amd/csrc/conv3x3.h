@@ -621,6 +621,7 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
   load_halo(tile);
   store_halo();
   dma_w(0, 0);
+  __syncthreads();  // the halo's ds_writes land before any wave reads (the tap barriers are raw)
   int wbuf = 0;
 
   const int xl = lane & 31, h = lane >> 5;
@@ -712,10 +713,11 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
         if constexpr (ks + 1 < 6) read_x(IC<ks + 1>{}, cur ^ 1);
         static_for([&](auto NI) {
           constexpr int n = decltype(NI)::value;
-          if constexpr (n < 2) wf[(n + 1) & 1] = read_w(IC<ks>{}, n + 1);
-          else if constexpr (ks + 1 < 6) wf[(n + 1) & 1] = read_w(IC<ks + 1>{}, 0);
+          constexpr int j = 3 * ks + n;  // weight fragment sequence number: register set j & 1
+          if constexpr (n < 2) wf[(j + 1) & 1] = read_w(IC<ks>{}, n + 1);
+          else if constexpr (ks + 1 < 6) wf[(j + 1) & 1] = read_w(IC<ks + 1>{}, 0);
 #pragma unroll
-          for (int m = 0; m < MT; ++m) acc[m][n] = Fmt16<T>::mma32(wf[n & 1], xa[cur][m], acc[m][n]);
+          for (int m = 0; m < MT; ++m) acc[m][n] = Fmt16<T>::mma32(wf[j & 1], xa[cur][m], acc[m][n]);
         }, std::make_integer_sequence<int, 3>{});
         __builtin_amdgcn_sched_barrier(0);
       }, std::make_integer_sequence<int, 6>{});
