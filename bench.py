@@ -6,9 +6,9 @@
 A step = one full training step of the reference's trainer.py:308-316 on one batch per
 rank: bf16-autocast forward of MS-UNet -> DynamicLoss -> backward -> bucketed RCCL
 gradient all-reduce (N > 1) -> non-finite check -> fused AdamW.  The Trainer runs its first
-two steps eagerly, times the second, and replays the captured step as a HIP graph from then
-on when that step was launch-bound (host issue time >= 0.9 x GPU time), else stays eager
-(MSU_GRAPH=1/0 forces either; the decision falls inside the warmup when W >= 3).  Synthetic StyleGAN2-shaped inputs are generated in HBM before timing
+four steps eagerly, times the last two, and replays the captured step as a HIP graph from then
+on when the steadier of them was launch-bound (host issue time >= 0.9 x GPU time), else stays
+eager (MSU_GRAPH=1/0 forces either; the decision falls inside the warmup when W >= 5).  Synthetic StyleGAN2-shaped inputs are generated in HBM before timing
 and copied into the graph's input buffers inside every timed step.  Rank 0 prints ONE
 JSON line.
 
@@ -40,7 +40,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--img", type=int, default=1024)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--backbone", default="swin_t")

@@ -18,8 +18,9 @@ Here:
   the buckets instead (half the bytes; BASELINE config 5's "fp16 grads");
 * AdamW = one fused HIP launch per group over the flat buffer, lr / step read from device
   memory, skipped (GradScaler semantics) when a gradient is non-finite;
-* after two eager steps the device side of the step is captured into a HIP graph and
-  replayed (``Trainer.step``): the host issues one launch per step;
+* after four eager steps the device side of the step is captured into a HIP graph and
+  replayed (``Trainer.step``) when the eager step is launch-bound: the host then issues one
+  launch per step;
 * parameters whose outputs the reference discards (dead central-decoder branches) never
   receive gradients there; they are excluded here, matching torch AdamW's skip of
   ``grad is None``.
@@ -281,7 +282,7 @@ def reseed(seed, rank=0):
 class Trainer:
     def __init__(self, model, config, device, lr=None, amp_dtype=torch.bfloat16, bucket_mb=32,
                  world_size=1, process_group=None, rank=0, seed=None, skip_nonfinite=True, use_graph=None,
-                 graph_warmup=2, grad_wire_dtype=None, always_reduce=False):
+                 graph_warmup=4, grad_wire_dtype=None, always_reduce=False):
         self.model = model
         self.device = device
         self.amp_dtype = amp_dtype
@@ -340,7 +341,7 @@ class Trainer:
             # (tests/test_gpu_rccl.py): replay under DP only when asked for (MSU_GRAPH=1)
             self.graph_mode = "0"
         self.use_graph = self.graph_mode != "0"
-        self._probe = None  # (host seconds, start event, end event) of the auto-mode probe step
+        self._probe = []  # [(host seconds, start event, end event)] of the auto-mode probe steps
         self.graph_warmup = graph_warmup
         self._graph = None
         self._graph_failed = False
@@ -508,12 +509,14 @@ class Trainer:
 
     def _decide_graph(self):
         """auto mode: graph replay iff the probed eager step was launch-bound."""
-        if self._probe is None:
+        if not self._probe:
             self.use_graph = False
             return
-        host_s, e0, e1 = self._probe
-        e1.synchronize()
-        gpu_s = e0.elapsed_time(e1) * 1e-3
+        # the probe step with the shorter GPU time: a step that stalled on a one-off (allocator
+        # growth, a lazy library load: the host waits on the GPU there) reads host ~ GPU
+        self._probe[-1][2].synchronize()
+        timed = [(e0.elapsed_time(e1) * 1e-3, host_s) for host_s, e0, e1 in self._probe]
+        gpu_s, host_s = min(timed)
         self.graph_probe = {"host_ms": round(host_s * 1e3, 3), "gpu_ms": round(gpu_s * 1e3, 3)}
         self.use_graph = host_s >= self.GRAPH_HOST_FRACTION * gpu_s
         self.graph_mode = "1" if self.use_graph else "0"
@@ -523,7 +526,7 @@ class Trainer:
             for g in self.groups:
                 g.refresh_shadow()
         self._shadow_fresh = False
-        probe = self.graph_mode == "auto" and self.step_count == self.graph_warmup - 1
+        probe = self.graph_mode == "auto" and self.graph_warmup - 2 <= self.step_count <= self.graph_warmup - 1
         if probe:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -532,7 +535,7 @@ class Trainer:
         if probe:
             host = time.perf_counter() - t0
             e1.record()
-            self._probe = (host, e0, e1)
+            self._probe.append((host, e0, e1))
         self.step_count += 1
         # the next step's refresh is skipped; a write through a parameter in between bumps its
         # version and the Linear ops cast that weight themselves (ops._shadow)
