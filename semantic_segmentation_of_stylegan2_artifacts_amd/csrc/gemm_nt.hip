@@ -29,7 +29,7 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 128;
+constexpr int BN = 128, BK = 64, CH = BK / 8;  // N tile, K step, 16-B chunks per row and step
 enum { EPI_PLAIN = 0, EPI_GELU_DUAL = 1, EPI_GELU_GRAD = 2 };
 
 struct NtArgs {
@@ -44,27 +44,27 @@ struct NtArgs {
   int tiles_m, tiles_n;
 };
 
-// Tile geometry for a K step of BK: CH = BK / 8 16-B chunks per row; a 256-B LDS bank row
-// holds 128 / BK rows, and chunk c of row r is stored at chunk c ^ ((r >> SH) & (CH - 1)), so a
-// half-wave's 16 fragment rows (16 B each) land on 16 distinct bank groups.
-template <int BK>
-struct NtTile {
-  static constexpr int CH = BK / 8, SH = BK == 64 ? 1 : 2;
+// A ROWS x BK operand tile (K-contiguous rows) staged by NTHR threads.  A 256-B LDS bank row
+// holds 2 tile rows; chunk c of row r is stored at chunk c ^ ((r >> 1) & 7), so a half-wave's 16
+// fragment rows (16 B each) land on 16 distinct bank groups.
+template <int ROWS, int NTHR>
+struct RowTile {
+  static constexpr int PER = ROWS * CH / NTHR;  // DMA instructions per thread
+  static_assert(PER * NTHR == ROWS * CH, "whole DMA instructions");
   // LDS element offset of k-chunk `chunk` (8 elements) of tile row `row`
-  static MSU_DEV int off(int row, int chunk) { return row * BK + ((chunk ^ ((row >> SH) & (CH - 1))) << 3); }
-  // One 128 x BK operand tile -> LDS: 128 * CH 16-B slots, CH / 2 per thread.  Slot p = c*256 +
-  // tid is row p / CH, LDS chunk p % CH, which holds the global chunk that off() puts there; rows
-  // past the tensor re-read its last row (their results are never stored).
+  static MSU_DEV int off(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
+  // slot p = c * NTHR + tid is row p / CH, LDS chunk p % CH, which holds the global chunk that
+  // off() puts there; rows past the tensor re-read its last row (their results are never stored)
   static MSU_DEV void stage(const bf16_t* __restrict__ src, int row0, int rows, int K, int k0, bf16_t* tile,
                             int tid) {
     const int wave = tid >> 6;
 #pragma unroll
-    for (int c = 0; c < CH / 2; ++c) {
-      const int p = c * 256 + tid;
-      const int row = p / CH, g = (p % CH) ^ ((row >> SH) & (CH - 1));
+    for (int c = 0; c < PER; ++c) {
+      const int p = c * NTHR + tid;
+      const int row = p / CH, g = (p % CH) ^ ((row >> 1) & 7);
       int r = row0 + row;
       if (r >= rows) r = rows - 1;
-      glds16(src + (size_t)r * K + k0 + 8 * g, tile + (c * 256 + wave * 64) * 8);
+      glds16(src + (size_t)r * K + k0 + 8 * g, tile + (c * NTHR + wave * 64) * 8);
     }
   }
   // 32-row fragment: lane l -> row row0 + (l & 31), k = 16 ks + 8 (l >> 5) .. +7
@@ -78,18 +78,20 @@ struct NtTile {
 // dX = dY . W, read without a transposed copy).  Its BK x 128 tile is staged as a [k][n] image
 // (256-B rows); 16-B chunk c of row r sits at chunk c ^ 4(r & 3), so the four rows a half-wave's
 // transposed read covers fall on four different 64-B bank groups.
+template <int NTHR>
 struct KnTile {
+  static constexpr int PER = BK * BN / 8 / NTHR;
   static MSU_DEV int off(int row, int col) { return row * BN + ((((col >> 3) ^ (4 * (row & 3)))) << 3) + (col & 7); }
-  // 64 x 128 tile: 1024 16-B slots, 4 per thread; columns past N re-read column n0
+  // 64 x 128 tile: 1024 16-B slots; columns past N re-read column n0
   static MSU_DEV void stage(const bf16_t* __restrict__ W, int n0, int N, int k0, bf16_t* tile, int tid) {
     const int wave = tid >> 6;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int p = c * 256 + tid;
+    for (int c = 0; c < PER; ++c) {
+      const int p = c * NTHR + tid;
       const int row = p >> 4, lc = (p & 15) ^ (4 * (row & 3));
       int n = n0 + 8 * lc;
       if (n >= N) n = n0;
-      glds16(W + (size_t)(k0 + row) * N + n, tile + (c * 256 + wave * 64) * 8);
+      glds16(W + (size_t)(k0 + row) * N + n, tile + (c * NTHR + wave * 64) * 8);
     }
   }
   // 32-column fragment (the MFMA A operand): lane l -> column col0 + (l & 31), element e -> k =
@@ -106,25 +108,37 @@ struct KnTile {
   }
 };
 
-// Persistent: a grid of at most NT_WG_PER_CU workgroups per CU walks the output tiles t = L,
-// L + G, L + 2G, ... (L = the XCD-remapped block index, G = grid size) as ONE flat sequence of
-// K steps, so the LDS ring never drains at a tile boundary: the first K step of the next tile
-// is staged while the last one of the current tile is multiplied, and the epilogue's stores
-// leave while that DMA is in flight.  The stage-1..3 shapes have only 3-12 K steps per tile
-// (K = 192..768), so a per-tile prologue / epilogue was a large share of a non-persistent
-// tile's time.  In one round of tiles an XCD takes a contiguous range of tile indices, i.e.
-// the N tiles of a few M tiles: their A rows come from HBM once and from that XCD's L2 after.
-// Ring: NST = 2 stages of BK = 64 (64 KB of LDS: two workgroups per CU); the wait before a
-// step is vmcnt(0), which also retires the previous tile's epilogue stores.
-template <typename T, int EPI, int BK, int NST, bool WKN>
-__global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs a) {
-  typedef NtTile<BK> Tl;
-  static_assert(NST == 2, "the epilogue stores are retired by the per-step vmcnt(0)");
-  static_assert(!WKN || BK == 64, "[K][N] weights: 64-deep K steps");
+// Persistent: a grid of at most one (WM = 4) or two (WM = 2) workgroups per CU walks the output
+// tiles t = L, L + G, L + 2G, ... (L = the XCD-remapped block index, G = grid size) as ONE flat
+// sequence of K steps, so the LDS ring never drains at a tile boundary: the first K steps of
+// the next tile are staged while the last ones of the current tile are multiplied, and the
+// epilogue's stores leave while those DMAs are in flight.  The stage-1..3 shapes have only
+// 3-24 K steps per tile (K = 192..1536), so a per-tile prologue / epilogue was a large share of
+// a non-persistent tile's time.  In one round of tiles an XCD takes a contiguous range of tile
+// indices, i.e. the N tiles of a few M tiles: their A rows come from HBM once and from that
+// XCD's L2 after.
+// Tiles: (64 WM) x 128 outputs, WM x 2 waves of 64 x 64 (four 32 x 32 accumulators each).
+//   WM = 2, NST = 2: 128 x 128, 64 KB ring, two workgroups per CU, vmcnt(0) before each step;
+//   WM = 4, NST = 3: 256 x 128, 144 KB ring, one 8-wave workgroup per CU, two K steps in flight
+//   across the raw barrier (counted vmcnt: the DMAs of the younger step and the epilogue stores
+//   issued after the awaited step's DMA may stay outstanding).
+template <typename T, int EPI, int WM, int NST, bool WKN>
+__global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
+  constexpr int NTHR = 128 * WM, BM = 64 * WM;
+  typedef RowTile<BM, NTHR> TA;
+  typedef RowTile<BN, NTHR> TW;
+  typedef KnTile<NTHR> TK;
   constexpr int KSL = BK / 16;  // 16-wide k slices per step
-  __shared__ __attribute__((aligned(16))) bf16_t lds[NST][2][BM * BK];  // [stage][A | W]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;  // this wave's 64 x 64 quarter (tokens, columns)
+  constexpr int STG = (BM + BN) * BK;  // elements per ring stage
+  // per thread and step: DMA instructions, and epilogue stores of a tile
+  constexpr int D = TA::PER + (WKN ? TK::PER : TW::PER);
+  constexpr int E = EPI == EPI_GELU_DUAL ? 16 : 8;
+  static_assert(NST == 2 || NST == 3, "ring depth");
+  static_assert(NST == 2 || (D + E < 64), "vmcnt range");
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NST * STG];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WM, wn = wave / WM;  // this wave's 64 x 64 piece (tokens, columns)
   const int G = gridDim.x;
   const int L = xcd_remap(blockIdx.x, G);
   const int ntiles = a.tiles_m * a.tiles_n;
@@ -132,17 +146,17 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs a) {
   const int mine = L < ntiles ? (ntiles - 1 - L) / G + 1 : 0;
   const int nsteps = mine * nk;
 
-  // K step s of this workgroup's sequence -> LDS stage s % NST
-  auto issue = [&](int s) __attribute__((always_inline)) {
+  // K step s of this workgroup's sequence -> LDS stage `st`
+  auto issue = [&](int s, int st) __attribute__((always_inline)) {
     const int ti = s / nk, kk = s - ti * nk;
     const int t = L + ti * G;
     const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
-    bf16_t* dst = lds[s & (NST - 1)][0];
-    if (a.A2 == nullptr) Tl::stage(a.A, mt * BM, a.M, a.K, kk * BK, dst, tid);
-    else if (kk * BK < a.K1) Tl::stage(a.A, mt * BM, a.M, a.K1, kk * BK, dst, tid);  // K1 % BK == 0
-    else Tl::stage(a.A2, mt * BM, a.M, a.K - a.K1, kk * BK - a.K1, dst, tid);
-    if constexpr (WKN) KnTile::stage(a.W, nt * BN, a.N, kk * BK, dst + BM * BK, tid);
-    else Tl::stage(a.W, nt * BN, a.N, a.K, kk * BK, dst + BM * BK, tid);
+    bf16_t* dst = lds + st * STG;
+    if (a.A2 == nullptr) TA::stage(a.A, mt * BM, a.M, a.K, kk * BK, dst, tid);
+    else if (kk * BK < a.K1) TA::stage(a.A, mt * BM, a.M, a.K1, kk * BK, dst, tid);  // K1 % BK == 0
+    else TA::stage(a.A2, mt * BM, a.M, a.K - a.K1, kk * BK - a.K1, dst, tid);
+    if constexpr (WKN) TK::stage(a.W, nt * BN, a.N, kk * BK, dst + BM * BK, tid);
+    else TW::stage(a.W, nt * BN, a.N, a.K, kk * BK, dst + BM * BK, tid);
   };
 
   f32x16 acc[2][2];  // [column tile ni][token tile mi]: C^T, W rows on the accumulator rows
@@ -151,20 +165,36 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
 
-  if (nsteps > 0) issue(0);
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nsteps) issue(s, s);
   int kk = 0, ti = 0;  // K step within the tile, tile ordinal (within this workgroup)
+  int cst = 0;         // LDS stage of step s
+  int epi_age = 99;    // steps since the last epilogue (its stores follow that step's DMA issue)
   for (int s = 0; s < nsteps; ++s) {
-    wait_vmcnt<0>();                // step s's DMA (and the last epilogue's stores) done
+    // step s's DMA landed; younger DMAs (step s + 1) and epilogue stores issued after step s's
+    // DMA may stay in flight (NST = 3, tiles of >= 3 K steps); else everything retires
+    if constexpr (NST == 2) {
+      wait_vmcnt<0>();
+    } else {
+      const bool younger = s + 1 < nsteps;
+      const bool stores = epi_age <= 1 && nk >= 3;
+      if (nk < 3) wait_vmcnt<0>();
+      else if (younger && stores) wait_vmcnt<D + E>();
+      else if (younger) wait_vmcnt<D>();
+      else if (stores) wait_vmcnt<E>();
+      else wait_vmcnt<0>();
+    }
     __builtin_amdgcn_s_barrier();   // every wave's DMA of step s has landed, and every wave is
     asm volatile("" ::: "memory");  // done reading step s-1's stage (refilled below)
-    if (s + 1 < nsteps) issue(s + 1);
+    ++epi_age;
     const bool last = kk + 1 == nk;
     const int t = L + ti * G;
     const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
     const int m0 = mt * BM, n0 = nt * BN;
     const int hh = lane >> 5;
-    // the epilogue's operands (bias columns, GELU' pre-activations) are loaded before the
-    // tile's last MFMAs, all at once: one wait in the epilogue instead of one per store
+    // the epilogue's operands (bias columns, GELU' pre-activations), loaded before the tile's
+    // last MFMAs and before the next stage's DMA: one counted wait in the epilogue
     float4 eb[2][2][2];
     u32x4 eh[2][2][2];
     if (last) {
@@ -185,19 +215,22 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs a) {
           }
         }
     }
-    const bf16_t* ta = lds[s & (NST - 1)][0];
+    const bool more = s + NST - 1 < nsteps;
+    if (more) issue(s + NST - 1, cst == 0 ? NST - 1 : cst - 1);
+    const bf16_t* ta = lds + cst * STG;
     const bf16_t* tw = ta + BM * BK;
+    cst = cst + 1 == NST ? 0 : cst + 1;
     bf16x8 fw[2][2], fx[2][2];
     auto rd = [&](int ks, int set) {
       if constexpr (WKN) {
-        fw[set][0] = KnTile::frag(tw, 64 * wn, ks, lane);
-        fw[set][1] = KnTile::frag(tw, 64 * wn + 32, ks, lane);
+        fw[set][0] = TK::frag(tw, 64 * wn, ks, lane);
+        fw[set][1] = TK::frag(tw, 64 * wn + 32, ks, lane);
       } else {
-        fw[set][0] = Tl::frag(tw, 64 * wn, ks, lane);
-        fw[set][1] = Tl::frag(tw, 64 * wn + 32, ks, lane);
+        fw[set][0] = TW::frag(tw, 64 * wn, ks, lane);
+        fw[set][1] = TW::frag(tw, 64 * wn + 32, ks, lane);
       }
-      fx[set][0] = Tl::frag(ta, 64 * wm, ks, lane);
-      fx[set][1] = Tl::frag(ta, 64 * wm + 32, ks, lane);
+      fx[set][0] = TA::frag(ta, 64 * wm, ks, lane);
+      fx[set][1] = TA::frag(ta, 64 * wm + 32, ks, lane);
     };
     rd(0, 0);
 #pragma unroll
@@ -216,8 +249,11 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(NtArgs a) {
     }
     kk = 0;
     ++ti;
-    wait_vmcnt<0>();  // the epilogue operands (and the next step's DMA) have landed: one wait,
-                      // not one per exec-masked store branch
+    epi_age = 0;
+    // the epilogue operands (and every older DMA) have landed; the DMA just issued may stay
+    // in flight (NST = 3).  One wait, not one per exec-masked store branch.
+    if (NST == 3 && more) wait_vmcnt<D>();
+    else wait_vmcnt<0>();
     // ---- epilogue of tile t: lane (l & 31) is token m; after the swap, 8 consecutive columns
     // per store
 #pragma unroll
@@ -276,31 +312,40 @@ bool nt_shape_ok(long M, int N, int K) {
   return M > 0 && M < (1L << 31) && N > 0 && N % 32 == 0 && K > 0 && K % 64 == 0 && (long)M * N < (1L << 40);
 }
 
-// Workgroups per CU of the persistent grid (A/B switch MSU_NT_WG_PER_CU, 1 or 2; default 2:
-// the LDS of two 64 KB rings) and the CU budget (MSU_NT_CUS: leave CUs to the weight-gradient
-// side stream; default all).
-int nt_grid_cap() {
-  static const int cap = [] {
-    int cus = 0, dev = 0;
+int num_cus_nt() {
+  static const int cus = [] {
+    int n = 0, dev = 0;
     (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    const char* e = getenv("MSU_NT_CUS");
-    if (e && atoi(e) > 0 && atoi(e) < cus) cus = atoi(e);
-    const char* w = getenv("MSU_NT_WG_PER_CU");
-    const int per = (w && atoi(w) == 1) ? 1 : 2;
-    return cus * per;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    return n;
   }();
-  return cap;
+  return cus;
 }
 
-template <typename T, int BK, int NST, bool WKN>
-void launch_nt(int epi, long tiles, const NtArgs& a, hipStream_t st) {
-  const long cap = nt_grid_cap();
-  if (tiles > cap) tiles = cap;
+// Tile configuration of a shape: the 256 x 128 tile (WM = 4, three-stage ring, one workgroup
+// per CU) when it still gives every CU a tile, else 128 x 128 (two workgroups per CU).  A/B
+// switch MSU_NT_TILE = 128 | 256 forces one.
+int nt_wm(long M, int N) {
+  static const int force = [] {
+    const char* e = getenv("MSU_NT_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  if (force == 128) return 2;
+  if (force == 256) return 4;
+  const long big = ((M + 255) / 256) * (long)((N + BN - 1) / BN);
+  return big >= num_cus_nt() ? 4 : 2;
+}
+
+template <typename T, int WM, int NST, bool WKN>
+void launch_nt(int epi, const NtArgs& a, hipStream_t st) {
+  const long tiles = (long)a.tiles_m * a.tiles_n;
+  const long cap = (long)num_cus_nt() * (WM == 4 ? 1 : 2);
+  const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
+  const dim3 blk(128 * WM);
   switch (epi) {
-    case EPI_PLAIN: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_PLAIN, BK, NST, WKN>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
-    case EPI_GELU_DUAL: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_DUAL, BK, NST, WKN>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_GRAD, BK, NST, WKN>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
+    case EPI_PLAIN: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_PLAIN, WM, NST, WKN>), dim3(grid), blk, 0, st, a); break;
+    case EPI_GELU_DUAL: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_DUAL, WM, NST, WKN>), dim3(grid), blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_GRAD, WM, NST, WKN>), dim3(grid), blk, 0, st, a); break;
   }
 }
 
@@ -324,14 +369,19 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
   a.M = (int)M;
   a.N = N;
   a.K = K;
+  const int wm = nt_wm(M, N);
   a.tiles_n = (N + BN - 1) / BN;
-  a.tiles_m = (int)((M + BM - 1) / BM);
-  const long tiles = (long)a.tiles_m * a.tiles_n;
-  if (tiles >= (1L << 31)) return -2;
+  a.tiles_m = (int)((M + 64 * wm - 1) / (64 * wm));
+  if ((long)a.tiles_m * a.tiles_n >= (1L << 31)) return -2;
   hipStream_t st = (hipStream_t)stream;
   MSU_DISPATCH16(dtype, T,
-    if (wkn) launch_nt<T, 64, 2, true>(epi, tiles, a, st);
-    else launch_nt<T, 64, 2, false>(epi, tiles, a, st));
+    if (wm == 4) {
+      if (wkn) launch_nt<T, 4, 3, true>(epi, a, st);
+      else launch_nt<T, 4, 3, false>(epi, a, st);
+    } else {
+      if (wkn) launch_nt<T, 2, 2, true>(epi, a, st);
+      else launch_nt<T, 2, 2, false>(epi, a, st);
+    });
   return MSU_CHECK_LAUNCH();
 }
 

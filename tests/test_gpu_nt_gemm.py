@@ -15,6 +15,9 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 SHAPES = [(4096, 1152, 384), (4096, 384, 1152), (1000, 384, 384), (2048, 768, 192), (777, 192, 768),
           (300, 2304, 768), (128, 768, 3072), (513, 96, 64), (64, 160, 128), (1, 32, 64)]
+# shapes that take the 256 x 128 tile (8 waves, three-stage ring: >= one tile per CU), incl. a
+# ragged M, an N that is not a multiple of 128 and two-K-step tiles (vmcnt(0) fallback)
+BIG = [(32768, 1152, 384), (32768, 384, 1536), (131072, 192, 768), (32000 + 77, 416, 192), (65536, 640, 128)]
 
 
 def _ops():
@@ -42,7 +45,7 @@ def _inputs(M, N, K, seed, low):
     return a, w, b
 
 
-@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("M,N,K", SHAPES + BIG)
 @pytest.mark.parametrize("bias", [False, True])
 def test_nt_gemm_plain(M, N, K, bias, low):
     ops = _ops()
@@ -54,7 +57,7 @@ def test_nt_gemm_plain(M, N, K, bias, low):
     _check(y, ref, "y")
 
 
-@pytest.mark.parametrize("M,N,K", [(4096, 1536, 384), (777, 768, 192), (300, 3072, 768)])
+@pytest.mark.parametrize("M,N,K", [(4096, 1536, 384), (777, 768, 192), (300, 3072, 768), (32768, 1536, 384)])
 def test_nt_gemm_gelu_epilogues(M, N, K, low):
     """EPI 1: (H, GELU(H)) of mlp.0; EPI 2: (dY . W2) * GELU'(H) -- mlp.3's input gradient
     through the activation (W2^T [N, K'] passed as the weight)."""
@@ -74,7 +77,7 @@ def test_nt_gemm_gelu_epilogues(M, N, K, low):
     _check(dh, ref, "dh")
 
 
-@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("M,N,K", SHAPES + BIG)
 def test_nt_gemm_kn_plain(M, N, K, low):
     """msu_nt_gemm_kn: Y = A . Wk with Wk [K, N] read in place (a Linear's input gradient dX = dY . W
     with its forward weight W); same bar as the [N, K] form."""
@@ -86,7 +89,7 @@ def test_nt_gemm_kn_plain(M, N, K, low):
     _check(y, a.float() @ wk.float(), "y")
 
 
-@pytest.mark.parametrize("M,N,K", [(4096, 1536, 384), (777, 768, 192), (300, 3072, 768)])
+@pytest.mark.parametrize("M,N,K", [(4096, 1536, 384), (777, 768, 192), (300, 3072, 768), (32768, 1536, 384)])
 def test_nt_gemm_kn_gelu_grad(M, N, K, low):
     """EPI 2 with the weight in place: dH = (dY . W2) * GELU'(H), W2 [K, N] = mlp.3's weight."""
     ops = _ops()

@@ -35,10 +35,11 @@ def run(graph, steps):
     tr = Trainer(m, load_config(None, "swin_t", **{"TRAIN.BASE_LR": 0.0}), "cuda", use_graph=graph, graph_warmup=2)
     losses = [tr.step(x, t).item() for _ in range(steps)]
     torch.cuda.synchronize()
-    per = {}
+    flat = {}
     for g in tr.groups:
         for n, p, off in zip(g.names, g.params, g.offsets):
-            per[n] = g.exp_avg[off:off + p.numel()].clone()
+            flat[n] = g.exp_avg[off:off + p.numel()].clone()
+    per = {n: flat[n] for n, _ in m.named_parameters() if n in flat}  # forward (registration) order
     return losses, per, tr._graph is not None
 
 
@@ -55,6 +56,13 @@ def main():
         print(f"   params differing from eager0: {len(nz)} / {len(diffs)}")
         for d, n in nz[:12]:
             print(f"     {d:.3e}  {n}")
+    # the divergence point: in forward (registration) order, the LAST parameter that differs
+    # between the two eager runs is the first one backward reached with a different gradient
+    order = list(runs["eager0"][1].keys())
+    e1 = runs["eager1"][1]
+    bad = [n for n in order if not torch.equal(e1[n], base[n])]
+    print("eager1 vs eager0, differing params in forward order (last = first reached by backward):")
+    print("   " + ", ".join(bad))
     g0, g1 = runs["graph0"][1], runs["graph1"][1]
     diffs = sorted(((float((g0[n] - g1[n]).abs().max()), n) for n in g0), reverse=True)
     nz = [d for d in diffs if d[0] > 0]
