@@ -64,6 +64,9 @@ def main():
     print("eager1 vs eager0, differing params in forward order (last = first reached by backward):")
     print("   " + ", ".join(bad))
     g0, g1 = runs["graph0"][1], runs["graph1"][1]
+    badg = [n for n in order if not torch.equal(g0[n], g1[n])]
+    print("graph1 vs graph0, differing params in forward order (last = first reached by backward):")
+    print("   " + ", ".join(badg))
     diffs = sorted(((float((g0[n] - g1[n]).abs().max()), n) for n in g0), reverse=True)
     nz = [d for d in diffs if d[0] > 0]
     print(f"graph0 vs graph1: {len(nz)} params differ")
