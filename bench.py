@@ -92,7 +92,9 @@ def conv_roofline(device, batch, img, C):
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
-    return {"kernel": "conv3x3_v2_kernel (refine2 fwd, bf16 MFMA implicit GEMM)", "bound": "mfma",
+    # the C-ABI dispatches C = 96 to the 16-row-tile v3 kernel unless MSU_CONV_V=2 (csrc/conv3x3.h)
+    kname = "conv3x3_v3_kernel" if C == 96 and os.environ.get("MSU_CONV_V", "") != "2" else "conv3x3_v2_kernel"
+    return {"kernel": f"{kname} (refine2 fwd, bf16 MFMA implicit GEMM)", "bound": "mfma",
             "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
             "flops_per_launch": flops, "ms_per_launch": round(ms, 4)}
@@ -179,22 +181,28 @@ def _cpu_model():
 
 def _cpu_train_steps(backbone, steps=10, first=2):
     """The CPU oracle's fp32 training step (fwd + DynamicLoss + bwd + AdamW) of one backbone
-    on 4 x 256^2 (BASELINE config 1); returns (images/s averaged over steps first..steps-1,
-    s/step, list of step times)."""
+    on 4 x 256^2 (BASELINE config 1) in training semantics: the config's drop-path (0.1) and
+    attention dropout (0.05) drawn per step, as the reference's ``model.train()`` step does
+    (config.py MODEL defaults; the reference's CPU profile spends ~12 % in ``bernoulli_``).
+    Returns (images/s averaged over steps first..steps-1, s/step, list of step times)."""
     from oracle.msunet import make_cfg, init_params, msunet_forward, SWIN_T, SWIN_B
     from oracle.dynamic_loss import dynamic_loss
+    from semantic_segmentation_of_stylegan2_artifacts_amd.config import load_config
     from semantic_segmentation_of_stylegan2_artifacts_amd.data import synthetic_batch
     arch = {"swin_t": SWIN_T, "swin_b": SWIN_B}[backbone]
-    cfg = make_cfg(img_size=256, drop_path_rate=0.0, **arch)
+    mc = load_config(None, backbone).MODEL
+    cfg = make_cfg(img_size=256, drop_path_rate=mc.DROP_PATH_RATE, attn_drop_rate=mc.ATTN_DROP_RATE,
+                   drop_rate=mc.DROP_RATE, **arch)
     p = init_params(cfg, seed=0)
     params = {k: v.requires_grad_(True) for k, v in p.items() if v.is_floating_point()}
     p.update(params)
     opt = torch.optim.AdamW(list(params.values()), lr=1e-5, weight_decay=1e-3)
     x, y = synthetic_batch(4, 256, "cpu", 120)
+    gen = torch.Generator().manual_seed(0)
     times = []
     for _ in range(steps):
         t0 = time.perf_counter()
-        out = msunet_forward(p, cfg, x)
+        out = msunet_forward(p, cfg, x, training=True, generator=gen)
         loss = dynamic_loss(out, y, 0.2, 0.8, 0.45)
         opt.zero_grad(set_to_none=True)
         loss.backward()
@@ -219,7 +227,8 @@ def cpu_baseline():
     b_ips, b_sps, b_times = _cpu_train_steps("swin_b")
     return {"value": round(t_ips, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "cpu_model": _cpu_model(), "cpus_in_affinity_mask": affinity,
-            "sample": f"CPU oracle (torch fp32) MS-UNet train step, 4x256^2 (config 1), 10 steps, "
+            "sample": f"CPU oracle (torch fp32) MS-UNet train step with drop-path 0.1 and attention "
+                      f"dropout 0.05 drawn, 4x256^2 (config 1), 10 steps, "
                       f"steps 2-9 averaged: Swin-T {t_sps:.2f} s/step",
             "swin_b": {"value": round(b_ips, 4), "unit": "images/s", "s_per_step": round(b_sps, 3)},
             "step_times_s": {"swin_t": [round(v, 3) for v in t_times], "swin_b": [round(v, 3) for v in b_times]}}

@@ -22,7 +22,7 @@ grep '^{' $O/${TAG}_bench.log > $O/${TAG}_bench.json
 step prof 300 env MSU_GRAPH=0 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o run --output-format csv -- \
     python3 $R/bench.py --steps 4 --warmup 4 --no-cpu-baseline --no-roofline --no-input-pipeline
 python3 $R/tools/stream_summary.py $O/prof_$TAG/run_kernel_trace.csv > $O/${TAG}_streams.txt
-python3 $R/tools/profsum.py $O/prof_$TAG/run_kernel_stats.csv 6 40 > $O/${TAG}_summary.txt
+python3 $R/tools/profsum.py $O/prof_$TAG/run_kernel_stats.csv 8 40 > $O/${TAG}_summary.txt
 step pmc_conv_f 90 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_$TAG -o conv_fetch --output-format csv -- \
     python3 $R/tools/conv_one.py 0 3 fwd act
 step pmc_conv_w 90 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_$TAG -o conv_write --output-format csv -- \
