@@ -180,6 +180,13 @@ int msu_gelu_fwd(int dtype, const void* x, void* y, long n, void* stream);
 int msu_gelu_bwd(int dtype, const void* x, const void* dy, void* dx, long n, void* stream);
 /* PatchEmbed.proj im2col (model_parts.py:211, :222): img [B,Cin,H,W] f32 ->
  * [B*(H/p)*(W/p), Cin*p*p] in (c, ky, kx) order. */
+/* Batched 16-bit transpose: for each of nent entries {src offset, dst offset, N, K, first tile}
+ * (int64, device memory; element offsets into src / dst; N, K multiples of 8; first tiles
+ * ascending, entry e owning ceil(N/64) * ceil(K/64) tiles) dst[K][N] = src[N][K].  The
+ * trainer's per-step transposed bf16 weight shadow: the Linear input gradients dX = dY . W
+ * (model_parts.py:143-151 Linears' backward) read W^T with the forward GEMM's layout. */
+int msu_transpose16_multi(const void* src, void* dst, const long long* table, int nent, int ntiles,
+                          void* stream);
 /* out = a + b * scale[i / per_sample] (a may be NULL: out = b * scale[...]); n, per_sample
  * multiples of 4.  The Swin block's residual add with StochasticDepth's per-sample scale
  * (torchvision SwinTransformerBlock: x + stochastic_depth(f(x))) and its branch gradient. */

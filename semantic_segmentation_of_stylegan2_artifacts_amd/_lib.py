@@ -46,6 +46,7 @@ SIGNATURES = {
     "msu_adamw_dev": (I, [P, P, P, P, L, P, D, D, D, D, P, P, P]),
     "msu_step_advance": (I, [P, P, P]),
     "msu_cast": (I, [I, P, P, L, P]),
+    "msu_transpose16_multi": (I, [P, P, P, I, I, P]),
     "msu_conv3x3_fwd": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),
     "msu_conv3x3_fwd2": (I, [I, I, P, P, P, P, P, I, I, I, I, I, P]),
     "msu_conv3x3_dgrad": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),

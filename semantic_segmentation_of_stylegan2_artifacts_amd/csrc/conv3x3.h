@@ -536,7 +536,12 @@ constexpr int SPRE = 12;  // GELU' operand loads per lane (dgrad), issued at tap
 
 MSU_DEV int swz(int p) { return (p >> 2) & 3; }
 
-template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL>
+// SPREAD: the next tile's halo loads are issued in seven parts at taps 1..7 (each part issued
+// after that tap's weight DMA, so it only has to land two taps later) instead of all at tap 1,
+// where the wait for tap 3's weights also waited for the whole 117 KB halo.
+MSU_DEV constexpr int halo_part_lo(int t, int nhc) { return (t - 1) * nhc / 7; }  // t = 1..7
+
+template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL, bool SPREAD>
 __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restrict__ X,
                                                          const bf16_t* __restrict__ Wt,
                                                          const float* __restrict__ bias,
@@ -568,12 +573,14 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
     x0 = (r - (r / tiles_x) * tiles_x) * TWV;
   };
   u32x4 hr[NHC];
-  auto load_halo = [&](int tile) {
+  // chunks [c0, c1) of this thread's share of tile `tile`'s halo -> registers
+  auto load_halo = [&](int tile, auto C0, auto C1) {
+    constexpr int c0 = decltype(C0)::value, c1 = decltype(C1)::value;
     int b, y0, x0;
     coords(tile, b, y0, x0);
     const int t = opaque(tid);
 #pragma unroll
-    for (int c = 0; c < NHC; ++c) {
+    for (int c = c0; c < c1; ++c) {
       const int i = t + NTHR * c;
       const int pix = i / CH, ch = i - (i / CH) * CH;
       const int row = pix / HWD, col = pix - (pix / HWD) * HWD;
@@ -618,7 +625,7 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
 
   int tile = blockIdx.x;
   if (tile >= ntiles) return;
-  load_halo(tile);
+  load_halo(tile, IC<0>{}, IC<NHC>{});
   store_halo();
   dma_w(0, 0);
   __syncthreads();  // the halo's ds_writes land before any wave reads (the tap barriers are raw)
@@ -648,13 +655,16 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
       constexpr int dy = tap / 3, dx = tap % 3;
       // W(tap) landed (this wave's DMAs; the halo loads issued after them may stay in flight),
       // then the barrier: every wave's DMA landed, every wave done with the other buffer
-      if constexpr (tap == V3_HALO_TAP + 1) {
-        if (next < ntiles) wait_vmcnt<NHC>();
-        else wait_vmcnt<0>();
-      } else if constexpr (OUT_GGRAD && tap == 8) {
-        wait_vmcnt<SPRE>();  // the GELU' operands issued at tap 7 stay in flight
+      // loads issued at tap - 1 after that tap's weight DMA may stay in flight: the halo
+      // part(s) of the next tile and (dgrad, tap 7) the GELU' operands
+      constexpr int hprev = SPREAD ? (tap >= 2 ? halo_part_lo(tap, NHC) - halo_part_lo(tap - 1, NHC) : 0)
+                                   : (tap == V3_HALO_TAP + 1 ? NHC : 0);
+      constexpr int sprev = (OUT_GGRAD && tap == 8) ? SPRE : 0;
+      if constexpr (hprev > 0) {
+        if (next < ntiles) wait_vmcnt<hprev + sprev>();
+        else wait_vmcnt<sprev>();
       } else {
-        wait_vmcnt<0>();
+        wait_vmcnt<sprev>();
       }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -664,8 +674,10 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
       } else {
         if (next < ntiles) dma_w(0, wbuf ^ 1);
       }
-      if constexpr (tap == V3_HALO_TAP) {
-        if (next < ntiles) load_halo(next);
+      if constexpr (SPREAD && tap >= 1 && tap <= 7) {
+        if (next < ntiles) load_halo(next, IC<halo_part_lo(tap, NHC)>{}, IC<halo_part_lo(tap + 1, NHC)>{});
+      } else if constexpr (!SPREAD && tap == V3_HALO_TAP) {
+        if (next < ntiles) load_halo(next, IC<0>{}, IC<NHC>{});
       }
       if constexpr (OUT_GGRAD && tap == 7) {
         // dgrad: the pre-activation S of this tile's outputs for the GELU' epilogue
@@ -1019,18 +1031,25 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
     const uint32_t xa = lds_u32(sX + laneoff + dy * HWD * PS + 48 * cih);
     const uint32_t da = lds_u32(sD + laneoff + 48 * coh);
     unroll_for<TH>([&](auto R) {
+      constexpr int r = decltype(R)::value;
+      // the dY fragments of row r serve all three dx (read once per row, not once per dx:
+      // 12 instead of 18 fragment reads per 27 MFMAs -- the LDS reads bound this loop)
+      bf16x8 af[3];
+      unroll_for<3>([&](auto I) {
+        constexpr int o = 2 * (r * TWV * PS + 16 * decltype(I)::value);
+        af[decltype(I)::value] = tr8_untracked<o, o + 32 * PS>(da);
+      });
       unroll_for<3>([&](auto D) {
-        constexpr int r = decltype(R)::value, d = decltype(D)::value;
-        bf16x8 bf[3], af[3];
+        constexpr int d = decltype(D)::value;
+        bf16x8 bf[3];
         unroll_for<3>([&](auto J) {
           constexpr int o = 2 * ((r * HWD + d) * PS + 16 * decltype(J)::value);
           bf[decltype(J)::value] = tr8_untracked<o, o + 32 * PS>(xa);
         });
-        unroll_for<3>([&](auto I) {
-          constexpr int o = 2 * (r * TWV * PS + 16 * decltype(I)::value);
-          af[decltype(I)::value] = tr8_untracked<o, o + 32 * PS>(da);
-        });
-        lds_wait_tie<0>(bf[0], bf[1], bf[2], af[0], af[1], af[2]);
+        if constexpr (d == 0)
+          lds_wait_tie<0>(bf[0], bf[1], bf[2], af[0], af[1], af[2]);
+        else
+          lds_wait_tie<0>(bf[0], bf[1], bf[2]);
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -1161,12 +1180,21 @@ inline bool conv_v3_enabled() {
   return on;
 }
 
-template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL>
-int launch_v3(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S, bf16_t* Y,
-              bf16_t* Y2, hipStream_t st) {
+// halo load schedule of v3 (A/B switch MSU_CONV_HALO=1: the whole halo at tap 1)
+inline bool conv_v3_spread() {
+  static const bool on = [] {
+    const char* e = getenv("MSU_CONV_HALO");
+    return !(e && e[0] == '1');
+  }();
+  return on;
+}
+
+template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL, bool SPREAD>
+int launch_v3s(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S, bf16_t* Y,
+               bf16_t* Y2, hipStream_t st) {
   constexpr size_t lds = sizeof(bf16_t) * ((size_t)18 * 34 * 96 + 2 * 96 * 96);
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = conv3x3_v3_kernel<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL>;
+  auto kern = conv3x3_v3_kernel<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, SPREAD>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1178,6 +1206,14 @@ int launch_v3(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float*
   const int grid = (int)(ntiles < num_cus() ? ntiles : num_cus());
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, X, Wt, bias, S, Y, Y2, g, (int)ntiles);
   return MSU_CHECK_LAUNCH();
+}
+
+template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL>
+int launch_v3(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S, bf16_t* Y,
+              bf16_t* Y2, hipStream_t st) {
+  if (conv_v3_spread())
+    return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, true>(g, X, Wt, bias, S, Y, Y2, st);
+  return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, false>(g, X, Wt, bias, S, Y, Y2, st);
 }
 
 template <typename T, bool IN_D2S, bool IN_GELU, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL = false>

@@ -291,6 +291,47 @@ __global__ void __launch_bounds__(256) cast_kernel(const float* x, T* y, long n)
     y[i] = from_f32<T>(x[i]);
 }
 
+// Batched 16-bit transpose: entry e = {src offset, dst offset, N, K, first tile} (int64, in
+// elements of the two flat bases) turns src[N][K] into dst[K][N]; a block moves one 64 x 64
+// tile through LDS with 16-B loads and stores (N, K multiples of 8).  Entries are found by a
+// binary search over their first tiles (ascending).
+__global__ void __launch_bounds__(256) transpose16_multi_kernel(const uint16_t* __restrict__ src,
+                                                                uint16_t* __restrict__ dst,
+                                                                const long long* __restrict__ tab, int nent) {
+  __shared__ uint16_t t[64][64 + 8];
+  const int tile = blockIdx.x;
+  int lo = 0, hi = nent - 1;
+  while (lo < hi) {  // last entry whose first tile <= tile
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[5 * mid + 4] <= tile) lo = mid; else hi = mid - 1;
+  }
+  const long long* e = tab + 5 * lo;
+  const uint16_t* s = src + e[0];
+  uint16_t* d = dst + e[1];
+  const int N = (int)e[2], K = (int)e[3];
+  const int r = tile - (int)e[4];
+  const int tk = (K + 63) / 64;
+  const int n0 = (r / tk) * 64, k0 = (r % tk) * 64;
+  const int c8 = (threadIdx.x & 7) * 8;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rr = (threadIdx.x >> 3) + 32 * i;
+    if (n0 + rr < N && k0 + c8 < K) {
+      const uint4 v = *reinterpret_cast<const uint4*>(s + (long)(n0 + rr) * K + k0 + c8);
+      const uint16_t* pv = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[c8 + j][rr] = pv[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int kk = (threadIdx.x >> 3) + 32 * i;
+    if (k0 + kk < K && n0 + c8 < N)
+      *reinterpret_cast<uint4*>(d + (long)(k0 + kk) * N + n0 + c8) = *reinterpret_cast<const uint4*>(&t[kk][c8]);
+  }
+}
+
 inline unsigned grid_for(long n, long per_block = 256, long cap = 8192) {
   long nb = (n + per_block - 1) / per_block;
   if (nb > cap) nb = cap;
@@ -410,6 +451,14 @@ int msu_nonfinite(const float* x, long n, float* flag, void* stream) {
 int msu_cast(int dtype, const float* x, void* y, long n, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(cast_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, x, (T*)y, n));
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_transpose16_multi(const void* src, void* dst, const long long* table, int nent, int ntiles,
+                          void* stream) {
+  if (nent <= 0 || ntiles <= 0) return 0;
+  hipLaunchKernelGGL(transpose16_multi_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream,
+                     (const uint16_t*)src, (uint16_t*)dst, table, nent);
   return MSU_CHECK_LAUNCH();
 }
 

@@ -132,32 +132,39 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ dY, co
 
 // bf16: wave-sized output tiles.  Each wave owns a full WT x WT output tile (WT = 96 or
 // 128, 36 / 64 accumulators of 16x16) so every fragment read from LDS feeds NTW MFMAs;
-// the 4 waves split either N (WN waves along N, sharing the X rows of the stage) or the
-// rows of the stage (WM = 4 / WN waves, each its own partial slab).  Staging is LDS-DMA:
-// a stage is RS = 32 * WM rows of dY [RS][BN+8] and X [RS][WT+8] written lane-linearly by
+// the NW = 4 (or 3) waves split N (WN waves along N, sharing the X rows of the stage), K
+// (WK waves along K, sharing the dY rows) and the rows of the stage (WM = NW / (WN WK)
+// waves, each its own partial slab).  A workgroup covering more of the N x K output reads
+// dY and X fewer times over all workgroups: dY is read K / (WK WT) times, X N / (WN WT)
+// times.  Staging is LDS-DMA:
+// a stage is RS = 32 * WM rows of dY [RS][BN+8] and X [RS][BK+8] written lane-linearly by
 // global_load_lds_dwordx4 (pad slots re-read chunk 0 of their row; rows past the block's
 // range read the spread zero region); a ring of NST stages keeps NST-1 in flight; raw
 // s_barrier + counted vmcnt keep the prefetch alive across barriers.
-template <typename T, int NTW, int WN, int NST>
+template <int WN, int WK> constexpr int wgrad_nw() { return WN * WK == 3 ? 3 : 4; }
+
+template <typename T, int NTW, int WN, int WK, int NST>
 __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                                          float* __restrict__ part, float* __restrict__ dbpart,
                                                          long M, int N, int K, long mchunk) {
-  constexpr int WM = 4 / WN, WT = 16 * NTW, BN = WN * WT, RS = 32 * WM;
-  constexpr int SA = (BN + 8) / 8, SB = (WT + 8) / 8;  // 16-B slots per row
+  constexpr int NW = wgrad_nw<WN, WK>();
+  constexpr int WM = NW / (WN * WK), WT = 16 * NTW, BN = WN * WT, BK = WK * WT, RS = 32 * WM;
+  static_assert(WM * WN * WK == NW, "wave split");
+  constexpr int SA = (BN + 8) / 8, SB = (BK + 8) / 8;  // 16-B slots per row
   constexpr int LA = 8 * SA, LB = 8 * SB;              // row strides (elements)
   constexpr int SLOTS = RS * (SA + SB);
-  constexpr int INS = ((SLOTS + 63) / 64 + 3) / 4 * 4;
-  constexpr int PER_WAVE = INS / 4;
+  constexpr int INS = ((SLOTS + 63) / 64 + NW - 1) / NW * NW;
+  constexpr int PER_WAVE = INS / NW;
   constexpr int STG = INS * 64 * 8;
   static_assert(PER_WAVE * (NST - 2) < 64, "vmcnt");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wni = wave % WN, wmi = wave / WN;
-  const int ntk = K / WT;
+  const int wni = wave % WN, wki = (wave / WN) % WK, wmi = wave / (WN * WK);
+  const int ntk = K / BK;
   const int tn = blockIdx.x / ntk, tk = blockIdx.x - (blockIdx.x / ntk) * ntk;
-  const int n0 = tn * BN, k0 = tk * WT;
+  const int n0 = tn * BN, k0 = tk * BK;
   const long m_begin = (long)blockIdx.y * mchunk;
   long m_end = m_begin + mchunk;
   if (m_end > M) m_end = M;
@@ -169,7 +176,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
   bool sisA[PER_WAVE];
 #pragma unroll
   for (int r = 0; r < PER_WAVE; ++r) {
-    const int s = 64 * (wave + 4 * r) + lane;
+    const int s = 64 * (wave + NW * r) + lane;
     if (s < RS * SA) {
       const int row = s / SA, c = s - (s / SA) * SA;
       srow[r] = row;
@@ -193,7 +200,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
 #pragma unroll
     for (int r = 0; r < PER_WAVE; ++r) {
       const bf16_t* src = (sisA[r] ? baseA : baseB) + soff[r];
-      glds16(srow[r] < valid ? (const void*)src : zero_src(64 * r + lane), buf + 64 * 8 * (wave + 4 * r));
+      glds16(srow[r] < valid ? (const void*)src : zero_src(64 * r + lane), buf + 64 * 8 * (wave + NW * r));
     }
   };
 
@@ -205,7 +212,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const bool do_bias = dbpart != nullptr && tk == 0;
+  const bool do_bias = dbpart != nullptr && tk == 0 && wki == 0;
   const bf16x8 ones = splat8<T>(1.0f, 1.0f, 1.0f);
   // lane part of a k-strided fragment read (ds_read_b64_tr_b16), columns 4p.  The k order
   // is free (both operands use the same one): each 32-lane half reads 8 rows of one parity,
@@ -214,7 +221,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
   // mod 64 for both row strides (52 and 196 dwords): the 32 lanes cover all 64 banks
   // exactly once (rows 8(lane>>4) + q put two rows on each bank span: 2-way conflicts).
   const int q = (lane & 15) >> 2, p4 = 4 * (lane & 3), r0 = wmi * 32 + 2 * (4 * ((lane >> 4) & 1) + q) + (lane >> 5);
-  const int laneA = r0 * LA + wni * WT + p4, laneB = RS * LA + r0 * LB + p4;
+  const int laneA = r0 * LA + wni * WT + p4, laneB = RS * LA + r0 * LB + wki * WT + p4;
   auto tr8 = [](const bf16_t* p, int second) {
     typedef __attribute__((address_space(3))) msu_v4s lds_v4s;
     const msu_v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
@@ -262,11 +269,12 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
   wait_vmcnt<0>();  // every DMA has landed: the ring may be reused
   // row-waves of the same output tile are summed in LDS first: one slab per split
   if constexpr (WM > 1) {
-    float* red = reinterpret_cast<float*>(smem_raw);  // [WM][NTW*NTW*4][64] per N-wave
+    float* red = reinterpret_cast<float*>(smem_raw);  // [WM][NTW*NTW*4][64] per (N, K)-wave
     __syncthreads();
     constexpr int PW = (NTW * NTW * 4 + NTW * 4) * 64;  // floats per wave
-    static_assert((size_t)WN * (WM - 1) * PW * 4 <= 160 * 1024, "LDS reduction");
-    float* mine = red + ((long)wni * (WM - 1) + (wmi > 0 ? wmi - 1 : 0)) * PW;
+    static_assert((size_t)WN * WK * (WM - 1) * PW * 4 <= 160 * 1024, "LDS reduction");
+    const int wnk = wni + WN * wki;
+    float* mine = red + ((long)wnk * (WM - 1) + (wmi > 0 ? wmi - 1 : 0)) * PW;
     if (wmi > 0) {
 #pragma unroll
     for (int i = 0; i < NTW; ++i) {
@@ -282,7 +290,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
     if (wmi == 0) {
 #pragma unroll
       for (int w = 1; w < WM; ++w) {
-        const float* other = red + ((long)wni * (WM - 1) + w - 1) * PW;
+        const float* other = red + ((long)wnk * (WM - 1) + w - 1) * PW;
 #pragma unroll
         for (int i = 0; i < NTW; ++i) {
 #pragma unroll
@@ -304,7 +312,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + wni * WT + 16 * i + (lane >> 4) * 4 + r;
-        const int k = k0 + 16 * j + (lane & 15);
+        const int k = k0 + wki * WT + 16 * j + (lane & 15);
         out[(long)n * K + k] = acc[i][j][r];
       }
   if (do_bias && (lane & 15) == 0) {
@@ -317,22 +325,46 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
   }
 }
 
-// bf16 plan: wave tile, waves along N, ring depth, splits (each split writes WM slabs)
+// bf16 plan: wave tile, waves along N and K, ring depth, splits
 struct WavePlan {
-  int ntw = 0, wn = 1, nst = 3, S = 1;
+  int ntw = 0, wn = 1, wk = 1, nst = 3, S = 1;
   int slabs() const { return S; }
 };
+
+// the (WN, WK) split of a workgroup's waves over the N x K tiles: least operand traffic
+// M (N kt / WK + K nt / WN) (dY re-read per K group, X per N group), more waves on ties;
+// MSU_WGRAD_WK=0: the round-2 plan (waves along N only)
+inline void pick_wave_split(int nt, int kt, int& wn, int& wk) {
+  static const bool k_split = !(getenv("MSU_WGRAD_WK") && getenv("MSU_WGRAD_WK")[0] == '0');
+  if (!k_split) {
+    wn = nt % 4 == 0 ? 4 : (nt % 2 == 0 ? 2 : 1);
+    wk = 1;
+    return;
+  }
+  static const int cand[8][2] = {{4, 1}, {2, 2}, {1, 4}, {3, 1}, {1, 3}, {2, 1}, {1, 2}, {1, 1}};
+  long best = -1;
+  for (const auto& c : cand) {
+    if (nt % c[0] || kt % c[1]) continue;
+    const long cost = (long)nt * kt / c[1] + (long)kt * nt / c[0];  // in units of M * WT
+    if (best < 0 || cost < best) {
+      best = cost;
+      wn = c[0];
+      wk = c[1];
+    }
+  }
+}
 
 inline WavePlan wave_plan(long M, int N, int K) {
   WavePlan p;
   if (N % 96 == 0 && K % 96 == 0) p.ntw = 6;
   else if (N % 128 == 0 && K % 128 == 0) p.ntw = 8;
   else return p;  // not supported: generic kernel
-  const int wt = 16 * p.ntw, nt = N / wt;
-  p.wn = nt % 4 == 0 ? 4 : (nt % 2 == 0 ? 2 : 1);
-  const int wm = 4 / p.wn, rs = 32 * wm;
-  const int sa = (p.wn * wt + 8) / 8, sb = (wt + 8) / 8;
-  const int ins = ((rs * (sa + sb) + 63) / 64 + 3) / 4 * 4;
+  const int wt = 16 * p.ntw, nt = N / wt, kt = K / wt;
+  pick_wave_split(nt, kt, p.wn, p.wk);
+  const int nw = p.wn * p.wk == 3 ? 3 : 4;
+  const int wm = nw / (p.wn * p.wk), rs = 32 * wm;
+  const int sa = (p.wn * wt + 8) / 8, sb = (p.wk * wt + 8) / 8;
+  const int ins = ((rs * (sa + sb) + 63) / 64 + nw - 1) / nw * nw;
   const long stage_bytes = (long)ins * 64 * 16;
   p.nst = (int)((160L * 1024) / stage_bytes);
   if (p.nst > 6) p.nst = 6;
@@ -345,7 +377,7 @@ inline WavePlan wave_plan(long M, int N, int K) {
     p.ntw = 0;
     return p;
   }
-  const long tiles = (long)(N / (p.wn * wt)) * (K / wt);
+  const long tiles = (long)(nt / p.wn) * (kt / p.wk);
   long s = 256 / tiles;  // at most one workgroup per CU (no tail wave), long row ranges
   const long max_s = (M + 8 * rs - 1) / (8 * rs);  // at least 8 stages per split
   if (s > max_s) s = max_s;
@@ -354,41 +386,45 @@ inline WavePlan wave_plan(long M, int N, int K) {
   return p;
 }
 
-template <typename T, int NTW, int WN, int NST>
+template <typename T, int NTW, int WN, int WK, int NST>
 void launch_wave(dim3 grid, const bf16_t* dY, const bf16_t* X, float* part, float* dbpart, long M, int N, int K,
                  long mchunk, hipStream_t st) {
-  constexpr int WM = 4 / WN, WT = 16 * NTW, RS = 32 * WM;
-  constexpr int SLOTS = RS * ((WN * WT + 8) / 8 + (WT + 8) / 8);
-  constexpr int INS = ((SLOTS + 63) / 64 + 3) / 4 * 4;
+  constexpr int NW = wgrad_nw<WN, WK>();
+  constexpr int WM = NW / (WN * WK), WT = 16 * NTW, RS = 32 * WM;
+  constexpr int SLOTS = RS * ((WN * WT + 8) / 8 + (WK * WT + 8) / 8);
+  constexpr int INS = ((SLOTS + 63) / 64 + NW - 1) / NW * NW;
   constexpr size_t lds = (size_t)NST * INS * 64 * 16;
   if constexpr (lds <= 160 * 1024) {  // ring depths the plan never picks are not instantiated
-    auto kern = wgrad_wave_kernel<T, NTW, WN, NST>;
+    auto kern = wgrad_wave_kernel<T, NTW, WN, WK, NST>;
     static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
-    hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, dY, X, part, dbpart, M, N, K, mchunk);
+    hipLaunchKernelGGL(kern, grid, dim3(64 * NW), lds, st, dY, X, part, dbpart, M, N, K, mchunk);
   }
 }
 
 template <typename T>
 int run_wave(const WavePlan& p, const bf16_t* dY, const bf16_t* X, float* part, float* dbpart, long M, int N, int K,
              hipStream_t st) {
-  const int wt = 16 * p.ntw, wm = 4 / p.wn, rs = 32 * wm;
+  const int wt = 16 * p.ntw, nw = p.wn * p.wk == 3 ? 3 : 4, wm = nw / (p.wn * p.wk), rs = 32 * wm;
   long mchunk = (M + p.S - 1) / p.S;
   mchunk = (mchunk + rs - 1) / rs * rs;
-  const dim3 grid((unsigned)((N / (p.wn * wt)) * (K / wt)), (unsigned)p.S);
-#define MSU_WAVE(NTW, WN)                                                                                   \
-  if (p.ntw == NTW && p.wn == WN) {                                                                         \
+  const dim3 grid((unsigned)((N / (p.wn * wt)) * (K / (p.wk * wt))), (unsigned)p.S);
+#define MSU_WAVE(NTW, WN, WK)                                                                                \
+  if (p.ntw == NTW && p.wn == WN && p.wk == WK) {                                                           \
     switch (p.nst) {                                                                                        \
-      case 3: launch_wave<T, NTW, WN, 3>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;         \
-      case 4: launch_wave<T, NTW, WN, 4>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;         \
-      case 5: launch_wave<T, NTW, WN, 5>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;         \
-      case 6: launch_wave<T, NTW, WN, 6>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;         \
+      case 3: launch_wave<T, NTW, WN, WK, 3>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;     \
+      case 4: launch_wave<T, NTW, WN, WK, 4>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;     \
+      case 5: launch_wave<T, NTW, WN, WK, 5>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;     \
+      case 6: launch_wave<T, NTW, WN, WK, 6>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;     \
     }                                                                                                       \
   }
-  MSU_WAVE(6, 1) MSU_WAVE(6, 2) MSU_WAVE(6, 4) MSU_WAVE(8, 1) MSU_WAVE(8, 2) MSU_WAVE(8, 4)
+  MSU_WAVE(6, 1, 1) MSU_WAVE(6, 2, 1) MSU_WAVE(6, 4, 1) MSU_WAVE(6, 1, 2) MSU_WAVE(6, 2, 2) MSU_WAVE(6, 1, 4)
+  MSU_WAVE(6, 3, 1) MSU_WAVE(6, 1, 3)
+  MSU_WAVE(8, 1, 1) MSU_WAVE(8, 2, 1) MSU_WAVE(8, 4, 1) MSU_WAVE(8, 1, 2) MSU_WAVE(8, 2, 2) MSU_WAVE(8, 1, 4)
+  MSU_WAVE(8, 3, 1) MSU_WAVE(8, 1, 3)
 #undef MSU_WAVE
   return -3;
 }

@@ -135,8 +135,15 @@ MSU_DEV float keep_sel(uint32_t m, int n, float x) {
   return __int_as_float(((int)(m << (31 - n)) >> 31) & __float_as_int(x));
 }
 
+// Accumulator register r of key tile jt holds key jt*32 + crow(r, hh): for jt = 1 and r >= 9
+// that key is >= 49 in BOTH lane halves -- a padded key of every window (bias -inf, P = 0).
+// Those 7 of the 32 score registers skip the softmax / dropout / dS work.
+MSU_DEV constexpr bool live_key(int jt, int r) { return !(jt == 1 && r >= 9); }
+constexpr int DROP_WORDS = 13;  // stream words holding a live key (word n: bits 2n, 2n + 1)
+
 // keep bits of the lane's 32 keys of query column tile it: bit jt*16 + r <-> key
-// jt*32 + crow(r, hh) (word n of the lane's stream holds bits 2n, 2n+1, common.h)
+// jt*32 + crow(r, hh) (word n of the lane's stream holds bits 2n, 2n+1, common.h); the words
+// past DROP_WORDS only cover padded keys and are not drawn (their bits stay 0)
 // SERIAL: not unrolled (the backward's re-hash path, whose register peak an unrolled stream raises)
 template <bool SERIAL>
 MSU_DEV uint32_t drop_bits(uint32_t seed, uint32_t item, int i, int hh, uint32_t thr) {
@@ -144,10 +151,10 @@ MSU_DEV uint32_t drop_bits(uint32_t seed, uint32_t item, int i, int hh, uint32_t
   uint32_t m = 0;
   if constexpr (SERIAL) {
 #pragma unroll 1
-    for (int n = 0; n < 16; ++n) m |= drop_next2(s, thr) << (2 * n);
+    for (int n = 0; n < DROP_WORDS; ++n) m |= drop_next2(s, thr) << (2 * n);
   } else {
 #pragma unroll
-    for (int n = 0; n < 16; ++n) m |= drop_next2(s, thr) << (2 * n);
+    for (int n = 0; n < DROP_WORDS; ++n) m |= drop_next2(s, thr) << (2 * n);
   }
   return m;
 }
@@ -164,7 +171,8 @@ MSU_DEV void softmax_col(f32x16 (&P)[2], float scale) {
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) m = fmaxf(m, P[jt][r]);
+    for (int r = 0; r < 16; ++r)
+      if (live_key(jt, r)) m = fmaxf(m, P[jt][r]);
   m = fmaxf(m, __shfl_xor(m, 32, 64));
   const float c = scale * 1.44269504088896341f;
   const float mc = m * c;
@@ -173,15 +181,20 @@ MSU_DEV void softmax_col(f32x16 (&P)[2], float scale) {
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      P[jt][r] = __builtin_amdgcn_exp2f(fmaf(P[jt][r], c, -mc));
-      sum += P[jt][r];
+      if (live_key(jt, r)) {
+        P[jt][r] = __builtin_amdgcn_exp2f(fmaf(P[jt][r], c, -mc));
+        sum += P[jt][r];
+      } else {
+        P[jt][r] = 0.f;
+      }
     }
   sum += __shfl_xor(sum, 32, 64);
   const float inv = 1.0f / sum;
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) P[jt][r] *= inv;
+    for (int r = 0; r < 16; ++r)
+      if (live_key(jt, r)) P[jt][r] *= inv;
 }
 
 // shifted-window mask of one query-column tile: -100/scale where query and key regions differ
@@ -192,7 +205,7 @@ MSU_DEV void mask_col(f32x16 (&P)[2], const int* sReg, int it, float scale, int 
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-      if (sReg[jt * 32 + crow(r, hh)] != ri) P[jt][r] += mval;
+      if (live_key(jt, r) && sReg[jt * 32 + crow(r, hh)] != ri) P[jt][r] += mval;
 }
 
 struct Aux {
@@ -324,7 +337,8 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) P[jt][r] = (kmasks[it] >> (jt * 16 + r)) & 1u ? P[jt][r] * kscale : 0.f;
+          for (int r = 0; r < 16; ++r)
+            if (live_key(jt, r)) P[jt][r] = (kmasks[it] >> (jt * 16 + r)) & 1u ? P[jt][r] * kscale : 0.f;
       }
       // O^T[d][i] = sum_j V[j][d] P^T[j][i]: P^T is the B operand straight from the registers
       f32x16 O = f32x16{0};
@@ -575,6 +589,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
+        if (!live_key(jt, r)) continue;  // P = 0: no share of delta, dS = 0
         if constexpr (DROP)  // dP = dPd * keep/(1-p)
           D[jt][r] = keep_sel(kmask, jt * 16 + r, D[jt][r] * kscale);
         delta += P[jt][r] * D[jt][r];
@@ -589,6 +604,10 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * gq + e;
+          if (!live_key(jt, r)) {
+            ds[e] = pd[e] = 0.f;
+            continue;
+          }
           const float p = P[jt][r];
           ds[e] = p * (D[jt][r] - delta);
           pd[e] = DROP ? keep_sel(kmask, jt * 16 + r, p * kscale) : p;

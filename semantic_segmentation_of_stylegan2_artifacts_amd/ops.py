@@ -148,6 +148,9 @@ def set_grad_ready_callback(fn):
 _side_enabled = os.environ.get("MSU_WGRAD_SIDE", "1") != "0"
 _SIDE_PRIORITY = int(os.environ.get("MSU_SIDE_PRIORITY", "1"))  # A/B switch (0: same as main)
 _side_streams = {}
+# per-use switches of the side stream (tools/graph_side_probe.py bisects the forked capture)
+_side_wgrad = True      # Linear weight gradients
+_side_attn_tail = True  # attention relative-table / qkv-bias reductions
 
 
 def side_stream(device):
@@ -524,7 +527,7 @@ def _attn_backward(ctx, dout, _dkeep):
                      dtype=torch.float32)
     dqkv = torch.empty_like(qkv)
     bp, tp = ctx.bias_param, ctx.table_param
-    if bp is not None and tp is not None and _side_enabled and _direct(bp, tp):
+    if bp is not None and tp is not None and _side_enabled and _side_attn_tail and _direct(bp, tp):
         # parameter-gradient tail on the side stream: the relative-table / qkv-bias
         # reductions and their .grad adds (the qkv bias also receives its Linear's db
         # there, so every write to its .grad is ordered on one stream)
@@ -652,14 +655,17 @@ def _wt(w):
     return w.t().contiguous()
 
 
-def _gemm_dx(dy, w, epi=TOK_PLAIN, h=None):
-    """16-bit epi(dy . w): the input gradient of y = x . w^T (w [N, K]) on the routed GEMM; the
-    NT route reads w in place, the token GEMM takes W^T."""
+def _gemm_dx(dy, w, epi=TOK_PLAIN, h=None, param=None):
+    """16-bit epi(dy . w): the input gradient of y = x . w^T (w [N, K]) on the routed GEMM.  W^T
+    comes from the trainer's transposed shadow of ``param`` when it has one (both GEMMs then run
+    their forward layout); otherwise the NT route reads w in place (KN variant) and the token
+    GEMM takes a per-call W^T copy."""
     N, K = w.shape
     M = dy.numel() // N
-    if gemm_route(M, K, N, epi) == "nt":
+    wt = _shadow_t(param, w.dtype)
+    if gemm_route(M, K, N, epi) == "nt" and wt is None:
         return nt_gemm_kn(dy, w, epi, h)
-    return _gemm(dy, _wt(w), None, epi, h)
+    return _gemm(dy, _wt(w) if wt is None else wt, None, epi, h)
 
 
 def _wgrad(dy, x, weight, bias, M, N, K):
@@ -667,7 +673,7 @@ def _wgrad(dy, x, weight, bias, M, N, K):
     straight into the trainer's flat .grad views."""
     L = _lib.lib()
     if _direct(weight) and (bias is None or _direct(bias)):
-        if _side_enabled:
+        if _side_enabled and _side_wgrad:
             main = torch.cuda.current_stream(x.device)
             side = _side_stream_for(x.device)
             side.wait_stream(main)  # dy and x are ready
@@ -705,6 +711,27 @@ def _shadow(param, dt):
     if sh is not None and sh.dtype == dt and getattr(param, "_msu_shadow_ver", -1) == param._version:
         return sh
     return param.to(dt)
+
+
+# A/B switch: the trainer's transposed weight shadow for the input-gradient GEMMs (0: W^T is
+# read in place by the NT GEMM's KN variant / copied per call for the token GEMM)
+_SHADOW_T = os.environ.get("MSU_SHADOW_T", "1") != "0"
+
+
+def _shadow_t(param, dt):
+    """The trainer's transposed 16-bit shadow W^T [K, N] of a Linear weight W [N, K], refreshed
+    with the shadow (None when there is none or it is stale)."""
+    if param is None or not _SHADOW_T:
+        return None
+    sh = getattr(param, "_msu_shadow_t", None)
+    if sh is not None and sh.dtype == dt and getattr(param, "_msu_shadow_ver", -1) == param._version:
+        return sh
+    return None
+
+
+def transpose16_multi(src, dst, table, ntiles):
+    """dst segments = transposes of src segments (table rows {src off, dst off, N, K, first tile})."""
+    _lib.call("msu_transpose16_multi", _p(src), _p(dst), _p(table), int(table.shape[0]), int(ntiles), _s(src))
 
 
 # GEMM routing of the 16-bit Linears (forward and input gradient): the token GEMM (weight in
@@ -797,7 +824,7 @@ def _linear_backward(ctx, dy):
     dx = None
     if ctx.needs_input_grad[0]:
         if x.dtype in _LOW and gemm_route(M, K, N) != "lib":
-            dx = _gemm_dx(dy, w)
+            dx = _gemm_dx(dy, w, param=weight)
         else:
             with torch.autocast("cuda", enabled=False):
                 dx = dy.matmul(w)
@@ -880,8 +907,9 @@ def _linear_cat_backward(ctx, dy):
     C1, C2 = x.shape[-1], skip.shape[-1]
     M = dy.numel() // N
     outs = []
+    wt = _shadow_t(weight, W.dtype)  # W^T [K, N]: the halves are row ranges, no copies
     for lo, hi in ((0, C1), (C1, C1 + C2)):
-        outs.append(_gemm(dy, W[:, lo:hi].t().contiguous()))
+        outs.append(_gemm(dy, W[:, lo:hi].t().contiguous() if wt is None else wt[lo:hi]))
     # weight gradient per half into temporaries ([N, C1], [N, C2]), bias with the first
     dw1, db = _wgrad_tmp(dy, x, N, C1, M, with_bias=True)
     dw2, _ = _wgrad_tmp(dy, skip, N, C2, M, with_bias=False)
@@ -964,9 +992,9 @@ def _mlp_backward(ctx, dy, _dh, _dg):
     Hd, C = W1.shape
     M = x.numel() // C
     dw2, db2 = _wgrad(dy, g, w2, b2, M, C, Hd)
-    dh = _gemm_dx(dy, W2, TOK_GELU_GRAD, h=h)
+    dh = _gemm_dx(dy, W2, TOK_GELU_GRAD, h=h, param=w2)
     dw1, db1 = _wgrad(dh, x, w1, b1, M, Hd, C)
-    dx = _gemm_dx(dh, W1) if ctx.needs_input_grad[0] else None
+    dx = _gemm_dx(dh, W1, param=w1) if ctx.needs_input_grad[0] else None
     return dx, dw1, db1, dw2, db2
 
 
@@ -1282,7 +1310,7 @@ def _linear_gelu_backward(ctx, dy, _dg):
     dx = None
     if ctx.needs_input_grad[0]:
         if x.dtype in _LOW and gemm_route(M, K, N) != "lib":
-            dx = _gemm_dx(dy, w)
+            dx = _gemm_dx(dy, w, param=weight)
         else:
             with torch.autocast("cuda", enabled=False):
                 dx = dy.matmul(w)

@@ -91,6 +91,24 @@ class FlatGroup:
             p._msu_shadow = self.shadow[off:off + k].view_as(p)
             p._msu_shadow_ver = -1  # not valid until the first refresh
             p._msu_direct = True  # backward kernels accumulate straight into p.grad
+        # transposed bf16 shadow of the 2-D weights (Linear weights: both dims multiples of 8),
+        # written by one batched transpose after each refresh: the input-gradient GEMMs read
+        # W^T in the forward GEMM's layout instead of transposing per call (ops._shadow_t)
+        tab, owners, toff, tiles = [], [], 0, 0
+        for p, off in zip(self.params, self.offsets):
+            if p.ndim == 2 and p.shape[0] % 8 == 0 and p.shape[1] % 8 == 0:
+                N, K = p.shape
+                tab.append((off, toff, N, K, tiles))
+                owners.append(p)
+                tiles += -(-N // 64) * -(-K // 64)
+                toff += (N * K + 7) // 8 * 8
+        self.tshadow = self.ttable = None
+        self.ntiles = tiles
+        if tab and torch.device(device).type == "cuda":
+            self.tshadow = torch.empty(toff, device=device, dtype=torch.bfloat16)
+            self.ttable = torch.tensor(tab, dtype=torch.int64).to(device)
+            for (_, to, N, K, _), p in zip(tab, owners):
+                p._msu_shadow_t = self.tshadow[to:to + N * K].view(K, N)
 
     def refresh_shadow(self):
         """Re-cast the bf16 shadow after the master weights changed (AdamW writes them through
@@ -102,6 +120,8 @@ class FlatGroup:
 
     def copy_shadow(self):
         self.shadow.copy_(self.data)
+        if self.tshadow is not None and ops._SHADOW_T:
+            ops.transpose16_multi(self.shadow, self.tshadow, self.ttable, self.ntiles)
 
     def mark_shadow(self):
         """Host-only half of the refresh: the raw-pointer AdamW and the shadow copy do not

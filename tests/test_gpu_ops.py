@@ -517,7 +517,9 @@ def test_adamw_matches_torch():
 
 
 @pytest.mark.parametrize("M,N,K", [(100, 96, 288), (4096, 288, 96), (777, 32, 48), (65536, 384, 96),
-                                   (3000, 1536, 96), (512, 192, 768), (8192, 1152, 384), (2000, 384, 384)])
+                                   (3000, 1536, 96), (512, 192, 768), (8192, 1152, 384), (2000, 384, 384),
+                                   # wave splits of the weight-gradient plan (N x K tiles of 96): 1x4, 1x2, 2x1
+                                   (65536, 96, 384), (1024, 96, 192), (1024, 192, 96), (8192, 576, 192)])
 @pytest.mark.parametrize("dtype", ALL)
 def test_linear(M, N, K, dtype):
     """ops.linear: hipBLASLt fwd/dgrad + HIP split-M weight/bias gradient vs fp32 torch."""
