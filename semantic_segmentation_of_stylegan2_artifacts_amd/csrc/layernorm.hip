@@ -95,10 +95,7 @@ MSU_DEV long src_off(const LnArgs& a, long r, int col) {
   }
 }
 
-// NR rows per lane group in flight: the loads of all NR rows are issued before any row's
-// reductions (a row's load -> shuffle-sum -> store chain is latency-bound; at one row per
-// group the whole chip keeps too few bytes in flight to stream HBM)
-template <typename T, int MODE, int TPR, int KMAX, int NR>
+template <typename T, int MODE, int TPR, int KMAX>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs a) {
   constexpr int VW = VecW<T>::W;  // elements per 16-B chunk
   const int lane = threadIdx.x % TPR;
@@ -107,83 +104,63 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs a) {
   const int nchunk = a.C / VW;
   const T* X = reinterpret_cast<const T*>(a.x);
   const T* Bv = reinterpret_cast<const T*>(a.b);
-  const long step = (long)gridDim.x * GPB;
-  for (long r0 = (long)blockIdx.x * GPB + grp; r0 < a.rows; r0 += step * NR) {
-    float v[NR][KMAX][VW];
-    float w[NR][KMAX][VW];
-    float sc[NR];
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const long r = r0 + j * step;
-      sc[j] = 1.f;
-      if (r >= a.rows) continue;  // group-uniform
-      if constexpr (MODE == IN_ADD) {
-        if (a.bscale) sc[j] = a.bscale[r / a.rows_per_sample];
-      }
-#pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        const int ch = lane + k * TPR;
-        if (ch < nchunk) {
-          const long off = src_off<MODE>(a, r, ch * VW);
-          VecW<T>::load(X + off, v[j][k]);
-          if constexpr (MODE == IN_ADD) {
-            if (Bv) VecW<T>::load(Bv + off, w[j][k]);
-          }
-        }
-      }
+  for (long r = (long)blockIdx.x * GPB + grp; r < a.rows; r += (long)gridDim.x * GPB) {
+    float v[KMAX][VW];
+    float sum = 0.f;
+    float sc = 1.f;
+    if constexpr (MODE == IN_ADD) {
+      if (a.bscale) sc = a.bscale[r / a.rows_per_sample];
     }
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const long r = r0 + j * step;
-      if (r >= a.rows) continue;
-      float sum = 0.f;
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        const long off = src_off<MODE>(a, r, ch * VW);
+        VecW<T>::load(X + off, v[k]);
+        if constexpr (MODE == IN_ADD) {
+          if (Bv) {
+            float w[VW];
+            VecW<T>::load(Bv + off, w);
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        const int ch = lane + k * TPR;
-        if (ch < nchunk) {
-          if constexpr (MODE == IN_ADD) {
-            if (Bv) {
-#pragma unroll
-              for (int e = 0; e < VW; ++e) v[j][k][e] += sc[j] * w[j][k][e];
-            }
-            // round the residual stream to storage precision first: the stored value is
-            // what later layers (and backward) see, so normalise exactly that value
-#pragma unroll
-            for (int e = 0; e < VW; ++e) v[j][k][e] = to_f32(from_f32<T>(v[j][k][e]));
-            if (a.s_out) VecW<T>::store(reinterpret_cast<T*>(a.s_out) + src_off<MODE>(a, r, ch * VW), v[j][k]);
+            for (int e = 0; e < VW; ++e) v[k][e] += sc * w[e];
           }
+          // round the residual stream to storage precision first: the stored value is
+          // what later layers (and backward) see, so normalise exactly that value
 #pragma unroll
-          for (int e = 0; e < VW; ++e) sum += v[j][k][e];
+          for (int e = 0; e < VW; ++e) v[k][e] = to_f32(from_f32<T>(v[k][e]));
+          if (a.s_out) VecW<T>::store(reinterpret_cast<T*>(a.s_out) + off, v[k]);
         }
+#pragma unroll
+        for (int e = 0; e < VW; ++e) sum += v[k][e];
       }
-      sum = group_sum<TPR>(sum);
-      const float mu = sum / a.C;
-      float var = 0.f;
-#pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        const int ch = lane + k * TPR;
-        if (ch < nchunk) {
-#pragma unroll
-          for (int e = 0; e < VW; ++e) { const float d = v[j][k][e] - mu; var += d * d; }
-        }
-      }
-      var = group_sum<TPR>(var);
-      const float rs = rsqrtf(var / a.C + a.eps);
-      T* Y = reinterpret_cast<T*>(a.y);
-#pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        const int ch = lane + k * TPR;
-        if (ch < nchunk) {
-          float o[VW], g[VW], bt[VW];
-          load_f32<VW>(a.gamma + ch * VW, g);
-          load_f32<VW>(a.beta + ch * VW, bt);
-#pragma unroll
-          for (int e = 0; e < VW; ++e) o[e] = (v[j][k][e] - mu) * rs * g[e] + bt[e];
-          VecW<T>::store(Y + r * (long)a.C + ch * VW, o);
-        }
-      }
-      if (lane == 0) { a.mean[r] = mu; a.rstd[r] = rs; }
     }
+    sum = group_sum<TPR>(sum);
+    const float mu = sum / a.C;
+    float var = 0.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+#pragma unroll
+        for (int e = 0; e < VW; ++e) { const float d = v[k][e] - mu; var += d * d; }
+      }
+    }
+    var = group_sum<TPR>(var);
+    const float rs = rsqrtf(var / a.C + a.eps);
+    T* Y = reinterpret_cast<T*>(a.y);
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        float o[VW], g[VW], bt[VW];
+        load_f32<VW>(a.gamma + ch * VW, g);
+        load_f32<VW>(a.beta + ch * VW, bt);
+#pragma unroll
+        for (int e = 0; e < VW; ++e) o[e] = (v[k][e] - mu) * rs * g[e] + bt[e];
+        VecW<T>::store(Y + r * (long)a.C + ch * VW, o);
+      }
+    }
+    if (lane == 0) { a.mean[r] = mu; a.rstd[r] = rs; }
   }
 }
 
@@ -203,7 +180,7 @@ struct LnBwdArgs {
   long rows_per_sample;
 };
 
-template <typename T, int MODE, int TPR, int KMAX, int NR>
+template <typename T, int MODE, int TPR, int KMAX>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
   constexpr int VW = VecW<T>::W;  // elements per 16-B chunk
   const int lane = threadIdx.x % TPR;
@@ -219,82 +196,62 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
     for (int e = 0; e < VW; ++e) { accg[k][e] = 0.f; accb[k][e] = 0.f; }
   LnArgs fa;
   fa.C = a.C; fa.H = a.H; fa.W = a.W; fa.Cin = a.Cin;
-  const long step = (long)gridDim.x * GPB;
-  constexpr bool HAS_RES = MODE == IN_ADD || MODE == IN_PLAIN;
-  for (long r0 = (long)blockIdx.x * GPB + grp; r0 < a.rows; r0 += step * NR) {
-    // x, dy and the residual gradient of all NR rows in flight before any row's reductions
-    float xv[NR][KMAX][VW], dv[NR][KMAX][VW];
-    float dr[NR][KMAX][VW];
-    float mu[NR], rs[NR];
+  for (long r = (long)blockIdx.x * GPB + grp; r < a.rows; r += (long)gridDim.x * GPB) {
+    const float mu = a.mean[r], rs = a.rstd[r];
+    float xh[KMAX][VW], g[KMAX][VW];
+    // the residual gradient is loaded with x and dy: one memory round trip per row, not two
+    float dr[KMAX][VW];
+    constexpr bool HAS_RES = MODE == IN_ADD || MODE == IN_PLAIN;
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const long r = r0 + j * step;
-      if (r >= a.rows) continue;  // group-uniform
-      mu[j] = a.mean[r];
-      rs[j] = a.rstd[r];
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        float xv[VW], dv[VW], gg[VW];
+        const long off = src_off<MODE>(fa, r, ch * VW);
+        VecW<T>::load(X + off, xv);
+        VecW<T>::load(DY + r * (long)a.C + ch * VW, dv);
+        if constexpr (HAS_RES) {
+          if (a.dres) VecW<T>::load(reinterpret_cast<const T*>(a.dres) + off, dr[k]);
+        }
+        load_f32<VW>(a.gamma + ch * VW, gg);
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        const int ch = lane + k * TPR;
-        if (ch < nchunk) {
-          const long off = src_off<MODE>(fa, r, ch * VW);
-          VecW<T>::load(X + off, xv[j][k]);
-          VecW<T>::load(DY + r * (long)a.C + ch * VW, dv[j][k]);
-          if constexpr (HAS_RES) {
-            if (a.dres) VecW<T>::load(reinterpret_cast<const T*>(a.dres) + off, dr[j][k]);
-          }
+        for (int e = 0; e < VW; ++e) {
+          xh[k][e] = (xv[e] - mu) * rs;
+          g[k][e] = dv[e] * gg[e];
+          s1 += g[k][e];
+          s2 += g[k][e] * xh[k][e];
+          accg[k][e] += dv[e] * xh[k][e];
+          accb[k][e] += dv[e];
         }
       }
     }
+    s1 = group_sum<TPR>(s1) / a.C;
+    s2 = group_sum<TPR>(s2) / a.C;
+    float sc = 1.f;
+    if constexpr (MODE == IN_ADD) {
+      if (a.bscale) sc = a.bscale[r / a.rows_per_sample];
+    }
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const long r = r0 + j * step;
-      if (r >= a.rows) continue;
-      float xh[KMAX][VW], g[KMAX][VW];
-      float s1 = 0.f, s2 = 0.f;
+    for (int k = 0; k < KMAX; ++k) {
+      const int ch = lane + k * TPR;
+      if (ch < nchunk) {
+        float o[VW];
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        const int ch = lane + k * TPR;
-        if (ch < nchunk) {
-          float gg[VW];
-          load_f32<VW>(a.gamma + ch * VW, gg);
+        for (int e = 0; e < VW; ++e) o[e] = rs * (g[k][e] - s1 - xh[k][e] * s2);
+        const long off = src_off<MODE>(fa, r, ch * VW);
+        if constexpr (HAS_RES) {
+          if (a.dres) {
 #pragma unroll
-          for (int e = 0; e < VW; ++e) {
-            xh[k][e] = (xv[j][k][e] - mu[j]) * rs[j];
-            g[k][e] = dv[j][k][e] * gg[e];
-            s1 += g[k][e];
-            s2 += g[k][e] * xh[k][e];
-            accg[k][e] += dv[j][k][e] * xh[k][e];
-            accb[k][e] += dv[j][k][e];
+            for (int e = 0; e < VW; ++e) o[e] += dr[k][e];
           }
         }
-      }
-      s1 = group_sum<TPR>(s1) / a.C;
-      s2 = group_sum<TPR>(s2) / a.C;
-      float sc = 1.f;
-      if constexpr (MODE == IN_ADD) {
-        if (a.bscale) sc = a.bscale[r / a.rows_per_sample];
-      }
+        VecW<T>::store(reinterpret_cast<T*>(a.dx) + off, o);
+        if constexpr (MODE == IN_ADD) {
+          if (a.db) {
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        const int ch = lane + k * TPR;
-        if (ch < nchunk) {
-          float o[VW];
-#pragma unroll
-          for (int e = 0; e < VW; ++e) o[e] = rs[j] * (g[k][e] - s1 - xh[k][e] * s2);
-          const long off = src_off<MODE>(fa, r, ch * VW);
-          if constexpr (HAS_RES) {
-            if (a.dres) {
-#pragma unroll
-              for (int e = 0; e < VW; ++e) o[e] += dr[j][k][e];
-            }
-          }
-          VecW<T>::store(reinterpret_cast<T*>(a.dx) + off, o);
-          if constexpr (MODE == IN_ADD) {
-            if (a.db) {
-#pragma unroll
-              for (int e = 0; e < VW; ++e) o[e] *= sc;
-              VecW<T>::store(reinterpret_cast<T*>(a.db) + off, o);
-            }
+            for (int e = 0; e < VW; ++e) o[e] *= sc;
+            VecW<T>::store(reinterpret_cast<T*>(a.db) + off, o);
           }
         }
       }
@@ -351,20 +308,15 @@ int launch_fwd(const LnArgs& a, hipStream_t st, int max_blocks) {
   // and the same up to C <= 512 on 32 / 64 lanes: +0.25 % more (3 of 3 pairs).  A/B switch
   // MSU_LN_WIDE: 0 = 4-lane rows, 1 = one chunk per lane up to C = 128 only)
   static const int wide = getenv("MSU_LN_WIDE") ? atoi(getenv("MSU_LN_WIDE")) : 2;
-  // rows in flight per lane group for the one-chunk-per-lane kernels (A/B switch MSU_LN_NR=1)
-  static const int nr = getenv("MSU_LN_NR") ? atoi(getenv("MSU_LN_NR")) : 2;
-  if (wide && nchunk <= 16)
-    return nr >= 2 ? go(ln_fwd_kernel<T, MODE, 16, 1, 2>, 8) : go(ln_fwd_kernel<T, MODE, 16, 1, 1>, 16);
-  if (wide >= 2 && nchunk <= 32)
-    return nr >= 2 ? go(ln_fwd_kernel<T, MODE, 32, 1, 2>, 16) : go(ln_fwd_kernel<T, MODE, 32, 1, 1>, 32);
-  if (wide >= 2 && nchunk <= 64)
-    return nr >= 2 ? go(ln_fwd_kernel<T, MODE, 64, 1, 2>, 32) : go(ln_fwd_kernel<T, MODE, 64, 1, 1>, 64);
-  if (nchunk <= 4 * 4) return go(ln_fwd_kernel<T, MODE, 4, 4, 1>, 4);
-  if (nchunk <= 8 * 4) return go(ln_fwd_kernel<T, MODE, 8, 4, 1>, 8);
-  if (nchunk <= 16 * 4) return go(ln_fwd_kernel<T, MODE, 16, 4, 1>, 16);
-  if (nchunk <= 32 * 4) return go(ln_fwd_kernel<T, MODE, 32, 4, 1>, 32);
-  if (nchunk <= 64 * 4) return go(ln_fwd_kernel<T, MODE, 64, 4, 1>, 64);
-  if (nchunk <= 64 * 8) return go(ln_fwd_kernel<T, MODE, 64, 8, 1>, 64);
+  if (wide && nchunk <= 16) return go(ln_fwd_kernel<T, MODE, 16, 1>, 16);
+  if (wide >= 2 && nchunk <= 32) return go(ln_fwd_kernel<T, MODE, 32, 1>, 32);
+  if (wide >= 2 && nchunk <= 64) return go(ln_fwd_kernel<T, MODE, 64, 1>, 64);
+  if (nchunk <= 4 * 4) return go(ln_fwd_kernel<T, MODE, 4, 4>, 4);
+  if (nchunk <= 8 * 4) return go(ln_fwd_kernel<T, MODE, 8, 4>, 8);
+  if (nchunk <= 16 * 4) return go(ln_fwd_kernel<T, MODE, 16, 4>, 16);
+  if (nchunk <= 32 * 4) return go(ln_fwd_kernel<T, MODE, 32, 4>, 32);
+  if (nchunk <= 64 * 4) return go(ln_fwd_kernel<T, MODE, 64, 4>, 64);
+  if (nchunk <= 64 * 8) return go(ln_fwd_kernel<T, MODE, 64, 8>, 64);
   return -2;
 }
 
@@ -376,19 +328,16 @@ int launch_bwd(const LnBwdArgs& a, hipStream_t st, int nblocks) {
     return MSU_CHECK_LAUNCH();
   };
   static const int wide = getenv("MSU_LN_WIDE") ? atoi(getenv("MSU_LN_WIDE")) : 2;  // see launch_fwd
-  static const int nr = getenv("MSU_LN_NR") ? atoi(getenv("MSU_LN_NR")) : 2;
-  if (wide && nchunk <= 16) return nr >= 2 ? go(ln_bwd_kernel<T, MODE, 16, 1, 2>) : go(ln_bwd_kernel<T, MODE, 16, 1, 1>);
-  if (wide >= 2 && nchunk <= 32)
-    return nr >= 2 ? go(ln_bwd_kernel<T, MODE, 32, 1, 2>) : go(ln_bwd_kernel<T, MODE, 32, 1, 1>);
-  if (wide >= 2 && nchunk <= 64)
-    return nr >= 2 ? go(ln_bwd_kernel<T, MODE, 64, 1, 2>) : go(ln_bwd_kernel<T, MODE, 64, 1, 1>);
-  if (nchunk <= 4 * 3) return go(ln_bwd_kernel<T, MODE, 4, 3, 1>);  // C = 96 bf16: no idle slot
-  if (nchunk <= 4 * 4) return go(ln_bwd_kernel<T, MODE, 4, 4, 1>);
-  if (nchunk <= 8 * 4) return go(ln_bwd_kernel<T, MODE, 8, 4, 1>);
-  if (nchunk <= 16 * 4) return go(ln_bwd_kernel<T, MODE, 16, 4, 1>);
-  if (nchunk <= 32 * 4) return go(ln_bwd_kernel<T, MODE, 32, 4, 1>);
-  if (nchunk <= 64 * 4) return go(ln_bwd_kernel<T, MODE, 64, 4, 1>);
-  if (nchunk <= 64 * 8) return go(ln_bwd_kernel<T, MODE, 64, 8, 1>);
+  if (wide && nchunk <= 16) return go(ln_bwd_kernel<T, MODE, 16, 1>);
+  if (wide >= 2 && nchunk <= 32) return go(ln_bwd_kernel<T, MODE, 32, 1>);
+  if (wide >= 2 && nchunk <= 64) return go(ln_bwd_kernel<T, MODE, 64, 1>);
+  if (nchunk <= 4 * 3) return go(ln_bwd_kernel<T, MODE, 4, 3>);  // C = 96 bf16: no idle slot
+  if (nchunk <= 4 * 4) return go(ln_bwd_kernel<T, MODE, 4, 4>);
+  if (nchunk <= 8 * 4) return go(ln_bwd_kernel<T, MODE, 8, 4>);
+  if (nchunk <= 16 * 4) return go(ln_bwd_kernel<T, MODE, 16, 4>);
+  if (nchunk <= 32 * 4) return go(ln_bwd_kernel<T, MODE, 32, 4>);
+  if (nchunk <= 64 * 4) return go(ln_bwd_kernel<T, MODE, 64, 4>);
+  if (nchunk <= 64 * 8) return go(ln_bwd_kernel<T, MODE, 64, 8>);
   return -2;
 }
 

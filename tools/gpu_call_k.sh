@@ -21,5 +21,7 @@ run wgrad1_wk1 180 env KB_STAGE=1 MSU_WGRAD_WK=1 python -u $R/tools/kbench.py wg
 run wgrad1_wk0 180 env KB_STAGE=1 MSU_WGRAD_WK=0 python -u $R/tools/kbench.py wgrad
 run conv_hs0 240 env MSU_CONV_HALO=0 python -u $R/tools/kbench.py conv
 run conv_hs1 240 env MSU_CONV_HALO=1 python -u $R/tools/kbench.py conv
+[ -f $R/tools/exp/libmsunet_noslp_conv.so ] && run conv_noslp 240 env MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_noslp_conv.so python -u $R/tools/kbench.py conv
 run attn 240 python -u $R/tools/kbench.py attn
+[ -f $R/tools/exp/libmsunet_noslp_attn.so ] && run attn_noslp 240 env MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_noslp_attn.so python -u $R/tools/kbench.py attn
 echo done
