@@ -273,9 +273,17 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
     static_for([&](auto CI) {
       constexpr int c = decltype(CI)::value;
       const bf16_t* rb = rowbase(L.tok[buf][(lane >> 2) + 16 * c]);
-      kr[buf][c] = *reinterpret_cast<const u32x4*>(rb + ck);
-      qr[buf][c] = *reinterpret_cast<const u32x4*>(rb + cq);
-      vr[buf][c] = *reinterpret_cast<const u32x4*>(rb + cv);
+      if constexpr ((MSU_EXP & 16) != 0) {  // ablation: no q / k / v loads (compute-side time)
+        const uint32_t f = 0x3c003c00u + (uint32_t)(lane & 7) + (uint32_t)c;
+        kr[buf][c] = u32x4{f, f + 1, f + 2, f + 3};
+        qr[buf][c] = u32x4{f + 4, f, f + 1, f + 2};
+        vr[buf][c] = u32x4{f + 2, f + 3, f, f + 4};
+        (void)rb;
+      } else {
+        kr[buf][c] = *reinterpret_cast<const u32x4*>(rb + ck);
+        qr[buf][c] = *reinterpret_cast<const u32x4*>(rb + cq);
+        vr[buf][c] = *reinterpret_cast<const u32x4*>(rb + cv);
+      }
     }, std::make_integer_sequence<int, 4>{});
   };
 
@@ -294,7 +302,10 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
     // dropout keep bits (bit jt*16 + r of kmasks[it], the backward's layout), drawn while
     // the fewest registers are live: this window's rows are in LDS, the next one's not issued
     uint32_t kmasks[2] = {~0u, ~0u};
-    if constexpr (DROP) {
+    if constexpr (DROP && (MSU_EXP & 32) != 0) {  // ablation: no mask stream (fixed pattern)
+      kmasks[0] = 0xfff7fffeu ^ (uint32_t)lane;
+      kmasks[1] = 0xffeffffdu ^ (uint32_t)win;
+    } else if constexpr (DROP) {
 #pragma unroll
       for (int it = 0; it < 2; ++it)
         kmasks[it] = drop_bits<false>(drop_seed32(seed), (uint32_t)win * g.nh + h, it * 32 + (lane & 31), hh,
@@ -369,7 +380,7 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      if (otok[c] >= 0)
+      if (otok[c] >= 0 && (!(MSU_EXP & 64) || scale == 1.2345e-30f))  // ablation 64: no output stores
         *reinterpret_cast<u32x4*>(out + (size_t)((unsigned)otok[c] * (unsigned)g.C) + h * HD + 8 * (lane & 3)) = ov[c];
     if (DROP && keep_out) {
       // keep bits for the backward: [item][it][lane] words, two 256-B stores per wave.  Issued
