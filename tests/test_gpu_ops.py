@@ -387,7 +387,7 @@ def test_refine_conv_act(B, H, W, C, d2s, dtype):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_refine_conv_act_fwd_matches_fp32(B, H, W, d2s, dtype):
     """The 16-bit C = 96 forward as the model runs it (activation precomputed by the producer:
-    the 16-row x 32-pixel persistent kernel, conv3x3_v3_kernel) against fp32 conv2d of the same
+    the 16-row x 32-pixel persistent kernel, conv3x3_v4_kernel) against fp32 conv2d of the same
     16-bit activation -- z and the dual output GELU(z); tiles cut by the image edge included."""
     ops = _ops()
     C = 96

@@ -20,7 +20,7 @@ for mode in fwd bwd; do
   run ${mode}_sq3 "$S3" $a
   timeout -k 10 60 rocprofv3 --kernel-trace --stats -d $O -o ${mode}_kt --output-format csv -- python3 $R/tools/conv_one.py $a > $O/${mode}_kt.log 2>&1 || { tail -5 $O/${mode}_kt.log; exit 1; }
 done
-for mk in fwd:conv3x3_v3 bwd:conv3x3_v3 bwd:conv3x3_wgrad_v2; do
+for mk in fwd:conv3x3_v${CONV_V:-4} bwd:conv3x3_v${CONV_V:-4} bwd:conv3x3_wgrad_v2; do
   m=${mk%%:*}; k=${mk#*:}
   echo "== $m $k"
   for f in $O/${m}_sq?_counter_collection.csv; do python3 $R/tools/pmc_sum.py $k $f; done
