@@ -35,6 +35,7 @@ struct ConvGeom {
   int PS;          // LDS pixel stride (elements) of the input image
   int PSW;         // LDS row stride of the weight tile (fwd/dgrad)
   int PSD;         // LDS pixel stride of the dY tile (wgrad)
+  int prio;        // v3: waves 4-7 (the second wave of each SIMD) at s_setprio 1 (A/B MSU_CONV_PRIO)
 };
 
 // element offset of channel 0 of pixel (b, y, x) of the logical [B,H,W,C] image
@@ -643,6 +644,10 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
 
   int tile = blockIdx.x;
   if (tile >= ntiles) return;
+  // the second-dispatched wave of each SIMD (waves w and w + 4 share one) loses every issue
+  // arbitration by age; static priority lets it keep pace, so fewer waves idle at the per-tap
+  // barrier (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (g.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   load_halo(tile, IC<0>{}, IC<NHC>{});
   store_halo();
   dma_w(0, 0);
@@ -722,7 +727,7 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
       // X fragments double buffered (k step ks + 1 read before the MFMAs of ks); each weight
       // fragment is read one co tile ahead of its two MFMAs (registers: the halo prefetch
       // holds 60 VGPRs across the taps)
-      bf16x8 xa[2][MT], wf[3];
+      bf16x8 xa[2][MT], wf[2];
       auto read_x = [&](auto KSI, int set) __attribute__((always_inline)) {
         constexpr int ks = decltype(KSI)::value;
         constexpr int kb = 32 * (ks >> 1);  // elements: 4 chunks per even / odd pair
@@ -737,19 +742,18 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
       };
       read_x(IC<0>{}, 0);
       wf[0] = read_w(IC<0>{}, 0);
-      wf[1] = read_w(IC<0>{}, 1);
       static_for([&](auto KSI) {
         constexpr int ks = decltype(KSI)::value;
         constexpr int cur = ks & 1;
         if constexpr (ks + 1 < 6) read_x(IC<ks + 1>{}, cur ^ 1);
         static_for([&](auto NI) {
           constexpr int n = decltype(NI)::value;
-          // weight fragment j = 3 ks + n sits in wf[n]; fragment j + 2 is read now, two MFMA
-          // groups ahead of its use (one group of MT MFMAs did not cover the LDS latency)
-          constexpr int jn = 3 * ks + n + 2;
-          if constexpr (jn < 18) wf[jn % 3] = read_w(IC<jn / 3>{}, jn % 3);
+          constexpr int j = 3 * ks + n;  // weight fragment sequence number: register set j & 1
+          // (reading it two groups ahead in a ring of three measured no faster and spills the dgrad)
+          if constexpr (n < 2) wf[(j + 1) & 1] = read_w(IC<ks>{}, n + 1);
+          else if constexpr (ks + 1 < 6) wf[(j + 1) & 1] = read_w(IC<ks + 1>{}, 0);
 #pragma unroll
-          for (int m = 0; m < MT; ++m) acc[m][n] = Fmt16<T>::mma32(wf[n], xa[cur][m], acc[m][n]);
+          for (int m = 0; m < MT; ++m) acc[m][n] = Fmt16<T>::mma32(wf[j & 1], xa[cur][m], acc[m][n]);
         }, std::make_integer_sequence<int, 3>{});
         __builtin_amdgcn_sched_barrier(0);
       }, std::make_integer_sequence<int, 6>{});
@@ -1402,6 +1406,7 @@ ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int elem_bytes) {
   g.PS = g.CinP + pad;
   g.PSW = g.CinP + pad;
   g.PSD = Cout + pad;
+  g.prio = 0;
   return g;
 }
 
@@ -1491,15 +1496,19 @@ int launch_v3s(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float
   if (ntiles == 0) return 0;
   if ((long)g.B * g.H * g.W * 96 >= (1L << 31)) return -2;
   const int grid = (int)(ntiles < num_cus() ? ntiles : num_cus());
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, X, Wt, bias, S, Y, Y2, g, (int)ntiles);
+  static const int prio = getenv("MSU_CONV_PRIO") ? atoi(getenv("MSU_CONV_PRIO")) : 0;
+  ConvGeom gp = g;
+  gp.prio = prio;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, X, Wt, bias, S, Y, Y2, gp, (int)ntiles);
   return MSU_CHECK_LAUNCH();
 }
 
-// v4 (one wave per SIMD, 4 rows per wave): A/B switch MSU_CONV_V=3 keeps v3
+// v4 (one wave per SIMD, 4 rows per wave): opt-in A/B switch MSU_CONV_V=4 (measured 7-10 %
+// slower than v3 on every launch: DESIGN.md section 7, round 3)
 inline int conv_v4_enabled() {
   static const bool on = [] {
     const char* e = getenv("MSU_CONV_V");
-    return !(e && (e[0] == '2' || e[0] == '3'));
+    return e && e[0] == '4';
   }();
   return on;
 }

@@ -580,6 +580,15 @@ class Trainer:
         # deterministic again with DEBUG_HIP_FORCE_GRAPH_QUEUES=1).  Replay is only chosen
         # when the step is launch-bound, where the side-stream overlap matters least.
         # MSU_GRAPH_SIDE=1 keeps the side stream (A/B switch).
+        if self.reducer is not None and self.reducer.pg is not None and \
+                os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE", "1") != "0":
+            # ProcessGroupNCCL's event cache can hand an event recorded inside this capture to a
+            # work its watchdog thread still queries; HIP refuses that query and the watchdog
+            # terminates the process (tests/test_gpu_rccl.py).  Set it to 0 before creating the
+            # process group when the step is captured over RCCL.
+            import warnings
+            warnings.warn("capturing a step with collectives while TORCH_NCCL_CUDA_EVENT_CACHE is on: "
+                          "set TORCH_NCCL_CUDA_EVENT_CACHE=0 before init_process_group")
         side_prev = ops._side_enabled
         if os.environ.get("MSU_GRAPH_SIDE", "0") != "1":
             ops._side_enabled = False

@@ -13,9 +13,10 @@ the code the 8-GPU scaling run executes; with one rank the sum is the identity, 
 * the f16 gradient wire (BASELINE config 5) with its dynamic scale stays within f16 rounding
   of the f32 step.
 
-The scenarios run in one spawned child process (``rccl_runs``): in the full GPU suite the
-determinism capture once aborted the whole pytest process from a non-Python thread while
-the test process carried the earlier tests' graphs and streams (r03j); run alone it passed.
+The scenarios run in one spawned child process (``rccl_runs``) with
+``TORCH_NCCL_CUDA_EVENT_CACHE=0``: with the event cache, a later capture in the same process
+could hand the watchdog thread an event recorded in the capture, and its query terminated the
+process (r03j: the whole pytest run; r03p: the child, log attached to the failure).
 """
 import os
 import socket
@@ -63,7 +64,11 @@ def _run(pg, graph, reduce, wire=None, steps=5, bucket_mb=1.0, lr=1e-3):
     info = {"captured": tr._graph is not None, "skipped": tr.skipped_steps(),
             "buckets": len(tr.reducer.buckets) if tr.reducer is not None else 0,
             "comm": tr.reducer.comm is not None if tr.reducer is not None else None}
+    _KEEP.append(tr)  # see _child
     return losses, [torch.cat([g.data, g.exp_avg, g.exp_avg_sq]) for g in tr.groups], info
+
+
+_KEEP = []
 
 
 def _scenarios():
@@ -84,8 +89,19 @@ def _child(rank, port, outdir):
     streams, allocator pools -- stays out of these captures; an abort here fails these tests
     instead of ending the whole suite)."""
     import torch.distributed as dist
+    # the child's stdout / stderr (RCCL / HIP / c10d messages included) go to a log the fixture
+    # attaches to a failure
+    fd = os.open(os.path.join(outdir, "child.log"), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    os.dup2(fd, 1)
+    os.dup2(fd, 2)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    # ProcessGroupNCCL's event cache hands a retired work's HIP events to new works: an event
+    # recorded inside a capture could then be queried by the watchdog thread for an eager work
+    # ("operation not permitted on an event last recorded in a capturing stream", which
+    # terminates the process -- seen at the second capture of a process, r03o / r03p).
+    # Fresh events per work, as the Trainer documents for captured steps over RCCL.
+    os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] = "0"
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     assert dist.get_backend() == "nccl"
@@ -96,10 +112,11 @@ def _child(rank, port, outdir):
         losses, states, info = _run(pg if dp else None, **kw)
         torch.save({"losses": losses, "states": [t.cpu() for t in states], "info": info},
                    os.path.join(outdir, f"{name}.pt"))
-        import gc
-        gc.collect()
         torch.cuda.synchronize()
+    # every Trainer (and its captured graph) stays alive until the group is destroyed (_KEEP)
+    torch.cuda.synchronize()
     dist.destroy_process_group()
+    _KEEP.clear()
 
 
 @pytest.fixture(scope="module")
@@ -119,11 +136,14 @@ def rccl_runs(tmp_path_factory):
         if os.path.exists(f):
             res[name] = torch.load(f, weights_only=True)
     res["_exitcode"] = p.exitcode
+    log = os.path.join(out, "child.log")
+    res["_log"] = open(log).read()[-3000:] if os.path.exists(log) else ""
     return res
 
 
 def _get(runs, name):
-    assert name in runs, f"RCCL child process ended (exit code {runs['_exitcode']}) before scenario {name}"
+    assert name in runs, (f"RCCL child process ended (exit code {runs['_exitcode']}) before scenario {name}; "
+                          f"its log ends:\n{runs['_log']}")
     r = runs[name]
     return r["losses"], r["states"], r["info"]
 
