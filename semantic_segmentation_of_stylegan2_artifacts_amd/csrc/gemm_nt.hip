@@ -42,6 +42,7 @@ struct NtArgs {
   const bf16_t* H;     // [M][N] (GELU_GRAD: pre-activation)
   int M, N, K, K1;
   int tiles_m, tiles_n;
+  int prio;            // waves WM.. (the second wave of each SIMD) at s_setprio 1 (A/B MSU_NT_PRIO)
 };
 
 // A ROWS x BK operand tile (K-contiguous rows) staged by NTHR threads.  A 256-B LDS bank row
@@ -144,6 +145,7 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   const int ntiles = a.tiles_m * a.tiles_n;
   const int nk = a.K / BK;  // K % 64 == 0 (nt_shape_ok)
   const int mine = L < ntiles ? (ntiles - 1 - L) / G + 1 : 0;
+  if (WM == 4 && a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int nsteps = mine * nk;
 
   // K step s of this workgroup's sequence -> LDS stage `st`
@@ -171,14 +173,20 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   int kk = 0, ti = 0;  // K step within the tile, tile ordinal (within this workgroup)
   int cst = 0;         // LDS stage of step s
   int epi_age = 99;    // steps since the last epilogue (its stores follow that step's DMA issue)
+  bool epi_full = true;  // that epilogue issued all E stores of this wave (no ragged M / N edge)
   for (int s = 0; s < nsteps; ++s) {
     // step s's DMA landed; younger DMAs (step s + 1) and epilogue stores issued after step s's
-    // DMA may stay in flight (NST = 3, tiles of >= 3 K steps); else everything retires
+    // DMA may stay in flight (NST = 3, tiles of >= 3 K steps); else everything retires.
+    // The counts must never exceed the ops really issued after step s's DMA: a wave whose last
+    // epilogue sat on a ragged edge skipped some stores (all of them when its 64 columns lie
+    // past N), so it does not count them -- counting them let that wave pass the barrier with
+    // its share of step s's DMA still in flight, and the other waves read stale LDS (found as
+    // run-to-run differences of the eager step with the side stream on, round 3)
     if constexpr (NST == 2) {
       wait_vmcnt<0>();
     } else {
       const bool younger = s + 1 < nsteps;
-      const bool stores = epi_age <= 1 && nk >= 3;
+      const bool stores = epi_age <= 1 && nk >= 3 && epi_full;
       if (nk < 3) wait_vmcnt<0>();
       else if (younger && stores) wait_vmcnt<D + E>();
       else if (younger) wait_vmcnt<D>();
@@ -250,6 +258,7 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     kk = 0;
     ++ti;
     epi_age = 0;
+    epi_full = m0 + 64 * wm + 64 <= a.M && n0 + 64 * wn + 64 <= a.N;
     // the epilogue operands (and every older DMA) have landed; the DMA just issued may stay
     // in flight (NST = 3).  One wait, not one per exec-masked store branch.
     if (NST == 3 && more) wait_vmcnt<D>();
@@ -369,6 +378,8 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
   a.M = (int)M;
   a.N = N;
   a.K = K;
+  static const int prio = getenv("MSU_NT_PRIO") ? atoi(getenv("MSU_NT_PRIO")) : 0;
+  a.prio = prio;
   const int wm = nt_wm(M, N);
   a.tiles_n = (N + BN - 1) / BN;
   a.tiles_m = (int)((M + 64 * wm - 1) / (64 * wm));

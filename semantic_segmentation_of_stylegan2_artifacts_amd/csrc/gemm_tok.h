@@ -210,14 +210,19 @@ __global__ void __launch_bounds__(64 * NW) tokgemm_kernel(TokArgs a) {
   for (int s = 0; s < NST - 1; ++s) issue();
   long st = 0;
   int c_slot = 0, last_slot = 0;
+  bool ragged = false;  // a tile that ended within the last two stages stored fewer than E rows
   for (long ti = 0; ti < my_tiles; ++ti) {
     const long mrow = (ws + ti * (long)S) * RT + fr;
     for (int kc = 0; kc < nkc; ++kc, ++st) {
       // ---- wait for stage st: VM ops retire in issue order; the ops younger than DMA(st)
-      // are the later DMAs plus the stores / H loads of tiles that ended in between
+      // are the later DMAs plus the stores / H loads of tiles that ended in between.  A tile
+      // cut by M skips whole store instructions, so after one the counts drop to zero (a count
+      // above the ops really issued would let the wave read a stage whose DMA is in flight)
       const bool p1 = st >= 1 && kc == 0;                  // stage st-1 ended a tile
       const bool p2 = st >= 2 && (nkc == 1 || kc == 1);    // stage st-2 ended a tile
-      if constexpr (NST == 2) {
+      if (ragged) {
+        wait_vmcnt<0>();
+      } else if constexpr (NST == 2) {
         if (p1) wait_vmcnt<(E > 63 ? 63 : E)>();
         else wait_vmcnt<0>();
       } else {
@@ -263,6 +268,7 @@ __global__ void __launch_bounds__(64 * NW) tokgemm_kernel(TokArgs a) {
       }
     }
 
+    ragged = mrow - fr + RT > a.M;  // (wave-uniform) this tile's stores are cut by M
     // ---- epilogue: lane owns token row mrow; pair p covers columns 16p .. 16p+15
     if constexpr (GGRAD) {
       // the H loads are older than the one DMA issued after them

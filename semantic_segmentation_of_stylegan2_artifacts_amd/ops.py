@@ -150,6 +150,9 @@ _SIDE_PRIORITY = int(os.environ.get("MSU_SIDE_PRIORITY", "1"))  # A/B switch (0:
 _side_streams = {}
 # per-use switches of the side stream (tools/graph_side_probe.py bisects the forked capture)
 _side_wgrad = True      # Linear weight gradients
+# timing ablation only (results WRONG by design): MSU_EXP_SKIP_WGRAD=1 launches no Linear
+# weight gradient, to measure what the side stream's kernels cost the main stream
+_EXP_SKIP_WGRAD = os.environ.get("MSU_EXP_SKIP_WGRAD", "0") == "1"
 _side_attn_tail = True  # attention relative-table / qkv-bias reductions
 
 
@@ -672,6 +675,9 @@ def _wgrad(dy, x, weight, bias, M, N, K):
     """Linear weight/bias gradients on msu_linear_wgrad; (None, None) when accumulated
     straight into the trainer's flat .grad views."""
     L = _lib.lib()
+    if _EXP_SKIP_WGRAD and _direct(weight) and (bias is None or _direct(bias)):
+        _notify(weight, bias)  # ablation: no weight-gradient work at all (wrong by design)
+        return None, None
     if _direct(weight) and (bias is None or _direct(bias)):
         if _side_enabled and _side_wgrad:
             main = torch.cuda.current_stream(x.device)
