@@ -140,6 +140,18 @@ long msu_wgrad_workspace(long M, int N, int K);
 int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float* db, float* workspace,
                      long M, int N, int K, int accumulate, void* stream);
 
+/* ---------------------------------------------------------------- Linear backward in one pass
+ * Stage-0 Linears of the Swin block (qkv, proj, mlp.0, mlp.3; model_parts.py:143-151, called at
+ * :170 / :538; (K, N) = (in, out) features in {(96, 288), (96, 96), (96, 384), (384, 96)}):
+ * dX = dY . W (times GELU'(H) when H != null: mlp.3's input gradient through mlp.1, (384, 96)
+ * only), dW[N][K] (+)= dY^T X and db[N] (+)= column sums of dY in ONE read of dY (replaces the
+ * input-gradient GEMM plus msu_linear_wgrad).  Wt = W^T [K][N] 16-bit; dW / db f32, added to
+ * when accumulate != 0 (db may be null); workspace f32 elements from msu_linear_bwd_workspace. */
+int msu_linear_bwd_supported(long M, int K, int N);
+long msu_linear_bwd_workspace(long M, int K, int N);
+int msu_linear_bwd(int dtype, const void* dY, const void* X, const void* Wt, const void* H, void* dX, float* dW,
+                   float* db, float* workspace, long M, int K, int N, int accumulate, void* stream);
+
 /* ---------------------------------------------------------------- Linear forward / input gradient
  * Token GEMM (dtype 1 bf16 / 2 f16 in and out, f32 accumulate) for the same Linears as
  * msu_linear_wgrad:

@@ -55,6 +55,9 @@ SIGNATURES = {
     "msu_wgrad_splits": (I, [L, I, I]),
     "msu_wgrad_workspace": (L, [L, I, I]),
     "msu_linear_wgrad": (I, [I, P, P, P, P, P, L, I, I, I, P]),
+    "msu_linear_bwd_supported": (I, [L, I, I]),
+    "msu_linear_bwd_workspace": (L, [L, I, I]),
+    "msu_linear_bwd": (I, [I, P, P, P, P, P, P, P, P, L, I, I, I, P]),
     "msu_tok_gemm_supported": (I, [L, I, I]),
     "msu_tok_gemm_supported_epi": (I, [L, I, I, I]),
     "msu_tok_gemm": (I, [I, P, P, I, P, P, P, P, P, L, I, I, I, P]),

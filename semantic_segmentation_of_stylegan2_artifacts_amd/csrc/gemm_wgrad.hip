@@ -378,7 +378,10 @@ inline WavePlan wave_plan(long M, int N, int K) {
     return p;
   }
   const long tiles = (long)(nt / p.wn) * (kt / p.wk);
-  long s = 256 / tiles;  // at most one workgroup per CU (no tail wave), long row ranges
+  // workgroup target: one per CU (no tail wave), long row ranges.  A/B switch
+  // MSU_WGRAD_TARGET_S23: the target for the stage 2-3 shapes (M <= 32768 at the bench)
+  static const long tgt23 = getenv("MSU_WGRAD_TARGET_S23") ? atol(getenv("MSU_WGRAD_TARGET_S23")) : 256;
+  long s = (M <= 32768 ? tgt23 : 256) / tiles;
   const long max_s = (M + 8 * rs - 1) / (8 * rs);  // at least 8 stages per split
   if (s > max_s) s = max_s;
   if (s < 1) s = 1;

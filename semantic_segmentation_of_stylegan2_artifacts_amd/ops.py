@@ -820,6 +820,41 @@ def _linear_setup(ctx, inputs, output):
     ctx.params = (weight, bias)
 
 
+# One-pass Linear backward (csrc/gemm_linbwd.hip) for the stage-0 block Linears: dX, dW and db
+# from one read of dY on the main stream, instead of the input-gradient GEMM plus a side-stream
+# weight gradient that reads dY again.  Opt-in (MSU_LINBWD=1): correct, but alone on the GPU
+# slower than the two kernels together and neutral in the step.
+_LINBWD = os.environ.get("MSU_LINBWD", "0") == "1"
+_LINBWD_MIN_M = 65536
+
+
+def _linbwd(dy, x, weight, bias, M, N, K, h=None):
+    """dX = dy . W (* GELU'(h)) with dW / db accumulated into the trainer's .grad in the same
+    pass; None when the shape, dtype or parameters are not covered (caller: two-kernel path)."""
+    if not _LINBWD or x.dtype not in _LOW or M < _LINBWD_MIN_M:
+        return None
+    if not _direct(weight) or (bias is not None and not _direct(bias)):
+        return None
+    wt = _shadow_t(weight, x.dtype)
+    if wt is None:
+        return None
+    L = _lib.lib()
+    if not L.msu_linear_bwd_supported(M, K, N):
+        return None
+    if bias is not None:
+        # the qkv bias also receives the attention's padded-token share on the side stream
+        # (msu_win_attn_bwd_tail, issued earlier in this backward): add after it
+        ev = getattr(bias, "_msu_side_event", None)
+        if ev is not None:
+            torch.cuda.current_stream(x.device).wait_event(ev)
+    dx = torch.empty(*dy.shape[:-1], K, device=dy.device, dtype=dy.dtype)
+    ws = torch.empty(L.msu_linear_bwd_workspace(M, K, N), device=x.device, dtype=torch.float32)
+    _lib.call("msu_linear_bwd", _dt(x), _p(dy), _p(x.contiguous()), _p(wt), _p(h), _p(dx), _p(weight.grad),
+              _p(None if bias is None else bias.grad), _p(ws), M, K, N, 1, _s(x))
+    _notify(weight, bias)
+    return dx
+
+
 def _linear_backward(ctx, dy):
     (x,) = ctx.saved_tensors
     weight, bias = ctx.params
@@ -827,6 +862,10 @@ def _linear_backward(ctx, dy):
     dy = _as(dy, x.dtype)
     N, K = w.shape
     M = dy.numel() // N
+    if ctx.needs_input_grad[0]:
+        dx = _linbwd(dy.contiguous(), x, weight, bias, M, N, K)
+        if dx is not None:
+            return dx, None, None
     dx = None
     if ctx.needs_input_grad[0]:
         if x.dtype in _LOW and gemm_route(M, K, N) != "lib":
@@ -997,10 +1036,19 @@ def _mlp_backward(ctx, dy, _dh, _dg):
     dy = _as(dy, x.dtype)
     Hd, C = W1.shape
     M = x.numel() // C
-    dw2, db2 = _wgrad(dy, g, w2, b2, M, C, Hd)
-    dh = _gemm_dx(dy, W2, TOK_GELU_GRAD, h=h, param=w2)
-    dw1, db1 = _wgrad(dh, x, w1, b1, M, Hd, C)
-    dx = _gemm_dx(dh, W1, param=w1) if ctx.needs_input_grad[0] else None
+    dy = dy.contiguous()
+    dh = _linbwd(dy, g, w2, b2, M, C, Hd, h=h)  # mlp.3 in one pass (dh through GELU')
+    if dh is None:
+        dw2, db2 = _wgrad(dy, g, w2, b2, M, C, Hd)
+        dh = _gemm_dx(dy, W2, TOK_GELU_GRAD, h=h, param=w2)
+    else:
+        dw2 = db2 = None
+    dx = _linbwd(dh, x, w1, b1, M, Hd, C) if ctx.needs_input_grad[0] else None  # mlp.0 in one pass
+    if dx is None:
+        dw1, db1 = _wgrad(dh, x, w1, b1, M, Hd, C)
+        dx = _gemm_dx(dh, W1, param=w1) if ctx.needs_input_grad[0] else None
+    else:
+        dw1 = db1 = None
     return dx, dw1, db1, dw2, db2
 
 
