@@ -15,16 +15,17 @@
 // One 8-wave workgroup per CU, two waves per SIMD (the weight-gradient accumulators of a
 // workgroup are the whole 32 x 32-tiled K x N product, at most 6 tiles = 96 registers per wave).
 // W^T [K][N] (the trainer's transposed bf16 shadow) sits in LDS for the kernel's life; the token
-// rows of dY and X come through a two-stage LDS image, register-staged two steps ahead (two
-// register sets: ~50 KB per CU in flight, what the HBM latency needs; a first version with one
-// step ahead and one wave per SIMD ran at half the HBM rate).  Per 32-token step:
+// rows of dY and X come through a two-stage LDS image, register-staged three or four steps
+// ahead with loads the compiler does not track (its own waits drained the ring every step) and
+// hand-counted vmcnt waits.  Per 32-token step:
 //   * input gradient: C^T[k][t] = W^T[k][:] . dY[t][:]^T, k-tiles dealt to the waves;
 //   * weight gradient: C[k][n] += X[:, k]^T . dY[:, n] over the step's 32 tokens (two 16-deep
 //     k steps, both operands read token-strided with ds_read_b64_tr_b16), the K/32 x N/32 tiles
 //     dealt so that every wave issues about the same number of MFMAs;
-//   * bias gradient: column sums of the dY image (VALU, N/2 threads).
-// Every LDS row is padded by 8 elements (row stride = 4 mod 8 dwords: the 16 rows of a
-// ds_read_b128 lane group fall on 16 distinct bank groups).
+//   * bias gradient: column sums of the dY image (VALU, rows dealt over all waves).
+// W^T and dY rows are padded by 8 elements (row stride = 4 mod 8 dwords: the 16 rows of a
+// ds_read_b128 lane group fall on 16 distinct bank groups); X rows, read only token-strided,
+// use a stride of 16 or 48 mod 64 dwords (ldx_of).
 #include <utility>
 
 #include "common.h"
@@ -51,6 +52,17 @@ MSU_DEV __attribute__((always_inline)) void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
+// LDS row stride of the X image (elements).  X is only read token-strided (ds_read_b64_tr_b16:
+// 32 lanes = 4 rows x 16 dwords), which is conflict-free when the row stride is 16 or 48
+// dwords mod 64 (K = 96: unpadded; K = 384: + 32 elements).  The dY image is also read
+// row-wise with ds_read_b128 by the input gradient and keeps the 4-mod-8-dword pad.
+template <int K>
+constexpr int ldx_of() {
+  int p = 0;
+  while (((K + p) / 2) % 64 != 16 && ((K + p) / 2) % 64 != 48) p += 8;
+  return K + p;
+}
+
 // register sets of staged token rows (steps of prefetch): as deep as the registers allow
 template <int K, int N, bool GG>
 constexpr int ring_depth() {
@@ -74,6 +86,12 @@ MSU_DEV v4s tr_read(const bf16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_
 MSU_DEV u32x4 gload16(const void* p) {
   u32x4 v;
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+// the same from a wave-uniform base and a per-lane byte offset (no 64-bit address VALU)
+MSU_DEV u32x4 gload16_s(const void* base, unsigned off) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v) : "v"(off), "s"(base) : "memory");
   return v;
 }
 
@@ -148,7 +166,7 @@ __global__ void __launch_bounds__(NTHR, 1)
 linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
               const bf16_t* __restrict__ H, bf16_t* __restrict__ dX, float* __restrict__ part, long M) {
   using P = Plan<K, N>;
-  constexpr int LDW = N + 8, LDY = N + 8, LDX = K + 8;
+  constexpr int LDW = N + 8, LDY = N + 8, LDX = ldx_of<K>();
   constexpr int CY = N / 8, CX = K / 8;              // 16-B chunks per dY / X row
   constexpr int CHUNKS = TM * (CY + CX);
   constexpr int PER = (CHUNKS + NTHR - 1) / NTHR;    // staged chunks per thread and step
@@ -176,25 +194,58 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
   // CHUNKS re-read dY row 0 and are dropped)
   constexpr int D = ring_depth<K, N, GG>();
   u32x4 st[D][PER];
+  // chunk c = tid + NTHR j of a step: dY chunks first, then X chunks, then none.  The kind is
+  // wave-uniform (the boundaries are multiples of 64); the offsets are step-invariant: element
+  // offset from the step's first row in global memory and in the LDS stage
+  int goff[PER], loff[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int c = tid + NTHR * j;
+    goff[j] = 0;
+    loff[j] = 0;
+    if (c < TM * CY) {
+      const int r = c / CY, cc = c - r * CY;
+      goff[j] = r * N + 8 * cc;
+      loff[j] = r * LDY + 8 * cc;
+    } else if (c < CHUNKS) {
+      const int c2 = c - TM * CY;
+      const int r = c2 / CX, cc = c2 - r * CX;
+      goff[j] = r * K + 8 * cc;
+      loff[j] = TM * LDY + r * LDX + 8 * cc;
+    }
+  }
+  auto kind = [&](int j) __attribute__((always_inline)) {  // 0 dY, 1 X, 2 none (wave-uniform)
+    const int cw = wave * 64 + NTHR * j;
+    return cw < TM * CY ? 0 : cw < CHUNKS ? 1 : 2;
+  };
   auto load = [&](long step, auto SET) __attribute__((always_inline)) {
     constexpr int set = decltype(SET)::value;
     const long m0 = (b + step * G) * TM;
-    const int t0 = opaque(tid);
+    if (m0 + TM <= M) {  // whole step: uniform row base + per-lane 32-bit offset
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int c = t0 + NTHR * j;
-      const bf16_t* src = dY;
-      if (c < TM * CY) {
-        const int r = c / CY, cc = c - r * CY;
-        const long m = m0 + r < M ? m0 + r : M - 1;
-        src = dY + m * N + 8 * cc;
-      } else if (c < CHUNKS) {
-        const int c2 = c - TM * CY;
-        const int r = c2 / CX, cc = c2 - r * CX;
-        const long m = m0 + r < M ? m0 + r : M - 1;
-        src = X + m * K + 8 * cc;
+      for (int j = 0; j < PER; ++j) {
+        const int kd = kind(j);
+        const bf16_t* base = kd == 0 ? dY + m0 * N : kd == 1 ? X + m0 * K : dY;
+        st[set][j] = gload16_s(base, 2u * (unsigned)goff[j]);
       }
-      st[set][j] = gload16(src);
+    } else {  // the ragged last step: rows past M re-read row M - 1
+      const int t0 = opaque(tid);
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int c = t0 + NTHR * j;
+        const bf16_t* src = dY;
+        if (c < TM * CY) {
+          const int r = c / CY, cc = c - r * CY;
+          const long m = m0 + r < M ? m0 + r : M - 1;
+          src = dY + m * N + 8 * cc;
+        } else if (c < CHUNKS) {
+          const int c2 = c - TM * CY;
+          const int r = c2 / CX, cc = c2 - r * CX;
+          const long m = m0 + r < M ? m0 + r : M - 1;
+          src = X + m * K + 8 * cc;
+        }
+        st[set][j] = gload16(src);
+      }
     }
   };
   // set SET (rows of step `step`) -> LDS stage step & 1; `younger` = how many sets were loaded
@@ -209,20 +260,19 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
 #pragma unroll
     for (int j = 0; j < PER; ++j) asm volatile("" : "+v"(st[set][j]));
     bf16_t* y = sS + (int)(step & 1) * STAGE;
-    bf16_t* x = y + TM * LDY;
     const long m0 = (b + step * G) * TM;
-    const int t0 = opaque(tid);
+    if (m0 + TM <= M) {
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int c = t0 + NTHR * j;
-      const u32x4 z = {0u, 0u, 0u, 0u};
-      if (c < TM * CY) {
-        const int r = c / CY, cc = c - r * CY;
-        *reinterpret_cast<u32x4*>(y + r * LDY + 8 * cc) = m0 + r < M ? st[set][j] : z;
-      } else if (c < CHUNKS) {
-        const int c2 = c - TM * CY;
-        const int r = c2 / CX, cc = c2 - r * CX;
-        *reinterpret_cast<u32x4*>(x + r * LDX + 8 * cc) = m0 + r < M ? st[set][j] : z;
+      for (int j = 0; j < PER; ++j)
+        if (kind(j) != 2) *reinterpret_cast<u32x4*>(y + loff[j]) = st[set][j];
+    } else {  // rows past M go to LDS as zeros
+      const int t0 = opaque(tid);
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int c = t0 + NTHR * j;
+        const int r = c < TM * CY ? c / CY : (c - TM * CY) / CX;
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        if (kind(j) != 2) *reinterpret_cast<u32x4*>(y + loff[j]) = m0 + r < M ? st[set][j] : z;
       }
     }
   };
@@ -230,7 +280,11 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
   f32x16 accw[WMAX];  // weight-gradient tiles C[k][n] of this wave
 #pragma unroll
   for (int i = 0; i < WMAX; ++i) accw[i] = f32x16{0};
-  float db0 = 0.f, db1 = 0.f;  // bias-gradient column pair tid (tid < N / 2)
+  // bias gradient: thread tid sums column pair bp over the rows bg, bg + RG, ... of each step
+  // (every wave takes a share instead of the N / 2 threads of the input-gradient waves)
+  constexpr int NP = N / 2, RG = NTHR / NP < TM ? NTHR / NP : TM;
+  const int bp = tid % NP, bg = tid / NP;
+  float db0 = 0.f, db1 = 0.f;
 
   static_for<D>([&](auto I) __attribute__((always_inline)) {
     if (decltype(I)::value < nsteps) load(decltype(I)::value, I);
@@ -280,11 +334,10 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // ---- bias gradient: column sums of the dY image
-    if (tid < N / 2) {
-#pragma unroll 8
-      for (int r = 0; r < TM; ++r) {
-        const uint32_t w2 = *reinterpret_cast<const uint32_t*>(y + r * LDY + 2 * tid);
+    // ---- bias gradient: column sums of the dY image, rows dealt over RG thread groups
+    if (bg < RG) {
+      for (int r = bg; r < TM; r += RG) {
+        const uint32_t w2 = *reinterpret_cast<const uint32_t*>(y + r * LDY + 2 * bp);
         db0 += Fmt16<T>::lo(w2);
         db1 += Fmt16<T>::hi(w2);
       }
@@ -366,15 +419,25 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
       }
     }
   }
-  if (tid < N / 2) {
-    pw[N * K + 2 * tid] = db0;
-    pw[N * K + 2 * tid + 1] = db1;
+  // row groups -> one sum per column pair, through the (now idle) LDS stages
+  float2* red = reinterpret_cast<float2*>(sS);
+  if (bg < RG) red[bg * NP + bp] = make_float2(db0, db1);
+  __syncthreads();
+  if (tid < NP) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int g = 0; g < RG; ++g) {
+      const float2 v = red[g * NP + tid];
+      s0 += v.x;
+      s1 += v.y;
+    }
+    pw[N * K + 2 * tid] = s0;
+    pw[N * K + 2 * tid + 1] = s1;
   }
 }
 
 template <int K, int N>
 constexpr size_t linbwd_lds() {
-  return sizeof(bf16_t) * ((size_t)K * (N + 8) + 2 * (size_t)TM * ((N + 8) + (K + 8)));
+  return sizeof(bf16_t) * ((size_t)K * (N + 8) + 2 * (size_t)TM * ((N + 8) + ldx_of<K>()));
 }
 
 int num_cus_lb() {

@@ -822,9 +822,8 @@ def _linear_setup(ctx, inputs, output):
 
 # One-pass Linear backward (csrc/gemm_linbwd.hip) for the stage-0 block Linears: dX, dW and db
 # from one read of dY on the main stream, instead of the input-gradient GEMM plus a side-stream
-# weight gradient that reads dY again.  Opt-in (MSU_LINBWD=1): correct, but alone on the GPU
-# slower than the two kernels together and neutral in the step.
-_LINBWD = os.environ.get("MSU_LINBWD", "0") == "1"
+# weight gradient that reads dY again.  A/B switch MSU_LINBWD=0: the two-kernel path.
+_LINBWD = os.environ.get("MSU_LINBWD", "1") != "0"
 _LINBWD_MIN_M = 65536
 
 

@@ -91,7 +91,7 @@ def _grads(params):
 
 @pytest.mark.parametrize("which", ["linear_qkv", "linear_proj", "mlp"])
 def test_ops_one_pass_backward_equals_two_kernel_path(which):
-    """ops.linear / ops.mlp with trainer-style parameters: the one-pass backward (MSU_LINBWD=1) and the
+    """ops.linear / ops.mlp with trainer-style parameters: the one-pass backward (default) and the
     two-kernel path (input-gradient GEMM + side-stream weight gradient) give the same dX to
     16-bit rounding and the same dW / db to f32 summation order."""
     from semantic_segmentation_of_stylegan2_artifacts_amd import ops
