@@ -15,9 +15,8 @@
 // One 8-wave workgroup per CU, two waves per SIMD (the weight-gradient accumulators of a
 // workgroup are the whole 32 x 32-tiled K x N product, at most 6 tiles = 96 registers per wave).
 // W^T [K][N] (the trainer's transposed bf16 shadow) sits in LDS for the kernel's life; the token
-// rows of dY and X come through a two-stage LDS image, register-staged three or four steps
-// ahead with loads the compiler does not track (its own waits drained the ring every step) and
-// hand-counted vmcnt waits.  Per 32-token step:
+// rows of dY and X come through a two-stage LDS image, register-staged D steps ahead.  Per
+// 32-token step:
 //   * input gradient: C^T[k][t] = W^T[k][:] . dY[t][:]^T, k-tiles dealt to the waves;
 //   * weight gradient: C[k][n] += X[:, k]^T . dY[:, n] over the step's 32 tokens (two 16-deep
 //     k steps, both operands read token-strided with ds_read_b64_tr_b16), the K/32 x N/32 tiles
@@ -30,6 +29,13 @@
 
 #include "common.h"
 #include "reduce.h"
+
+// MSU_EXP: ablation bits for timing experiments only (tools/build_exp.sh); 0 in every real build
+// (1 no dX stores, 2 no input-gradient MFMAs / reads, 4 no weight-gradient MFMAs / reads,
+// 8 no staging loads, 16 no bias sums)
+#ifndef MSU_EXP
+#define MSU_EXP 0
+#endif
 
 namespace {
 
@@ -66,7 +72,7 @@ constexpr int ldx_of() {
 // register sets of staged token rows (steps of prefetch): as deep as the registers allow
 template <int K, int N, bool GG>
 constexpr int ring_depth() {
-  return GG ? 3 : 4;
+  return GG ? 2 : 3;
 }
 
 // opaque copy of a value: keeps the compiler from hoisting per-chunk / per-tile index math out
@@ -78,21 +84,15 @@ MSU_DEV int opaque(int v) {
 
 MSU_DEV v4s tr_read(const bf16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p); }
 
-// 16-B global load the compiler does not track.  The token rows are register-staged two steps
-// ahead; with tracked loads the compiler's wait before the LDS store of the older set is a
-// vmcnt(0) (loop-carried operands), which also drains the younger set and leaves one step of
-// prefetch.  The waits are counted by hand instead (wait_vmcnt<PER> = all but the younger
-// set), and every wave issues exactly PER of these per step (no branches around them).
-MSU_DEV u32x4 gload16(const void* p) {
-  u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
+// 16-B global loads of the staged token rows.  Plain (compiler-tracked) loads: the compiler
+// places the vmcnt waits.  Loads it does not track (inline asm, waits counted by hand) kept
+// more of the ring in flight, but the compiler then believes the destination registers are
+// written at issue and may copy, spill or reuse them while the data is still on its way -- a
+// build of that variant faulted on the GPU.
+MSU_DEV u32x4 gload16(const void* p) { return *reinterpret_cast<const u32x4*>(p); }
 // the same from a wave-uniform base and a per-lane byte offset (no 64-bit address VALU)
 MSU_DEV u32x4 gload16_s(const void* base, unsigned off) {
-  u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v) : "v"(off), "s"(base) : "memory");
-  return v;
+  return *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(base) + off);
 }
 
 // row-major k-contiguous fragment: lane l -> row row0 + (l & 31), k = k0 + 8 (l >> 5) .. +7
@@ -181,7 +181,7 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
   const long ntiles = (M + TM - 1) / TM;
   const int G = gridDim.x;
   const int b = blockIdx.x;
-  const long nsteps = b < ntiles ? (ntiles - 1 - b) / G + 1 : 0;
+  const long nsteps = (ntiles - 1 - b) / G + 1;  // >= 1: the grid is at most ntiles (grid_of)
 
   // ---- W^T -> LDS (once)
   for (int i = tid; i < K * CY; i += NTHR) {
@@ -218,15 +218,20 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
     const int cw = wave * 64 + NTHR * j;
     return cw < TM * CY ? 0 : cw < CHUNKS ? 1 : 2;
   };
-  auto load = [&](long step, auto SET) __attribute__((always_inline)) {
+  // Issued on every path (past the last step: a dummy re-read of the last step's rows) so
+  // that the compiler's wait before each LDS store leaves the younger sets in flight (with the
+  // issue behind a branch it counts the path without it and waits for everything).
+  auto load = [&](long step_, auto SET) __attribute__((always_inline)) {
     constexpr int set = decltype(SET)::value;
+    const long step = step_ < nsteps ? step_ : nsteps - 1;
     const long m0 = (b + step * G) * TM;
     if (m0 + TM <= M) {  // whole step: uniform row base + per-lane 32-bit offset
 #pragma unroll
       for (int j = 0; j < PER; ++j) {
         const int kd = kind(j);
         const bf16_t* base = kd == 0 ? dY + m0 * N : kd == 1 ? X + m0 * K : dY;
-        st[set][j] = gload16_s(base, 2u * (unsigned)goff[j]);
+        if constexpr ((MSU_EXP & 8) != 0) st[set][j] = u32x4{(unsigned)goff[j], 0u, 0u, 0u};
+        else st[set][j] = gload16_s(base, 2u * (unsigned)goff[j]);
       }
     } else {  // the ragged last step: rows past M re-read row M - 1
       const int t0 = opaque(tid);
@@ -248,17 +253,12 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
       }
     }
   };
-  // set SET (rows of step `step`) -> LDS stage step & 1; `younger` = how many sets were loaded
+  // set SET (rows of step `step`) -> LDS stage step & 1
   // after this one (they may stay in flight; other VMEM ops issued in between make the wait
   // retire more, never less)
-  auto store = [&](long step, auto SET, long younger) __attribute__((always_inline)) {
+  auto store = [&](long step, auto SET) __attribute__((always_inline)) {
     constexpr int set = decltype(SET)::value;
-    static_for<D>([&](auto I) __attribute__((always_inline)) {
-      constexpr int n = D - 1 - decltype(I)::value;  // D - 1 .. 0: the deepest first
-      if (n == 0 ? younger <= 0 : younger == n) wait_vmcnt<PER * n>();
-    });
-#pragma unroll
-    for (int j = 0; j < PER; ++j) asm volatile("" : "+v"(st[set][j]));
+    // every path passes one wait (the last D - 1 steps of a workgroup drain fully)
     bf16_t* y = sS + (int)(step & 1) * STAGE;
     const long m0 = (b + step * G) * TM;
     if (m0 + TM <= M) {
@@ -287,9 +287,9 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
   float db0 = 0.f, db1 = 0.f;
 
   static_for<D>([&](auto I) __attribute__((always_inline)) {
-    if (decltype(I)::value < nsteps) load(decltype(I)::value, I);
+    load(decltype(I)::value, I);
   });
-  if (nsteps > 0) store(0, IC<0>{}, (nsteps < D ? nsteps : D) - 1);
+  store(0, IC<0>{});
   __syncthreads();
 
   // one step (compile-time slot Q = s % D): compute from LDS stage s & 1; the rows of step s + D
@@ -300,7 +300,6 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
     const bf16_t* y = sS + (int)(s & 1) * STAGE;
     const bf16_t* x = y + TM * LDY;
     const long m0 = (b + s * G) * TM;
-    const bool ahead = s + D < nsteps;
     // GELU' operands of this wave's input-gradient tiles (lane: token m0 + (lane & 31)), issued
     // before the step s + 2 rows so that the counted wait below retires them first
     u32x4 hv[DMAX][2];
@@ -316,13 +315,13 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
         }
       }
     }
-    if (ahead) load(s + D, SLOT);
+    load(s + D, SLOT);
 
     // ---- weight gradient: this wave's tiles, two 16-token k steps
 #pragma unroll
     for (int i = 0; i < WMAX; ++i) {
       const int jt = wg_tile<K, N>(wave, i);
-      if (jt >= 0) {
+      if (jt >= 0 && (MSU_EXP & 4) == 0) {
         const int jo = opaque(jt);
         const int kt = jo / P::NT, nt = jo - (jo / P::NT) * P::NT;
 #pragma unroll
@@ -335,7 +334,7 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
     }
 
     // ---- bias gradient: column sums of the dY image, rows dealt over RG thread groups
-    if (bg < RG) {
+    if (bg < RG && (MSU_EXP & 16) == 0) {
       for (int r = bg; r < TM; r += RG) {
         const uint32_t w2 = *reinterpret_cast<const uint32_t*>(y + r * LDY + 2 * bp);
         db0 += Fmt16<T>::lo(w2);
@@ -352,19 +351,8 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
         const long m = m0 + (lane & 31);
         f32x16 acc = f32x16{0};
 #pragma unroll 3
-        for (int ns = 0; ns < NS16; ++ns)
+        for (int ns = 0; ns < ((MSU_EXP & 2) ? 0 : NS16); ++ns)
           acc = Fmt16<T>::mma32(frag_rows(sW, LDW, 32 * kt, 16 * ns, lane), frag_rows(y, LDY, 0, 16 * ns, lane), acc);
-        if constexpr (GG) {
-          if (d == 0) {  // no store issued yet this step: only the step s + 2 rows are younger
-            if (ahead) wait_vmcnt<PER>();
-            else wait_vmcnt<0>();
-#pragma unroll
-            for (int dd = 0; dd < DMAX; ++dd) {
-              asm volatile("" : "+v"(hv[dd][0]));
-              asm volatile("" : "+v"(hv[dd][1]));
-            }
-          }
-        }
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
           const int g0 = 2 * pp;
@@ -384,7 +372,7 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
             }
           }
           const u32x4 pk = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
-          if (m < M) *reinterpret_cast<u32x4*>(dX + m * K + 32 * kt + 16 * pp + 8 * h) = pk;
+          if (m < M && (MSU_EXP & 1) == 0) *reinterpret_cast<u32x4*>(dX + m * K + 32 * kt + 16 * pp + 8 * h) = pk;
         }
       }
     }
@@ -392,8 +380,7 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
     // (counted wait: the rows of steps s + 2 .. s + D may stay in flight; this step's dX stores
     // and GELU' loads are not counted, so the wait errs towards retiring more)
     if (s + 1 < nsteps) {
-      const long left = nsteps - s - 2;
-      store(s + 1, IC<(slot + 1) % D>{}, left < D - 1 ? left : D - 1);
+      store(s + 1, IC<(slot + 1) % D>{});
     }
     __syncthreads();
   };
