@@ -1,7 +1,7 @@
 """Time the one-pass stage-0 Linear backward (msu_linear_bwd) against the two-kernel path
 (token-GEMM input gradient + msu_linear_wgrad) at the bench's stage-0 shapes, alone on the GPU.
 
-    python tools/linbwd_bench.py
+    python tools/linbwd_bench.py [K N [gg]]      (default: every stage-0 shape)
 """
 import os
 import sys
@@ -33,7 +33,10 @@ def timeit(fn, n=10):
 def main():
     L = _lib.lib()
     s = torch.cuda.current_stream().cuda_stream
-    for K, N, gg in [(96, 288, False), (96, 96, False), (96, 384, False), (384, 96, False), (384, 96, True)]:
+    shapes = [(96, 288, False), (96, 96, False), (96, 384, False), (384, 96, False), (384, 96, True)]
+    if len(sys.argv) > 2:
+        shapes = [(int(sys.argv[1]), int(sys.argv[2]), len(sys.argv) > 3 and sys.argv[3] == "1")]
+    for K, N, gg in shapes:
         dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
         x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
         w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
