@@ -106,6 +106,12 @@ def _child(rank, port, outdir):
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     assert dist.get_backend() == "nccl"
     pg = dist.group.WORLD
+    # the stage-0 block Linears take the one-pass backward (msu_linear_bwd, main stream, dW / db
+    # straight into the flat .grad) as they do at the bench's size: the bucketer's readiness
+    # counts and stream edges cover it too
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    assert ops._LINBWD
+    ops._LINBWD_MIN_M = 1
     for name, kw in _scenarios():
         kw = dict(kw)
         dp = kw.pop("dp", True)
