@@ -70,9 +70,21 @@ constexpr int ldx_of() {
 }
 
 // register sets of staged token rows (steps of prefetch): as deep as the registers allow
+// (MSU_LB_D96 / MSU_LB_DGG: A/B builds of the 96 x 96 and GELU' depths)
+#ifndef MSU_LB_D96
+#define MSU_LB_D96 4
+#endif
+#ifndef MSU_LB_DGG
+#define MSU_LB_DGG 2
+#endif
+// MSU_LB_HALL: GELU' operands loaded by every wave for every slot (a wave without a second
+// k-tile re-reads its first), so that the compiler's counts do not depend on the wave
+#ifndef MSU_LB_HALL
+#define MSU_LB_HALL 0
+#endif
 template <int K, int N, bool GG>
 constexpr int ring_depth() {
-  return GG ? 2 : 3;
+  return GG ? MSU_LB_DGG : (K == 96 && N == 96 ? MSU_LB_D96 : 3);
 }
 
 // opaque copy of a value: keeps the compiler from hoisting per-chunk / per-tile index math out
@@ -301,15 +313,16 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
     const bf16_t* x = y + TM * LDY;
     const long m0 = (b + s * G) * TM;
     // GELU' operands of this wave's input-gradient tiles (lane: token m0 + (lane & 31)), issued
-    // before the step s + 2 rows so that the counted wait below retires them first
+    // before the step s + D rows
     u32x4 hv[DMAX][2];
     if constexpr (GG) {
       const long m = m0 + (lane & 31);
       const long mh = m < M ? m : M - 1;
 #pragma unroll
       for (int d = 0; d < DMAX; ++d) {
-        const int kt = wave + NW * d;
-        if (kt < KT) {
+        const int kt0 = wave + NW * d;
+        if (MSU_LB_HALL || kt0 < KT) {
+          const int kt = kt0 < KT ? kt0 : wave;
 #pragma unroll
           for (int pp = 0; pp < 2; ++pp) hv[d][pp] = gload16(H + mh * K + 32 * kt + 16 * pp + 8 * h);
         }
