@@ -39,7 +39,13 @@
 
 namespace {
 
-constexpr int TM = 32;  // tokens per step
+// Tokens per step: 64 for the K = 96 shapes whose W^T image leaves room for two 64-token
+// stages (qkv, proj: half the barriers and LDS round trips per token), else 32.
+// MSU_LB_TS64=0: every shape at 32 (A/B builds).
+#ifndef MSU_LB_TS64
+#define MSU_LB_TS64 1
+#endif
+constexpr int ts_of(int K, int N) { return (MSU_LB_TS64 && K == 96 && (N == 288 || N == 96)) ? 64 : 32; }
 constexpr int NW = 8;                  // waves per workgroup
 constexpr int NTHR = 64 * NW;
 
@@ -84,7 +90,7 @@ constexpr int ldx_of() {
 #endif
 template <int K, int N, bool GG>
 constexpr int ring_depth() {
-  return GG ? MSU_LB_DGG : (K == 96 && N == 96 ? MSU_LB_D96 : 3);
+  return GG ? MSU_LB_DGG : ts_of(K, N) == 64 ? 2 : (K == 96 && N == 96 ? MSU_LB_D96 : 3);
 }
 
 // opaque copy of a value: keeps the compiler from hoisting per-chunk / per-tile index math out
@@ -178,6 +184,8 @@ __global__ void __launch_bounds__(NTHR, 1)
 linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
               const bf16_t* __restrict__ H, bf16_t* __restrict__ dX, float* __restrict__ part, long M) {
   using P = Plan<K, N>;
+  constexpr int TM = ts_of(K, N);
+  static_assert(!GG || TM == 32, "the GELU' operands are staged for 32-token steps");
   constexpr int LDW = N + 8, LDY = N + 8, LDX = ldx_of<K>();
   constexpr int CY = N / 8, CX = K / 8;              // 16-B chunks per dY / X row
   constexpr int CHUNKS = TM * (CY + CX);
@@ -338,7 +346,7 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
         const int jo = opaque(jt);
         const int kt = jo / P::NT, nt = jo - (jo / P::NT) * P::NT;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
+        for (int ks = 0; ks < TM / 16; ++ks)
           accw[i] = Fmt16<T>::mma32(frag_tr(x, LDX, 16 * ks, 32 * kt, lane), frag_tr(y, LDY, 16 * ks, 32 * nt, lane),
                                     accw[i]);
       }
@@ -355,17 +363,19 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
       }
     }
 
-    // ---- input gradient: k-tiles kt = wave + NW d, C^T[k][token]
+    // ---- input gradient: k-tiles kt = wave + NW d, C^T[k][token], 32-token tiles tt
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) {
       const int kt = wave + NW * d;
-      if (kt < KT) {
-        // lane: token m0 + (lane & 31); after the permlane32 swap, 8 consecutive k per pair
-        const long m = m0 + (lane & 31);
+#pragma unroll
+      for (int tt = 0; tt < TM / 32; ++tt) if (kt < KT) {
+        // lane: token m0 + 32 tt + (lane & 31); after the permlane32 swap, 8 consecutive k per pair
+        const long m = m0 + 32 * tt + (lane & 31);
         f32x16 acc = f32x16{0};
 #pragma unroll 3
         for (int ns = 0; ns < ((MSU_EXP & 2) ? 0 : NS16); ++ns)
-          acc = Fmt16<T>::mma32(frag_rows(sW, LDW, 32 * kt, 16 * ns, lane), frag_rows(y, LDY, 0, 16 * ns, lane), acc);
+          acc = Fmt16<T>::mma32(frag_rows(sW, LDW, 32 * kt, 16 * ns, lane), frag_rows(y, LDY, 32 * tt, 16 * ns, lane),
+                                acc);
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
           const int g0 = 2 * pp;
@@ -437,7 +447,7 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
 
 template <int K, int N>
 constexpr size_t linbwd_lds() {
-  return sizeof(bf16_t) * ((size_t)K * (N + 8) + 2 * (size_t)TM * ((N + 8) + ldx_of<K>()));
+  return sizeof(bf16_t) * ((size_t)K * (N + 8) + 2 * (size_t)ts_of(K, N) * ((N + 8) + ldx_of<K>()));
 }
 
 int num_cus_lb() {
@@ -450,8 +460,9 @@ int num_cus_lb() {
   return cus;
 }
 
-long grid_of(long M) {
-  const long ntiles = (M + TM - 1) / TM;
+long grid_of(long M, int K, int N) {
+  const int ts = ts_of(K, N);
+  const long ntiles = (M + ts - 1) / ts;
   const long g = num_cus_lb();
   return ntiles < g ? ntiles : g;
 }
@@ -468,7 +479,7 @@ int launch_lb(const void* dY, const void* X, const void* Wt, const void* H, void
       return -4;
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid_of(M)), dim3(NTHR), lds, st, (const bf16_t*)dY, (const bf16_t*)X,
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid_of(M, K, N)), dim3(NTHR), lds, st, (const bf16_t*)dY, (const bf16_t*)X,
                      (const bf16_t*)Wt, (const bf16_t*)H, (bf16_t*)dX, part, M);
   return 0;
 }
@@ -485,7 +496,7 @@ extern "C" {
 int msu_linear_bwd_supported(long M, int K, int N) { return M > 0 && lb_shape(K, N) ? 1 : 0; }
 
 // f32 workspace floats msu_linear_bwd needs (per-workgroup dW / db partials).
-long msu_linear_bwd_workspace(long M, int K, int N) { return grid_of(M) * ((long)N * K + N); }
+long msu_linear_bwd_workspace(long M, int K, int N) { return grid_of(M, K, N) * ((long)N * K + N); }
 
 // One pass over the tokens of y = x . W^T + b (x [M][K], W [N][K], 16-bit dtype 1 bf16 / 2 f16):
 //   dX = dY . W (times GELU'(H) when H != null: mlp.3's input gradient into mlp.0's output),
@@ -509,7 +520,7 @@ int msu_linear_bwd(int dtype, const void* dY, const void* X, const void* Wt, con
   MSU_LB(384, 96, true)
 #undef MSU_LB
   if (rc) return rc;
-  const int parts = (int)grid_of(M);
+  const int parts = (int)grid_of(M, K, N);
   const long stride = (long)N * K + N;
   const ColSeg segs[2] = {{workspace, (long)N * K, stride, dW}, {workspace + (long)N * K, N, stride, db}};
   colsum_multi(segs, db ? 2 : 1, parts, accumulate, st);
