@@ -1,7 +1,14 @@
 """MS-UNet (Swin-T) training throughput on MI355X: images/sec at 1024^2, bs=8 per GPU.
 
-    python bench.py [--gpus N --steps K --warmup W]        # N=1 default
-    torchrun --nproc-per-node N bench.py --gpus N ...     # one rank per GPU (RCCL)
+    python bench.py [--gpus N --steps K --warmup W]        # N=1 default; N>1 starts N ranks itself
+    torchrun --nproc-per-node N bench.py --gpus N ...     # one rank per GPU (RCCL), launcher-started
+
+With ``--gpus N > 1`` and no ``WORLD_SIZE`` in the environment, this process touches no GPU: it
+starts N child processes of itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+a free MASTER_PORT), waits for them and exits with the first failing child's status.  Each
+rank binds GPU LOCAL_RANK and joins an RCCL (``--dist-backend nccl``, default) process group
+of exactly N ranks; ``--dist-backend gloo`` runs the same step with gloo collectives and lets
+N ranks share one GPU (the one-GPU rehearsal of the N-rank path, tests/test_gpu_bench_dp.py).
 
 A step = one full training step of the reference's trainer.py:308-316 on one batch per
 rank: bf16-autocast forward of MS-UNet -> DynamicLoss -> backward -> bucketed RCCL
@@ -51,7 +58,48 @@ def parse():
     ap.add_argument("--skip-dead", action="store_true", help="skip the reference's discarded branches (exact)")
     ap.add_argument("--grad-wire", choices=["f32", "bf16", "fp16"], default="f32",
                     help="DP gradient all-reduce precision (BASELINE config 5: fp16 grads)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1: RCCL (one GPU per rank) or gloo (ranks may share a GPU; rehearsal)")
+    ap.add_argument("--dump-state", default=None,
+                    help="write each rank's final flat parameters to <path>.rank<R>.pt (DP tests)")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """Start n rank processes of this script (no GPU call in this process: the children are
+    fresh interpreters, not forks or execs of a GPU-initialised one) and return the exit status
+    of the first that fails (0 when all succeed).  A failing rank ends the others, so a hung
+    collective does not outlive it."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCH_NCCL_CUDA_EVENT_CACHE="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    status = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            rc = p.poll()
+            if rc is None:
+                continue
+            alive.remove(p)
+            if rc != 0 and status == 0:
+                status = rc
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.2)
+    return status if status >= 0 else 128 - status
 
 
 def conv_roofline(device, batch, img, C):
@@ -449,12 +497,26 @@ def input_pipeline_leg(device, trainer, batch, img, seed, resident_ms):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # ProcessGroupNCCL's event cache hands a retired work's events to new works; with a
+        # captured step its watchdog then queries an event recorded in a capture and aborts
+        # (DESIGN 4b).  Must be set before the process group exists.
+        os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] = "0"
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     device = torch.device("cuda", local)
 
     from semantic_segmentation_of_stylegan2_artifacts_amd import load_config
@@ -515,6 +577,8 @@ def main():
                                    f"{world}xMI355X DP {args.img}x{args.img} global bs={args.batch * world} "
                                    f"{BACKBONE_NAME[args.backbone]} MS-UNet train step",
                        "model": f"MS-UNet {args.backbone}", "global_batch": args.batch * world,
+                       "world_size": dist.get_world_size() if world > 1 else 1,
+                       "dist_backend": (args.dist_backend if world > 1 else None),
                        "img_size": args.img, "parallelism": f"dp{world}", "grad_allreduce": args.grad_wire,
                        "dead_branches": "skipped" if args.skip_dead else "executed (no grad)",
                        "step_execution": "hip_graph_replay" if trainer._graph is not None else "eager",
@@ -533,6 +597,9 @@ def main():
             res["cpu_baseline"] = cpu_baseline()
             res["dice_vs_ref"] = dice_vs_reference(device)
         print(json.dumps(res), flush=True)
+    if args.dump_state:
+        torch.save({"data": [g.data.detach().cpu() for g in trainer.groups], "loss": loss_val,
+                    "world": world, "rank": rank}, f"{args.dump_state}.rank{rank}.pt")
     if world > 1:
         dist.destroy_process_group()
 

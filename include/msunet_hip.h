@@ -139,6 +139,12 @@ int msu_wgrad_splits(long M, int N, int K);
 long msu_wgrad_workspace(long M, int N, int K);
 int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float* db, float* workspace,
                      long M, int N, int K, int accumulate, void* stream);
+/* Same, with dW a column slice of a wider row-major gradient (row stride ldw >= K): each input
+ * half of a skip-fusion Linear (concat_back_dim, model_parts.py:639-641, applied to
+ * torch.cat([x, skip], -1) at :792-794, :804-806, :823-824) accumulates straight into its
+ * columns of the weight's gradient. */
+int msu_linear_wgrad_ld(int dtype, const void* dY, const void* X, float* dW, long ldw, float* db,
+                        float* workspace, long M, int N, int K, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------- Linear backward in one pass
  * Stage-0 Linears of the Swin block (qkv, proj, mlp.0, mlp.3; model_parts.py:143-151, called at

@@ -55,6 +55,7 @@ SIGNATURES = {
     "msu_wgrad_splits": (I, [L, I, I]),
     "msu_wgrad_workspace": (L, [L, I, I]),
     "msu_linear_wgrad": (I, [I, P, P, P, P, P, L, I, I, I, P]),
+    "msu_linear_wgrad_ld": (I, [I, P, P, P, L, P, P, L, I, I, I, P]),
     "msu_linear_bwd_supported": (I, [L, I, I]),
     "msu_linear_bwd_workspace": (L, [L, I, I]),
     "msu_linear_bwd": (I, [I, P, P, P, P, P, P, P, P, L, I, I, I, P]),

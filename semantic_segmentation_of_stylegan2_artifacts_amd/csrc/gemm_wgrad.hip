@@ -146,7 +146,7 @@ template <int WN, int WK> constexpr int wgrad_nw() { return WN * WK == 3 ? 3 : 4
 template <typename T, int NTW, int WN, int WK, int NST>
 __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                                          float* __restrict__ part, float* __restrict__ dbpart,
-                                                         long M, int N, int K, long mchunk) {
+                                                         long M, int N, int K, long mchunk, int ntiles, int xcd) {
   constexpr int NW = wgrad_nw<WN, WK>();
   constexpr int WM = NW / (WN * WK), WT = 16 * NTW, BN = WN * WT, BK = WK * WT, RS = 32 * WM;
   static_assert(WM * WN * WK == NW, "wave split");
@@ -163,9 +163,16 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wni = wave % WN, wki = (wave / WN) % WK, wmi = wave / (WN * WK);
   const int ntk = K / BK;
-  const int tn = blockIdx.x / ntk, tk = blockIdx.x - (blockIdx.x / ntk) * ntk;
+  // 1-D grid of ntiles x splits work items.  xcd: consecutive items (the output tiles of one
+  // row split, which stream the same dY / X rows) go to one XCD (dispatch is round-robin over
+  // the 8 XCDs by block id), so the rows a split's tiles share are fetched from HBM once and
+  // re-read from that XCD's L2; otherwise item = block id (the tiles of a split spread over
+  // all XCDs and each XCD fetches the rows again)
+  const int item = xcd ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int split = item / ntiles, tile = item - split * ntiles;
+  const int tn = tile / ntk, tk = tile - (tile / ntk) * ntk;
   const int n0 = tn * BN, k0 = tk * BK;
-  const long m_begin = (long)blockIdx.y * mchunk;
+  const long m_begin = (long)split * mchunk;
   long m_end = m_begin + mchunk;
   if (m_end > M) m_end = M;
   const int nstage = m_end > m_begin ? (int)((m_end - m_begin + RS - 1) / RS) : 0;
@@ -304,7 +311,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
     }
   }
   if (wmi != 0) return;
-  float* out = part + (long)blockIdx.y * N * K;
+  float* out = part + (long)split * N * K;
 #pragma unroll
   for (int i = 0; i < NTW; ++i)
 #pragma unroll
@@ -321,7 +328,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
     for (int i = 0; i < NTW; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        dbpart[(long)blockIdx.y * N + n0 + wni * WT + 16 * i + (lane >> 4) * 4 + r] = accb[i][r];
+        dbpart[(long)split * N + n0 + wni * WT + 16 * i + (lane >> 4) * 4 + r] = accb[i][r];
   }
 }
 
@@ -391,7 +398,7 @@ inline WavePlan wave_plan(long M, int N, int K) {
 
 template <typename T, int NTW, int WN, int WK, int NST>
 void launch_wave(dim3 grid, const bf16_t* dY, const bf16_t* X, float* part, float* dbpart, long M, int N, int K,
-                 long mchunk, hipStream_t st) {
+                 long mchunk, int ntiles, hipStream_t st) {
   constexpr int NW = wgrad_nw<WN, WK>();
   constexpr int WM = NW / (WN * WK), WT = 16 * NTW, RS = 32 * WM;
   constexpr int SLOTS = RS * ((WN * WT + 8) / 8 + (WK * WT + 8) / 8);
@@ -404,7 +411,8 @@ void launch_wave(dim3 grid, const bf16_t* dY, const bf16_t* X, float* part, floa
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
-    hipLaunchKernelGGL(kern, grid, dim3(64 * NW), lds, st, dY, X, part, dbpart, M, N, K, mchunk);
+    static const int xcd = !(getenv("MSU_WGRAD_XCD") && getenv("MSU_WGRAD_XCD")[0] == '0');  // A/B switch
+    hipLaunchKernelGGL(kern, grid, dim3(64 * NW), lds, st, dY, X, part, dbpart, M, N, K, mchunk, ntiles, xcd);
   }
 }
 
@@ -414,15 +422,16 @@ int run_wave(const WavePlan& p, const bf16_t* dY, const bf16_t* X, float* part, 
   const int wt = 16 * p.ntw, nw = p.wn * p.wk == 3 ? 3 : 4, wm = nw / (p.wn * p.wk), rs = 32 * wm;
   long mchunk = (M + p.S - 1) / p.S;
   mchunk = (mchunk + rs - 1) / rs * rs;
-  const dim3 grid((unsigned)((N / (p.wn * wt)) * (K / (p.wk * wt))), (unsigned)p.S);
-#define MSU_WAVE(NTW, WN, WK)                                                                                \
-  if (p.ntw == NTW && p.wn == WN && p.wk == WK) {                                                           \
-    switch (p.nst) {                                                                                        \
-      case 3: launch_wave<T, NTW, WN, WK, 3>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;     \
-      case 4: launch_wave<T, NTW, WN, WK, 4>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;     \
-      case 5: launch_wave<T, NTW, WN, WK, 5>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;     \
-      case 6: launch_wave<T, NTW, WN, WK, 6>(grid, dY, X, part, dbpart, M, N, K, mchunk, st); return 0;     \
-    }                                                                                                       \
+  const int ntiles = (N / (p.wn * wt)) * (K / (p.wk * wt));
+  const dim3 grid((unsigned)(ntiles * p.S));
+#define MSU_WAVE(NTW, WN, WK)                                                                                        \
+  if (p.ntw == NTW && p.wn == WN && p.wk == WK) {                                                                   \
+    switch (p.nst) {                                                                                                \
+      case 3: launch_wave<T, NTW, WN, WK, 3>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st); return 0;     \
+      case 4: launch_wave<T, NTW, WN, WK, 4>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st); return 0;     \
+      case 5: launch_wave<T, NTW, WN, WK, 5>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st); return 0;     \
+      case 6: launch_wave<T, NTW, WN, WK, 6>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st); return 0;     \
+    }                                                                                                               \
   }
   MSU_WAVE(6, 1, 1) MSU_WAVE(6, 2, 1) MSU_WAVE(6, 4, 1) MSU_WAVE(6, 1, 2) MSU_WAVE(6, 2, 2) MSU_WAVE(6, 1, 4)
   MSU_WAVE(6, 3, 1) MSU_WAVE(6, 1, 3)
@@ -461,13 +470,15 @@ long msu_wgrad_workspace(long M, int N, int K) {
   return ws;
 }
 
-// dW [N][K] f32 (overwritten, or accumulated when accumulate != 0), db [N] f32 (may be null).
-int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float* db, float* workspace,
-                     long M, int N, int K, int accumulate, void* stream) {
-  if (N % 8 || K % 8 || M < 0) return -2;  // 16-B staging chunks
+// dW [N][K] f32 with row stride ldw >= K (overwritten, or accumulated when accumulate != 0;
+// ldw > K: a column slice of a wider weight gradient, e.g. one input half of a skip-fusion
+// Linear), db [N] f32 (may be null).
+int msu_linear_wgrad_ld(int dtype, const void* dY, const void* X, float* dW, long ldw, float* db,
+                        float* workspace, long M, int N, int K, int accumulate, void* stream) {
+  if (N % 8 || K % 8 || M < 0 || ldw < K) return -2;  // 16-B staging chunks
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) {
-    if (!accumulate) hipMemsetAsync(dW, 0, sizeof(float) * (long)N * K, st);
+    if (!accumulate) hipMemset2DAsync(dW, sizeof(float) * ldw, 0, sizeof(float) * K, N, st);
     if (db && !accumulate) hipMemsetAsync(db, 0, sizeof(float) * N, st);
     return MSU_CHECK_LAUNCH();
   }
@@ -480,7 +491,7 @@ int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float*
       int rc = -3;
       MSU_DISPATCH16(dtype, T, rc = run_wave<T>(p, (const bf16_t*)dY, (const bf16_t*)X, part, dbpart, M, N, K, st));
       if (rc) return rc;
-      const ColSeg segs[2] = {{part, (long)N * K, (long)N * K, dW}, {dbpart, N, N, db}};
+      const ColSeg segs[2] = {{part, (long)N * K, (long)N * K, dW, K, ldw}, {dbpart, N, N, db}};
       colsum_multi(segs, db ? 2 : 1, p.slabs(), accumulate, st);
       return MSU_CHECK_LAUNCH();
     }
@@ -499,9 +510,14 @@ int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float*
     else
       hipLaunchKernelGGL((wgrad_kernel<T, 4>), grid, dim3(256), 0, st, (const T*)dY, (const T*)X, part, dbpart, M,
                          N, K, mchunk));
-  const ColSeg segs[2] = {{part, (long)N * K, (long)N * K, dW}, {dbpart, N, N, db}};
+  const ColSeg segs[2] = {{part, (long)N * K, (long)N * K, dW, K, ldw}, {dbpart, N, N, db}};
   colsum_multi(segs, db ? 2 : 1, S, accumulate, st);
   return MSU_CHECK_LAUNCH();
+}
+
+int msu_linear_wgrad(int dtype, const void* dY, const void* X, float* dW, float* db, float* workspace,
+                     long M, int N, int K, int accumulate, void* stream) {
+  return msu_linear_wgrad_ld(dtype, dY, X, dW, K, db, workspace, M, N, K, accumulate, stream);
 }
 
 }  // extern "C"

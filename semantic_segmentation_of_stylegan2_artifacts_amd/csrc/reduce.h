@@ -1,4 +1,6 @@
 // Deterministic column reduction of per-block partial rows: out[i] (+)= sum_p part[p*stride + i].
+// The output may be a column slice of a wider row-major matrix: element i goes to
+// out[(i / rowlen) * ldo + i % rowlen] (rowlen = n, ldo = n: contiguous).
 // Block = (256/PL) column groups (V = 4 floats each, 16-B loads, when aligned) x PL part-lanes;
 // each part-lane walks parts p = ly, ly+PL, ... in a fixed order with 8 loads in flight, then
 // the PL lane partials are added in a fixed order through LDS.  Narrow reductions (LayerNorm
@@ -17,6 +19,7 @@ struct ColSegs {
   float* out[3];
   long n[3];
   long stride[3];
+  long rowlen[3], ldo[3];
   int bend[3];
   int nseg;
 };
@@ -53,25 +56,31 @@ __global__ void __launch_bounds__(256) colsum_kernel(ColSegs sg, int nparts, int
     vec t = red[0][lx];
 #pragma unroll
     for (int k = 1; k < PL; ++k) t += red[k][lx];
-    vec* o = reinterpret_cast<vec*>(out + i);
+    const long rl = sg.rowlen[seg];
+    const long oi = rl == n ? i : (i / rl) * sg.ldo[seg] + (i - (i / rl) * rl);
+    vec* o = reinterpret_cast<vec*>(out + oi);
     *o = accumulate ? *o + t : t;
   }
 }
 
-// segs: {part, n, stride, out} x nseg (nseg <= 3), all over nparts parts
+// segs: {part, n, stride, out[, rowlen, ldo]} x nseg (nseg <= 3), all over nparts parts
 struct ColSeg {
   const float* part;
   long n;
   long stride;
   float* out;
+  long rowlen = 0;  // 0: contiguous output
+  long ldo = 0;
 };
 
 inline void colsum_multi(const ColSeg* segs, int nseg, int nparts, int accumulate, hipStream_t st) {
   bool v4 = true;
   long total = 0;
   for (int j = 0; j < nseg; ++j) {
-    v4 = v4 && segs[j].n % 4 == 0 && segs[j].stride % 4 == 0 && ((uintptr_t)segs[j].part & 15) == 0 &&
-         ((uintptr_t)segs[j].out & 15) == 0;
+    const long rl = segs[j].rowlen > 0 ? segs[j].rowlen : segs[j].n;
+    const long lo = segs[j].rowlen > 0 ? segs[j].ldo : segs[j].n;
+    v4 = v4 && segs[j].n % 4 == 0 && segs[j].stride % 4 == 0 && rl % 4 == 0 && lo % 4 == 0 &&
+         ((uintptr_t)segs[j].part & 15) == 0 && ((uintptr_t)segs[j].out & 15) == 0;
     total += segs[j].n;
   }
   const int V = v4 ? 4 : 1;
@@ -86,6 +95,8 @@ inline void colsum_multi(const ColSeg* segs, int nseg, int nparts, int accumulat
     sg.out[j] = segs[j].out;
     sg.n[j] = segs[j].n;
     sg.stride[j] = segs[j].stride;
+    sg.rowlen[j] = segs[j].rowlen > 0 ? segs[j].rowlen : segs[j].n;
+    sg.ldo[j] = segs[j].rowlen > 0 ? segs[j].ldo : segs[j].n;
     blocks += (int)((segs[j].n / V + NC - 1) / NC);
     sg.bend[j] = blocks;
   }

@@ -150,9 +150,6 @@ _SIDE_PRIORITY = int(os.environ.get("MSU_SIDE_PRIORITY", "1"))  # A/B switch (0:
 _side_streams = {}
 # per-use switches of the side stream (tools/graph_side_probe.py bisects the forked capture)
 _side_wgrad = True      # Linear weight gradients
-# timing ablation only (results WRONG by design): MSU_EXP_SKIP_WGRAD=1 launches no Linear
-# weight gradient, to measure what the side stream's kernels cost the main stream
-_EXP_SKIP_WGRAD = os.environ.get("MSU_EXP_SKIP_WGRAD", "0") == "1"
 _side_attn_tail = True  # attention relative-table / qkv-bias reductions
 
 
@@ -190,6 +187,7 @@ def _guard_side_write(p, ev):
     the attention op returns the padded tokens' share), that AccumulateGrad must wait for it:
     a tensor hook on p makes the current stream wait for the last such event first."""
     p._msu_side_event = ev
+    _side_event_params.append(p)
     if not getattr(p, "_msu_side_hooked", False):
         def hook(grad, p=p):
             # called with None when the backward that owns p returned no gradient (direct
@@ -209,6 +207,9 @@ def _guard_side_write(p, ev):
 # main stream would then add into it while a side-stream weight gradient still reads it.  One
 # extra reference per tensor, held until the end-of-backward join, keeps it out of reach.
 _side_keep = []
+# parameters whose _msu_side_event was set in this backward: cleared at its end, so no later
+# wait (a hook, _linbwd) orders on an event of an earlier step or from outside a capture
+_side_event_params = []
 
 
 def _end_of_backward():
@@ -216,6 +217,9 @@ def _end_of_backward():
     _join_queued = False
     join_side_streams()
     _side_keep.clear()  # the main stream now waits for every side-stream read
+    for p in _side_event_params:
+        p._msu_side_event = None
+    _side_event_params.clear()
 
 
 def _join_at_end_of_backward():
@@ -532,8 +536,11 @@ def _attn_backward(ctx, dout, _dkeep):
     bp, tp = ctx.bias_param, ctx.table_param
     if bp is not None and tp is not None and _side_enabled and _side_attn_tail and _direct(bp, tp):
         # parameter-gradient tail on the side stream: the relative-table / qkv-bias
-        # reductions and their .grad adds (the qkv bias also receives its Linear's db
-        # there, so every write to its .grad is ordered on one stream)
+        # reductions and their .grad adds.  The qkv bias's .grad has a second writer, its
+        # Linear's db: on the side stream too when that Linear runs the two-kernel backward
+        # (one stream, program order), or on the main stream in the one-pass backward
+        # (_linbwd, stage 0), which runs later in this backward and first makes the main
+        # stream wait on the event recorded below (bias._msu_side_event)
         # (the fork is a fresh torch event per call: a HIP graph capture of the step turns
         # every record / wait pair into its own edge)
         main = torch.cuda.current_stream(qkv.device)
@@ -675,9 +682,6 @@ def _wgrad(dy, x, weight, bias, M, N, K):
     """Linear weight/bias gradients on msu_linear_wgrad; (None, None) when accumulated
     straight into the trainer's flat .grad views."""
     L = _lib.lib()
-    if _EXP_SKIP_WGRAD and _direct(weight) and (bias is None or _direct(bias)):
-        _notify(weight, bias)  # ablation: no weight-gradient work at all (wrong by design)
-        return None, None
     if _direct(weight) and (bias is None or _direct(bias)):
         if _side_enabled and _side_wgrad:
             main = torch.cuda.current_stream(x.device)
@@ -827,19 +831,25 @@ _LINBWD = os.environ.get("MSU_LINBWD", "1") != "0"
 _LINBWD_MIN_M = 65536
 
 
+linbwd_calls = 0  # one-pass backward launches (tests assert which path a backward took)
+
+
 def _linbwd(dy, x, weight, bias, M, N, K, h=None):
     """dX = dy . W (* GELU'(h)) with dW / db accumulated into the trainer's .grad in the same
-    pass; None when the shape, dtype or parameters are not covered (caller: two-kernel path)."""
+    pass; None when the shape, dtype or parameters are not covered (caller: two-kernel path).
+    W^T is the trainer's transposed shadow when it has one in x's dtype, else a per-call
+    transpose of the 16-bit weight (fp16 autocast over a bf16 shadow, MSU_SHADOW_T=0)."""
+    global linbwd_calls
     if not _LINBWD or x.dtype not in _LOW or M < _LINBWD_MIN_M:
         return None
     if not _direct(weight) or (bias is not None and not _direct(bias)):
         return None
-    wt = _shadow_t(weight, x.dtype)
-    if wt is None:
-        return None
     L = _lib.lib()
     if not L.msu_linear_bwd_supported(M, K, N):
         return None
+    wt = _shadow_t(weight, x.dtype)
+    if wt is None:
+        wt = _wt(_shadow(weight, x.dtype))
     if bias is not None:
         # the qkv bias also receives the attention's padded-token share on the side stream
         # (msu_win_attn_bwd_tail, issued earlier in this backward): add after it
@@ -850,6 +860,7 @@ def _linbwd(dy, x, weight, bias, M, N, K, h=None):
     ws = torch.empty(L.msu_linear_bwd_workspace(M, K, N), device=x.device, dtype=torch.float32)
     _lib.call("msu_linear_bwd", _dt(x), _p(dy), _p(x.contiguous()), _p(wt), _p(h), _p(dx), _p(weight.grad),
               _p(None if bias is None else bias.grad), _p(ws), M, K, N, 1, _s(x))
+    linbwd_calls += 1
     _notify(weight, bias)
     return dx
 
@@ -933,13 +944,13 @@ def _linear_cat_setup(ctx, inputs, output):
     ctx.params = (weight, bias)
 
 
-def _wgrad_tmp(dy, x, N, K, M, with_bias):
+def _wgrad_into(dy, x, dw, db, M, N, K, acc):
+    """msu_linear_wgrad of one input half: dw [N, K] may be a column slice of a wider [N, Kt]
+    gradient (row stride Kt, the kernel's ldw); acc = 1 adds into it."""
     L = _lib.lib()
     ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
-    dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
-    db = torch.empty(N, device=x.device, dtype=torch.float32) if with_bias else None
-    _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(dw), _p(db), _p(ws), M, N, K, 0, _s(x))
-    return dw, db
+    _lib.call("msu_linear_wgrad_ld", _dt(x), _p(dy), _p(x), _p(dw), dw.stride(0), _p(db), _p(ws), M, N, K, acc,
+              _s(x))
 
 
 def _linear_cat_backward(ctx, dy):
@@ -954,16 +965,21 @@ def _linear_cat_backward(ctx, dy):
     wt = _shadow_t(weight, W.dtype)  # W^T [K, N]: the halves are row ranges, no copies
     for lo, hi in ((0, C1), (C1, C1 + C2)):
         outs.append(_gemm(dy, W[:, lo:hi].t().contiguous() if wt is None else wt[lo:hi]))
-    # weight gradient per half into temporaries ([N, C1], [N, C2]), bias with the first
-    dw1, db = _wgrad_tmp(dy, x, N, C1, M, with_bias=True)
-    dw2, _ = _wgrad_tmp(dy, skip, N, C2, M, with_bias=False)
-    if _direct(weight, bias):
-        weight.grad[:, :C1] += dw1
-        weight.grad[:, C1:] += dw2
-        bias.grad += db
+    # weight gradient per half straight into the column slices of dW (bias with the first):
+    # the trainer's flat .grad (accumulate) or a fresh [N, C1 + C2] gradient
+    direct = _direct(weight, bias)
+    if direct:
+        dw, db, acc = weight.grad, bias.grad, 1
+    else:
+        dw = torch.empty(N, C1 + C2, device=x.device, dtype=torch.float32)
+        db = torch.empty(N, device=x.device, dtype=torch.float32)
+        acc = 0
+    _wgrad_into(dy, x, dw[:, :C1], db, M, N, C1, acc)
+    _wgrad_into(dy, skip, dw[:, C1:], None, M, N, C2, acc)
+    if direct:
         _notify(weight, bias)
         return outs[0], outs[1], None, None
-    return outs[0], outs[1], torch.cat([dw1, dw2], 1), db
+    return outs[0], outs[1], dw, db
 
 
 _linear_cat = _define("linear_cat", "(Tensor x, Tensor skip, Tensor weight, Tensor bias) -> Tensor",

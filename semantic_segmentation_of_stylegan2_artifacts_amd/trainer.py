@@ -299,6 +299,26 @@ def reseed(seed, rank=0):
     model_parts.reseed(s)
 
 
+def rccl_capture_blocker(process_group):
+    """Why a HIP-graph capture of the step over ``process_group`` would be unsafe, or None.
+
+    ProcessGroupNCCL's event cache (TORCH_NCCL_CUDA_EVENT_CACHE, on by default) hands a retired
+    work's HIP events to new works; after a capture its watchdog thread can query an event last
+    recorded inside the capture, HIP refuses the query (hipErrorCapturedEvent) and the watchdog
+    terminates the process (round-3 record).  The variable must be 0 before the
+    process group is created; gloo groups never capture (their collectives run on the host)."""
+    if process_group is None:
+        return None
+    try:
+        backend = dist.get_backend(process_group)
+    except (RuntimeError, ValueError):
+        return None
+    if backend == "nccl" and os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE", "1") != "0":
+        return ("the RCCL process group was created with TORCH_NCCL_CUDA_EVENT_CACHE on; set "
+                "TORCH_NCCL_CUDA_EVENT_CACHE=0 before init_process_group to capture the step")
+    return None
+
+
 class Trainer:
     def __init__(self, model, config, device, lr=None, amp_dtype=torch.bfloat16, bucket_mb=32,
                  world_size=1, process_group=None, rank=0, seed=None, skip_nonfinite=True, use_graph=None,
@@ -356,6 +376,13 @@ class Trainer:
         self.graph_mode = mode if on_gpu else "0"
         if self.graph_mode != "0" and self.reducer is not None and dist.get_backend(process_group) != "nccl":
             self.graph_mode = "0"  # gloo collectives run on the host: not capturable
+        blocker = rccl_capture_blocker(process_group if self.reducer is not None else None)
+        if self.graph_mode != "0" and blocker:
+            # never capture into a process group whose watchdog can abort the process;
+            # every rank sees the same environment, so every rank stays eager together
+            import warnings
+            warnings.warn(f"HIP-graph replay disabled: {blocker}")
+            self.graph_mode = "0"
         if self.graph_mode == "auto" and world_size > 1:
             # a captured multi-rank step has only been replayed on a 1-rank RCCL group
             # (tests/test_gpu_rccl.py): replay under DP only when asked for (MSU_GRAPH=1)
@@ -567,6 +594,9 @@ class Trainer:
 
     def _capture(self, images, labels):
         """Capture _device_step into a HIP graph (nothing executes during capture)."""
+        blocker = rccl_capture_blocker(self.reducer.pg if self.reducer is not None else None)
+        if blocker:  # use_graph forced on after construction: refuse instead of aborting later
+            raise RuntimeError(f"cannot capture the training step: {blocker}")
         if self.amp_dtype == torch.bfloat16 and not self._shadow_fresh:
             for g in self.groups:
                 g.refresh_shadow()
@@ -580,15 +610,6 @@ class Trainer:
         # deterministic again with DEBUG_HIP_FORCE_GRAPH_QUEUES=1).  Replay is only chosen
         # when the step is launch-bound, where the side-stream overlap matters least.
         # MSU_GRAPH_SIDE=1 keeps the side stream (A/B switch).
-        if self.reducer is not None and self.reducer.pg is not None and \
-                os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE", "1") != "0":
-            # ProcessGroupNCCL's event cache can hand an event recorded inside this capture to a
-            # work its watchdog thread still queries; HIP refuses that query and the watchdog
-            # terminates the process (tests/test_gpu_rccl.py).  Set it to 0 before creating the
-            # process group when the step is captured over RCCL.
-            import warnings
-            warnings.warn("capturing a step with collectives while TORCH_NCCL_CUDA_EVENT_CACHE is on: "
-                          "set TORCH_NCCL_CUDA_EVENT_CACHE=0 before init_process_group")
         side_prev = ops._side_enabled
         if os.environ.get("MSU_GRAPH_SIDE", "0") != "1":
             ops._side_enabled = False

@@ -113,3 +113,18 @@ def test_graph_replay_sees_parameter_writes():
     model.load_state_dict(sd)  # back: the replay must see this write too
     again = tr.step(x, t).item()
     assert again == pytest.approx(base, rel=1e-6, abs=1e-7)
+
+
+@pytest.mark.xfail(strict=False, reason="open: with the side stream on, about 1 eager run in 9 differed at f32 "
+                                        "rounding level in encoder gradients (profiles/r03u_determinism.txt, DESIGN 4b)")
+def test_eager_side_stream_step_is_deterministic():
+    """The DEFAULT eager configuration (weight gradients and the attention parameter tail on the
+    side stream): four independent runs of three steps at lr 0 give bitwise-identical AdamW
+    moments.  Kept next to the side-stream-off test above so that a regression or a fix of the
+    open rounding-level difference shows up (xfail, non-strict)."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    assert ops._side_enabled
+    runs = [_run(False, 0.0, steps=3) for _ in range(4)]
+    for r in runs[1:]:
+        for u, v in zip(runs[0][1], r[1]):
+            assert torch.equal(u, v)

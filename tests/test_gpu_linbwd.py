@@ -3,8 +3,9 @@ PyTorch, and the ops path that uses it against the two-kernel path.
 
 Reference: fp32 products of the same 16-bit-rounded operands.  dX is rounded to 16 bits once
 (tolerance as tests/test_gpu_tok_gemm.py: |y - ref| <= 1e-2 |ref| + 4e-3 max|ref|; the GELU'
-epilogue uses the A&S erf); dW / db are f32 sums over up to 65 549 tokens in another order
-(relative 1e-4 of the largest entry).  Shapes: the block Linears of stage 0 (K x N = in x out:
+epilogue uses the A&S erf); dW / db are f32 sums over up to 524 288 tokens in another order
+(relative 1e-4 of the largest entry).  M = 524288 is the bench's stage 0 (8 x 256^2 tokens), where
+every workgroup walks many 64- / 32-token steps.  Shapes: the block Linears of stage 0 (K x N = in x out:
 qkv 96 x 288, proj 96 x 96, mlp.0 96 x 384, mlp.3 384 x 96 with and without the GELU' epilogue)
 at a ragged M and above the ops threshold; both 16-bit formats.
 """
@@ -36,7 +37,7 @@ def low(request):
 
 
 @pytest.mark.parametrize("K,N,gg", CASES)
-@pytest.mark.parametrize("M", [1000, 65549])
+@pytest.mark.parametrize("M", [1000, 65549, 524288])
 def test_linear_bwd_matches_fp32(K, N, gg, M, low):
     from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
     L = _lib.lib()
@@ -89,11 +90,14 @@ def _grads(params):
     return [p.grad.clone() for p in params]
 
 
+@pytest.mark.parametrize("amp", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
 @pytest.mark.parametrize("which", ["linear_qkv", "linear_proj", "mlp"])
-def test_ops_one_pass_backward_equals_two_kernel_path(which):
+def test_ops_one_pass_backward_equals_two_kernel_path(which, amp):
     """ops.linear / ops.mlp with trainer-style parameters: the one-pass backward (default) and the
     two-kernel path (input-gradient GEMM + side-stream weight gradient) give the same dX to
-    16-bit rounding and the same dW / db to f32 summation order."""
+    16-bit rounding and the same dW / db to f32 summation order.  The trainer's shadows are bf16:
+    under fp16 autocast the one-pass backward takes a per-call W^T of the f16 weight (it used to
+    be skipped silently); ops.linbwd_calls shows which path ran."""
     from semantic_segmentation_of_stylegan2_artifacts_amd import ops
     M = 8 * 128 * 128  # stage 0 at 512^2
     g = torch.Generator().manual_seed(7)
@@ -102,8 +106,9 @@ def test_ops_one_pass_backward_equals_two_kernel_path(which):
         prev = ops._LINBWD
         ops._LINBWD = fused
         try:
-            x = torch.randn(M, 96, generator=g.manual_seed(7)).to(DEV, torch.bfloat16).requires_grad_(True)
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            calls0 = ops.linbwd_calls
+            x = torch.randn(M, 96, generator=g.manual_seed(7)).to(DEV, amp).requires_grad_(True)
+            with torch.autocast("cuda", dtype=amp):
                 if which == "mlp":
                     params = _direct_params((384, 96), (384,), (96, 384), (96,), seed=3)
                     y = ops.mlp(x, *params)
@@ -115,6 +120,8 @@ def test_ops_one_pass_backward_equals_two_kernel_path(which):
             y.backward(dy)
             ops.join_side_streams()
             torch.cuda.synchronize()
+            ran = ops.linbwd_calls - calls0
+            assert ran == ((2 if which == "mlp" else 1) if fused else 0), (which, amp, fused, ran)
             outs.append((x.grad.float(), _grads(params)))
         finally:
             ops._LINBWD = prev

@@ -576,32 +576,9 @@ def test_window_attention_bf16_grad(B, H, W, nh, shift, low):
 
 
 def _attn_ref_from_qkv(qkv, qkv_bias, table, index, nh, shift):
-    """torchvision semantics given the post-Linear qkv of real tokens; padded tokens take
-    qkv_bias (= Linear of the zero pad)."""
-    B, H, W, C3 = qkv.shape
-    C = C3 // 3
-    ws = 7
-    pad_r, pad_b = (ws - W % ws) % ws, (ws - H % ws) % ws
-    x = torch.nn.functional.pad(qkv - qkv_bias, (0, 0, 0, pad_r, 0, pad_b)) + qkv_bias
-    _, pH, pW, _ = x.shape
-    _, _, sh = osb.effective_shift(H, W, ws, shift)
-    if sum(sh) > 0:
-        x = torch.roll(x, shifts=(-sh[0], -sh[1]), dims=(1, 2))
-    nW = (pH // ws) * (pW // ws)
-    x = x.view(B, pH // ws, ws, pW // ws, ws, C3).permute(0, 1, 3, 2, 4, 5).reshape(B * nW, ws * ws, C3)
-    qkv_ = x.reshape(x.size(0), x.size(1), 3, nh, C // nh).permute(2, 0, 3, 1, 4)
-    q, k, v = qkv_[0] * (C // nh) ** -0.5, qkv_[1], qkv_[2]
-    attn = q.matmul(k.transpose(-2, -1)) + osb.relative_position_bias(table, index, ws)
-    if sum(sh) > 0:
-        mask = osb.shift_mask(pH, pW, ws, sh)
-        attn = attn.view(B, nW, nh, ws * ws, ws * ws) + mask.unsqueeze(1).unsqueeze(0)
-        attn = attn.view(-1, nh, ws * ws, ws * ws)
-    attn = torch.softmax(attn, -1)
-    o = attn.matmul(v).transpose(1, 2).reshape(B * nW, ws * ws, C)
-    o = o.view(B, pH // ws, pW // ws, ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B, pH, pW, C)
-    if sum(sh) > 0:
-        o = torch.roll(o, shifts=(sh[0], sh[1]), dims=(1, 2))
-    return o[:, :H, :W, :]
+    """torchvision semantics given the post-Linear qkv of real tokens (tests/_parity_refs.py)."""
+    from _parity_refs import attn_ref_from_qkv
+    return attn_ref_from_qkv(qkv, qkv_bias, table, nh, shift)
 
 
 def test_window_attention_bf16_dropout_consistency():

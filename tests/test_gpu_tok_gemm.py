@@ -263,3 +263,33 @@ def test_fused_mlp_production_M(strict_fp32):
     and dgrad) at M = 524288 and the stage-1 one at 131072 vs fp32 autograd."""
     test_fused_mlp_matches_fp32(T0, 96, torch.bfloat16)
     test_fused_mlp_matches_fp32(T0 // 4, 192, torch.bfloat16)
+
+
+@pytest.mark.parametrize("M,C", [(4096, 96), (32768, 384)])
+def test_linear_cat_direct_grad_accumulates(M, C):
+    """Trainer-style parameters (flat .grad, _msu_direct): linear_cat's two weight-gradient halves
+    accumulate straight into the column slices of weight.grad (msu_linear_wgrad_ld, row stride
+    2C) and the bias gradient into bias.grad -- no temporaries, no torch adds; the result equals
+    the preset .grad plus the fp32 gradient of Linear(cat([x, skip]))."""
+    ops = _ops()
+    low = torch.bfloat16
+    g = torch.Generator().manual_seed(M + 3 * C)
+    x = torch.randn(M, C, generator=g).to(DEV, low)
+    sk = torch.randn(M, C, generator=g).to(DEV, low)
+    w = (torch.randn(C, 2 * C, generator=g) / (2 * C) ** 0.5).to(DEV)
+    b = torch.randn(C, generator=g).to(DEV)
+    dy = torch.randn(M, C, generator=g).to(DEV, low)
+    wp, bp = torch.nn.Parameter(w.clone()), torch.nn.Parameter(b.clone())
+    w0 = torch.randn(C, 2 * C, generator=g).to(DEV)
+    b0 = torch.randn(C, generator=g).to(DEV)
+    wp.grad, bp.grad = w0.clone(), b0.clone()
+    wp._msu_direct = bp._msu_direct = True
+    with torch.autocast("cuda", dtype=low):
+        y = ops.linear_cat(x, sk, wp, bp)
+    y.backward(dy)
+    ops.join_side_streams()
+    torch.cuda.synchronize()
+    ref_w = dy.float().t() @ torch.cat([x, sk], -1).float()
+    ref_b = dy.float().sum(0)
+    assert (wp.grad - w0 - ref_w).abs().max().item() <= 1e-4 * ref_w.abs().max().item()
+    assert (bp.grad - b0 - ref_b).abs().max().item() <= 1e-4 * ref_b.abs().max().item() + 1e-3

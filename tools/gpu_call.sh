@@ -1,0 +1,50 @@
+# One GPU call, named steps run in order, each under its own time limit; the call stops at the
+# first step that faults, aborts or times out (exit status > 1).  Logs: gpurun_out/TAG_<step>.log
+#   bash tools/gpu_call.sh TAG step [step ...]
+# steps: tests_new (the round's new GPU tests), tests (whole -m gpu suite), bench,
+#        wgrad_ab (wgrad timing, XCD-grouped vs linear grid), wgrad_pmc (HBM counters, both),
+#        prof (eager step under rocprofv3 --kernel-trace --stats)
+TAG=$1; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 $secs "$@" > $O/${TAG}_$name.log 2>&1
+  local rc=$?
+  tail -4 $O/${TAG}_$name.log
+  echo "== $name rc=$rc"
+  if [ $rc -gt 1 ]; then exit $rc; fi
+}
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
+for s in "$@"; do
+  case $s in
+    tests_new) step tests_new 600 $PYT -m gpu $R/tests/test_gpu_production_parity.py $R/tests/test_gpu_bench_dp.py \
+                 $R/tests/test_gpu_linbwd.py "$R/tests/test_gpu_tok_gemm.py::test_linear_cat_direct_grad_accumulates" \
+                 "$R/tests/test_gpu_graph.py::test_eager_side_stream_step_is_deterministic" ;;
+    tests) step tests 900 python -u -m pytest $R/tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    bench) step bench 480 python -u $R/bench.py
+           grep '^{' $O/${TAG}_bench.log > $O/${TAG}_bench.json ;;
+    wgrad_ab)
+      for x in 1 0 1 0; do
+        for shp in "32768 1152 384" "32768 384 1536" "131072 576 192" "8192 2304 768" "131072 192 768"; do
+          MSU_WGRAD_XCD=$x timeout -k 10 60 python -u $R/tools/wgrad_one.py $shp 50 >> $O/${TAG}_wgrad_ab.log 2>&1 || exit 3
+          echo "xcd=$x" >> $O/${TAG}_wgrad_ab.log
+        done
+      done
+      tail -20 $O/${TAG}_wgrad_ab.log ;;
+    wgrad_pmc)
+      for x in 1 0; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+          MSU_WGRAD_XCD=$x timeout -s KILL 90 rocprofv3 --pmc $c -d $O/${TAG}_wpmc_${x}_$c -o p --output-format csv -- \
+            python3 $R/tools/wgrad_one.py 32768 1152 384 10 > $O/${TAG}_wpmc_${x}_$c.log 2>&1 || exit 3
+        done
+      done ;;
+    prof) step prof 420 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o p --output-format csv -- \
+            python3 $R/bench.py --steps 8 --warmup 4 --no-roofline --no-cpu-baseline --no-input-pipeline ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo done
