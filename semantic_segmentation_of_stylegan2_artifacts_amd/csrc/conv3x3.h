@@ -536,13 +536,17 @@ constexpr int V3_HALO_TAP = 1;
 constexpr int SPRE = 12;  // GELU' operand loads per lane (dgrad), issued at tap 7
 
 MSU_DEV int swz(int p) { return (p >> 2) & 3; }
+// M16 (16x16x32 MFMA) fragment reads: 16 consecutive rows, chunk (lane >> 4) of a 4-chunk group;
+// the ds_read_b128 lane groups ({0-3, 12-15, 20-27}, ...) mix two chunks of 8 + 8 rows, which
+// (p >> 1) & 3 spreads over all 16 bank slots for ANY first row (checked exhaustively offline)
+template <bool M16> MSU_DEV int swzv(int p) { return M16 ? (p >> 1) & 3 : (p >> 2) & 3; }
 
 // SPREAD: the next tile's halo loads are issued in seven parts at taps 1..7 (each part issued
 // after that tap's weight DMA, so it only has to land two taps later) instead of all at tap 1,
 // where the wait for tap 3's weights also waited for the whole 117 KB halo.
 MSU_DEV constexpr int halo_part_lo(int t, int nhc) { return (t - 1) * nhc / 7; }  // t = 1..7
 
-template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL, bool SPREAD>
+template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL, bool SPREAD, bool M16>
 __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restrict__ X,
                                                          const bf16_t* __restrict__ Wt,
                                                          const float* __restrict__ bias,
@@ -614,7 +618,7 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
     int p = t / CH;
 #pragma unroll
     for (int c = 0; c < NHC; ++c) {
-      if (hact && p < HPIX) *reinterpret_cast<u32x4*>(sX + p * C + ((hch ^ swz(p)) << 3)) = hr[c];
+      if (hact && p < HPIX) *reinterpret_cast<u32x4*>(sX + p * C + ((hch ^ swzv<M16>(p)) << 3)) = hr[c];
       p += PSTEP;
     }
   };
@@ -630,7 +634,7 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
 #pragma unroll
     for (int r = 0; r < WPER; ++r) {
       const int k = wave + NW * r;
-      if (WINS % NW == 0 || k < WINS) glds16(src + row * C + ((pos ^ swz(row)) << 3), dst + 512 * k);
+      if (WINS % NW == 0 || k < WINS) glds16(src + row * C + ((pos ^ swzv<M16>(row)) << 3), dst + 512 * k);
       pos += (64 * NW) % CH;
       row += (64 * NW) / CH;
       if (pos >= CH) {
@@ -660,18 +664,34 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
   auto koff = [&](int sw, int odd) { return ((2 * odd + h) ^ sw) << 3; };
   const int wsw = swz(xl);  // weight rows 32n + xl
   const int wk0 = xl * C + koff(wsw, 0), wk1 = xl * C + koff(wsw, 1);
+  // M16: lane l reads row (l & 15) of a 16-row fragment, chunk 4 ks + (l >> 4)
+  const int l15 = lane & 15, g4 = lane >> 4;
+  const int wk16 = l15 * C + ((g4 ^ swzv<true>(l15)) << 3);  // weight rows 16n + l15
 
   for (; tile < ntiles; tile += gridDim.x) {
     const int next = tile + gridDim.x;
     int b, y0, x0;
     coords(tile, b, y0, x0);
     const int xo = x0 + xl;
-    f32x16 acc[MT][3];
+    // accumulators: 32x32 tiles [row m][co tile n] (!M16) or 16x16 tiles [row m][pixel tile
+    // pt][co tile n] (M16); the other form is a 1-element placeholder
+    f32x16 acc[M16 ? 1 : MT][M16 ? 1 : 3];
+    f32x4 acc4[M16 ? MT : 1][M16 ? 2 : 1][M16 ? 6 : 1];
+    if constexpr (M16) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int n = 0; n < 3; ++n) acc[m][n] = f32x16{0};
-    u32x4 sp[OUT_GGRAD ? MT : 1][OUT_GGRAD ? 3 : 1][2];
+        for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+          for (int n = 0; n < 6; ++n) acc4[m][pt][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n) acc[m][n] = f32x16{0};
+    }
+    // dgrad GELU' operands: 12 16-B pieces per lane in both forms
+    u32x4 sp[OUT_GGRAD ? MT : 1][OUT_GGRAD ? (M16 ? 2 : 3) : 1][OUT_GGRAD ? (M16 ? 3 : 2) : 1];
 
     static_for([&](auto TAP) {
       constexpr int tap = decltype(TAP)::value;
@@ -706,57 +726,111 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
         // dgrad: the pre-activation S of this tile's outputs for the GELU' epilogue
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          const int y = min(y0 + 2 * wave + m, g.H - 1), xs = min(xo, g.W - 1);
+          const int y = min(y0 + 2 * wave + m, g.H - 1);
+          if constexpr (M16) {
 #pragma unroll
-          for (int n = 0; n < 3; ++n)
+            for (int pt = 0; pt < 2; ++pt) {
+              const int xs = min(x0 + 16 * pt + l15, g.W - 1);
 #pragma unroll
-            for (int pp = 0; pp < 2; ++pp)
-              sp[m][n][pp] = *reinterpret_cast<const u32x4*>(S + pix_off32<OUT_D2S>(b, y, xs, g.H, g.W, C) + 32 * n +
-                                                             16 * pp + 8 * h);
+              for (int q = 0; q < 3; ++q)
+                sp[m][pt][q] = *reinterpret_cast<const u32x4*>(S + pix_off32<OUT_D2S>(b, y, xs, g.H, g.W, C) + 32 * q +
+                                                               16 * (g4 & 1) + 8 * (g4 >> 1));
+            }
+          } else {
+            const int xs = min(xo, g.W - 1);
+#pragma unroll
+            for (int n = 0; n < 3; ++n)
+#pragma unroll
+              for (int pp = 0; pp < 2; ++pp)
+                sp[m][n][pp] = *reinterpret_cast<const u32x4*>(S + pix_off32<OUT_D2S>(b, y, xs, g.H, g.W, C) + 32 * n +
+                                                               16 * pp + 8 * h);
+          }
         }
       }
-      // fragment lane offsets of this tap: X rows 2w + m + dy, pixels dx + xl
-      // (recomputed per tap through opaque(): hoisted, the nine taps' offsets would pin 36 VGPRs)
-      int xo0[MT], xo1[MT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int p = opaque((2 * wave + m + dy) * HWD + dx) + xl;
-        xo0[m] = p * C + koff(swz(p), 0);
-        xo1[m] = p * C + koff(swz(p), 1);
-      }
-      // X fragments double buffered (k step ks + 1 read before the MFMAs of ks); each weight
-      // fragment is read one co tile ahead of its two MFMAs (registers: the halo prefetch
-      // holds 60 VGPRs across the taps)
-      bf16x8 xa[2][MT], wf[2];
-      auto read_x = [&](auto KSI, int set) __attribute__((always_inline)) {
-        constexpr int ks = decltype(KSI)::value;
-        constexpr int kb = 32 * (ks >> 1);  // elements: 4 chunks per even / odd pair
+      if constexpr (M16) {
+        // fragment lane offsets of this tap: X rows 2w + m + dy, pixels dx + 16 pt + l15
+        int xq[MT][2];
 #pragma unroll
         for (int m = 0; m < MT; ++m)
-          xa[set][m] = *reinterpret_cast<const bf16x8*>(sX + ((ks & 1) ? xo1[m] : xo0[m]) + kb);
-      };
-      auto read_w = [&](auto KSI, int n) __attribute__((always_inline)) -> bf16x8 {
-        constexpr int ks = decltype(KSI)::value;
-        constexpr int kb = 32 * (ks >> 1);
-        return *reinterpret_cast<const bf16x8*>(wcur + 32 * n * C + ((ks & 1) ? wk1 : wk0) + kb);
-      };
-      read_x(IC<0>{}, 0);
-      wf[0] = read_w(IC<0>{}, 0);
-      static_for([&](auto KSI) {
-        constexpr int ks = decltype(KSI)::value;
-        constexpr int cur = ks & 1;
-        if constexpr (ks + 1 < 6) read_x(IC<ks + 1>{}, cur ^ 1);
-        static_for([&](auto NI) {
-          constexpr int n = decltype(NI)::value;
-          constexpr int j = 3 * ks + n;  // weight fragment sequence number: register set j & 1
-          // (reading it two groups ahead in a ring of three measured no faster and spills the dgrad)
-          if constexpr (n < 2) wf[(j + 1) & 1] = read_w(IC<ks>{}, n + 1);
-          else if constexpr (ks + 1 < 6) wf[(j + 1) & 1] = read_w(IC<ks + 1>{}, 0);
 #pragma unroll
-          for (int m = 0; m < MT; ++m) acc[m][n] = Fmt16<T>::mma32(wf[j & 1], xa[cur][m], acc[m][n]);
-        }, std::make_integer_sequence<int, 3>{});
-        __builtin_amdgcn_sched_barrier(0);
-      }, std::make_integer_sequence<int, 6>{});
+          for (int pt = 0; pt < 2; ++pt) {
+            const int p = opaque((2 * wave + m + dy) * HWD + dx + 16 * pt) + l15;
+            xq[m][pt] = p * C + ((g4 ^ swzv<true>(p)) << 3);
+          }
+        // groups (ks, m) in sequence: a group's two X fragments (pixel tiles) feed 12 MFMAs, the
+        // next group's are read at its start; weight fragments in a ring of two, one co tile
+        // ahead (re-read per row m: 16 reads per 24 MFMAs, within the LDS budget of 16x16x32
+        // gaps; double-buffering all four X fragments of a k step spilled)
+        bf16x8 xb[2][2], wf[2];
+        auto read_x = [&](auto GI, int set) __attribute__((always_inline)) {
+          constexpr int gi = decltype(GI)::value, ks = gi / MT, m = gi % MT;
+#pragma unroll
+          for (int pt = 0; pt < 2; ++pt) xb[set][pt] = *reinterpret_cast<const bf16x8*>(sX + xq[m][pt] + 32 * ks);
+        };
+        auto read_w = [&](auto GI, int n) __attribute__((always_inline)) -> bf16x8 {
+          constexpr int ks = decltype(GI)::value / MT;
+          return *reinterpret_cast<const bf16x8*>(wcur + 16 * n * C + wk16 + 32 * ks);
+        };
+        read_x(IC<0>{}, 0);
+        wf[0] = read_w(IC<0>{}, 0);
+        static_for([&](auto GI) {
+          constexpr int gi = decltype(GI)::value, m = gi % MT;
+          constexpr int cur = gi & 1;
+          if constexpr (gi + 1 < 3 * MT) read_x(IC<gi + 1>{}, cur ^ 1);
+          static_for([&](auto NI) {
+            constexpr int n = decltype(NI)::value;
+            constexpr int j = 6 * gi + n;  // weight fragment sequence number: register set j & 1
+            if constexpr (n < 5) wf[(j + 1) & 1] = read_w(IC<gi>{}, n + 1);
+            else if constexpr (gi + 1 < 3 * MT) wf[(j + 1) & 1] = read_w(IC<gi + 1>{}, 0);
+#pragma unroll
+            for (int pt = 0; pt < 2; ++pt) acc4[m][pt][n] = Fmt16<T>::mma16(wf[j & 1], xb[cur][pt], acc4[m][pt][n]);
+          }, std::make_integer_sequence<int, 6>{});
+          __builtin_amdgcn_sched_barrier(0);
+        }, std::make_integer_sequence<int, 3 * MT>{});
+      } else {
+        // fragment lane offsets of this tap: X rows 2w + m + dy, pixels dx + xl
+        // (recomputed per tap through opaque(): hoisted, the nine taps' offsets would pin 36 VGPRs)
+        int xo0[MT], xo1[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int p = opaque((2 * wave + m + dy) * HWD + dx) + xl;
+          xo0[m] = p * C + koff(swz(p), 0);
+          xo1[m] = p * C + koff(swz(p), 1);
+        }
+        // X fragments double buffered (k step ks + 1 read before the MFMAs of ks); each weight
+        // fragment is read one co tile ahead of its two MFMAs (registers: the halo prefetch
+        // holds 60 VGPRs across the taps)
+        bf16x8 xa[2][MT], wf[2];
+        auto read_x = [&](auto KSI, int set) __attribute__((always_inline)) {
+          constexpr int ks = decltype(KSI)::value;
+          constexpr int kb = 32 * (ks >> 1);  // elements: 4 chunks per even / odd pair
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            xa[set][m] = *reinterpret_cast<const bf16x8*>(sX + ((ks & 1) ? xo1[m] : xo0[m]) + kb);
+        };
+        auto read_w = [&](auto KSI, int n) __attribute__((always_inline)) -> bf16x8 {
+          constexpr int ks = decltype(KSI)::value;
+          constexpr int kb = 32 * (ks >> 1);
+          return *reinterpret_cast<const bf16x8*>(wcur + 32 * n * C + ((ks & 1) ? wk1 : wk0) + kb);
+        };
+        read_x(IC<0>{}, 0);
+        wf[0] = read_w(IC<0>{}, 0);
+        static_for([&](auto KSI) {
+          constexpr int ks = decltype(KSI)::value;
+          constexpr int cur = ks & 1;
+          if constexpr (ks + 1 < 6) read_x(IC<ks + 1>{}, cur ^ 1);
+          static_for([&](auto NI) {
+            constexpr int n = decltype(NI)::value;
+            constexpr int j = 3 * ks + n;  // weight fragment sequence number: register set j & 1
+            // (reading it two groups ahead in a ring of three measured no faster and spills the dgrad)
+            if constexpr (n < 2) wf[(j + 1) & 1] = read_w(IC<ks>{}, n + 1);
+            else if constexpr (ks + 1 < 6) wf[(j + 1) & 1] = read_w(IC<ks + 1>{}, 0);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) acc[m][n] = Fmt16<T>::mma32(wf[j & 1], xa[cur][m], acc[m][n]);
+          }, std::make_integer_sequence<int, 3>{});
+          __builtin_amdgcn_sched_barrier(0);
+        }, std::make_integer_sequence<int, 6>{});
+      }
       if constexpr (tap == 8) {
         if (next < ntiles) {
           __syncthreads();  // every wave's last halo read done (s_barrier + lgkmcnt)
@@ -767,6 +841,60 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
     }, std::make_integer_sequence<int, 9>{});
     (void)my_wdma;
 
+    if constexpr (M16) {
+      // epilogue: lane holds pixel x0 + 16 pt + l15, channels 16n + 4 g4 + r; a permlane16 swap
+      // of co tiles (2q, 2q + 1) gives every lane 8 consecutive channels co8 .. co8 + 7 with
+      // co8 = 16 (2q + (g4 & 1)) + 8 (g4 >> 1) (lanes l, l ^ 16 share the pixel)
+      const int cofs = 16 * (g4 & 1) + 8 * (g4 >> 1);
+      float4 bq[3][2];
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          bq[q][0] = *reinterpret_cast<const float4*>(bias + 32 * q + cofs);
+          bq[q][1] = *reinterpret_cast<const float4*>(bias + 32 * q + cofs + 4);
+        }
+      }
+      if constexpr (BIAS || OUT_GGRAD) wait_vmcnt<0>();
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) {
+        const int px = x0 + 16 * pt + l15;
+        if (px >= g.W) continue;  // lanes l and l ^ 16 agree
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          if constexpr (BIAS) {
+            const float4 t0 = bq[q][0], t1 = bq[q][1];
+            bv[0] = t0.x; bv[1] = t0.y; bv[2] = t0.z; bv[3] = t0.w;
+            bv[4] = t1.x; bv[5] = t1.y; bv[6] = t1.z; bv[7] = t1.w;
+          }
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            const int y = y0 + 2 * wave + m;
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc4[m][pt][2 * q][i]),
+                                                              __float_as_uint(acc4[m][pt][2 * q + 1][i]), false, false);
+              v[i] = __uint_as_float(r[0]) + bv[i];
+              v[4 + i] = __uint_as_float(r[1]) + bv[4 + i];
+            }
+            if (y >= g.H) continue;
+            if constexpr (OUT_GGRAD) {
+              const u32x4 t = sp[m][pt][q];
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                v[2 * i] *= gelu_grad_fast(Fmt16<T>::lo(t[i]));
+                v[2 * i + 1] *= gelu_grad_fast(Fmt16<T>::hi(t[i]));
+              }
+            }
+            const u32x4 pk = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
+            const int off = pix_off32<OUT_D2S>(b, y, px, g.H, g.W, C) + 32 * q + cofs;
+            *reinterpret_cast<u32x4*>(Y + off) = pk;
+            if constexpr (DUAL) *reinterpret_cast<u32x4*>(Y2 + off) = gelu8<T>(pk);
+          }
+        }
+      }
+    } else {
     // epilogue: lane holds pixel xo, channels 32n + 8q + 4h + e of rows 2w + m; the
     // permlane32 swap gives lane l < 32 channels 32n + 16pp + 0..7 and l + 32 the next 8
     // bias columns of this lane's 6 store groups, loaded together: one wait, not one per
@@ -821,6 +949,7 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
             if constexpr (DUAL) *reinterpret_cast<u32x4*>(Y2 + off) = gelu8<T>(pk);
           }
         }
+    }
     }
     if (next < ntiles) {
       // the next tile's halo (stored after tap 8) visible to every wave before its tap 0
@@ -1481,12 +1610,12 @@ inline bool conv_v3_spread() {
   return on;
 }
 
-template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL, bool SPREAD>
+template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL, bool SPREAD, bool M16>
 int launch_v3s(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S, bf16_t* Y,
                bf16_t* Y2, hipStream_t st) {
   constexpr size_t lds = sizeof(bf16_t) * ((size_t)18 * 34 * 96 + 2 * 96 * 96);
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = conv3x3_v3_kernel<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, SPREAD>;
+  auto kern = conv3x3_v3_kernel<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, SPREAD, M16>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1501,6 +1630,17 @@ int launch_v3s(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float
   gp.prio = prio;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, X, Wt, bias, S, Y, Y2, gp, (int)ntiles);
   return MSU_CHECK_LAUNCH();
+}
+
+// v3 on 16x16x32 MFMA (same tile, LDS images and schedule; (p >> 1) & 3 swizzle): A/B switch
+// MSU_CONV_MFMA=16 (bare MFMA loops of this shape ran at ~1.12-1.15x the FLOP/s of 32x32x16 on
+// MI355X at equal cycles, MI355X_MICROARCH.md: the clock it holds)
+inline bool conv_v3_m16() {
+  static const bool on = [] {
+    const char* e = getenv("MSU_CONV_MFMA");
+    return e && e[0] == '1' && e[1] == '6';
+  }();
+  return on;
 }
 
 // v4 (one wave per SIMD, 4 rows per wave): opt-in A/B switch MSU_CONV_V=4 (measured 7-10 %
@@ -1536,9 +1676,14 @@ template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool
 int launch_v3(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S, bf16_t* Y,
               bf16_t* Y2, hipStream_t st) {
   if (conv_v4_enabled()) return launch_v4<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL>(g, X, Wt, bias, S, Y, Y2, st);
+  // (forward launches only: with the dgrad's GELU' operands held from tap 7 the 16x16 form
+  // spills 260 B per lane)
+  if constexpr (!OUT_GGRAD)
+    if (conv_v3_m16())
+      return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, true, true>(g, X, Wt, bias, S, Y, Y2, st);
   if (conv_v3_spread())
-    return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, true>(g, X, Wt, bias, S, Y, Y2, st);
-  return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, false>(g, X, Wt, bias, S, Y, Y2, st);
+    return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, true, false>(g, X, Wt, bias, S, Y, Y2, st);
+  return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, false, false>(g, X, Wt, bias, S, Y, Y2, st);
 }
 
 template <typename T, bool IN_D2S, bool IN_GELU, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL = false>

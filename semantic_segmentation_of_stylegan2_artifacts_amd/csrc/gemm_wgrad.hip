@@ -348,6 +348,21 @@ inline void pick_wave_split(int nt, int kt, int& wn, int& wk) {
     wk = 1;
     return;
   }
+  // A/B switch MSU_WGRAD_SPLIT=WN,WK forces a split where the tile counts allow it
+  static const int forced = [] {
+    const char* e = getenv("MSU_WGRAD_SPLIT");
+    return e && e[0] >= '1' && e[0] <= '4' && e[1] == ',' && e[2] >= '1' && e[2] <= '4' ? (e[0] - '0') * 8 + (e[2] - '0')
+                                                                                          : 0;
+  }();
+  if (forced) {
+    const int fw = forced / 8, fk = forced % 8;
+    const bool instantiated = fw * fk <= 4 && (fw == 1 || fk == 1 || (fw == 2 && fk == 2));
+    if (instantiated && nt % fw == 0 && kt % fk == 0) {
+      wn = fw;
+      wk = fk;
+      return;
+    }
+  }
   static const int cand[8][2] = {{4, 1}, {2, 2}, {1, 4}, {3, 1}, {1, 3}, {2, 1}, {1, 2}, {1, 1}};
   long best = -1;
   for (const auto& c : cand) {

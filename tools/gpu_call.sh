@@ -42,6 +42,31 @@ for s in "$@"; do
             python3 $R/tools/wgrad_one.py 32768 1152 384 10 > $O/${TAG}_wpmc_${x}_$c.log 2>&1 || exit 3
         done
       done ;;
+    conv_ab)
+      for v in "" 16 "" 16; do
+        echo "MSU_CONV_MFMA=$v" >> $O/${TAG}_conv_ab.log
+        MSU_CONV_MFMA=$v timeout -k 10 180 python -u $R/tools/kbench.py conv >> $O/${TAG}_conv_ab.log 2>&1 || exit 3
+      done
+      tail -12 $O/${TAG}_conv_ab.log ;;
+    conv16_tests) MSU_CONV_MFMA=16 step conv16_tests 400 $PYT -m gpu $R/tests/test_gpu_production_parity.py -k refine \
+                    $R/tests/test_gpu_ops.py -k "refine_conv_act" ;;
+    wgrad_split)
+      for sp in "" "1,1" "2,1" "4,1"; do
+        echo "MSU_WGRAD_SPLIT=$sp" >> $O/${TAG}_wgrad_split.log
+        MSU_WGRAD_SPLIT=$sp timeout -k 10 60 python -u $R/tools/wgrad_one.py 32768 1152 384 50 >> $O/${TAG}_wgrad_split.log 2>&1 || exit 3
+        for c in FETCH_SIZE WRITE_SIZE; do
+          MSU_WGRAD_SPLIT=$sp timeout -s KILL 90 rocprofv3 --pmc $c -d $O/${TAG}_wsp_${sp/,/_}_$c -o p --output-format csv -- \
+            python3 $R/tools/wgrad_one.py 32768 1152 384 10 > /dev/null 2>&1 || exit 3
+        done
+      done
+      tail -8 $O/${TAG}_wgrad_split.log ;;
+    nt_pmc)
+      timeout -k 10 60 python -u $R/tools/nt_one.py 32768 1152 384 50 > $O/${TAG}_nt.log 2>&1 || exit 3
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT \
+        -d $O/${TAG}_ntpmc1 -o p --output-format csv -- python3 $R/tools/nt_one.py 32768 1152 384 10 >> $O/${TAG}_nt.log 2>&1 || exit 3
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT \
+        -d $O/${TAG}_ntpmc2 -o p --output-format csv -- python3 $R/tools/nt_one.py 32768 1152 384 10 >> $O/${TAG}_nt.log 2>&1 || exit 3
+      cat $O/${TAG}_nt.log | grep "nt M" ;;
     prof) step prof 420 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o p --output-format csv -- \
             python3 $R/bench.py --steps 8 --warmup 4 --no-roofline --no-cpu-baseline --no-input-pipeline ;;
     *) echo "unknown step $s"; exit 2 ;;
