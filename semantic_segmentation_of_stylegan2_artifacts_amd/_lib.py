@@ -64,6 +64,7 @@ SIGNATURES = {
     "msu_tok_gemm": (I, [I, P, P, I, P, P, P, P, P, L, I, I, I, P]),
     "msu_tok_gemm_plan": (I, [L, I, I, P]),
     "msu_nt_gemm_supported": (I, [L, I, I]),
+    "msu_nt_gemm_plan": (I, [L, I]),
     "msu_nt_gemm": (I, [I, P, P, P, P, P, P, L, I, I, I, P]),
     "msu_nt_gemm_kn": (I, [I, P, P, P, P, P, P, L, I, I, I, P]),
     "msu_nt_gemm_cat": (I, [I, P, P, I, P, P, P, L, I, I, P]),
@@ -95,6 +96,12 @@ def lib():
         fn.argtypes = args
     _lib = h
     return _lib
+
+
+def plan_nt(M, N):
+    """(tile rows, tile columns) msu_nt_gemm uses for an M x N output."""
+    v = lib().msu_nt_gemm_plan(M, N)
+    return v // 1000, v % 1000
 
 
 def call(name, *args):

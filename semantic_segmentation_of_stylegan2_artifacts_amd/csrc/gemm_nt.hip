@@ -29,7 +29,7 @@
 
 namespace {
 
-constexpr int BN = 128, BK = 64, CH = BK / 8;  // N tile, K step, 16-B chunks per row and step
+constexpr int BN = 128, BK = 64, CH = BK / 8;  // N tile (KN form), K step, 16-B chunks per row and step
 enum { EPI_PLAIN = 0, EPI_GELU_DUAL = 1, EPI_GELU_GRAD = 2 };
 
 struct NtArgs {
@@ -123,17 +123,22 @@ struct KnTile {
 //   WM = 4, NST = 3: 256 x 128, 144 KB ring, one 8-wave workgroup per CU, two K steps in flight
 //   across the raw barrier (counted vmcnt: the DMAs of the younger step and the epilogue stores
 //   issued after the awaited step's DMA may stay outstanding).
-template <typename T, int EPI, int WM, int NST, bool WKN>
+// BNT: the tile's column width, 128 or 192 (waves 64 x 64 or 64 x 96: NI = 2 or 3 column
+// accumulators).  192 makes the N = 384 / 768 / 1152 / 2304 shapes of Swin-T's stages 2-3 whole
+// rounds of tiles on 256 CUs (N = 384 at M = 32768: 256 tiles of 256 x 192 instead of 384 of
+// 256 x 128, i.e. 1.5 rounds); KN (input-gradient) form: 128 only.
+template <typename T, int EPI, int WM, int NST, bool WKN, int BNT>
 __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
-  constexpr int NTHR = 128 * WM, BM = 64 * WM;
+  constexpr int NTHR = 128 * WM, BM = 64 * WM, NI = BNT / 64;
+  static_assert(!WKN || BNT == BN, "KN tiles are 128 wide");
   typedef RowTile<BM, NTHR> TA;
-  typedef RowTile<BN, NTHR> TW;
+  typedef RowTile<BNT, NTHR> TW;
   typedef KnTile<NTHR> TK;
   constexpr int KSL = BK / 16;  // 16-wide k slices per step
-  constexpr int STG = (BM + BN) * BK;  // elements per ring stage
+  constexpr int STG = (BM + BNT) * BK;  // elements per ring stage
   // per thread and step: DMA instructions, and epilogue stores of a tile
   constexpr int D = TA::PER + (WKN ? TK::PER : TW::PER);
-  constexpr int E = EPI == EPI_GELU_DUAL ? 16 : 8;
+  constexpr int E = (EPI == EPI_GELU_DUAL ? 8 : 4) * NI;
   static_assert(NST == 2 || NST == 3, "ring depth");
   static_assert(NST == 2 || (D + E < 64), "vmcnt range");
   __shared__ __attribute__((aligned(16))) bf16_t lds[NST * STG];
@@ -157,13 +162,13 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     if (a.A2 == nullptr) TA::stage(a.A, mt * BM, a.M, a.K, kk * BK, dst, tid);
     else if (kk * BK < a.K1) TA::stage(a.A, mt * BM, a.M, a.K1, kk * BK, dst, tid);  // K1 % BK == 0
     else TA::stage(a.A2, mt * BM, a.M, a.K - a.K1, kk * BK - a.K1, dst, tid);
-    if constexpr (WKN) TK::stage(a.W, nt * BN, a.N, kk * BK, dst + BM * BK, tid);
-    else TW::stage(a.W, nt * BN, a.N, a.K, kk * BK, dst + BM * BK, tid);
+    if constexpr (WKN) TK::stage(a.W, nt * BNT, a.N, kk * BK, dst + BM * BK, tid);
+    else TW::stage(a.W, nt * BNT, a.N, a.K, kk * BK, dst + BM * BK, tid);
   };
 
-  f32x16 acc[2][2];  // [column tile ni][token tile mi]: C^T, W rows on the accumulator rows
+  f32x16 acc[NI][2];  // [column tile ni][token tile mi]: C^T, W rows on the accumulator rows
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
 
@@ -199,18 +204,19 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     const bool last = kk + 1 == nk;
     const int t = L + ti * G;
     const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
-    const int m0 = mt * BM, n0 = nt * BN;
+    const int m0 = mt * BM, n0 = nt * BNT;
     const int hh = lane >> 5;
+    constexpr int WNC = BNT / 2;  // columns per wave
     // the epilogue's operands (bias columns, GELU' pre-activations), loaded before the tile's
     // last MFMAs and before the next stage's DMA: one counted wait in the epilogue
-    float4 eb[2][2][2];
-    u32x4 eh[2][2][2];
+    float4 eb[NI][2][2];
+    u32x4 eh[2][NI][2];
     if (last) {
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
+      for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
-          const int n = min(n0 + 64 * wn + 32 * ni + 16 * g + 8 * hh, a.N - 8);
+          const int n = min(n0 + WNC * wn + 32 * ni + 16 * g + 8 * hh, a.N - 8);
           if constexpr (EPI == EPI_GELU_GRAD) {
 #pragma unroll
             for (int mi = 0; mi < 2; ++mi) {
@@ -228,14 +234,12 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     const bf16_t* ta = lds + cst * STG;
     const bf16_t* tw = ta + BM * BK;
     cst = cst + 1 == NST ? 0 : cst + 1;
-    bf16x8 fw[2][2], fx[2][2];
+    bf16x8 fw[2][NI], fx[2][2];
     auto rd = [&](int ks, int set) {
-      if constexpr (WKN) {
-        fw[set][0] = TK::frag(tw, 64 * wn, ks, lane);
-        fw[set][1] = TK::frag(tw, 64 * wn + 32, ks, lane);
-      } else {
-        fw[set][0] = TW::frag(tw, 64 * wn, ks, lane);
-        fw[set][1] = TW::frag(tw, 64 * wn + 32, ks, lane);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        if constexpr (WKN) fw[set][ni] = TK::frag(tw, WNC * wn + 32 * ni, ks, lane);
+        else fw[set][ni] = TW::frag(tw, WNC * wn + 32 * ni, ks, lane);
       }
       fx[set][0] = TA::frag(ta, 64 * wm, ks, lane);
       fx[set][1] = TA::frag(ta, 64 * wm + 32, ks, lane);
@@ -245,10 +249,11 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     for (int ks = 0; ks < KSL; ++ks) {
       const int cur = ks & 1;
       if (ks + 1 < KSL) rd(ks + 1, cur ^ 1);
-      acc[0][0] = Fmt16<T>::mma32(fw[cur][0], fx[cur][0], acc[0][0]);
-      acc[0][1] = Fmt16<T>::mma32(fw[cur][0], fx[cur][1], acc[0][1]);
-      acc[1][0] = Fmt16<T>::mma32(fw[cur][1], fx[cur][0], acc[1][0]);
-      acc[1][1] = Fmt16<T>::mma32(fw[cur][1], fx[cur][1], acc[1][1]);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        acc[ni][0] = Fmt16<T>::mma32(fw[cur][ni], fx[cur][0], acc[ni][0]);
+        acc[ni][1] = Fmt16<T>::mma32(fw[cur][ni], fx[cur][1], acc[ni][1]);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if (!last) {
@@ -258,7 +263,7 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     kk = 0;
     ++ti;
     epi_age = 0;
-    epi_full = m0 + 64 * wm + 64 <= a.M && n0 + 64 * wn + 64 <= a.N;
+    epi_full = m0 + 64 * wm + 64 <= a.M && n0 + WNC * wn + WNC <= a.N;
     // the epilogue operands (and every older DMA) have landed; the DMA just issued may stay
     // in flight (NST = 3).  One wait, not one per exec-masked store branch.
     if (NST == 3 && more) wait_vmcnt<D>();
@@ -269,7 +274,7 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     for (int mi = 0; mi < 2; ++mi) {
       const int m = m0 + 64 * wm + 32 * mi + (lane & 31);
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
+      for (int ni = 0; ni < NI; ++ni) {
 #pragma unroll
         for (int g0 = 0; g0 < 4; g0 += 2) {
           float v[8];
@@ -280,7 +285,7 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
             v[i] = __uint_as_float(r[0]);
             v[4 + i] = __uint_as_float(r[1]);
           }
-          const int n = n0 + 64 * wn + 32 * ni + 8 * g0 + 8 * hh;
+          const int n = n0 + WNC * wn + 32 * ni + 8 * g0 + 8 * hh;
           if (m >= a.M || n >= a.N) continue;
           if (EPI != EPI_GELU_GRAD && a.bias) {
             const float4 b0 = eb[ni][g0 >> 1][0], b1 = eb[ni][g0 >> 1][1];
@@ -311,7 +316,7 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
   }
@@ -331,30 +336,57 @@ int num_cus_nt() {
   return cus;
 }
 
-// Tile configuration of a shape: the 256 x 128 tile (WM = 4, three-stage ring, one workgroup
-// per CU) when it still gives every CU a tile, else 128 x 128 (two workgroups per CU).  A/B
-// switch MSU_NT_TILE = 128 | 256 forces one.
-int nt_wm(long M, int N) {
-  static const int force = [] {
+// Tile configuration of a shape, by a rounds-of-tiles cost model: the output is covered in
+// rounds of (CUs x workgroups per CU) tiles, each round costing a workgroup's tile area times the
+// workgroups sharing a CU (x 1.05 for the two-stage ring of the 192-wide tile):
+//   wm 4, bn 128: 256 x 128, three-stage ring, one workgroup per CU;
+//   wm 2, bn 128: 128 x 128, two-stage ring, two workgroups per CU;
+//   wm 4, bn 192: 256 x 192, two-stage ring (3 x 56 KB does not fit), one workgroup per CU.
+// KN (input-gradient with the forward weight in place) keeps bn 128.  A/B switches:
+// MSU_NT_TILE = 128 | 256 (rows), MSU_NT_BN = 128 | 192 (columns).
+struct NtCfg {
+  int wm, bn;
+};
+
+NtCfg nt_cfg(long M, int N, bool wkn) {
+  static const int force_m = [] {
     const char* e = getenv("MSU_NT_TILE");
     return e ? atoi(e) : 0;
   }();
-  if (force == 128) return 2;
-  if (force == 256) return 4;
-  const long big = ((M + 255) / 256) * (long)((N + BN - 1) / BN);
-  return big >= num_cus_nt() ? 4 : 2;
+  static const int force_n = [] {
+    const char* e = getenv("MSU_NT_BN");
+    return e ? atoi(e) : 0;
+  }();
+  const long cus = num_cus_nt();
+  const NtCfg cands[3] = {{4, 128}, {2, 128}, {4, 192}};
+  NtCfg best = cands[0];
+  double best_cost = -1.0;
+  for (const NtCfg& c : cands) {
+    if (c.bn == 192 && (wkn || N % 192 != 0)) continue;
+    if (force_m && (force_m == 128) != (c.wm == 2)) continue;
+    if (force_n && force_n != c.bn) continue;
+    const long bm = 64L * c.wm, per_cu = c.wm == 2 ? 2 : 1;
+    const long tiles = ((M + bm - 1) / bm) * ((N + c.bn - 1) / c.bn);
+    const long rounds = (tiles + cus * per_cu - 1) / (cus * per_cu);
+    const double cost = (double)rounds * bm * c.bn * per_cu * (c.bn == 192 ? 1.05 : 1.0);
+    if (best_cost < 0 || cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  return best;
 }
 
-template <typename T, int WM, int NST, bool WKN>
+template <typename T, int WM, int NST, bool WKN, int BNT>
 void launch_nt(int epi, const NtArgs& a, hipStream_t st) {
   const long tiles = (long)a.tiles_m * a.tiles_n;
   const long cap = (long)num_cus_nt() * (WM == 4 ? 1 : 2);
   const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
   const dim3 blk(128 * WM);
   switch (epi) {
-    case EPI_PLAIN: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_PLAIN, WM, NST, WKN>), dim3(grid), blk, 0, st, a); break;
-    case EPI_GELU_DUAL: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_DUAL, WM, NST, WKN>), dim3(grid), blk, 0, st, a); break;
-    default: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_GRAD, WM, NST, WKN>), dim3(grid), blk, 0, st, a); break;
+    case EPI_PLAIN: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_PLAIN, WM, NST, WKN, BNT>), dim3(grid), blk, 0, st, a); break;
+    case EPI_GELU_DUAL: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_DUAL, WM, NST, WKN, BNT>), dim3(grid), blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_GRAD, WM, NST, WKN, BNT>), dim3(grid), blk, 0, st, a); break;
   }
 }
 
@@ -380,18 +412,20 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
   a.K = K;
   static const int prio = getenv("MSU_NT_PRIO") ? atoi(getenv("MSU_NT_PRIO")) : 0;
   a.prio = prio;
-  const int wm = nt_wm(M, N);
-  a.tiles_n = (N + BN - 1) / BN;
-  a.tiles_m = (int)((M + 64 * wm - 1) / (64 * wm));
+  const NtCfg cfg = nt_cfg(M, N, wkn);
+  a.tiles_n = (N + cfg.bn - 1) / cfg.bn;
+  a.tiles_m = (int)((M + 64 * cfg.wm - 1) / (64 * cfg.wm));
   if ((long)a.tiles_m * a.tiles_n >= (1L << 31)) return -2;
   hipStream_t st = (hipStream_t)stream;
   MSU_DISPATCH16(dtype, T,
-    if (wm == 4) {
-      if (wkn) launch_nt<T, 4, 3, true>(epi, a, st);
-      else launch_nt<T, 4, 3, false>(epi, a, st);
+    if (cfg.bn == 192) {
+      launch_nt<T, 4, 2, false, 192>(epi, a, st);
+    } else if (cfg.wm == 4) {
+      if (wkn) launch_nt<T, 4, 3, true, 128>(epi, a, st);
+      else launch_nt<T, 4, 3, false, 128>(epi, a, st);
     } else {
-      if (wkn) launch_nt<T, 2, 2, true>(epi, a, st);
-      else launch_nt<T, 2, 2, false>(epi, a, st);
+      if (wkn) launch_nt<T, 2, 2, true, 128>(epi, a, st);
+      else launch_nt<T, 2, 2, false, 128>(epi, a, st);
     });
   return MSU_CHECK_LAUNCH();
 }
@@ -402,6 +436,12 @@ extern "C" {
 
 // Whether msu_nt_gemm covers this shape (K % 64, N % 32).
 int msu_nt_gemm_supported(long M, int N, int K) { return nt_shape_ok(M, N, K) ? 1 : 0; }
+
+// The tile msu_nt_gemm picks for M x N (the [N, K] weight form): rows * 1000 + columns.
+int msu_nt_gemm_plan(long M, int N) {
+  const NtCfg c = nt_cfg(M, N, false);
+  return 64 * c.wm * 1000 + c.bn;
+}
 
 // Y[M][N] = epi(A . W^T + bias), 16-bit in / out (dtype 1 bf16, 2 f16), f32 accumulation.
 // epi 0: plain (+ bias when given); 1: Y = H and Y2 = GELU(H) (needs bias); 2: Y = (A . W^T) *

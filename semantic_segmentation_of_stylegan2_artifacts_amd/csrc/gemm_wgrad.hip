@@ -492,6 +492,9 @@ int msu_linear_wgrad_ld(int dtype, const void* dY, const void* X, float* dW, lon
                         float* workspace, long M, int N, int K, int accumulate, void* stream) {
   if (N % 8 || K % 8 || M < 0 || ldw < K) return -2;  // 16-B staging chunks
   hipStream_t st = (hipStream_t)stream;
+  // ablation build only (tools/build_exp.sh gemm_wgrad 256): no weight-gradient work at all, to
+  // time what the side stream's weight gradients cost the step (results WRONG by design)
+  if constexpr ((MSU_EXP & 256) != 0) return 0;
   if (M == 0) {
     if (!accumulate) hipMemset2DAsync(dW, sizeof(float) * ldw, 0, sizeof(float) * K, N, st);
     if (db && !accumulate) hipMemsetAsync(db, 0, sizeof(float) * N, st);

@@ -17,7 +17,11 @@ SHAPES = [(4096, 1152, 384), (4096, 384, 1152), (1000, 384, 384), (2048, 768, 19
           (300, 2304, 768), (128, 768, 3072), (513, 96, 64), (64, 160, 128), (1, 32, 64)]
 # shapes that take the 256 x 128 tile (8 waves, three-stage ring: >= one tile per CU), incl. a
 # ragged M, an N that is not a multiple of 128 and two-K-step tiles (vmcnt(0) fallback)
-BIG = [(32768, 1152, 384), (32768, 384, 1536), (131072, 192, 768), (32000 + 77, 416, 192), (65536, 640, 128)]
+BIG = [(32768, 1152, 384), (32768, 384, 1536), (131072, 192, 768), (32000 + 77, 416, 192), (65536, 640, 128),
+       (32000 + 77, 384, 192)]
+# shapes the tile model puts on the 256 x 192 tile (two-stage ring; round 4): N = 384 / 1152 at
+# the stage-2 token count, incl. a ragged M (BIG's 32768 x 1152, 32768 x 384, 32077 x 384 too)
+WIDE = [(32768, 384, 384), (32768, 1152, 384), (32000 + 77, 384, 192), (131072, 576, 192)]
 
 
 def _ops():
@@ -57,7 +61,8 @@ def test_nt_gemm_plain(M, N, K, bias, low):
     _check(y, ref, "y")
 
 
-@pytest.mark.parametrize("M,N,K", [(4096, 1536, 384), (777, 768, 192), (300, 3072, 768), (32768, 1536, 384)])
+@pytest.mark.parametrize("M,N,K", [(4096, 1536, 384), (777, 768, 192), (300, 3072, 768), (32768, 1536, 384),
+                                   (32768, 1152, 384), (32000 + 77, 384, 384)])
 def test_nt_gemm_gelu_epilogues(M, N, K, low):
     """EPI 1: (H, GELU(H)) of mlp.0; EPI 2: (dY . W2) * GELU'(H) -- mlp.3's input gradient
     through the activation (W2^T [N, K'] passed as the weight)."""
@@ -101,6 +106,19 @@ def test_nt_gemm_kn_gelu_grad(M, N, K, low):
     hf = h.float().requires_grad_(True)
     F.gelu(hf).backward(torch.ones_like(hf))
     _check(dh, (dy.float() @ w2.float()) * hf.grad, "dh")
+
+
+@pytest.mark.parametrize("M,N,K", WIDE)
+def test_nt_gemm_wide_tile_is_chosen_and_exact(M, N, K):
+    """The shapes the round-4 tile model sends to the 192-column tile (a launch with that tile is
+    told apart by the whole-round tile count; msu_nt_gemm_plan reports the choice), bias epilogue."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
+    ops = _ops()
+    wm, bn = _lib.plan_nt(M, N)
+    assert bn == 192, (M, N, wm, bn)
+    a, w, b = _inputs(M, N, K, 11 * M + N, torch.bfloat16)
+    y = ops.nt_gemm(a, w, b)
+    _check(y, F.linear(a.float(), w.float(), b), "y")
 
 
 def test_nt_gemm_rejects_uncovered_shapes():

@@ -60,6 +60,17 @@ for s in "$@"; do
         done
       done
       tail -8 $O/${TAG}_wgrad_split.log ;;
+    nt_ab)
+      for r in 1 2; do
+        for bn in 128 192; do
+          for shp in "32768 384 384" "32768 384 1152" "32768 384 1536" "32768 1152 384" "131072 192 768" "131072 576 192" "32000 384 192"; do
+            echo -n "bn=$bn " >> $O/${TAG}_nt_ab.log
+            MSU_NT_BN=$bn timeout -k 10 60 python -u $R/tools/nt_one.py $shp 50 >> $O/${TAG}_nt_ab.log 2>&1 || exit 3
+          done
+        done
+      done
+      tail -14 $O/${TAG}_nt_ab.log ;;
+    nt_tests) step nt_tests 400 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py $R/tests/test_routing.py ;;
     nt_pmc)
       timeout -k 10 60 python -u $R/tools/nt_one.py 32768 1152 384 50 > $O/${TAG}_nt.log 2>&1 || exit 3
       timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT \
