@@ -129,6 +129,17 @@ int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, flo
                       float* workspace, void* unused, int nchunk, int B, int H, int W, int Cin,
                       int Cout, void* stream);
 
+/* ---------------------------------------------------------------- fused qkv Linear + window attention
+ * Stage 0 of the Swin block (C = 96, 3 heads; model_parts.py:166-170 -> torchvision's qkv Linear and
+ * shifted_window_attention in one kernel): out[B,H,W,C] = attention(x W_qkv^T + b_qkv), x the LN1
+ * rows (16-bit), W_qkv [3C][C] 16-bit, b_qkv f32.  qkv_out (nullable) receives x W^T + b (the qkv
+ * Linear's output, for the backward); dropout / keep bits / aux workspace as msu_win_attn_fwd. */
+int msu_win_attn_qkv_supported(int C, int nh);
+int msu_win_attn_qkv_fwd(int dtype, const void* x, const void* w_qkv, const float* b_qkv, const float* table,
+                         void* out, void* qkv_out, void* keep, float* workspace, int B, int H, int W, int C, int nh,
+                         int shift, float p_drop, unsigned long long seed, const unsigned long long* seed_dev,
+                         void* stream);
+
 /* ---------------------------------------------------------------- Linear weight gradient
  * Every nn.Linear on the path (torchvision block qkv / proj / mlp.0 / mlp.3,
  * PatchMerging.reduction model_parts.py:72, PatchExpand.expand :379, concat_back_dim

@@ -871,3 +871,271 @@ int msu_attn_mfma_bwd_tail(float* ws, float* dtable, float* dqkv_bias_pad, long 
   colsum_multi(segs, 2, (int)parts, 0, st);
   return MSU_CHECK_LAUNCH();
 }
+
+// =====================================================================================
+// Fused stage-0 unit: qkv Linear + shifted-window attention in ONE kernel (the
+// qkv -> attention round trip).  torchvision's block computes qkv = LN1(x) W^T + b for the
+// padded, rolled window grid and runs the attention on it (model_parts.py:166-170 ->
+// shifted_window_attention); here a workgroup loads a window's 64 LN1 rows (zeros for the
+// padded / filler tokens: their qkv is then exactly the bias, as torchvision's pad-after-norm
+// gives), multiplies them with the resident W_qkv on MFMA, keeps q / k / v in LDS and runs the
+// attention of all heads on them.  The qkv tensor never has to be read back; in training it is
+// still written once (the attention backward and the qkv weight gradient read it), in
+// inference it is not written at all.
+//   * one 6-wave workgroup per CU (persistent over windows): wave w = (head h = w >> 1, tile
+//     t = w & 1) computes q, k, v of head h for tokens 32t .. 32t + 31 (3 x 32x32 tiles, K =
+//     96: 18 MFMAs) and then the attention of head h for the queries of tile t;
+//   * LDS: W_qkv [288][96] (55 KB, loaded once), the window's LN1 rows [64][96] (register-
+//     staged one window ahead), q / k / v images per head [64][40] (46 KB), qkv bias;
+//     rows of W / x use the 16-B chunk swizzle c ^ ((r >> 2) & 3) (conflict-free 32-row
+//     fragment reads);
+//   * attention as attn_fwd_mfma (transposed scores, bias image from the aux workspace, the
+//     same dropout streams and keep-bit layout, so the existing backward consumes it).
+// Stage-0 widths only (C = 96, 3 heads).
+namespace {
+
+constexpr int FQ_C = 96, FQ_NH = 3, FQ_C3 = 3 * FQ_C, FQ_CH = FQ_C / 8;  // 12 16-B chunks per row
+constexpr int FQ_WAVES = 2 * FQ_NH;
+
+struct FusedLds {
+  bf16_t w[FQ_C3 * FQ_C];        // W_qkv rows (swizzled chunks)
+  bf16_t x[64 * FQ_C];           // the window's LN1 rows (swizzled chunks)
+  bf16_t qkv[FQ_NH][3][64 * LD];  // per head: q, k, v images [t][d] (padded rows)
+  float bias[FQ_C3];
+  int tok[64], reg[64];
+};
+
+MSU_DEV int fq_swz(int r) { return (r >> 2) & 3; }
+
+// 32-row k-contiguous fragment of a swizzled [rows][96] image: lane -> row r0 + (lane & 31),
+// k = 16 ks + 8 (lane >> 5) .. + 7
+MSU_DEV bf16x8 fq_frag(const bf16_t* img, int r0, int ks, int lane) {
+  const int r = r0 + (lane & 31);
+  return *reinterpret_cast<const bf16x8*>(img + r * FQ_C + (((2 * ks + (lane >> 5)) ^ fq_swz(r)) << 3));
+}
+
+template <typename T, bool DROP, bool STORE_QKV>
+__global__ void __launch_bounds__(64 * FQ_WAVES) attn_qkv_fwd_mfma(const bf16_t* __restrict__ xin,
+                                                                  const bf16_t* __restrict__ wqkv,
+                                                                  const float* __restrict__ bqkv, Aux aux,
+                                                                  bf16_t* __restrict__ out, bf16_t* __restrict__ qkv_out,
+                                                                  Geom g, float scale, float p_drop, uint64_t seed0,
+                                                                  const unsigned long long* seed_dev,
+                                                                  uint32_t* __restrict__ keep_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  FusedLds& L = *reinterpret_cast<FusedLds*>(smem_raw);
+  const uint64_t seed = launch_seed(seed0, seed_dev);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = wave >> 1, t = wave & 1, hh = lane >> 5;
+  constexpr int NTHR = 64 * FQ_WAVES;
+  // resident W_qkv and bias
+  for (int s = tid; s < FQ_C3 * FQ_CH; s += NTHR) {
+    const int r = s / FQ_CH, c = s - (s / FQ_CH) * FQ_CH;
+    *reinterpret_cast<u32x4*>(L.w + r * FQ_C + ((c ^ fq_swz(r)) << 3)) =
+        *reinterpret_cast<const u32x4*>(wqkv + r * FQ_C + 8 * c);
+  }
+  for (int s = tid; s < FQ_C3; s += NTHR) L.bias[s] = bqkv[s];
+  // the window's 64 x 12 chunks of LN1 rows: thread -> slots tid, tid + NTHR
+  constexpr int XS = (64 * FQ_CH + NTHR - 1) / NTHR;  // 2
+  u32x4 xr[XS];
+  int tokr = TOK_ZERO, regr = 0;  // thread tid < 64: token-table entry tid of the staged window
+  auto load_x = [&](long win) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < XS; ++k) {
+      const int s = tid + NTHR * k;
+      const int r = s / FQ_CH, c = s - (s / FQ_CH) * FQ_CH;
+      int rg;
+      const int tok = s < 64 * FQ_CH ? token_of(g, (int)win, r, &rg) : TOK_ZERO;
+      const bf16_t* src = tok >= 0 ? xin + (size_t)((unsigned)tok * (unsigned)FQ_C) + 8 * c : aux.zrow;
+      xr[k] = *reinterpret_cast<const u32x4*>(src);
+    }
+    if (tid < 64) tokr = token_of(g, (int)win, tid, &regr);
+  };
+  const long stride = gridDim.x;
+  long win = xcd_remap(blockIdx.x, gridDim.x);
+  if (win < g.nwin) load_x(win);
+  const float kscale = 1.0f / (1.0f - p_drop);
+  const float* bimg = aux.bimg + (long)h * 4096;
+  for (; win < g.nwin; win += stride) {
+    // ---- stage the window: rows -> LDS, token table (the previous window's readers are done:
+    // every wave passed the barrier after its attention below)
+#pragma unroll
+    for (int k = 0; k < XS; ++k) {
+      const int s = tid + NTHR * k;
+      const int r = s / FQ_CH, c = s - (s / FQ_CH) * FQ_CH;
+      if (s < 64 * FQ_CH) *reinterpret_cast<u32x4*>(L.x + r * FQ_C + ((c ^ fq_swz(r)) << 3)) = xr[k];
+    }
+    if (tid < 64) {
+      L.tok[tid] = tokr;
+      L.reg[tid] = regr;
+    }
+    __syncthreads();
+    const bool bnd = window_boundary(g, (int)win);
+    // bias-image tiles (jt, it = t) of this wave's scores: issued now, consumed after the qkv GEMM
+    f32x16 P[2];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      const float4* bp = reinterpret_cast<const float4*>(bimg + ((jt * 2 + t) * 64 + lane) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = bp[q];
+        P[jt][4 * q] = v.x; P[jt][4 * q + 1] = v.y; P[jt][4 * q + 2] = v.z; P[jt][4 * q + 3] = v.w;
+      }
+    }
+    // next window's rows -> registers (latency hidden under this window)
+    const long nxt = win + stride;
+    if (nxt < g.nwin) load_x(nxt);
+    // ---- q, k, v of head h for tokens 32t .. 32t + 31: D[ch][token], W rows as the A operand
+    f32x16 acc[3];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) acc[m] = f32x16{0};
+#pragma unroll
+    for (int ks = 0; ks < FQ_C / 16; ++ks) {
+      const bf16x8 xf = fq_frag(L.x, 32 * t, ks, lane);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) acc[m] = mfma32<T>(fq_frag(L.w, m * FQ_C + 32 * h, ks, lane), xf, acc[m]);
+    }
+    // + bias, round to 16 bits, rows of the q / k / v images (lane = token, registers 4g .. 4g+3 =
+    // channels 8g + 4hh .. + 3)
+    const int tk = 32 * t + (lane & 31);
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      bf16_t* img = L.qkv[h][m];
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const float4 b = *reinterpret_cast<const float4*>(L.bias + m * FQ_C + 32 * h + 8 * gq + 4 * hh);
+        uint2 wv;
+        wv.x = pack2<T>(acc[m][4 * gq] + b.x, acc[m][4 * gq + 1] + b.y);
+        wv.y = pack2<T>(acc[m][4 * gq + 2] + b.z, acc[m][4 * gq + 3] + b.w);
+        *reinterpret_cast<uint2*>(img + tk * LD + 8 * gq + 4 * hh) = wv;
+      }
+    }
+    __syncthreads();  // q / k / v of every head and token tile in LDS; the LN1 rows are free
+    if constexpr (STORE_QKV) {
+      // the training path keeps qkv for the backward: this wave's tokens, head h's three
+      // 64-B slices, 4 lanes per slice (16 whole slices per store instruction)
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int r = 32 * t + (lane >> 2) + 16 * c;
+          const int tok = L.tok[r];
+          const u32x4 v = *reinterpret_cast<const u32x4*>(L.qkv[h][m] + r * LD + 8 * (lane & 3));
+          if (tok >= 0)
+            *reinterpret_cast<u32x4*>(qkv_out + (size_t)((unsigned)tok * (unsigned)FQ_C3) + m * FQ_C + h * HD +
+                                      8 * (lane & 3)) = v;
+        }
+    }
+    // ---- attention of head h, query tile t (as attn_fwd_mfma)
+    const bf16_t* Lq = L.qkv[h][0];
+    const bf16_t* Lk = L.qkv[h][1];
+    const bf16_t* Lv = L.qkv[h][2];
+    uint32_t kmask = ~0u;
+    if constexpr (DROP)
+      kmask = drop_bits<false>(drop_seed32(seed), (uint32_t)win * g.nh + h, t * 32 + (lane & 31), hh,
+                               drop_thresh16(p_drop));
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 qf = frag_rows(Lq, LD, 32 * t, 16 * ks, lane);
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) P[jt] = mfma32<T>(frag_rows(Lk, LD, 32 * jt, 16 * ks, lane), qf, P[jt]);
+    }
+    if (bnd) mask_col(P, L.reg, t, scale, lane);
+    softmax_col(P, scale);
+    if constexpr (DROP) {
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (live_key(jt, r)) P[jt][r] = (kmask >> (jt * 16 + r)) & 1u ? P[jt][r] * kscale : 0.f;
+    }
+    f32x16 O = f32x16{0};
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) O = mfma32<T>(frag_tr_perm(Lv, LD, jt * 32 + 16 * sb, 0, lane), pack8<T>(P[jt], sb), O);
+    // output through this tile's q rows (read only by this wave)
+    bf16_t* Lo = L.qkv[h][0];
+    const int i = t * 32 + (lane & 31);
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      uint2 wv;
+      wv.x = pack2<T>(O[4 * gq], O[4 * gq + 1]);
+      wv.y = pack2<T>(O[4 * gq + 2], O[4 * gq + 3]);
+      *reinterpret_cast<uint2*>(Lo + i * LD + 8 * gq + 4 * hh) = wv;
+    }
+    lds_sync();
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int r = 32 * t + (lane >> 2) + 16 * c;
+      const int tok = L.tok[r];
+      const u32x4 v = *reinterpret_cast<const u32x4*>(Lo + r * LD + 8 * (lane & 3));
+      if (tok >= 0) *reinterpret_cast<u32x4*>(out + (size_t)((unsigned)tok * (unsigned)FQ_C) + h * HD + 8 * (lane & 3)) = v;
+    }
+    if (DROP && keep_out) keep_out[((size_t)win * g.nh + h) * 128 + 64 * t + lane] = kmask;
+    __syncthreads();  // every wave done with this window's images before the next is staged
+  }
+}
+
+int num_cus_fq() {
+  static const int cus = [] {
+    int n = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    return n;
+  }();
+  return cus;
+}
+
+template <typename T, bool DROP, bool STORE_QKV>
+void launch_fq(dim3 grid, const void* x, const void* w, const float* b, const Aux& aux, void* out, void* qkv, Geom g,
+               float scale, float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* keep,
+               hipStream_t st) {
+  auto kern = attn_qkv_fwd_mfma<T, DROP, STORE_QKV>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(FusedLds));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(64 * FQ_WAVES), sizeof(FusedLds), st, (const bf16_t*)x, (const bf16_t*)w, b, aux,
+                     (bf16_t*)out, (bf16_t*)qkv, g, scale, p_drop, (uint64_t)seed, seed_dev, (uint32_t*)keep);
+}
+
+}  // namespace
+
+extern "C" {
+
+// Whether msu_win_attn_qkv_fwd covers a block of width C with nh heads (16-bit only).
+int msu_win_attn_qkv_supported(int C, int nh) { return C == FQ_C && nh == FQ_NH ? 1 : 0; }
+
+// Fused qkv Linear + window attention (stage 0): out[B,H,W,C] = attention(x W_qkv^T + b_qkv);
+// x = LN1 rows [B,H,W,C] 16-bit, W_qkv [3C][C] 16-bit, b_qkv f32; qkv_out [B,H,W,3C] (x W^T + b,
+// what the qkv Linear would store) or null; keep / dropout / seeds and the aux workspace
+// (msu_win_attn_fwd_workspace) as msu_win_attn_fwd.
+int msu_win_attn_qkv_fwd(int dtype, const void* x, const void* w_qkv, const float* b_qkv, const float* table,
+                         void* out, void* qkv_out, void* keep, float* workspace, int B, int H, int W, int C, int nh,
+                         int shift, float p_drop, unsigned long long seed, const unsigned long long* seed_dev,
+                         void* stream) {
+  if (!msu_is16(dtype) || !msu_win_attn_qkv_supported(C, nh)) return -2;
+  if ((long)B * H * W * 3 * C >= (1L << 32)) return -2;
+  const Geom g = make_geom(B, H, W, C, nh, shift);
+  if (g.nwin == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const float scale = 1.0f / sqrtf((float)HD);
+  float* img; bf16_t* brow; bf16_t* zrow;
+  const Aux aux = carve_aux(workspace, C, nh, &img, &brow, &zrow);
+  const long nb = g.nwin < num_cus_fq() ? g.nwin : num_cus_fq();
+  const dim3 grid((unsigned)nb);
+  const bool drop = p_drop > 0.f;
+  MSU_DISPATCH16(dtype, T,
+    hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, b_qkv, nh, 3 * C,
+                       1.0f / scale, img, brow, zrow);
+    if (drop && qkv_out) launch_fq<T, true, true>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st);
+    else if (drop) launch_fq<T, true, false>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st);
+    else if (qkv_out) launch_fq<T, false, true>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st);
+    else launch_fq<T, false, false>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st));
+  return MSU_CHECK_LAUNCH();
+}
+
+}  // extern "C"

@@ -142,13 +142,19 @@ class ShiftedWindowAttention(nn.Module):
 
     def forward(self, x):
         """x: [B, H, W, C] (already norm1-ed)."""
-        qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
-        qb = self.qkv.bias if self.qkv.bias is not None else torch.zeros(
-            3 * x.shape[-1], device=x.device, dtype=torch.float32)
         p = self.attention_dropout if self.training else 0.0
-        o = ops.window_attention(qkv, qb, self.relative_position_bias_table, self.num_heads,
-                                 self.shift_size[0], p, _next_seed() if p > 0 else 0,
-                                 _dev_seed if p > 0 else None)
+        if ops.window_attention_qkv_fusable(x, self.num_heads, self.qkv.bias):
+            # stage 0: the qkv Linear fused into the attention kernel (no qkv round trip)
+            o = ops.window_attention_qkv(x, self.qkv.weight, self.qkv.bias, self.relative_position_bias_table,
+                                         self.num_heads, self.shift_size[0], p, _next_seed() if p > 0 else 0,
+                                         _dev_seed if p > 0 else None)
+        else:
+            qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
+            qb = self.qkv.bias if self.qkv.bias is not None else torch.zeros(
+                3 * x.shape[-1], device=x.device, dtype=torch.float32)
+            o = ops.window_attention(qkv, qb, self.relative_position_bias_table, self.num_heads,
+                                     self.shift_size[0], p, _next_seed() if p > 0 else 0,
+                                     _dev_seed if p > 0 else None)
         o = ops.linear(o, self.proj.weight, self.proj.bias)
         if self.dropout > 0 and self.training:
             o = F.dropout(o, self.dropout, True)

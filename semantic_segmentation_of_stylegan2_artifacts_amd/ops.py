@@ -591,6 +591,107 @@ def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0,
                              int(shift), float(p_drop), int(seed) & ((1 << 63) - 1), seed_dev)[0]
 
 
+# ----------------------------------------------------------------------------- fused qkv + attention
+# Stage-0 fused unit (csrc/window_attention_mfma.hip attn_qkv_fwd_mfma): the qkv Linear and the
+# window attention in one kernel, qkv never read back (in inference never written).  The backward
+# is the two existing ones in sequence: the attention backward (dqkv, relative table, padded-token
+# bias share) then the qkv Linear's (one-pass msu_linear_bwd at stage 0).  A/B switch
+# MSU_ATTN_QKV=0: the unfused qkv Linear + window_attention path.
+_ATTN_QKV = os.environ.get("MSU_ATTN_QKV", "1") != "0"
+
+
+class _Ctx:
+    """A stand-in autograd ctx for calling an op's backward function from another op's."""
+
+    def __init__(self, saved, **kw):
+        self.saved_tensors = saved
+        self.__dict__.update(kw)
+
+
+def _attn_qkv_impl(x, weight, bias, table, num_heads, shift, p_drop, seed, seed_dev, store_qkv):
+    _need_cuda(x)
+    x = x.contiguous()
+    B, H, W, C = x.shape
+    dt = x.dtype
+    w = _shadow(weight, dt)
+    L = _lib.lib()
+    out = torch.empty(B, H, W, C, device=x.device, dtype=dt)
+    qkv = torch.empty(B, H, W, 3 * C, device=x.device, dtype=dt) if store_qkv else x.new_empty(0)
+    ws = torch.empty(L.msu_win_attn_fwd_workspace(_dt(x), C, num_heads), device=x.device, dtype=torch.float32)
+    keep = torch.empty(L.msu_win_attn_keep_words(_dt(x), B, H, W, num_heads) if p_drop > 0 and _ATTN_KEEP else 0,
+                       device=x.device, dtype=torch.int32)
+    _lib.call("msu_win_attn_qkv_fwd", _dt(x), _p(x), _p(w), _p(bias), _p(table), _p(out),
+              _p(qkv) if store_qkv else None, _p(keep) if keep.numel() else None, _p(ws), B, H, W, C, num_heads,
+              shift, float(p_drop), seed, _p(seed_dev), _s(x))
+    return out, qkv, keep
+
+
+def _attn_qkv_fake(x, weight, bias, table, num_heads, shift, p_drop, seed, seed_dev, store_qkv):
+    B, H, W, C = x.shape
+    nwin = B * (-(-H // 7)) * (-(-W // 7))
+    kw = nwin * num_heads * 128 if (p_drop > 0 and _ATTN_KEEP) else 0
+    return (x.new_empty(B, H, W, C), x.new_empty(B, H, W, 3 * C) if store_qkv else x.new_empty(0),
+            x.new_empty(kw, dtype=torch.int32))
+
+
+def _attn_qkv_setup(ctx, inputs, output):
+    x, weight, bias, table, num_heads, shift, p_drop, seed, seed_dev, store_qkv = inputs
+    _, qkv, keep = output
+    ctx.mark_non_differentiable(qkv, keep)
+    ctx.set_materialize_grads(False)
+    ctx.save_for_backward(x.contiguous(), qkv, bias, table, seed_dev, keep)
+    ctx.params = (weight, bias)
+    ctx.bias_param = bias if isinstance(bias, torch.nn.Parameter) else None
+    ctx.table_param = table if isinstance(table, torch.nn.Parameter) else None
+    ctx.cfg = (num_heads, shift, float(p_drop), seed)
+
+
+def _attn_qkv_backward(ctx, dout, _dqkv, _dkeep):
+    x, qkv, bias, table, seed_dev, keep = ctx.saved_tensors
+    if dout is None:
+        return (None,) * 10
+    if qkv.numel() == 0:
+        raise RuntimeError("window_attention_qkv: backward through a forward that did not keep qkv (store_qkv=False)")
+    weight, _ = ctx.params
+    actx = _Ctx((qkv, bias, table, seed_dev, keep), cfg=ctx.cfg, bias_param=ctx.bias_param,
+                table_param=ctx.table_param)
+    dqkv, dbias_pad, dtable = _attn_backward(actx, dout, None)[:3]
+    lctx = _Ctx((x,), params=(weight, bias), needs_input_grad=(ctx.needs_input_grad[0], True, True))
+    dx, dw, db = _linear_backward(lctx, dqkv)
+    if db is not None and dbias_pad is not None:
+        db = db + dbias_pad
+    elif dbias_pad is not None:
+        db = dbias_pad
+    return dx, dw, db, dtable, None, None, None, None, None, None
+
+
+_window_attention_qkv = _define(
+    "window_attention_qkv",
+    "(Tensor x, Tensor weight, Tensor bias, Tensor table, int num_heads, int shift, float p_drop, int seed,"
+    " Tensor? seed_dev, bool store_qkv) -> (Tensor, Tensor, Tensor)",
+    _attn_qkv_impl, _attn_qkv_fake, _attn_qkv_setup, _attn_qkv_backward)
+
+
+def window_attention_qkv_fusable(x, num_heads, bias):
+    """Whether the fused stage-0 unit takes this block: 16-bit, C = 96 with 3 heads, a qkv bias."""
+    if not _ATTN_QKV or bias is None or not x.is_cuda or act_dtype() not in _LOW:
+        return False
+    C = x.shape[-1]
+    return bool(_lib.lib().msu_win_attn_qkv_supported(C, num_heads))
+
+
+def window_attention_qkv(x, weight, bias, table, num_heads, shift, p_drop=0.0, seed=0, seed_dev=None):
+    """window_attention(linear(x, weight, bias), bias, table, ...) with the qkv Linear fused in:
+    x [B, H, W, C] (LN1 output) -> [B, H, W, C] (before proj)."""
+    dt = act_dtype()
+    x = _as(x, dt)
+    store = torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad or bias.requires_grad or
+                                         table.requires_grad)
+    return _window_attention_qkv(x, weight, _f32(bias) if not isinstance(bias, torch.nn.Parameter) else bias,
+                                 table if isinstance(table, torch.nn.Parameter) else _f32(table), int(num_heads),
+                                 int(shift), float(p_drop), int(seed) & ((1 << 63) - 1), seed_dev, bool(store))[0]
+
+
 # ----------------------------------------------------------------------------- token GEMM
 TOK_PLAIN, TOK_GELU_DUAL, TOK_GELU_GRAD = 0, 1, 2
 _tok_cache = {}

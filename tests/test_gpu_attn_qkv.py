@@ -1,0 +1,140 @@
+"""GPU: the fused stage-0 qkv Linear + window attention unit (ops.window_attention_qkv,
+csrc/window_attention_mfma.hip attn_qkv_fwd_mfma) against fp32 PyTorch and against the unfused
+path it replaces (ops.linear -> ops.window_attention; reference network/model_parts.py:166-170 ->
+torchvision qkv Linear + shifted_window_attention).
+
+* forward vs fp32: attention(x W^T + b) on the same 16-bit operands (tests/_parity_refs.py), at
+  small padded / shifted maps and at stage 0 of 1 x 1024^2 (1369 windows, each persistent
+  workgroup loops over ~5 windows), bf16 and f16, dropout off and on (the stored keep bits are
+  the reference's mask);
+* the training outputs: the qkv tensor it keeps for the backward equals the qkv Linear's output,
+  and the keep bits equal the unfused forward's (same dropout streams);
+* backward (dx, dW, db, d table) equals the unfused path's to 16-bit rounding, and the trainer's
+  direct-.grad parameters take the same values;
+* inference (no grad) writes no qkv.
+"""
+import math
+
+import pytest
+import torch
+
+from _parity_refs import attn_ref_from_qkv, decode_keep_bits
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+TOL = {torch.bfloat16: 3e-2, torch.float16: 7.5e-3}
+C, NH = 96, 3
+
+
+def _ops():
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    return ops
+
+
+def _check(y, ref, t, what):
+    y, ref = y.detach().float(), ref.detach().float()
+    scale = ref.abs().max().item()
+    err = (y - ref).abs().max().item()
+    rel2 = ((y - ref).norm() / ref.norm()).item()
+    assert err <= t * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+    assert rel2 <= t / 4, f"{what}: relative L2 {rel2:.3e}"
+
+
+def _inputs(B, H, W, seed, low):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, H, W, C, generator=g).to(DEV, low)
+    w = (torch.randn(3 * C, C, generator=g) / math.sqrt(C)).to(DEV)
+    b = (0.3 * torch.randn(3 * C, generator=g)).to(DEV)
+    table = torch.randn(169, NH, generator=g).to(DEV)
+    dy = torch.randn(B, H, W, C, generator=g).to(DEV, low)
+    return x, w, b, table, dy
+
+
+@pytest.fixture(params=[torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+def low(request):
+    return request.param
+
+
+CASES = [(2, 8, 8, 3), (1, 14, 14, 0), (2, 28, 28, 3), (1, 10, 12, 3), (1, 256, 256, 3), (1, 256, 256, 0)]
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.05])
+@pytest.mark.parametrize("B,H,W,shift", CASES)
+def test_fused_forward_matches_fp32(B, H, W, shift, p_drop, low):
+    ops = _ops()
+    x, w, b, table, _ = _inputs(B, H, W, B * H + W + shift, low)
+    with torch.no_grad(), torch.autocast("cuda", dtype=low):
+        assert ops.window_attention_qkv_fusable(x, NH, b)
+        y, qkv, keep = torch.ops.msunet.window_attention_qkv(x, w, b, table, NH, shift, p_drop, 99, None, True)
+    torch.cuda.synchronize()
+    nwin = B * ((H + 6) // 7) * ((W + 6) // 7)
+    mask = decode_keep_bits(keep, nwin * NH) if p_drop > 0 else None
+    qkv_ref = torch.nn.functional.linear(x.float(), w.to(low).float(), b)
+    _check(qkv, qkv_ref, TOL[low] / 4, "qkv kept for the backward")
+    ref = attn_ref_from_qkv(qkv.float(), b, table, NH, shift, keep=mask, p_drop=p_drop)
+    _check(y, ref, TOL[low], "out")
+
+
+@pytest.mark.parametrize("B,H,W,shift", [(2, 28, 28, 3), (1, 256, 256, 3)])
+def test_fused_equals_unfused_including_backward(B, H, W, shift, low):
+    """Same keep bits and qkv as the unfused forward; the outputs and all gradients agree to
+    16-bit rounding (the backward kernels are the unfused path's own)."""
+    ops = _ops()
+    x, w, b, table, dy = _inputs(B, H, W, 7 + H, low)
+    res = {}
+    for fused in (True, False):
+        xg = x.clone().requires_grad_(True)
+        wg, bg, tg = [t.clone().requires_grad_(True) for t in (w, b, table)]
+        with torch.autocast("cuda", dtype=low):
+            if fused:
+                y, qkv, keep = torch.ops.msunet.window_attention_qkv(xg, wg, bg, tg, NH, shift, 0.1, 1234, None, True)
+            else:
+                qkv = ops.linear(xg, wg, bg)
+                y, keep = torch.ops.msunet.window_attention(qkv, bg, tg, NH, shift, 0.1, 1234, None)
+        y.backward(dy)
+        torch.cuda.synchronize()
+        res[fused] = (y, qkv.detach(), keep, xg.grad, wg.grad, bg.grad, tg.grad)
+    assert torch.equal(res[True][2], res[False][2]), "keep bits differ"
+    t = TOL[low] / 2
+    for name, a, r in zip(("out", "qkv", "keep", "dx", "dW", "db", "dtable"), res[True], res[False]):
+        if name != "keep":
+            _check(a, r, t, name)
+
+
+def test_fused_direct_params_match_autograd_params():
+    """Trainer-style parameters (flat .grad, bf16 shadow, direct accumulation: the one-pass Linear
+    backward and the side-stream attention tail) give the plain autograd gradients."""
+    ops = _ops()
+    B, H, W, shift = 2, 64, 64, 3
+    x, w, b, table, dy = _inputs(B, H, W, 5, torch.bfloat16)
+    res = {}
+    for direct in (False, True):
+        xg = x.clone().requires_grad_(True)
+        pw, pb, pt = (torch.nn.Parameter(t.clone()) for t in (w, b, table))
+        if direct:
+            for p_ in (pw, pb, pt):
+                p_.grad = torch.zeros_like(p_)
+                p_._msu_direct = True
+            pw._msu_shadow = pw.detach().to(torch.bfloat16)
+            pw._msu_shadow_t = pw.detach().t().contiguous().to(torch.bfloat16)
+            pw._msu_shadow_ver = pw._version
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = ops.window_attention_qkv(xg, pw, pb, pt, NH, shift, 0.05, 77)
+        y.backward(dy)
+        ops.join_side_streams()
+        torch.cuda.synchronize()
+        res[direct] = (xg.grad.float(), pw.grad.clone(), pb.grad.clone(), pt.grad.clone())
+    for name, a, r in zip(("dx", "dW", "db", "dtable"), res[True], res[False]):
+        _check(a, r, 1e-2, name)
+
+
+def test_fused_inference_keeps_no_qkv():
+    ops = _ops()
+    x, w, b, table, _ = _inputs(1, 28, 28, 3, torch.bfloat16)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y1 = ops.window_attention_qkv(x, w, b, table, NH, 3)
+        _, qkv, _ = torch.ops.msunet.window_attention_qkv(x, w, b, table, NH, 3, 0.0, 0, None, False)
+        y2 = ops.window_attention(ops.linear(x, w, b), b, table, NH, 3)
+    assert qkv.numel() == 0
+    _check(y1, y2, 1.5e-2, "no-grad fused vs unfused")

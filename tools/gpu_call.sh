@@ -21,6 +21,7 @@ step() {  # name seconds cmd...
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
 for s in "$@"; do
   case $s in
+    fused_tests) step fused_tests 300 $PYT -m gpu $R/tests/test_gpu_attn_qkv.py ;;
     tests_new) step tests_new 600 $PYT -m gpu $R/tests/test_gpu_production_parity.py $R/tests/test_gpu_bench_dp.py \
                  $R/tests/test_gpu_linbwd.py "$R/tests/test_gpu_tok_gemm.py::test_linear_cat_direct_grad_accumulates" \
                  "$R/tests/test_gpu_graph.py::test_eager_side_stream_step_is_deterministic" ;;
@@ -70,6 +71,15 @@ for s in "$@"; do
         done
       done
       tail -14 $O/${TAG}_nt_ab.log ;;
+    attn_pmc) step attn_pmc 400 bash $R/tools/pmc_attn.sh $TAG 256 3 3 0.05 ;;
+    fused_ab)
+      for r in 1 2; do
+        for v in 1 0; do
+          echo "MSU_ATTN_QKV=$v" >> $O/${TAG}_fused_ab.log
+          MSU_ATTN_QKV=$v timeout -k 10 240 python3 -u $R/bench.py --steps 15 --warmup 5 --no-cpu-baseline --no-roofline --no-input-pipeline 2>&1 | grep '^{' | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])" >> $O/${TAG}_fused_ab.log || exit 3
+        done
+      done
+      cat $O/${TAG}_fused_ab.log ;;
     nt_tests) step nt_tests 400 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py $R/tests/test_routing.py ;;
     nt_pmc)
       timeout -k 10 60 python -u $R/tools/nt_one.py 32768 1152 384 50 > $O/${TAG}_nt.log 2>&1 || exit 3
