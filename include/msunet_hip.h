@@ -139,6 +139,13 @@ int msu_win_attn_qkv_fwd(int dtype, const void* x, const void* w_qkv, const floa
                          void* out, void* qkv_out, void* keep, float* workspace, int B, int H, int W, int C, int nh,
                          int shift, float p_drop, unsigned long long seed, const unsigned long long* seed_dev,
                          void* stream);
+/* The whole attention half of the block: out = (attention(x W_qkv^T + b_qkv)) W_proj^T + b_proj
+ * (model_parts.py:166-170 with the proj Linear); o_out (nullable) receives the attention output
+ * before proj (the proj weight gradient's input), qkv_out as above. */
+int msu_win_attn_qkv_fwd2(int dtype, const void* x, const void* w_qkv, const float* b_qkv, const float* table,
+                          const void* w_proj, const float* b_proj, void* out, void* o_out, void* qkv_out, void* keep,
+                          float* workspace, int B, int H, int W, int C, int nh, int shift, float p_drop,
+                          unsigned long long seed, const unsigned long long* seed_dev, void* stream);
 
 /* ---------------------------------------------------------------- Linear weight gradient
  * Every nn.Linear on the path (torchvision block qkv / proj / mlp.0 / mlp.3,

@@ -899,9 +899,11 @@ constexpr int FQ_WAVES = 2 * FQ_NH;
 
 struct FusedLds {
   bf16_t w[FQ_C3 * FQ_C];        // W_qkv rows (swizzled chunks)
-  bf16_t x[64 * FQ_C];           // the window's LN1 rows (swizzled chunks)
-  bf16_t qkv[FQ_NH][3][64 * LD];  // per head: q, k, v images [t][d] (padded rows)
+  bf16_t wp[FQ_C * FQ_C];        // W_proj rows (swizzled chunks; PROJ)
+  bf16_t x[64 * FQ_C];           // the window's LN1 rows (swizzled chunks); PROJ: then its output rows
+  bf16_t qkv[FQ_NH][3][64 * LD];  // per head: q, k, v images [t][d] (padded rows); q then o
   float bias[FQ_C3];
+  float pbias[FQ_C];
   int tok[64], reg[64];
 };
 
@@ -914,14 +916,19 @@ MSU_DEV bf16x8 fq_frag(const bf16_t* img, int r0, int ks, int lane) {
   return *reinterpret_cast<const bf16x8*>(img + r * FQ_C + (((2 * ks + (lane >> 5)) ^ fq_swz(r)) << 3));
 }
 
-template <typename T, bool DROP, bool STORE_QKV>
+// PROJ: the proj Linear too -- y = o W_proj^T + b_proj from the three heads' o (in LDS) is the
+// output (`out`), and o itself goes to o_out (the proj weight gradient's input) when given.
+template <typename T, bool DROP, bool STORE_QKV, bool PROJ>
 __global__ void __launch_bounds__(64 * FQ_WAVES) attn_qkv_fwd_mfma(const bf16_t* __restrict__ xin,
                                                                   const bf16_t* __restrict__ wqkv,
                                                                   const float* __restrict__ bqkv, Aux aux,
                                                                   bf16_t* __restrict__ out, bf16_t* __restrict__ qkv_out,
                                                                   Geom g, float scale, float p_drop, uint64_t seed0,
                                                                   const unsigned long long* seed_dev,
-                                                                  uint32_t* __restrict__ keep_out) {
+                                                                  uint32_t* __restrict__ keep_out,
+                                                                  const bf16_t* __restrict__ wproj,
+                                                                  const float* __restrict__ bproj,
+                                                                  bf16_t* __restrict__ o_out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   FusedLds& L = *reinterpret_cast<FusedLds*>(smem_raw);
   const uint64_t seed = launch_seed(seed0, seed_dev);
@@ -936,6 +943,14 @@ __global__ void __launch_bounds__(64 * FQ_WAVES) attn_qkv_fwd_mfma(const bf16_t*
         *reinterpret_cast<const u32x4*>(wqkv + r * FQ_C + 8 * c);
   }
   for (int s = tid; s < FQ_C3; s += NTHR) L.bias[s] = bqkv[s];
+  if constexpr (PROJ) {
+    for (int s = tid; s < FQ_C * FQ_CH; s += NTHR) {
+      const int r = s / FQ_CH, c = s - (s / FQ_CH) * FQ_CH;
+      *reinterpret_cast<u32x4*>(L.wp + r * FQ_C + ((c ^ fq_swz(r)) << 3)) =
+          *reinterpret_cast<const u32x4*>(wproj + r * FQ_C + 8 * c);
+    }
+    for (int s = tid; s < FQ_C; s += NTHR) L.pbias[s] = bproj[s];
+  }
   // the window's 64 x 12 chunks of LN1 rows: thread -> slots tid, tid + NTHR
   constexpr int XS = (64 * FQ_CH + NTHR - 1) / NTHR;  // 2
   u32x4 xr[XS];
@@ -1066,14 +1081,52 @@ __global__ void __launch_bounds__(64 * FQ_WAVES) attn_qkv_fwd_mfma(const bf16_t*
       *reinterpret_cast<uint2*>(Lo + i * LD + 8 * gq + 4 * hh) = wv;
     }
     lds_sync();
+    bf16_t* const odst = PROJ ? o_out : out;
+    if (!PROJ || o_out != nullptr) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int r = 32 * t + (lane >> 2) + 16 * c;
-      const int tok = L.tok[r];
-      const u32x4 v = *reinterpret_cast<const u32x4*>(Lo + r * LD + 8 * (lane & 3));
-      if (tok >= 0) *reinterpret_cast<u32x4*>(out + (size_t)((unsigned)tok * (unsigned)FQ_C) + h * HD + 8 * (lane & 3)) = v;
+      for (int c = 0; c < 2; ++c) {
+        const int r = 32 * t + (lane >> 2) + 16 * c;
+        const int tok = L.tok[r];
+        const u32x4 v = *reinterpret_cast<const u32x4*>(Lo + r * LD + 8 * (lane & 3));
+        if (tok >= 0)
+          *reinterpret_cast<u32x4*>(odst + (size_t)((unsigned)tok * (unsigned)FQ_C) + h * HD + 8 * (lane & 3)) = v;
+      }
     }
     if (DROP && keep_out) keep_out[((size_t)win * g.nh + h) * 128 + 64 * t + lane] = kmask;
+    if constexpr (PROJ) {
+      __syncthreads();  // o of every head in LDS (q image rows)
+      // y[token][n] = sum_d o[token][d] W_proj[n][d] + b: wave -> (token tile t, n tile h); the
+      // k steps of 16 d walk the heads' o images (d = 32 h' + 16 (ks & 1) + ...)
+      f32x16 ya = f32x16{0};
+#pragma unroll
+      for (int ks = 0; ks < FQ_C / 16; ++ks) {
+        const bf16x8 of = frag_rows(L.qkv[ks >> 1][0], LD, 32 * t, 16 * (ks & 1), lane);
+        ya = mfma32<T>(fq_frag(L.wp, 32 * h, ks, lane), of, ya);
+      }
+      // + bias, rows of the output image (the LN1 rows' buffer, free since the qkv GEMM)
+      const int tk2 = 32 * t + (lane & 31);
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int n = 32 * h + 8 * gq + 4 * hh;
+        const float4 b = *reinterpret_cast<const float4*>(L.pbias + n);
+        uint2 wv;
+        wv.x = pack2<T>(ya[4 * gq] + b.x, ya[4 * gq + 1] + b.y);
+        wv.y = pack2<T>(ya[4 * gq + 2] + b.z, ya[4 * gq + 3] + b.w);
+        // chunk n / 8 of row tk2, 8-B half 4hh / 4 of it (swizzled chunks as the LN1 rows)
+        *reinterpret_cast<uint2*>(L.x + tk2 * FQ_C + (((n >> 3) ^ fq_swz(tk2)) << 3) + 4 * hh) = wv;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < XS; ++k) {
+        const int s = tid + NTHR * k;
+        const int r = s / FQ_CH, c = s - (s / FQ_CH) * FQ_CH;
+        if (s < 64 * FQ_CH) {
+          const int tok = L.tok[r];
+          const u32x4 v = *reinterpret_cast<const u32x4*>(L.x + r * FQ_C + ((c ^ fq_swz(r)) << 3));
+          if (tok >= 0) *reinterpret_cast<u32x4*>(out + (size_t)((unsigned)tok * (unsigned)FQ_C) + 8 * c) = v;
+        }
+      }
+    }
     __syncthreads();  // every wave done with this window's images before the next is staged
   }
 }
@@ -1088,18 +1141,30 @@ int num_cus_fq() {
   return cus;
 }
 
-template <typename T, bool DROP, bool STORE_QKV>
+template <typename T, bool DROP, bool STORE_QKV, bool PROJ>
 void launch_fq(dim3 grid, const void* x, const void* w, const float* b, const Aux& aux, void* out, void* qkv, Geom g,
                float scale, float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* keep,
-               hipStream_t st) {
-  auto kern = attn_qkv_fwd_mfma<T, DROP, STORE_QKV>;
+               const void* wp, const float* bp, void* o_out, hipStream_t st) {
+  auto kern = attn_qkv_fwd_mfma<T, DROP, STORE_QKV, PROJ>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(FusedLds));
     attr_set = true;
   }
   hipLaunchKernelGGL(kern, grid, dim3(64 * FQ_WAVES), sizeof(FusedLds), st, (const bf16_t*)x, (const bf16_t*)w, b, aux,
-                     (bf16_t*)out, (bf16_t*)qkv, g, scale, p_drop, (uint64_t)seed, seed_dev, (uint32_t*)keep);
+                     (bf16_t*)out, (bf16_t*)qkv, g, scale, p_drop, (uint64_t)seed, seed_dev, (uint32_t*)keep,
+                     (const bf16_t*)wp, bp, (bf16_t*)o_out);
+}
+
+template <typename T, bool PROJ>
+void launch_fq4(dim3 grid, const void* x, const void* w, const float* b, const Aux& aux, void* out, void* qkv, Geom g,
+                float scale, float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* keep,
+                const void* wp, const float* bp, void* o_out, hipStream_t st) {
+  const bool drop = p_drop > 0.f;
+  if (drop && qkv) launch_fq<T, true, true, PROJ>(grid, x, w, b, aux, out, qkv, g, scale, p_drop, seed, seed_dev, keep, wp, bp, o_out, st);
+  else if (drop) launch_fq<T, true, false, PROJ>(grid, x, w, b, aux, out, qkv, g, scale, p_drop, seed, seed_dev, keep, wp, bp, o_out, st);
+  else if (qkv) launch_fq<T, false, true, PROJ>(grid, x, w, b, aux, out, qkv, g, scale, p_drop, seed, seed_dev, keep, wp, bp, o_out, st);
+  else launch_fq<T, false, false, PROJ>(grid, x, w, b, aux, out, qkv, g, scale, p_drop, seed, seed_dev, keep, wp, bp, o_out, st);
 }
 
 }  // namespace
@@ -1113,10 +1178,10 @@ int msu_win_attn_qkv_supported(int C, int nh) { return C == FQ_C && nh == FQ_NH 
 // x = LN1 rows [B,H,W,C] 16-bit, W_qkv [3C][C] 16-bit, b_qkv f32; qkv_out [B,H,W,3C] (x W^T + b,
 // what the qkv Linear would store) or null; keep / dropout / seeds and the aux workspace
 // (msu_win_attn_fwd_workspace) as msu_win_attn_fwd.
-int msu_win_attn_qkv_fwd(int dtype, const void* x, const void* w_qkv, const float* b_qkv, const float* table,
-                         void* out, void* qkv_out, void* keep, float* workspace, int B, int H, int W, int C, int nh,
-                         int shift, float p_drop, unsigned long long seed, const unsigned long long* seed_dev,
-                         void* stream) {
+int msu_win_attn_qkv_fwd2(int dtype, const void* x, const void* w_qkv, const float* b_qkv, const float* table,
+                          const void* w_proj, const float* b_proj, void* out, void* o_out, void* qkv_out, void* keep,
+                          float* workspace, int B, int H, int W, int C, int nh, int shift, float p_drop,
+                          unsigned long long seed, const unsigned long long* seed_dev, void* stream) {
   if (!msu_is16(dtype) || !msu_win_attn_qkv_supported(C, nh)) return -2;
   if ((long)B * H * W * 3 * C >= (1L << 32)) return -2;
   const Geom g = make_geom(B, H, W, C, nh, shift);
@@ -1127,15 +1192,23 @@ int msu_win_attn_qkv_fwd(int dtype, const void* x, const void* w_qkv, const floa
   const Aux aux = carve_aux(workspace, C, nh, &img, &brow, &zrow);
   const long nb = g.nwin < num_cus_fq() ? g.nwin : num_cus_fq();
   const dim3 grid((unsigned)nb);
-  const bool drop = p_drop > 0.f;
+  if ((w_proj == nullptr) != (b_proj == nullptr)) return -3;
   MSU_DISPATCH16(dtype, T,
     hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, b_qkv, nh, 3 * C,
                        1.0f / scale, img, brow, zrow);
-    if (drop && qkv_out) launch_fq<T, true, true>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st);
-    else if (drop) launch_fq<T, true, false>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st);
-    else if (qkv_out) launch_fq<T, false, true>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st);
-    else launch_fq<T, false, false>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st));
+    if (w_proj) launch_fq4<T, true>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep,
+                                    w_proj, b_proj, o_out, st);
+    else launch_fq4<T, false>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep,
+                              nullptr, nullptr, nullptr, st));
   return MSU_CHECK_LAUNCH();
+}
+
+int msu_win_attn_qkv_fwd(int dtype, const void* x, const void* w_qkv, const float* b_qkv, const float* table,
+                         void* out, void* qkv_out, void* keep, float* workspace, int B, int H, int W, int C, int nh,
+                         int shift, float p_drop, unsigned long long seed, const unsigned long long* seed_dev,
+                         void* stream) {
+  return msu_win_attn_qkv_fwd2(dtype, x, w_qkv, b_qkv, table, nullptr, nullptr, out, nullptr, qkv_out, keep, workspace,
+                               B, H, W, C, nh, shift, p_drop, seed, seed_dev, stream);
 }
 
 }  // extern "C"

@@ -143,11 +143,15 @@ class ShiftedWindowAttention(nn.Module):
     def forward(self, x):
         """x: [B, H, W, C] (already norm1-ed)."""
         p = self.attention_dropout if self.training else 0.0
-        if ops.window_attention_qkv_fusable(x, self.num_heads, self.qkv.bias):
-            # stage 0: the qkv Linear fused into the attention kernel (no qkv round trip)
+        if ops.window_attention_qkv_fusable(x, self.num_heads, self.qkv.bias) and self.proj.bias is not None:
+            # stage 0: qkv Linear -> window attention -> proj Linear in one kernel (no qkv / o
+            # round trip through HBM; ops.window_attention_qkv)
             o = ops.window_attention_qkv(x, self.qkv.weight, self.qkv.bias, self.relative_position_bias_table,
                                          self.num_heads, self.shift_size[0], p, _next_seed() if p > 0 else 0,
-                                         _dev_seed if p > 0 else None)
+                                         _dev_seed if p > 0 else None, self.proj.weight, self.proj.bias)
+            if self.dropout > 0 and self.training:
+                o = F.dropout(o, self.dropout, True)
+            return o
         else:
             qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
             qb = self.qkv.bias if self.qkv.bias is not None else torch.zeros(

@@ -608,51 +608,66 @@ class _Ctx:
         self.__dict__.update(kw)
 
 
-def _attn_qkv_impl(x, weight, bias, table, num_heads, shift, p_drop, seed, seed_dev, store_qkv):
+def _attn_qkv_impl(x, weight, bias, table, proj_weight, proj_bias, num_heads, shift, p_drop, seed, seed_dev,
+                   store):
+    """(y, o, qkv, keep): y = proj(o) when proj_weight is given (else y = o and o is empty),
+    o = attention(x W^T + b); o / qkv are kept (written) only when ``store`` (training)."""
     _need_cuda(x)
     x = x.contiguous()
     B, H, W, C = x.shape
     dt = x.dtype
     w = _shadow(weight, dt)
+    proj = proj_weight is not None
+    wp = _shadow(proj_weight, dt) if proj else None
     L = _lib.lib()
-    out = torch.empty(B, H, W, C, device=x.device, dtype=dt)
-    qkv = torch.empty(B, H, W, 3 * C, device=x.device, dtype=dt) if store_qkv else x.new_empty(0)
+    y = torch.empty(B, H, W, C, device=x.device, dtype=dt)
+    o = torch.empty(B, H, W, C, device=x.device, dtype=dt) if (proj and store) else x.new_empty(0)
+    qkv = torch.empty(B, H, W, 3 * C, device=x.device, dtype=dt) if store else x.new_empty(0)
     ws = torch.empty(L.msu_win_attn_fwd_workspace(_dt(x), C, num_heads), device=x.device, dtype=torch.float32)
     keep = torch.empty(L.msu_win_attn_keep_words(_dt(x), B, H, W, num_heads) if p_drop > 0 and _ATTN_KEEP else 0,
                        device=x.device, dtype=torch.int32)
-    _lib.call("msu_win_attn_qkv_fwd", _dt(x), _p(x), _p(w), _p(bias), _p(table), _p(out),
-              _p(qkv) if store_qkv else None, _p(keep) if keep.numel() else None, _p(ws), B, H, W, C, num_heads,
-              shift, float(p_drop), seed, _p(seed_dev), _s(x))
-    return out, qkv, keep
+    _lib.call("msu_win_attn_qkv_fwd2", _dt(x), _p(x), _p(w), _p(bias), _p(table), _p(wp),
+              _p(proj_bias) if proj else None, _p(y), _p(o) if o.numel() else None, _p(qkv) if store else None,
+              _p(keep) if keep.numel() else None, _p(ws), B, H, W, C, num_heads, shift, float(p_drop), seed,
+              _p(seed_dev), _s(x))
+    return y, o, qkv, keep
 
 
-def _attn_qkv_fake(x, weight, bias, table, num_heads, shift, p_drop, seed, seed_dev, store_qkv):
+def _attn_qkv_fake(x, weight, bias, table, proj_weight, proj_bias, num_heads, shift, p_drop, seed, seed_dev, store):
     B, H, W, C = x.shape
     nwin = B * (-(-H // 7)) * (-(-W // 7))
     kw = nwin * num_heads * 128 if (p_drop > 0 and _ATTN_KEEP) else 0
-    return (x.new_empty(B, H, W, C), x.new_empty(B, H, W, 3 * C) if store_qkv else x.new_empty(0),
-            x.new_empty(kw, dtype=torch.int32))
+    return (x.new_empty(B, H, W, C),
+            x.new_empty(B, H, W, C) if (proj_weight is not None and store) else x.new_empty(0),
+            x.new_empty(B, H, W, 3 * C) if store else x.new_empty(0), x.new_empty(kw, dtype=torch.int32))
 
 
 def _attn_qkv_setup(ctx, inputs, output):
-    x, weight, bias, table, num_heads, shift, p_drop, seed, seed_dev, store_qkv = inputs
-    _, qkv, keep = output
-    ctx.mark_non_differentiable(qkv, keep)
+    x, weight, bias, table, proj_weight, proj_bias, num_heads, shift, p_drop, seed, seed_dev, store = inputs
+    _, o, qkv, keep = output
+    ctx.mark_non_differentiable(o, qkv, keep)
     ctx.set_materialize_grads(False)
-    ctx.save_for_backward(x.contiguous(), qkv, bias, table, seed_dev, keep)
-    ctx.params = (weight, bias)
+    ctx.save_for_backward(x.contiguous(), o, qkv, bias, table, seed_dev, keep)
+    ctx.params = (weight, bias, proj_weight, proj_bias)
     ctx.bias_param = bias if isinstance(bias, torch.nn.Parameter) else None
     ctx.table_param = table if isinstance(table, torch.nn.Parameter) else None
     ctx.cfg = (num_heads, shift, float(p_drop), seed)
 
 
-def _attn_qkv_backward(ctx, dout, _dqkv, _dkeep):
-    x, qkv, bias, table, seed_dev, keep = ctx.saved_tensors
-    if dout is None:
-        return (None,) * 10
+def _attn_qkv_backward(ctx, dy, _do, _dqkv, _dkeep):
+    x, o, qkv, bias, table, seed_dev, keep = ctx.saved_tensors
+    if dy is None:
+        return (None,) * 12
     if qkv.numel() == 0:
-        raise RuntimeError("window_attention_qkv: backward through a forward that did not keep qkv (store_qkv=False)")
-    weight, _ = ctx.params
+        raise RuntimeError("window_attention_qkv: backward through a forward that did not keep qkv (store=False)")
+    weight, _, wp, bp = ctx.params
+    dwp = dbp = None
+    if wp is not None:
+        # proj Linear first: do = dy . W_proj, dW_proj / db_proj from (dy, o)
+        pctx = _Ctx((o,), params=(wp, bp), needs_input_grad=(True, True, True))
+        dout, dwp, dbp = _linear_backward(pctx, dy)
+    else:
+        dout = dy
     actx = _Ctx((qkv, bias, table, seed_dev, keep), cfg=ctx.cfg, bias_param=ctx.bias_param,
                 table_param=ctx.table_param)
     dqkv, dbias_pad, dtable = _attn_backward(actx, dout, None)[:3]
@@ -662,13 +677,13 @@ def _attn_qkv_backward(ctx, dout, _dqkv, _dkeep):
         db = db + dbias_pad
     elif dbias_pad is not None:
         db = dbias_pad
-    return dx, dw, db, dtable, None, None, None, None, None, None
+    return dx, dw, db, dtable, dwp, dbp, None, None, None, None, None, None
 
 
 _window_attention_qkv = _define(
     "window_attention_qkv",
-    "(Tensor x, Tensor weight, Tensor bias, Tensor table, int num_heads, int shift, float p_drop, int seed,"
-    " Tensor? seed_dev, bool store_qkv) -> (Tensor, Tensor, Tensor)",
+    "(Tensor x, Tensor weight, Tensor bias, Tensor table, Tensor? proj_weight, Tensor? proj_bias, int num_heads,"
+    " int shift, float p_drop, int seed, Tensor? seed_dev, bool store) -> (Tensor, Tensor, Tensor, Tensor)",
     _attn_qkv_impl, _attn_qkv_fake, _attn_qkv_setup, _attn_qkv_backward)
 
 
@@ -680,16 +695,26 @@ def window_attention_qkv_fusable(x, num_heads, bias):
     return bool(_lib.lib().msu_win_attn_qkv_supported(C, num_heads))
 
 
-def window_attention_qkv(x, weight, bias, table, num_heads, shift, p_drop=0.0, seed=0, seed_dev=None):
-    """window_attention(linear(x, weight, bias), bias, table, ...) with the qkv Linear fused in:
-    x [B, H, W, C] (LN1 output) -> [B, H, W, C] (before proj)."""
+def _param_or_f32(t):
+    return t if isinstance(t, torch.nn.Parameter) else _f32(t)
+
+
+def window_attention_qkv(x, weight, bias, table, num_heads, shift, p_drop=0.0, seed=0, seed_dev=None,
+                         proj_weight=None, proj_bias=None):
+    """window_attention(linear(x, weight, bias), bias, table, ...) with the qkv Linear fused in
+    (and the proj Linear, ``linear(., proj_weight, proj_bias)``, when given): x [B, H, W, C] (LN1
+    output) -> [B, H, W, C]."""
     dt = act_dtype()
     x = _as(x, dt)
-    store = torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad or bias.requires_grad or
-                                         table.requires_grad)
-    return _window_attention_qkv(x, weight, _f32(bias) if not isinstance(bias, torch.nn.Parameter) else bias,
-                                 table if isinstance(table, torch.nn.Parameter) else _f32(table), int(num_heads),
-                                 int(shift), float(p_drop), int(seed) & ((1 << 63) - 1), seed_dev, bool(store))[0]
+    proj = proj_weight is not None
+    if proj and proj_bias is None:
+        raise ValueError("the fused proj needs its bias")
+    params = [weight, bias, table] + ([proj_weight, proj_bias] if proj else [])
+    store = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
+    return _window_attention_qkv(x, weight, _param_or_f32(bias), _param_or_f32(table),
+                                 proj_weight if proj else None, _param_or_f32(proj_bias) if proj else None,
+                                 int(num_heads), int(shift), float(p_drop), int(seed) & ((1 << 63) - 1), seed_dev,
+                                 bool(store))[0]
 
 
 # ----------------------------------------------------------------------------- token GEMM

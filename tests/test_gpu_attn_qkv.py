@@ -1,7 +1,7 @@
-"""GPU: the fused stage-0 qkv Linear + window attention unit (ops.window_attention_qkv,
+"""GPU: the fused stage-0 unit qkv Linear -> window attention -> proj Linear (ops.window_attention_qkv,
 csrc/window_attention_mfma.hip attn_qkv_fwd_mfma) against fp32 PyTorch and against the unfused
-path it replaces (ops.linear -> ops.window_attention; reference network/model_parts.py:166-170 ->
-torchvision qkv Linear + shifted_window_attention).
+path it replaces (ops.linear -> ops.window_attention -> ops.linear; reference
+network/model_parts.py:166-170 -> torchvision qkv Linear + shifted_window_attention + proj).
 
 * forward vs fp32: attention(x W^T + b) on the same 16-bit operands (tests/_parity_refs.py), at
   small padded / shifted maps and at stage 0 of 1 x 1024^2 (1369 windows, each persistent
@@ -51,6 +51,11 @@ def _inputs(B, H, W, seed, low):
     return x, w, b, table, dy
 
 
+def _proj(seed):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(C, C, generator=g) / math.sqrt(C)).to(DEV), (0.1 * torch.randn(C, generator=g)).to(DEV)
+
+
 @pytest.fixture(params=[torch.bfloat16, torch.float16], ids=["bf16", "f16"])
 def low(request):
     return request.param
@@ -59,20 +64,26 @@ def low(request):
 CASES = [(2, 8, 8, 3), (1, 14, 14, 0), (2, 28, 28, 3), (1, 10, 12, 3), (1, 256, 256, 3), (1, 256, 256, 0)]
 
 
+@pytest.mark.parametrize("proj", [False, True], ids=["attn", "attn_proj"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.05])
 @pytest.mark.parametrize("B,H,W,shift", CASES)
-def test_fused_forward_matches_fp32(B, H, W, shift, p_drop, low):
+def test_fused_forward_matches_fp32(B, H, W, shift, p_drop, proj, low):
     ops = _ops()
     x, w, b, table, _ = _inputs(B, H, W, B * H + W + shift, low)
+    wp, bp = _proj(B + H) if proj else (None, None)
     with torch.no_grad(), torch.autocast("cuda", dtype=low):
         assert ops.window_attention_qkv_fusable(x, NH, b)
-        y, qkv, keep = torch.ops.msunet.window_attention_qkv(x, w, b, table, NH, shift, p_drop, 99, None, True)
+        y, o, qkv, keep = torch.ops.msunet.window_attention_qkv(x, w, b, table, wp, bp, NH, shift, p_drop, 99, None,
+                                                                True)
     torch.cuda.synchronize()
     nwin = B * ((H + 6) // 7) * ((W + 6) // 7)
     mask = decode_keep_bits(keep, nwin * NH) if p_drop > 0 else None
     qkv_ref = torch.nn.functional.linear(x.float(), w.to(low).float(), b)
     _check(qkv, qkv_ref, TOL[low] / 4, "qkv kept for the backward")
     ref = attn_ref_from_qkv(qkv.float(), b, table, NH, shift, keep=mask, p_drop=p_drop)
+    if proj:
+        _check(o, ref, TOL[low], "o kept for the proj backward")
+        ref = torch.nn.functional.linear(o.float(), wp.to(low).float(), bp)
     _check(y, ref, TOL[low], "out")
 
 
@@ -83,21 +94,24 @@ def test_fused_equals_unfused_including_backward(B, H, W, shift, low):
     ops = _ops()
     x, w, b, table, dy = _inputs(B, H, W, 7 + H, low)
     res = {}
+    wp0, bp0 = _proj(11)
     for fused in (True, False):
         xg = x.clone().requires_grad_(True)
-        wg, bg, tg = [t.clone().requires_grad_(True) for t in (w, b, table)]
+        wg, bg, tg, wpg, bpg = [t.clone().requires_grad_(True) for t in (w, b, table, wp0, bp0)]
         with torch.autocast("cuda", dtype=low):
             if fused:
-                y, qkv, keep = torch.ops.msunet.window_attention_qkv(xg, wg, bg, tg, NH, shift, 0.1, 1234, None, True)
+                y, _, qkv, keep = torch.ops.msunet.window_attention_qkv(xg, wg, bg, tg, wpg, bpg, NH, shift, 0.1, 1234,
+                                                                        None, True)
             else:
                 qkv = ops.linear(xg, wg, bg)
-                y, keep = torch.ops.msunet.window_attention(qkv, bg, tg, NH, shift, 0.1, 1234, None)
+                o, keep = torch.ops.msunet.window_attention(qkv, bg, tg, NH, shift, 0.1, 1234, None)
+                y = ops.linear(o, wpg, bpg)
         y.backward(dy)
         torch.cuda.synchronize()
-        res[fused] = (y, qkv.detach(), keep, xg.grad, wg.grad, bg.grad, tg.grad)
+        res[fused] = (y, qkv.detach(), keep, xg.grad, wg.grad, bg.grad, tg.grad, wpg.grad, bpg.grad)
     assert torch.equal(res[True][2], res[False][2]), "keep bits differ"
     t = TOL[low] / 2
-    for name, a, r in zip(("out", "qkv", "keep", "dx", "dW", "db", "dtable"), res[True], res[False]):
+    for name, a, r in zip(("out", "qkv", "keep", "dx", "dW", "db", "dtable", "dWproj", "dbproj"), res[True], res[False]):
         if name != "keep":
             _check(a, r, t, name)
 
@@ -109,32 +123,36 @@ def test_fused_direct_params_match_autograd_params():
     B, H, W, shift = 2, 64, 64, 3
     x, w, b, table, dy = _inputs(B, H, W, 5, torch.bfloat16)
     res = {}
+    wp0, bp0 = _proj(3)
     for direct in (False, True):
         xg = x.clone().requires_grad_(True)
-        pw, pb, pt = (torch.nn.Parameter(t.clone()) for t in (w, b, table))
+        pw, pb, pt, ppw, ppb = (torch.nn.Parameter(t.clone()) for t in (w, b, table, wp0, bp0))
         if direct:
-            for p_ in (pw, pb, pt):
+            for p_ in (pw, pb, pt, ppw, ppb):
                 p_.grad = torch.zeros_like(p_)
                 p_._msu_direct = True
-            pw._msu_shadow = pw.detach().to(torch.bfloat16)
-            pw._msu_shadow_t = pw.detach().t().contiguous().to(torch.bfloat16)
-            pw._msu_shadow_ver = pw._version
+            for p_ in (pw, ppw):
+                p_._msu_shadow = p_.detach().to(torch.bfloat16)
+                p_._msu_shadow_t = p_.detach().t().contiguous().to(torch.bfloat16)
+                p_._msu_shadow_ver = p_._version
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            y = ops.window_attention_qkv(xg, pw, pb, pt, NH, shift, 0.05, 77)
+            y = ops.window_attention_qkv(xg, pw, pb, pt, NH, shift, 0.05, 77, None, ppw, ppb)
         y.backward(dy)
         ops.join_side_streams()
         torch.cuda.synchronize()
-        res[direct] = (xg.grad.float(), pw.grad.clone(), pb.grad.clone(), pt.grad.clone())
-    for name, a, r in zip(("dx", "dW", "db", "dtable"), res[True], res[False]):
+        res[direct] = (xg.grad.float(), pw.grad.clone(), pb.grad.clone(), pt.grad.clone(), ppw.grad.clone(),
+                       ppb.grad.clone())
+    for name, a, r in zip(("dx", "dW", "db", "dtable", "dWproj", "dbproj"), res[True], res[False]):
         _check(a, r, 1e-2, name)
 
 
 def test_fused_inference_keeps_no_qkv():
     ops = _ops()
     x, w, b, table, _ = _inputs(1, 28, 28, 3, torch.bfloat16)
+    wp, bp = _proj(5)
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-        y1 = ops.window_attention_qkv(x, w, b, table, NH, 3)
-        _, qkv, _ = torch.ops.msunet.window_attention_qkv(x, w, b, table, NH, 3, 0.0, 0, None, False)
-        y2 = ops.window_attention(ops.linear(x, w, b), b, table, NH, 3)
-    assert qkv.numel() == 0
+        y1 = ops.window_attention_qkv(x, w, b, table, NH, 3, proj_weight=wp, proj_bias=bp)
+        _, o, qkv, _ = torch.ops.msunet.window_attention_qkv(x, w, b, table, wp, bp, NH, 3, 0.0, 0, None, False)
+        y2 = ops.linear(ops.window_attention(ops.linear(x, w, b), b, table, NH, 3), wp, bp)
+    assert qkv.numel() == 0 and o.numel() == 0
     _check(y1, y2, 1.5e-2, "no-grad fused vs unfused")
