@@ -1632,13 +1632,14 @@ int launch_v3s(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float
   return MSU_CHECK_LAUNCH();
 }
 
-// v3 on 16x16x32 MFMA (same tile, LDS images and schedule; (p >> 1) & 3 swizzle): A/B switch
-// MSU_CONV_MFMA=16 (bare MFMA loops of this shape ran at ~1.12-1.15x the FLOP/s of 32x32x16 on
-// MI355X at equal cycles, MI355X_MICROARCH.md: the clock it holds)
+// v3 on 16x16x32 MFMA (same tile, LDS images and schedule; (p >> 1) & 3 swizzle), the default
+// for the forward launches since round 4: same-box kbench (r04b) conv1 2.22-2.28 vs 2.44 ms, conv2
+// 1.48 vs 1.55 ms (bare MFMA loops of this shape run at ~1.12-1.15x the FLOP/s of 32x32x16 on
+// MI355X at equal cycles: the clock it holds, MI355X_MICROARCH.md).  A/B switch MSU_CONV_MFMA=32.
 inline bool conv_v3_m16() {
   static const bool on = [] {
     const char* e = getenv("MSU_CONV_MFMA");
-    return e && e[0] == '1' && e[1] == '6';
+    return !(e && e[0] == '3' && e[1] == '2');
   }();
   return on;
 }

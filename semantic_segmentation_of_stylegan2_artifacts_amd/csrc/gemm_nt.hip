@@ -338,10 +338,14 @@ int num_cus_nt() {
 
 // Tile configuration of a shape, by a rounds-of-tiles cost model: the output is covered in
 // rounds of (CUs x workgroups per CU) tiles, each round costing a workgroup's tile area times the
-// workgroups sharing a CU (x 1.05 for the two-stage ring of the 192-wide tile):
+// workgroups sharing a CU, times the measured cost per output of the tile form (x 0.78 for the
+// 192-wide tiles: 64 x 96 wave tiles read 5 fragments per 6 MFMAs instead of 4 per 4; r04b
+// same-box kbench at whole-round shapes: 32768 x 384 x 1152 39-42 vs 57-58 us, 131072 x 192 x 768
+// 59-61 vs 84-88 us):
 //   wm 4, bn 128: 256 x 128, three-stage ring, one workgroup per CU;
 //   wm 2, bn 128: 128 x 128, two-stage ring, two workgroups per CU;
-//   wm 4, bn 192: 256 x 192, two-stage ring (3 x 56 KB does not fit), one workgroup per CU.
+//   wm 4, bn 192: 256 x 192, two-stage ring (3 x 56 KB does not fit), one workgroup per CU;
+//   wm 2, bn 192: 128 x 192, two-stage ring, two workgroups per CU (2 x 80 KB of LDS).
 // KN (input-gradient with the forward weight in place) keeps bn 128.  A/B switches:
 // MSU_NT_TILE = 128 | 256 (rows), MSU_NT_BN = 128 | 192 (columns).
 struct NtCfg {
@@ -358,7 +362,7 @@ NtCfg nt_cfg(long M, int N, bool wkn) {
     return e ? atoi(e) : 0;
   }();
   const long cus = num_cus_nt();
-  const NtCfg cands[3] = {{4, 128}, {2, 128}, {4, 192}};
+  const NtCfg cands[4] = {{4, 128}, {2, 128}, {4, 192}, {2, 192}};
   NtCfg best = cands[0];
   double best_cost = -1.0;
   for (const NtCfg& c : cands) {
@@ -368,7 +372,7 @@ NtCfg nt_cfg(long M, int N, bool wkn) {
     const long bm = 64L * c.wm, per_cu = c.wm == 2 ? 2 : 1;
     const long tiles = ((M + bm - 1) / bm) * ((N + c.bn - 1) / c.bn);
     const long rounds = (tiles + cus * per_cu - 1) / (cus * per_cu);
-    const double cost = (double)rounds * bm * c.bn * per_cu * (c.bn == 192 ? 1.05 : 1.0);
+    const double cost = (double)rounds * bm * c.bn * per_cu * (c.bn == 192 ? 0.78 : 1.0);
     if (best_cost < 0 || cost < best_cost) {
       best_cost = cost;
       best = c;
@@ -419,7 +423,8 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
   hipStream_t st = (hipStream_t)stream;
   MSU_DISPATCH16(dtype, T,
     if (cfg.bn == 192) {
-      launch_nt<T, 4, 2, false, 192>(epi, a, st);
+      if (cfg.wm == 4) launch_nt<T, 4, 2, false, 192>(epi, a, st);
+      else launch_nt<T, 2, 2, false, 192>(epi, a, st);
     } else if (cfg.wm == 4) {
       if (wkn) launch_nt<T, 4, 3, true, 128>(epi, a, st);
       else launch_nt<T, 4, 3, false, 128>(epi, a, st);

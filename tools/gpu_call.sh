@@ -73,7 +73,7 @@ for s in "$@"; do
       tail -14 $O/${TAG}_nt_ab.log ;;
     attn_pmc) step attn_pmc 400 bash $R/tools/pmc_attn.sh $TAG 256 3 3 0.05 ;;
     fused_ab)
-      for r in 1 2; do
+      for r in 1 2 3; do
         for v in 1 0; do
           echo "MSU_ATTN_QKV=$v" >> $O/${TAG}_fused_ab.log
           MSU_ATTN_QKV=$v timeout -k 10 240 python3 -u $R/bench.py --steps 15 --warmup 5 --no-cpu-baseline --no-roofline --no-input-pipeline 2>&1 | grep '^{' | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])" >> $O/${TAG}_fused_ab.log || exit 3
