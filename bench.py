@@ -218,7 +218,8 @@ def attention_roofline(device, batch, img, C, heads, p_drop):
 
 
 def fused_unit_roofline(device, batch, img, C, heads, p_drop):
-    """The stage-0 fused unit (qkv Linear -> window attention -> proj Linear in one kernel,
+    """The stage-0 fused unit (qkv Linear -> window attention -> proj Linear: by default the
+    head-stationary msu_win_attn_qkv_hs_fwd + the proj Linear's GEMM, MSU_ATTN_QKV=1 all three in
     msu_win_attn_qkv_fwd2) at the bench shape: inference (no qkv / o written) and the training
     forward (qkv and o kept for the backward, dropout keep bits), HIP events on the launching
     stream.  Algorithmic FLOP per launch = 2 M C 3C (qkv) + 4 49^2 32 per window x head (QK^T, PV
@@ -257,7 +258,9 @@ def fused_unit_roofline(device, batch, img, C, heads, p_drop):
 
     nwin = batch * ((res + 6) // 7) ** 2
     flops = 2.0 * M * C * 3 * C + 4.0 * 49 * 49 * 32 * nwin * heads + 2.0 * M * C * C
-    out = {"kernel": "attn_qkv_fwd_mfma<PROJ> (qkv Linear + window attention + proj, one kernel)",
+    kern = ("attn_qkv_hs_mfma (qkv Linear + window attention) + proj GEMM" if ops._ATTN_QKV_MODE == "hs" else
+            "attn_qkv_fwd_mfma<PROJ> (qkv Linear + window attention + proj, one kernel)")
+    out = {"kernel": kern,
            "flops_per_launch": flops}
     for name, store, byts in (("inference", False, 2 * M * C * 2), ("training_fwd", True, (2 * C + 3 * C + C) * M * 2)):
         ms = timed(store)

@@ -595,9 +595,12 @@ def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0,
 # Stage-0 fused unit (csrc/window_attention_mfma.hip attn_qkv_fwd_mfma): the qkv Linear and the
 # window attention in one kernel, qkv never read back (in inference never written).  The backward
 # is the two existing ones in sequence: the attention backward (dqkv, relative table, padded-token
-# bias share) then the qkv Linear's (one-pass msu_linear_bwd at stage 0).  A/B switch
-# MSU_ATTN_QKV=0: the unfused qkv Linear + window_attention path.
-_ATTN_QKV = os.environ.get("MSU_ATTN_QKV", "1") != "0"
+# bias share) then the qkv Linear's (one-pass msu_linear_bwd at stage 0).  Two kernels:
+# MSU_ATTN_QKV=hs (default) the head-stationary one (msu_win_attn_qkv_hs_fwd: independent waves,
+# one (window, head) item each; proj a separate Linear), =1 the window-per-workgroup one with
+# proj inside (msu_win_attn_qkv_fwd2), =0 the unfused qkv Linear + window_attention path.
+_ATTN_QKV_MODE = os.environ.get("MSU_ATTN_QKV", "hs")
+_ATTN_QKV = _ATTN_QKV_MODE != "0"
 
 
 class _Ctx:
@@ -626,6 +629,16 @@ def _attn_qkv_impl(x, weight, bias, table, proj_weight, proj_bias, num_heads, sh
     ws = torch.empty(L.msu_win_attn_fwd_workspace(_dt(x), C, num_heads), device=x.device, dtype=torch.float32)
     keep = torch.empty(L.msu_win_attn_keep_words(_dt(x), B, H, W, num_heads) if p_drop > 0 and _ATTN_KEEP else 0,
                        device=x.device, dtype=torch.int32)
+    if _ATTN_QKV_MODE == "hs":
+        a = torch.empty(B, H, W, C, device=x.device, dtype=dt) if proj else y
+        _lib.call("msu_win_attn_qkv_hs_fwd", _dt(x), _p(x), _p(w), _p(bias), _p(table), _p(a),
+                  _p(qkv) if store else None, _p(keep) if keep.numel() else None, _p(ws), B, H, W, C, num_heads,
+                  shift, float(p_drop), seed, _p(seed_dev), _s(x))
+        if proj:
+            y = _linear_impl(a, proj_weight, proj_bias)
+            if store:
+                o = a
+        return y, o, qkv, keep
     _lib.call("msu_win_attn_qkv_fwd2", _dt(x), _p(x), _p(w), _p(bias), _p(table), _p(wp),
               _p(proj_bias) if proj else None, _p(y), _p(o) if o.numel() else None, _p(qkv) if store else None,
               _p(keep) if keep.numel() else None, _p(ws), B, H, W, C, num_heads, shift, float(p_drop), seed,

@@ -1,5 +1,6 @@
 """GPU: the fused stage-0 unit qkv Linear -> window attention -> proj Linear (ops.window_attention_qkv,
-csrc/window_attention_mfma.hip attn_qkv_fwd_mfma) against fp32 PyTorch and against the unfused
+csrc/window_attention_mfma.hip: attn_qkv_hs_mfma, the default head-stationary form, and
+attn_qkv_fwd_mfma, the window-per-workgroup form with proj inside) against fp32 PyTorch and against the unfused
 path it replaces (ops.linear -> ops.window_attention -> ops.linear; reference
 network/model_parts.py:166-170 -> torchvision qkv Linear + shifted_window_attention + proj).
 
@@ -61,13 +62,19 @@ def low(request):
     return request.param
 
 
+@pytest.fixture(params=["hs", "1"], ids=["head_stationary", "window_wg"])
+def kernel(request, monkeypatch):
+    monkeypatch.setattr(_ops(), "_ATTN_QKV_MODE", request.param)
+    return request.param
+
+
 CASES = [(2, 8, 8, 3), (1, 14, 14, 0), (2, 28, 28, 3), (1, 10, 12, 3), (1, 256, 256, 3), (1, 256, 256, 0)]
 
 
 @pytest.mark.parametrize("proj", [False, True], ids=["attn", "attn_proj"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.05])
 @pytest.mark.parametrize("B,H,W,shift", CASES)
-def test_fused_forward_matches_fp32(B, H, W, shift, p_drop, proj, low):
+def test_fused_forward_matches_fp32(B, H, W, shift, p_drop, proj, low, kernel):
     ops = _ops()
     x, w, b, table, _ = _inputs(B, H, W, B * H + W + shift, low)
     wp, bp = _proj(B + H) if proj else (None, None)
@@ -88,7 +95,7 @@ def test_fused_forward_matches_fp32(B, H, W, shift, p_drop, proj, low):
 
 
 @pytest.mark.parametrize("B,H,W,shift", [(2, 28, 28, 3), (1, 256, 256, 3)])
-def test_fused_equals_unfused_including_backward(B, H, W, shift, low):
+def test_fused_equals_unfused_including_backward(B, H, W, shift, low, kernel):
     """Same keep bits and qkv as the unfused forward; the outputs and all gradients agree to
     16-bit rounding (the backward kernels are the unfused path's own)."""
     ops = _ops()
@@ -116,7 +123,7 @@ def test_fused_equals_unfused_including_backward(B, H, W, shift, low):
             _check(a, r, t, name)
 
 
-def test_fused_direct_params_match_autograd_params():
+def test_fused_direct_params_match_autograd_params(kernel):
     """Trainer-style parameters (flat .grad, bf16 shadow, direct accumulation: the one-pass Linear
     backward and the side-stream attention tail) give the plain autograd gradients."""
     ops = _ops()
@@ -146,7 +153,7 @@ def test_fused_direct_params_match_autograd_params():
         _check(a, r, 1e-2, name)
 
 
-def test_fused_inference_keeps_no_qkv():
+def test_fused_inference_keeps_no_qkv(kernel):
     ops = _ops()
     x, w, b, table, _ = _inputs(1, 28, 28, 3, torch.bfloat16)
     wp, bp = _proj(5)

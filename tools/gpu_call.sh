@@ -80,6 +80,23 @@ for s in "$@"; do
         done
       done
       cat $O/${TAG}_fused_ab.log ;;
+    wgrad_nst)
+      for shp in "32768 1152 384" "32768 384 384" "32768 1536 384" "32768 384 1536" "131072 576 192" "131072 192 192" \
+                 "131072 768 192" "131072 192 768" "8192 2304 768" "8192 3072 768" "8192 768 3072" "524288 288 96"; do
+        for nst in 3 4 5 6; do
+          echo -n "NST=$nst " >> $O/${TAG}_wgrad_nst.log
+          MSU_WGRAD_NST=$nst timeout -k 10 60 python -u $R/tools/wgrad_one.py $shp 30 2>&1 | grep wgrad >> $O/${TAG}_wgrad_nst.log || exit 3
+        done
+      done
+      cat $O/${TAG}_wgrad_nst.log ;;
+    fused3_ab)
+      for r in 1 2; do
+        for v in hs 1 0; do
+          echo "MSU_ATTN_QKV=$v" >> $O/${TAG}_fused3_ab.log
+          MSU_ATTN_QKV=$v timeout -k 10 240 python3 -u $R/bench.py --steps 15 --warmup 5 --no-cpu-baseline --no-input-pipeline 2>&1 | grep '^{' | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], json.dumps(d.get('roofline_attention', {}).get('fused_unit')))" >> $O/${TAG}_fused3_ab.log || exit 3
+        done
+      done
+      cat $O/${TAG}_fused3_ab.log ;;
     nt_tests) step nt_tests 400 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py $R/tests/test_routing.py ;;
     nt_pmc)
       timeout -k 10 60 python -u $R/tools/nt_one.py 32768 1152 384 50 > $O/${TAG}_nt.log 2>&1 || exit 3
