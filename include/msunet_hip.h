@@ -147,7 +147,7 @@ int msu_win_attn_qkv_fwd2(int dtype, const void* x, const void* w_qkv, const flo
                           float* workspace, int B, int H, int W, int C, int nh, int shift, float p_drop,
                           unsigned long long seed, const unsigned long long* seed_dev, void* stream);
 /* msu_win_attn_qkv_fwd's contract, head-stationary kernel (one wave per (window, head) item, the
- * head's W_qkv rows resident in LDS); the default form behind ops.window_attention_qkv. */
+ * head's W_qkv rows resident in LDS); opt-in (MSU_ATTN_QKV=hs) form of ops.window_attention_qkv. */
 int msu_win_attn_qkv_hs_fwd(int dtype, const void* x, const void* w_qkv, const float* b_qkv, const float* table,
                             void* out, void* qkv_out, void* keep, float* workspace, int B, int H, int W, int C, int nh,
                             int shift, float p_drop, unsigned long long seed, const unsigned long long* seed_dev,

@@ -596,10 +596,11 @@ def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0,
 # window attention in one kernel, qkv never read back (in inference never written).  The backward
 # is the two existing ones in sequence: the attention backward (dqkv, relative table, padded-token
 # bias share) then the qkv Linear's (one-pass msu_linear_bwd at stage 0).  Two kernels:
-# MSU_ATTN_QKV=hs (default) the head-stationary one (msu_win_attn_qkv_hs_fwd: independent waves,
-# one (window, head) item each; proj a separate Linear), =1 the window-per-workgroup one with
-# proj inside (msu_win_attn_qkv_fwd2), =0 the unfused qkv Linear + window_attention path.
-_ATTN_QKV_MODE = os.environ.get("MSU_ATTN_QKV", "hs")
+# MSU_ATTN_QKV=1 (default) the window-per-workgroup one with proj inside
+# (msu_win_attn_qkv_fwd2), =hs the head-stationary one (msu_win_attn_qkv_hs_fwd: independent
+# waves, one (window, head) item each, proj a separate Linear; r04d same-box benches 165.6 /
+# 165.8 vs 166.4 / 166.5 img/s), =0 the unfused qkv Linear + window_attention path.
+_ATTN_QKV_MODE = os.environ.get("MSU_ATTN_QKV", "1")
 _ATTN_QKV = _ATTN_QKV_MODE != "0"
 
 

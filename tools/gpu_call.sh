@@ -89,6 +89,18 @@ for s in "$@"; do
         done
       done
       cat $O/${TAG}_wgrad_nst.log ;;
+    wgrad_diag)
+      for shp in "32768 1152 384" "8192 2304 768" "131072 576 192"; do
+        for lib in "" $R/tools/exp/libmsunet_gemm_wgrad_1.so $R/tools/exp/libmsunet_gemm_wgrad_2.so; do
+          echo -n "lib=${lib##*/} " >> $O/${TAG}_wgrad_diag.log
+          MSU_LIB_OVERRIDE=$lib timeout -k 10 60 python -u $R/tools/wgrad_one.py $shp 30 2>&1 | grep wgrad >> $O/${TAG}_wgrad_diag.log || exit 3
+        done
+      done
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT \
+        -d $O/${TAG}_wgpmc1 -o p --output-format csv -- python3 $R/tools/wgrad_one.py 32768 1152 384 10 > /dev/null 2>&1 || exit 3
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT \
+        -d $O/${TAG}_wgpmc2 -o p --output-format csv -- python3 $R/tools/wgrad_one.py 32768 1152 384 10 > /dev/null 2>&1 || exit 3
+      cat $O/${TAG}_wgrad_diag.log ;;
     fused3_ab)
       for r in 1 2; do
         for v in hs 1 0; do
