@@ -101,6 +101,19 @@ for s in "$@"; do
       timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT \
         -d $O/${TAG}_wgpmc2 -o p --output-format csv -- python3 $R/tools/wgrad_one.py 32768 1152 384 10 > /dev/null 2>&1 || exit 3
       cat $O/${TAG}_wgrad_diag.log ;;
+    vform_tests) MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_vform.so step vform_tests 900 python -u -m pytest $R/tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    vform_kern)
+      for lib in "" $R/tools/exp/libmsunet_vform.so "" $R/tools/exp/libmsunet_vform.so; do
+        echo "lib=${lib##*/}" >> $O/${TAG}_vform_kern.log
+        for shp in "32768 1152 384" "8192 2304 768" "131072 576 192" "524288 288 96"; do
+          MSU_LIB_OVERRIDE=$lib timeout -k 10 60 python -u $R/tools/wgrad_one.py $shp 30 2>&1 | grep wgrad >> $O/${TAG}_vform_kern.log || exit 3
+        done
+        for shp in "32768 1152 384" "131072 192 576" "8192 768 3072"; do
+          MSU_LIB_OVERRIDE=$lib timeout -k 10 60 python -u $R/tools/nt_one.py $shp 30 2>&1 | grep "nt M" >> $O/${TAG}_vform_kern.log || exit 3
+        done
+      done
+      cat $O/${TAG}_vform_kern.log ;;
+    vform_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_vform "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_vform.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_vform.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_vform.so" || exit 3 ;;
     fused3_ab)
       for r in 1 2; do
         for v in hs 1 0; do
