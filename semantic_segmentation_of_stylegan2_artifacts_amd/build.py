@@ -17,8 +17,13 @@ CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libmsunet_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -amdgpu-mfma-vgpr-form: MFMA accumulators in VGPRs.  In the default AGPR form the register
+# allocator shuffled accumulators between AGPRs and VGPRs inside the main loops (68 v_accvgpr
+# moves per 42 MFMAs in the weight-gradient loop, 300-500 per NT / token GEMM kernel); gfx950
+# MFMAs read and write either file at the same rate.  Same-box r04f: weight gradient -9 %,
+# bench 169.1 / 169.1 / 169.5 vs 168.1 / 167.8 / 167.9 img/s.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-         "-munsafe-fp-atomics"]
+         "-munsafe-fp-atomics", "-mllvm", "-amdgpu-mfma-vgpr-form=1"]
 
 
 def _sources():

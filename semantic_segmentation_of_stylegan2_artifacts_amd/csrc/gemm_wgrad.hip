@@ -270,6 +270,9 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
       }
       if constexpr (!(MSU_EXP & 1))
         accb[i] = Fmt16<T>::mma16(af[i & 1], ones, accb[i]);  // unconditional
+      // the group's MFMAs stay above the wait: left to the scheduler they sank below it, so each
+      // group waited on the read issued just before it (the LDS latency exposed 6x per stage)
+      __builtin_amdgcn_sched_barrier(0);
       if constexpr (i + 1 < NTW) lds_wait_tie<0>(af[(i + 1) & 1]);
     });
   }

@@ -477,16 +477,22 @@ struct BwdLds {
 // wave its 32 rows) while window k is computed.
 // KEPT: the forward's keep bits are read from keep_in ([item][it][lane] words) instead of
 // re-hashed (16 hashes per lane per window were ~15 % of the stage-0 backward).
-template <typename T, bool DROP, bool KEPT>
-__global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
+// HPW heads per workgroup (2 HPW waves): the heads of a window run side by side, so the 128-B
+// lines their 64-B q / k / v / dO slices share are fetched once (one head per workgroup read
+// them 1.55x over, r04e counters).  Each head pair has its own LDS, the workgroup shares the
+// barriers.
+template <typename T, bool DROP, bool KEPT, int HPW>
+__global__ void __launch_bounds__(128 * HPW, HPW == 3 ? 1 : 2) attn_bwd_mfma(
     const bf16_t* __restrict__ qkv, Aux aux, const bf16_t* __restrict__ dout, bf16_t* __restrict__ dqkv,
     float* __restrict__ dB_part, float* __restrict__ qb_part, Geom g, float scale, float p_drop,
     uint64_t seed0, const unsigned long long* seed_dev, const uint32_t* __restrict__ keep_in, int nblk) {
   static_assert(DROP || !KEPT, "keep bits only with dropout");
   const uint64_t seed = launch_seed(seed0, seed_dev);
-  __shared__ __attribute__((aligned(16))) BwdLds L;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;  // w: this wave's query / key tile
-  const int h = blockIdx.y;
+  __shared__ __attribute__((aligned(16))) BwdLds Ls[HPW];
+  const int slot = HPW == 1 ? 0 : (int)(threadIdx.x >> 7), tid = threadIdx.x & 127;
+  BwdLds& L = Ls[slot];
+  const int lane = threadIdx.x & 63, w = tid >> 6;  // w: this wave's query / key tile
+  const int h = blockIdx.y * HPW + slot;
   const long C3 = 3L * g.C;
   const int hh = lane >> 5;
   const float* bimg = aux.bimg + (long)h * 4096;
@@ -701,7 +707,7 @@ __global__ void __launch_bounds__(128, 2) attn_bwd_mfma(
     for (int k = 0; k < 3; ++k) img[4096 + 32 * k + lane] = padv[k];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < 169; e += 128) {
+  for (int e = tid; e < 169; e += 128) {
     const int dh = e / 13 - 6, dw = e % 13 - 6;
     float sum = 0.f;
     for (int ih = 0; ih < WS; ++ih) {
@@ -785,8 +791,37 @@ long head_blocks(long need, long cap) {
   return (need + 7) / 8 * 8;
 }
 
-// backward workgroups per head: about four 2-wave workgroups per CU over all heads
-int bwd_blocks(long nwin, int nh) { return (int)head_blocks(nwin, 1024 / nh); }
+// heads per backward workgroup: all three at nh = 3 (stage 0 of Swin-T/S: one 6-wave workgroup
+// per CU), pairs for even nh (a 128-B line holds two heads' slices), else one.  A/B switch
+// MSU_ATTN_BWD_HPW=1|2|3 (used where nh allows it).
+int bwd_hpw(int nh) {
+  static const int forced = getenv("MSU_ATTN_BWD_HPW") ? atoi(getenv("MSU_ATTN_BWD_HPW")) : 0;
+  if (forced >= 1 && forced <= 3 && nh % forced == 0) return forced;
+  return nh == 3 ? 3 : (nh % 2 == 0 ? 2 : 1);
+}
+
+// backward workgroups per head group: the LDS (40 KB per head) allows four heads per CU
+// (three at nh = 3), i.e. 1024 / nh workgroups of 2 HPW waves (768 / nh at HPW = 3)
+int bwd_blocks(long nwin, int nh) { return (int)head_blocks(nwin, (bwd_hpw(nh) == 3 ? 768 : 1024) / nh); }
+
+template <typename T, int HPW>
+void launch_bwd(dim3 grid, hipStream_t st, const void* qkv, const Aux& aux, const void* dout, void* dqkv,
+                float* dB_part, float* qb_part, const Geom& g, float scale, float p_drop, unsigned long long seed,
+                const unsigned long long* seed_dev, const void* keep, int nblk) {
+  const dim3 blk(128 * HPW);
+  if (p_drop > 0.f && keep)
+    hipLaunchKernelGGL((attn_bwd_mfma<T, true, true, HPW>), grid, blk, 0, st, (const bf16_t*)qkv, aux,
+                       (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale, p_drop, (uint64_t)seed,
+                       seed_dev, (const uint32_t*)keep, nblk);
+  else if (p_drop > 0.f)
+    hipLaunchKernelGGL((attn_bwd_mfma<T, true, false, HPW>), grid, blk, 0, st, (const bf16_t*)qkv, aux,
+                       (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale, p_drop, (uint64_t)seed,
+                       seed_dev, nullptr, nblk);
+  else
+    hipLaunchKernelGGL((attn_bwd_mfma<T, false, false, HPW>), grid, blk, 0, st, (const bf16_t*)qkv, aux,
+                       (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale, p_drop, (uint64_t)seed,
+                       seed_dev, nullptr, nblk);
+}
 
 }  // namespace
 
@@ -837,22 +872,14 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
   const Aux aux = carve_aux(ws, C, nh, &img, &brow, &zrow);
   float* dB_part = ws + aux_floats(C, nh);
   float* qb_part = dB_part + parts * nh * 169;
-  const dim3 grid(nblk, nh);
+  const int hpw = bwd_hpw(nh);
+  const dim3 grid(nblk, nh / hpw);
   MSU_DISPATCH16(dtype, T,
     hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
                        1.0f / scale, img, brow, zrow);
-    if (p_drop > 0.f && keep)
-      hipLaunchKernelGGL((attn_bwd_mfma<T, true, true>), grid, dim3(128), 0, st, (const bf16_t*)qkv, aux,
-                         (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale, p_drop, (uint64_t)seed,
-                         seed_dev, (const uint32_t*)keep, nblk);
-    else if (p_drop > 0.f)
-      hipLaunchKernelGGL((attn_bwd_mfma<T, true, false>), grid, dim3(128), 0, st, (const bf16_t*)qkv, aux,
-                         (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale, p_drop, (uint64_t)seed,
-                         seed_dev, nullptr, nblk);
-    else
-      hipLaunchKernelGGL((attn_bwd_mfma<T, false, false>), grid, dim3(128), 0, st, (const bf16_t*)qkv, aux,
-                         (const bf16_t*)dout, (bf16_t*)dqkv, dB_part, qb_part, g, scale, p_drop, (uint64_t)seed,
-                         seed_dev, nullptr, nblk));
+    if (hpw == 3) launch_bwd<T, 3>(grid, st, qkv, aux, dout, dqkv, dB_part, qb_part, g, scale, p_drop, seed, seed_dev, keep, nblk);
+    else if (hpw == 2) launch_bwd<T, 2>(grid, st, qkv, aux, dout, dqkv, dB_part, qb_part, g, scale, p_drop, seed, seed_dev, keep, nblk);
+    else launch_bwd<T, 1>(grid, st, qkv, aux, dout, dqkv, dB_part, qb_part, g, scale, p_drop, seed, seed_dev, keep, nblk));
   if (pst == (hipStream_t)(intptr_t)-1) return MSU_CHECK_LAUNCH();  // tail issued by the caller
   // parameter-gradient reductions: on pst (after the backward kernel) when given
   const int rc = attn_param_stream(st, pst);

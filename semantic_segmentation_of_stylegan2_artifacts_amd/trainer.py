@@ -182,6 +182,12 @@ class GradBucketer:
             if count:
                 self.buckets.append([g, start, g.numel])
         self.main_stream = None  # the stream the training step runs on (set per step)
+        # set by the Trainer while it captures the step: every bucket is then issued by finish()
+        # on the capturing thread.  Backward's hooks run on autograd's device thread, and a
+        # collective issued there during a thread-local capture was at times handed to the
+        # process group's watchdog as eager work; the watchdog's query of its event (recorded
+        # in the capturing stream) then aborted the process (hipErrorCapturedEvent, r04f)
+        self.capturing = False
         self.expected = None    # accumulations per bucket, learned on the first step
         self.pending = [0] * len(self.buckets)
         self.launched = [False] * len(self.buckets)
@@ -215,7 +221,7 @@ class GradBucketer:
         # autograd runs a side-stream node) and on the weight-gradient side stream
         dev = g.grad.device
         main = self.main_stream if self.main_stream is not None else torch.cuda.current_stream(dev)
-        if torch.cuda.is_current_stream_capturing():
+        if self.capturing or torch.cuda.is_current_stream_capturing():
             # under HIP-graph capture the collective is issued from the capturing main stream
             # (the graph runs it as a branch of its own anyway): a capture that also forked the
             # comm stream crashed hipStreamEndCapture on ROCm 7.2 (tests/test_gpu_rccl.py)
@@ -235,7 +241,7 @@ class GradBucketer:
     def _hook(self, p):
         b = self.param_bucket[id(p)]
         self.pending[b] += 1
-        if self.expected is not None and self.pending[b] == self.expected[b]:
+        if self.expected is not None and self.pending[b] == self.expected[b] and not self.capturing:
             self._launch(b)
 
     def _unwire(self, b, buf):
@@ -253,7 +259,7 @@ class GradBucketer:
         for b in range(len(self.buckets)):
             if not self.launched[b]:
                 self._launch(b)
-        if self.comm is None or torch.cuda.is_current_stream_capturing():
+        if self.comm is None or self.capturing or torch.cuda.is_current_stream_capturing():
             for b, w, buf in self.works:  # (the current stream waits for each collective)
                 w.wait()
                 if buf is not None:
@@ -617,9 +623,13 @@ class Trainer:
             # thread_local: the process group's watchdog thread keeps querying its events while
             # this thread captures; in the default "global" mode such a query from another
             # thread fails the capture (hipErrorStreamCaptureUnsupported, tests/test_gpu_rccl.py)
+            if self.reducer is not None:
+                self.reducer.capturing = True
             with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 loss = self._device_step(self._sx, self._sy)
         except Exception as e:  # noqa: BLE001 -- any capture failure: stay eager, loudly
+            if self.reducer is not None:
+                self.reducer.capturing = False
             ops._side_enabled = side_prev
             # the aborted capture left accumulation counts, launched flags and captured work
             # handles in the reducer: a later eager step must start from a clean bucket state
@@ -636,6 +646,8 @@ class Trainer:
             warnings.warn(f"HIP graph capture of the training step failed ({e!r}); continuing eagerly")
             self._graph_failed = True
             return
+        if self.reducer is not None:
+            self.reducer.capturing = False
         ops._side_enabled = side_prev
         self._graph = graph
         self._graph_loss_fn = self.loss_fn

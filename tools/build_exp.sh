@@ -8,7 +8,7 @@ B=$R/semantic_segmentation_of_stylegan2_artifacts_amd/_build
 mkdir -p $R/tools/exp
 OTHERS=$(ls $B/*.o | grep -v "/$SRC.o$")
 for M in "$@"; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -munsafe-fp-atomics -DMSU_EXP=$M $EXTRA \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -munsafe-fp-atomics -mllvm -amdgpu-mfma-vgpr-form=1 -DMSU_EXP=$M $EXTRA \
      -c $R/semantic_segmentation_of_stylegan2_artifacts_amd/csrc/$SRC.hip -o /tmp/exp_${SRC}_$M.o &
 done
 wait

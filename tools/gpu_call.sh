@@ -114,6 +114,15 @@ for s in "$@"; do
       done
       cat $O/${TAG}_vform_kern.log ;;
     vform_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_vform "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_vform.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_vform.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_vform.so" || exit 3 ;;
+    kern)
+      for shp in "32768 1152 384" "8192 2304 768" "131072 576 192" "524288 288 96"; do
+        timeout -k 10 60 python -u $R/tools/wgrad_one.py $shp 30 2>&1 | grep wgrad >> $O/${TAG}_kern.log || exit 3
+      done
+      for shp in "32768 1152 384" "131072 192 576" "8192 768 3072"; do
+        timeout -k 10 60 python -u $R/tools/nt_one.py $shp 30 2>&1 | grep "nt M" >> $O/${TAG}_kern.log || exit 3
+      done
+      cat $O/${TAG}_kern.log ;;
+    attn_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_attn "" "MSU_ATTN_BWD_HPW=1" "" "MSU_ATTN_BWD_HPW=1" "" "MSU_ATTN_BWD_HPW=1" || exit 3 ;;
     fused3_ab)
       for r in 1 2; do
         for v in hs 1 0; do
