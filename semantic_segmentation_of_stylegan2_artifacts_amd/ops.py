@@ -756,15 +756,18 @@ def tok_supported_epi(M, N, K, epi):
 
 
 
-def tok_gemm(a, w, bias=None, epi=TOK_PLAIN, h=None, a2=None):
+def tok_gemm(a, w, bias=None, epi=TOK_PLAIN, h=None, a2=None, gelu_only=False):
     """16-bit Y = epi(A . W^T + bias) on the token GEMM kernel.  a: [..., K1] (+ a2: [..., K-K1]),
-    w: [N, K] (a's dtype), bias: [N] f32.  Returns Y (and GELU(Y) for TOK_GELU_DUAL)."""
+    w: [N, K] (a's dtype), bias: [N] f32.  Returns Y (and GELU(Y) for TOK_GELU_DUAL).
+    gelu_only (TOK_GELU_DUAL): one buffer for both outputs -- the kernel's GELU store follows
+    its pre-activation store to the same address, so the returned pair is (GELU(Y), GELU(Y))
+    and the L2 merges the two writes of each line (no-grad MLPs: nobody needs Y)."""
     N, K = w.shape
     K1 = a.shape[-1]
     M = a.numel() // K1
     a = a.contiguous()
     y = torch.empty(*a.shape[:-1], N, device=a.device, dtype=a.dtype)
-    y2 = torch.empty_like(y) if epi == TOK_GELU_DUAL else None
+    y2 = (y if gelu_only else torch.empty_like(y)) if epi == TOK_GELU_DUAL else None
     _lib.call("msu_tok_gemm", _dt(a), _p(a), _p(None if a2 is None else a2.contiguous()),
               K1 if a2 is not None else 0, _p(w), _p(bias), _p(y), _p(y2), _p(h), M, N, K, epi, _s(a))
     return (y, y2) if epi == TOK_GELU_DUAL else y
@@ -779,13 +782,13 @@ def nt_supported(M, N, K):
     return r
 
 
-def nt_gemm(a, w, bias=None, epi=TOK_PLAIN, h=None):
-    """16-bit Y = epi(A . W^T + bias) on the tiled NT GEMM (tok_gemm's epilogues)."""
+def nt_gemm(a, w, bias=None, epi=TOK_PLAIN, h=None, gelu_only=False):
+    """16-bit Y = epi(A . W^T + bias) on the tiled NT GEMM (tok_gemm's epilogues and gelu_only)."""
     N, K = w.shape
     M = a.numel() // K
     a = a.contiguous()
     y = torch.empty(*a.shape[:-1], N, device=a.device, dtype=a.dtype)
-    y2 = torch.empty_like(y) if epi == TOK_GELU_DUAL else None
+    y2 = (y if gelu_only else torch.empty_like(y)) if epi == TOK_GELU_DUAL else None
     _lib.call("msu_nt_gemm", _dt(a), _p(a), _p(w), _p(bias), _p(y), _p(y2), _p(h), M, N, K, epi, _s(a))
     return (y, y2) if epi == TOK_GELU_DUAL else y
 
@@ -918,15 +921,15 @@ def gemm_route(M, N, K, epi=TOK_PLAIN):
     return r
 
 
-def _gemm(a, w, bias=None, epi=TOK_PLAIN, h=None):
+def _gemm(a, w, bias=None, epi=TOK_PLAIN, h=None, gelu_only=False):
     """16-bit epi(a . w^T + bias) on the routed GEMM (bias: f32 [N] or None)."""
     N, K = w.shape
     M = a.numel() // K
     r = gemm_route(M, N, K, epi)
     if r == "tok":
-        return tok_gemm(a, w, bias, epi, h)
+        return tok_gemm(a, w, bias, epi, h, gelu_only=gelu_only)
     if r == "nt":
-        return nt_gemm(a, w, bias, epi, h)
+        return nt_gemm(a, w, bias, epi, h, gelu_only=gelu_only)
     if epi != TOK_PLAIN:
         raise RuntimeError(f"no HIP GEMM covers the epilogue {epi} at M={M} N={N} K={K}")
     with torch.autocast("cuda", enabled=False):
@@ -1157,25 +1160,29 @@ def mlp_fusable(x, fc1_weight, fc2_weight):
             gemm_route(M, Hd, C, TOK_GELU_GRAD) != "lib")
 
 
-def _mlp_impl(x, w1, b1, w2, b2):
+def _mlp_impl(x, w1, b1, w2, b2, keep):
     """y = mlp.3(GELU(mlp.0(x))) (torchvision ops.misc.MLP without dropout): mlp.0's epilogue
     stores H and GELU(H) (returned for backward); mlp.3's input gradient applies GELU'(H) in
-    its epilogue."""
+    its epilogue.  keep = False (no backward will run: the reference's discarded branches,
+    inference): H is not kept -- the GELU store overwrites it in one buffer -- and H / G come
+    back empty."""
     _need_cuda(x)
     W1 = _shadow(w1, x.dtype)
     W2 = _shadow(w2, x.dtype)
-    h, g = _gemm(x, W1, _f32(b1), TOK_GELU_DUAL)
+    h, g = _gemm(x, W1, _f32(b1), TOK_GELU_DUAL, gelu_only=not keep)
     y = _gemm(g, W2, _f32(b2))
+    if not keep:
+        return y, x.new_empty(0), x.new_empty(0)
     return y, h, g
 
 
-def _mlp_fake(x, w1, b1, w2, b2):
-    hid = x.new_empty(*x.shape[:-1], w1.shape[0])
+def _mlp_fake(x, w1, b1, w2, b2, keep):
+    hid = x.new_empty(*x.shape[:-1], w1.shape[0]) if keep else x.new_empty(0)
     return x.new_empty(*x.shape[:-1], w2.shape[0]), hid, torch.empty_like(hid)
 
 
 def _mlp_setup(ctx, inputs, output):
-    x, w1, b1, w2, b2 = inputs
+    x, w1, b1, w2, b2, keep = inputs
     y, h, g = output
     ctx.save_for_backward(x, h, g)
     ctx.params = (w1, b1, w2, b2)
@@ -1185,6 +1192,10 @@ def _mlp_setup(ctx, inputs, output):
 
 def _mlp_backward(ctx, dy, _dh, _dg):
     x, h, g = ctx.saved_tensors
+    if dy is None:
+        return None, None, None, None, None, None
+    if h.numel() == 0:
+        raise RuntimeError("mlp: backward through a forward that did not keep its activations (keep=False)")
     w1, b1, w2, b2 = ctx.params
     W1 = _shadow(w1, x.dtype)
     W2 = _shadow(w2, x.dtype)
@@ -1204,17 +1215,18 @@ def _mlp_backward(ctx, dy, _dh, _dg):
         dx = _gemm_dx(dh, W1, param=w1) if ctx.needs_input_grad[0] else None
     else:
         dw1 = db1 = None
-    return dx, dw1, db1, dw2, db2
+    return dx, dw1, db1, dw2, db2, None
 
 
-_mlp = _define("mlp", "(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2) -> (Tensor, Tensor, Tensor)",
+_mlp = _define("mlp", "(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2, bool keep) -> (Tensor, Tensor, Tensor)",
                _mlp_impl, _mlp_fake, _mlp_setup, _mlp_backward)
 
 
 def mlp(x, fc1_weight, fc1_bias, fc2_weight, fc2_bias):
     """Fused torchvision MLP forward/backward (16-bit; see ``mlp_fusable``)."""
     _need_cuda(x)
-    return _mlp(_as(x, act_dtype()), fc1_weight, fc1_bias, fc2_weight, fc2_bias)[0]
+    keep = torch.is_grad_enabled() and any(t.requires_grad for t in (x, fc1_weight, fc1_bias, fc2_weight, fc2_bias))
+    return _mlp(_as(x, act_dtype()), fc1_weight, fc1_bias, fc2_weight, fc2_bias, bool(keep))[0]
 
 
 # ----------------------------------------------------------------------------- residual

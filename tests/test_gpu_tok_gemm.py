@@ -134,6 +134,32 @@ def test_fused_mlp_matches_fp32(M, C, low):
         assert err <= 3e-2 * r.abs().max().item(), f"{name}: {err:.3e} vs {r.abs().max().item():.3e}"
 
 
+@pytest.mark.parametrize("route", ["default", "nt"])
+@pytest.mark.parametrize("M,C", [(4096, 96), (1000, 96), (2048, 192), (1000, 384)])
+def test_mlp_no_grad_keeps_nothing_and_equals_grad_path(M, C, route, monkeypatch, low):
+    """Under no_grad (the reference's discarded branches) ops.mlp keeps neither H nor G: the
+    GELU store overwrites the pre-activation in one buffer.  Its output is bitwise the grad
+    path's (same kernels, same rounding of H before GELU)."""
+    ops = _ops()
+    if route == "nt":
+        monkeypatch.setattr(ops, "_ROUTE_FORCE", "nt")
+        monkeypatch.setattr(ops, "_tok_cache", {})
+    g = torch.Generator().manual_seed(M + 7 * C)
+    x = torch.randn(M, C, generator=g).to(DEV, low)
+    w1 = (torch.randn(4 * C, C, generator=g) / C ** 0.5).to(DEV)
+    b1 = (0.1 * torch.randn(4 * C, generator=g)).to(DEV)
+    w2 = (torch.randn(C, 4 * C, generator=g) / (4 * C) ** 0.5).to(DEV)
+    b2 = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    with torch.autocast("cuda", dtype=low):
+        with torch.no_grad():
+            y0 = ops.mlp(x, w1, b1, w2, b2)
+            _, h, gg = torch.ops.msunet.mlp(x, w1, b1, w2, b2, False)
+        y1, h1, g1 = torch.ops.msunet.mlp(x, w1, b1, w2, b2, True)
+    torch.cuda.synchronize()
+    assert h.numel() == 0 and gg.numel() == 0 and h1.shape == (M, 4 * C)
+    assert torch.equal(y0, y1)
+
+
 @pytest.mark.parametrize("M,C", [(1024, 384), (2048, 192), (1000, 768)])
 def test_fused_mlp_mixed_routing(M, C, monkeypatch, low):
     """Stage-1/2/3 widths with the NT GEMM routed in (MSU_GEMM_ROUTE=nt): the GELU-epilogue

@@ -123,6 +123,7 @@ for s in "$@"; do
       done
       cat $O/${TAG}_kern.log ;;
     attn_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_attn "" "MSU_ATTN_BWD_HPW=1" "" "MSU_ATTN_BWD_HPW=1" "" "MSU_ATTN_BWD_HPW=1" || exit 3 ;;
+    skipw_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_skipw "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_256.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_256.so" || exit 3 ;;
     fused3_ab)
       for r in 1 2; do
         for v in hs 1 0; do
