@@ -791,13 +791,16 @@ long head_blocks(long need, long cap) {
   return (need + 7) / 8 * 8;
 }
 
-// heads per backward workgroup: all three at nh = 3 (stage 0 of Swin-T/S: one 6-wave workgroup
-// per CU), pairs for even nh (a 128-B line holds two heads' slices), else one.  A/B switch
-// MSU_ATTN_BWD_HPW=1|2|3 (used where nh allows it).
+// heads per backward workgroup: pairs for even nh (a 128-B line holds two heads' slices; the
+// LDS still allows two 4-wave workgroups per CU), else one.  All three heads at nh = 3 (stage 0
+// of Swin-T/S) cut the fetched bytes by a third (r04g counters: 431 vs 649 MB per stage-0
+// backward, 1.03x the algorithmic 420 MB) but fit one 6-wave workgroup per CU instead of four
+// 2-wave ones, and ran 300 vs 267 us: opt-in.  A/B switch MSU_ATTN_BWD_HPW=1|2|3 (where nh
+// allows it).
 int bwd_hpw(int nh) {
   static const int forced = getenv("MSU_ATTN_BWD_HPW") ? atoi(getenv("MSU_ATTN_BWD_HPW")) : 0;
   if (forced >= 1 && forced <= 3 && nh % forced == 0) return forced;
-  return nh == 3 ? 3 : (nh % 2 == 0 ? 2 : 1);
+  return nh % 2 == 0 ? 2 : 1;
 }
 
 // backward workgroups per head group: the LDS (40 KB per head) allows four heads per CU

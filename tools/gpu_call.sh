@@ -124,6 +124,15 @@ for s in "$@"; do
       cat $O/${TAG}_kern.log ;;
     attn_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_attn "" "MSU_ATTN_BWD_HPW=1" "" "MSU_ATTN_BWD_HPW=1" "" "MSU_ATTN_BWD_HPW=1" || exit 3 ;;
     skipw_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_skipw "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_256.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_256.so" || exit 3 ;;
+    nt_tile)
+      for shp in "32768 1152 384" "32768 384 384" "32768 1536 384" "32768 384 1536" "131072 576 192" "131072 192 768" "8192 2304 768" "8192 768 3072"; do
+        for t in "256 192" "128 192" "256 128" "128 128"; do
+          set -- $t
+          echo -n "tile=$1x$2 " >> $O/${TAG}_nt_tile.log
+          MSU_NT_TILE=$1 MSU_NT_BN=$2 timeout -k 10 60 python -u $R/tools/nt_one.py $shp 30 2>&1 | grep "nt M" >> $O/${TAG}_nt_tile.log || exit 3
+        done
+      done
+      cat $O/${TAG}_nt_tile.log ;;
     fused3_ab)
       for r in 1 2; do
         for v in hs 1 0; do
