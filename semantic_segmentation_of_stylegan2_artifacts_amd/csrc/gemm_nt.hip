@@ -369,10 +369,16 @@ NtCfg nt_cfg(long M, int N, bool wkn) {
     if (c.bn == 192 && (wkn || N % 192 != 0)) continue;
     if (force_m && (force_m == 128) != (c.wm == 2)) continue;
     if (force_n && force_n != c.bn) continue;
-    const long bm = 64L * c.wm, per_cu = c.wm == 2 ? 2 : 1;
+    // rounds of resident tiles x the output area a CU computes per round (x 0.78 for the
+    // 192-wide form).  A 128-row (two-per-CU) form with no more tiles than CUs has ONE tile per
+    // CU, at a per-area cost of 1.57 (it shares the CU with nobody): r04h sweep, 8192 x 768 x
+    // 3072: 128 x 192 on all 256 CUs 59 us vs 256 x 128 (the previous pick) 65 us and 256 x 192
+    // on 128 CUs 75 us
+    const long bm = 64L * c.wm, slots = c.wm == 2 ? 2 : 1;
     const long tiles = ((M + bm - 1) / bm) * ((N + c.bn - 1) / c.bn);
-    const long rounds = (tiles + cus * per_cu - 1) / (cus * per_cu);
-    const double cost = (double)rounds * bm * c.bn * per_cu * (c.bn == 192 ? 0.78 : 1.0);
+    const long rounds = (tiles + cus * slots - 1) / (cus * slots);
+    const long occ = c.wm == 2 ? std::min(2L, (tiles + cus - 1) / cus) : 1;
+    const double cost = (double)rounds * bm * c.bn * occ * (c.bn == 192 ? 0.78 : 1.0) * (c.wm == 2 && occ == 1 ? 1.57 : 1.0);
     if (best_cost < 0 || cost < best_cost) {
       best_cost = cost;
       best = c;

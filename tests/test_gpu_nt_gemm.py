@@ -121,6 +121,19 @@ def test_nt_gemm_wide_tile_is_chosen_and_exact(M, N, K):
     _check(y, F.linear(a.float(), w.float(), b), "y")
 
 
+@pytest.mark.parametrize("M,N,K", [(8192, 768, 3072), (8192, 768, 768), (8192 - 5, 576, 256)])
+def test_nt_gemm_underfilled_shape_takes_all_cus(M, N, K):
+    """Stage-3 shapes whose 256-row tiles would leave CUs idle (tiles < CUs) go to 128-row
+    tiles, one per CU (r04h: 59 vs 65-75 us at 8192 x 768 x 3072); the result is unchanged."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
+    ops = _ops()
+    rows, cols = _lib.plan_nt(M, N)
+    assert rows == 128 and cols == 192, (M, N, rows, cols)
+    a, w, b = _inputs(M, N, K, 5 * M + N, torch.bfloat16)
+    y = ops.nt_gemm(a, w, b)
+    _check(y, F.linear(a.float(), w.float(), b), "y")
+
+
 def test_nt_gemm_rejects_uncovered_shapes():
     ops = _ops()
     assert not ops.nt_supported(4096, 100, 384)  # N % 32

@@ -133,6 +133,18 @@ for s in "$@"; do
         done
       done
       cat $O/${TAG}_nt_tile.log ;;
+    gemm_mem)
+      # memory-side counters of the NT GEMM and the weight gradient at a stage-2 shape: HBM bytes
+      # (FETCH_SIZE x2 / WRITE_SIZE) and the L2 hit rate, one counter group per pass
+      for prog in "nt_one.py 32768 1152 384 10" "wgrad_one.py 32768 1152 384 10"; do
+        n=${prog%%.py*}
+        for c in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+          tagc=$(echo $c | cut -d' ' -f1)
+          timeout -s KILL 90 rocprofv3 --pmc $c -d $O/${TAG}_mem_${n}_$tagc -o p --output-format csv -- python3 $R/tools/$prog > /dev/null 2>&1 || exit 3
+        done
+      done
+      for f in $O/${TAG}_mem_nt_one_*/p_counter_collection.csv; do echo "== $f"; python3 $R/tools/pmc_sum.py gemm_nt $f; done
+      for f in $O/${TAG}_mem_wgrad_one_*/p_counter_collection.csv; do echo "== $f"; python3 $R/tools/pmc_sum.py wgrad_wave $f; done ;;
     fused3_ab)
       for r in 1 2; do
         for v in hs 1 0; do
