@@ -145,6 +145,7 @@ for s in "$@"; do
       done
       for f in $O/${TAG}_mem_nt_one_*/p_counter_collection.csv; do echo "== $f"; python3 $R/tools/pmc_sum.py gemm_nt $f; done
       for f in $O/${TAG}_mem_wgrad_one_*/p_counter_collection.csv; do echo "== $f"; python3 $R/tools/pmc_sum.py wgrad_wave $f; done ;;
+    dma_probe) step dma_probe 120 python -u $R/tools/dma_probe.py ;;
     fused3_ab)
       for r in 1 2; do
         for v in hs 1 0; do
