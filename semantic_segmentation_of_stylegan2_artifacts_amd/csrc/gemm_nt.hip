@@ -347,7 +347,7 @@ int num_cus_nt() {
 //   wm 4, bn 192: 256 x 192, two-stage ring (3 x 56 KB does not fit), one workgroup per CU;
 //   wm 2, bn 192: 128 x 192, two-stage ring, two workgroups per CU (2 x 80 KB of LDS).
 // KN (input-gradient with the forward weight in place) keeps bn 128.  A/B switches:
-// MSU_NT_TILE = 128 | 256 (rows), MSU_NT_BN = 128 | 192 (columns).
+// MSU_NT_TILE = 128 | 192 | 256 (rows; 192 only with 192 columns), MSU_NT_BN = 128 | 192 (columns).
 struct NtCfg {
   int wm, bn;
 };
@@ -362,12 +362,13 @@ NtCfg nt_cfg(long M, int N, bool wkn) {
     return e ? atoi(e) : 0;
   }();
   const long cus = num_cus_nt();
-  const NtCfg cands[4] = {{4, 128}, {2, 128}, {4, 192}, {2, 192}};
+  // {3, 192}: 192 x 192 tiles, 6 waves, three-stage ring (144 KB) -- opt-in (MSU_NT_TILE=192)
+  const NtCfg cands[5] = {{4, 128}, {2, 128}, {4, 192}, {2, 192}, {3, 192}};
   NtCfg best = cands[0];
   double best_cost = -1.0;
   for (const NtCfg& c : cands) {
     if (c.bn == 192 && (wkn || N % 192 != 0)) continue;
-    if (force_m && (force_m == 128) != (c.wm == 2)) continue;
+    if (force_m ? force_m != 64 * c.wm : c.wm == 3) continue;
     if (force_n && force_n != c.bn) continue;
     // rounds of resident tiles x the output area a CU computes per round (x 0.78 for the
     // 192-wide form).  A 128-row (two-per-CU) form with no more tiles than CUs has ONE tile per
@@ -390,7 +391,7 @@ NtCfg nt_cfg(long M, int N, bool wkn) {
 template <typename T, int WM, int NST, bool WKN, int BNT>
 void launch_nt(int epi, const NtArgs& a, hipStream_t st) {
   const long tiles = (long)a.tiles_m * a.tiles_n;
-  const long cap = (long)num_cus_nt() * (WM == 4 ? 1 : 2);
+  const long cap = (long)num_cus_nt() * (WM == 2 ? 2 : 1);
   const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
   const dim3 blk(128 * WM);
   switch (epi) {
@@ -430,6 +431,7 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
   MSU_DISPATCH16(dtype, T,
     if (cfg.bn == 192) {
       if (cfg.wm == 4) launch_nt<T, 4, 2, false, 192>(epi, a, st);
+      else if (cfg.wm == 3) launch_nt<T, 3, 3, false, 192>(epi, a, st);
       else launch_nt<T, 2, 2, false, 192>(epi, a, st);
     } else if (cfg.wm == 4) {
       if (wkn) launch_nt<T, 4, 3, true, 128>(epi, a, st);

@@ -126,7 +126,7 @@ for s in "$@"; do
     skipw_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_skipw "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_256.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_256.so" || exit 3 ;;
     nt_tile)
       for shp in "32768 1152 384" "32768 384 384" "32768 1536 384" "32768 384 1536" "131072 576 192" "131072 192 768" "8192 2304 768" "8192 768 3072"; do
-        for t in "256 192" "128 192" "256 128" "128 128"; do
+        for t in "256 192" "128 192" "192 192" "256 128" "128 128"; do
           set -- $t
           echo -n "tile=$1x$2 " >> $O/${TAG}_nt_tile.log
           MSU_NT_TILE=$1 MSU_NT_BN=$2 timeout -k 10 60 python -u $R/tools/nt_one.py $shp 30 2>&1 | grep "nt M" >> $O/${TAG}_nt_tile.log || exit 3
@@ -145,6 +145,7 @@ for s in "$@"; do
       done
       for f in $O/${TAG}_mem_nt_one_*/p_counter_collection.csv; do echo "== $f"; python3 $R/tools/pmc_sum.py gemm_nt $f; done
       for f in $O/${TAG}_mem_wgrad_one_*/p_counter_collection.csv; do echo "== $f"; python3 $R/tools/pmc_sum.py wgrad_wave $f; done ;;
+    nt192_tests) MSU_NT_TILE=192 MSU_NT_BN=192 step nt192_tests 400 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py -k "not underfilled and not chosen" ;;
     dma_probe) step dma_probe 120 python -u $R/tools/dma_probe.py ;;
     fused3_ab)
       for r in 1 2; do
