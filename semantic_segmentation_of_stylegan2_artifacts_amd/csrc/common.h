@@ -232,8 +232,25 @@ MSU_DEV int xcd_remap(int b, int nb) {
 // wave-uniform); counted by vmcnt like any global load.
 typedef __attribute__((address_space(3))) void msu_lds_void;
 typedef __attribute__((address_space(1))) void msu_glb_void;
+// Issued as inline asm by default: while a builtin LDS-DMA is in flight hipcc waits
+// lgkmcnt(0) before every compiler-visible ds_read (it cannot order them against the DMA's LDS
+// write), so no LDS read of a k-step overlapped the MFMAs before it -- a read-wait-MFMA chain
+// in the conv, NT and token GEMM loops.  The asm form is invisible to hipcc's counters: every
+// consumer of the DMA'd data already waits by hand (wait_vmcnt<N> + raw barrier), and hipcc's
+// own vmcnt waits for its loads only over-count.  __syncthreads() does NOT drain it.
+// MSU_GLDS_BUILTIN: the builtin (A/B switch).
 MSU_DEV void glds16(const void* src, void* lds_base) {
+#ifdef MSU_GLDS_BUILTIN
   __builtin_amdgcn_global_load_lds((msu_glb_void*)src, (msu_lds_void*)lds_base, 16, 0, 0);
+#else
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)(lds_base));
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(dst)
+               : "memory");
+#endif
 }
 // s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0], expcnt[6:4], lgkmcnt[11:8], vmcnt_hi[15:14])
 template <int N> MSU_DEV void wait_vmcnt() {

@@ -249,6 +249,12 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     for (int ks = 0; ks < KSL; ++ks) {
       const int cur = ks & 1;
       if (ks + 1 < KSL) rd(ks + 1, cur ^ 1);
+#ifndef MSU_NT_NOSB
+      // all of slice ks + 1's fragment reads go out before slice ks's MFMAs (the wait before
+      // those is then lgkmcnt(reads of ks + 1)); left alone, the scheduler sank some reads
+      // between the MFMAs into registers freed by them and waited lgkmcnt(0) two MFMAs later
+      __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
         acc[ni][0] = Fmt16<T>::mma32(fw[cur][ni], fx[cur][0], acc[ni][0]);

@@ -248,6 +248,7 @@ __global__ void __launch_bounds__(64 * NW) tokgemm_kernel(TokArgs a) {
       const bf16_t* afrag = reinterpret_cast<const bf16_t*>(ring + c_slot * G::BYTES) + fr * G::LD + fk;
       if (++c_slot == NST) c_slot = 0;
       const bf16_t* wk = wfrag + kc * KC;
+#ifdef MSU_TOK_NOPIPE
 #pragma unroll
       for (int kk = 0; kk < KC / 16; ++kk) {
         const bf16x8 bx = *reinterpret_cast<const bf16x8*>(afrag + 16 * kk);
@@ -257,6 +258,30 @@ __global__ void __launch_bounds__(64 * NW) tokgemm_kernel(TokArgs a) {
           acc[n] = Fmt16<T>::mma32(wx, bx, acc[n]);
         }
       }
+#else
+      // MFMA j = (k slice kk, column tile n) in sequence, the W fragment of MFMA j + 2 and the
+      // token fragment of slice kk + 1 read before MFMA j, the order pinned: the compiler's own
+      // schedule read each W fragment right before its MFMA and waited lgkmcnt(0) on it, i.e.
+      // every 32-cycle MFMA paid an LDS round trip
+      {
+        constexpr int NKK = KC / 16, NJ = NKK * NT;
+        auto rdw = [&](int j) __attribute__((always_inline)) {
+          return *reinterpret_cast<const bf16x8*>(wk + (j % NT) * 32 * LDW + 16 * (j / NT));
+        };
+        bf16x8 wr[3], bxr[2];
+        bxr[0] = *reinterpret_cast<const bf16x8*>(afrag);
+        wr[0] = rdw(0);
+        if (NJ > 1) wr[1] = rdw(1);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int kk = j / NT, n = j % NT;
+          if (j + 2 < NJ) wr[(j + 2) % 3] = rdw(j + 2);
+          if (n == 0 && kk + 1 < NKK) bxr[(kk + 1) & 1] = *reinterpret_cast<const bf16x8*>(afrag + 16 * (kk + 1));
+          acc[n] = Fmt16<T>::mma32(wr[j % 3], bxr[kk & 1], acc[n]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#endif
       if (BIAS && last) {
         // + bias: the W image's bias k-block times a ones column (k = 0, 1 of lanes 0-31)
         const bf16x8 ones = lane < 32 ? splat8<T>(1.0f, 1.0f, 0.0f) : splat8<T>(0.0f, 0.0f, 0.0f);

@@ -147,6 +147,25 @@ for s in "$@"; do
       for f in $O/${TAG}_mem_wgrad_one_*/p_counter_collection.csv; do echo "== $f"; python3 $R/tools/pmc_sum.py wgrad_wave $f; done ;;
     nt192_tests) MSU_NT_TILE=192 MSU_NT_BN=192 step nt192_tests 400 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py -k "not underfilled and not chosen" ;;
     dma_probe) step dma_probe 120 python -u $R/tools/dma_probe.py ;;
+    ntsb_ab)
+      for lib in "" $R/tools/exp/libmsunet_gemm_nt_0.so "" $R/tools/exp/libmsunet_gemm_nt_0.so; do
+        echo "lib=${lib##*/}" >> $O/${TAG}_ntsb.log
+        for shp in "32768 1152 384" "32768 384 384" "32768 384 1536" "131072 576 192" "131072 192 768" "8192 2304 768" "8192 768 3072"; do
+          MSU_LIB_OVERRIDE=$lib timeout -k 10 60 python -u $R/tools/nt_one.py $shp 30 2>&1 | grep "nt M" >> $O/${TAG}_ntsb.log || exit 3
+        done
+      done
+      cat $O/${TAG}_ntsb.log
+      bash $R/tools/gpu_bench_ab.sh ${TAG}_ntsb "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_nt_0.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_nt_0.so" || exit 3 ;;
+    glds_ab)
+      for lib in "" $R/tools/exp/libmsunet_gldsb.so "" $R/tools/exp/libmsunet_gldsb.so; do
+        echo "lib=${lib##*/}" >> $O/${TAG}_glds.log
+        for shp in "32768 1152 384" "32768 384 1536" "131072 192 768" "8192 768 3072"; do
+          MSU_LIB_OVERRIDE=$lib timeout -k 10 60 python -u $R/tools/nt_one.py $shp 30 2>&1 | grep "nt M" >> $O/${TAG}_glds.log || exit 3
+        done
+        MSU_LIB_OVERRIDE=$lib timeout -k 10 180 python -u $R/tools/kbench.py conv >> $O/${TAG}_glds.log 2>&1 || exit 3
+      done
+      cat $O/${TAG}_glds.log
+      bash $R/tools/gpu_bench_ab.sh ${TAG}_glds "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gldsb.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gldsb.so" || exit 3 ;;
     fused3_ab)
       for r in 1 2; do
         for v in hs 1 0; do
