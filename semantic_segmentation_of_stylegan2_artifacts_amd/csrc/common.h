@@ -232,15 +232,15 @@ MSU_DEV int xcd_remap(int b, int nb) {
 // wave-uniform); counted by vmcnt like any global load.
 typedef __attribute__((address_space(3))) void msu_lds_void;
 typedef __attribute__((address_space(1))) void msu_glb_void;
-// Issued as inline asm by default: while a builtin LDS-DMA is in flight hipcc waits
-// lgkmcnt(0) before every compiler-visible ds_read (it cannot order them against the DMA's LDS
-// write), so no LDS read of a k-step overlapped the MFMAs before it -- a read-wait-MFMA chain
-// in the conv, NT and token GEMM loops.  The asm form is invisible to hipcc's counters: every
-// consumer of the DMA'd data already waits by hand (wait_vmcnt<N> + raw barrier), and hipcc's
-// own vmcnt waits for its loads only over-count.  __syncthreads() does NOT drain it.
-// MSU_GLDS_BUILTIN: the builtin (A/B switch).
+// MSU_GLDS_ASM (experiment): issue it as inline asm.  While a builtin LDS-DMA is in flight
+// hipcc waits lgkmcnt(0) before every compiler-visible ds_read (it cannot order them against
+// the DMA's LDS write), so no LDS read overlaps the MFMAs before it; the asm form is invisible to
+// hipcc's counters and gets counted lgkmcnt(N) waits instead (every consumer of DMA'd data
+// waits by hand: wait_vmcnt<N> + raw barrier; __syncthreads() would NOT drain it).  Measured
+// neutral at two waves per SIMD (r04l: NT / conv launches within +-3 %, bench 168.6 / 168.6 vs
+// 168.2 / 169.0 img/s): the partner wave already hides those waits.
 MSU_DEV void glds16(const void* src, void* lds_base) {
-#ifdef MSU_GLDS_BUILTIN
+#ifndef MSU_GLDS_ASM
   __builtin_amdgcn_global_load_lds((msu_glb_void*)src, (msu_lds_void*)lds_base, 16, 0, 0);
 #else
   const uint32_t dst = __builtin_amdgcn_readfirstlane(

@@ -141,13 +141,16 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ dY, co
 // global_load_lds_dwordx4 (pad slots re-read chunk 0 of their row; rows past the block's
 // range read the spread zero region); a ring of NST stages keeps NST-1 in flight; raw
 // s_barrier + counted vmcnt keep the prefetch alive across barriers.
-template <int WN, int WK> constexpr int wgrad_nw() { return WN * WK == 3 ? 3 : 4; }
+// W8: a second row group of four waves (eight waves, two per SIMD, 64-row stages; the MFMA-bound
+// one-wave-per-SIMD form waited 37 % of its cycles on DMA / LDS latency with nothing to fill the
+// SIMD, r04i counters); the two groups' partial tiles are summed in LDS before the slab store.
+template <int WN, int WK, bool W8 = false> constexpr int wgrad_nw() { return W8 ? 8 : (WN * WK == 3 ? 3 : 4); }
 
-template <typename T, int NTW, int WN, int WK, int NST>
-__global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
+template <typename T, int NTW, int WN, int WK, int NST, bool W8>
+__global__ void __launch_bounds__(W8 ? 512 : 256) wgrad_wave_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                                          float* __restrict__ part, float* __restrict__ dbpart,
                                                          long M, int N, int K, long mchunk, int ntiles, int xcd) {
-  constexpr int NW = wgrad_nw<WN, WK>();
+  constexpr int NW = wgrad_nw<WN, WK, W8>();
   constexpr int WM = NW / (WN * WK), WT = 16 * NTW, BN = WN * WT, BK = WK * WT, RS = 32 * WM;
   static_assert(WM * WN * WK == NW, "wave split");
   constexpr int SA = (BN + 8) / 8, SB = (BK + 8) / 8;  // 16-B slots per row
@@ -156,7 +159,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
   constexpr int INS = ((SLOTS + 63) / 64 + NW - 1) / NW * NW;
   constexpr int PER_WAVE = INS / NW;
   constexpr int STG = INS * 64 * 8;
-  static_assert(PER_WAVE * (NST - 2) < 64, "vmcnt");
+  static_assert(NST >= 2 && PER_WAVE * (NST - 2) < 64, "vmcnt");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -279,39 +282,47 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
   wait_vmcnt<0>();  // every DMA has landed: the ring may be reused
   // row-waves of the same output tile are summed in LDS first: one slab per split
   if constexpr (WM > 1) {
-    float* red = reinterpret_cast<float*>(smem_raw);  // [WM][NTW*NTW*4][64] per (N, K)-wave
-    __syncthreads();
-    constexpr int PW = (NTW * NTW * 4 + NTW * 4) * 64;  // floats per wave
+    // in HALVES passes over the accumulator rows i when one pass would not fit the LDS
+    float* red = reinterpret_cast<float*>(smem_raw);  // [(N, K)-wave][WM - 1][rows of the pass][64]
+    constexpr int PWF = (NTW * NTW * 4 + NTW * 4) * 64;  // floats per wave, all rows
+    constexpr int HALVES = (size_t)WN * WK * (WM - 1) * PWF * 4 <= 160 * 1024 ? 1 : 2;
+    constexpr int IH = NTW / HALVES;
+    static_assert(IH * HALVES == NTW, "pass rows");
+    constexpr int PW = (IH * NTW * 4 + IH * 4) * 64;  // floats per wave and pass
     static_assert((size_t)WN * WK * (WM - 1) * PW * 4 <= 160 * 1024, "LDS reduction");
     const int wnk = wni + WN * wki;
     float* mine = red + ((long)wnk * (WM - 1) + (wmi > 0 ? wmi - 1 : 0)) * PW;
-    if (wmi > 0) {
+    unroll_for<HALVES>([&](auto HI) {
+      constexpr int h0 = decltype(HI)::value * IH;
+      __syncthreads();  // the ring (first pass) / the previous pass's slots are free
+      if (wmi > 0) {
 #pragma unroll
-    for (int i = 0; i < NTW; ++i) {
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mine[((i * NTW + j) * 4 + r) * 64 + lane] = acc[i][j][r];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mine[(NTW * NTW * 4 + i * 4 + r) * 64 + lane] = accb[i][r];
-    }
-    }
-    __syncthreads();
-    if (wmi == 0) {
-#pragma unroll
-      for (int w = 1; w < WM; ++w) {
-        const float* other = red + ((long)wnk * (WM - 1) + w - 1) * PW;
-#pragma unroll
-        for (int i = 0; i < NTW; ++i) {
+        for (int i = h0; i < h0 + IH; ++i) {
 #pragma unroll
           for (int j = 0; j < NTW; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) acc[i][j][r] += other[((i * NTW + j) * 4 + r) * 64 + lane];
+            for (int r = 0; r < 4; ++r) mine[(((i - h0) * NTW + j) * 4 + r) * 64 + lane] = acc[i][j][r];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) accb[i][r] += other[(NTW * NTW * 4 + i * 4 + r) * 64 + lane];
+          for (int r = 0; r < 4; ++r) mine[(IH * NTW * 4 + (i - h0) * 4 + r) * 64 + lane] = accb[i][r];
         }
       }
-    }
+      __syncthreads();
+      if (wmi == 0) {
+#pragma unroll
+        for (int w = 1; w < WM; ++w) {
+          const float* other = red + ((long)wnk * (WM - 1) + w - 1) * PW;
+#pragma unroll
+          for (int i = h0; i < h0 + IH; ++i) {
+#pragma unroll
+            for (int j = 0; j < NTW; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[i][j][r] += other[(((i - h0) * NTW + j) * 4 + r) * 64 + lane];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) accb[i][r] += other[(IH * NTW * 4 + (i - h0) * 4 + r) * 64 + lane];
+          }
+        }
+      }
+    });
   }
   if (wmi != 0) return;
   float* out = part + (long)split * N * K;
@@ -338,6 +349,7 @@ __global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restric
 // bf16 plan: wave tile, waves along N and K, ring depth, splits
 struct WavePlan {
   int ntw = 0, wn = 1, wk = 1, nst = 3, S = 1;
+  bool w8 = false;  // eight waves (two row groups), see wgrad_nw
   int slabs() const { return S; }
 };
 
@@ -386,21 +398,34 @@ inline WavePlan wave_plan(long M, int N, int K) {
   else return p;  // not supported: generic kernel
   const int wt = 16 * p.ntw, nt = N / wt, kt = K / wt;
   pick_wave_split(nt, kt, p.wn, p.wk);
-  const int nw = p.wn * p.wk == 3 ? 3 : 4;
-  const int wm = nw / (p.wn * p.wk), rs = 32 * wm;
-  const int sa = (p.wn * wt + 8) / 8, sb = (p.wk * wt + 8) / 8;
-  const int ins = ((rs * (sa + sb) + 63) / 64 + nw - 1) / nw * nw;
-  const long stage_bytes = (long)ins * 64 * 16;
-  p.nst = (int)((160L * 1024) / stage_bytes);
-  if (p.nst > 6) p.nst = 6;
-  // 3 stages: the ring depth does not change the stage-0 streaming rate (measured), and the
-  // smaller LDS footprint (<= 96 KB) lets the kernel share CUs with the input-gradient
-  // kernels it overlaps on the side stream (+0.8 % per step).  MSU_WGRAD_NST: A/B switch.
-  static const int nst_cap = getenv("MSU_WGRAD_NST") ? atoi(getenv("MSU_WGRAD_NST")) : 3;
-  if (nst_cap >= 3 && p.nst > nst_cap) p.nst = nst_cap;
-  if (p.nst < 3) {  // ring too shallow: generic kernel
-    p.ntw = 0;
-    return p;
+  // ring depth that fits 160 KB for the four- or eight-wave form
+  auto ring = [&](bool w8, int& rs) {
+    const int nw = w8 ? 8 : (p.wn * p.wk == 3 ? 3 : 4);
+    const int wm = nw / (p.wn * p.wk);
+    rs = 32 * wm;
+    const int sa = (p.wn * wt + 8) / 8, sb = (p.wk * wt + 8) / 8;
+    const int ins = ((rs * (sa + sb) + 63) / 64 + nw - 1) / nw * nw;
+    int nst = (int)((160L * 1024) / ((long)ins * 64 * 16));
+    return nst > 6 ? 6 : nst;
+  };
+  // A/B switch MSU_WGRAD_W8=0: the four-wave form only
+  static const bool w8_on = !(getenv("MSU_WGRAD_W8") && getenv("MSU_WGRAD_W8")[0] == '0');
+  int rs = 32;
+  // (96-wide wave tiles only: the 128-wide ones spill at two waves per SIMD)
+  p.w8 = w8_on && p.ntw == 6 && p.wn * p.wk == 4 && ring(true, rs) >= 2;
+  if (p.w8) {
+    p.nst = 2;  // 2 x 56 KB (Swin-T/S widths): the second row group hides what the ring depth did
+  } else {
+    p.nst = ring(false, rs);
+    // 3 stages: the ring depth does not change the stage-0 streaming rate (measured), and the
+    // smaller LDS footprint (<= 96 KB) lets the kernel share CUs with the input-gradient
+    // kernels it overlaps on the side stream (+0.8 % per step).  MSU_WGRAD_NST: A/B switch.
+    static const int nst_cap = getenv("MSU_WGRAD_NST") ? atoi(getenv("MSU_WGRAD_NST")) : 3;
+    if (nst_cap >= 3 && p.nst > nst_cap) p.nst = nst_cap;
+    if (p.nst < 3) {  // ring too shallow: generic kernel
+      p.ntw = 0;
+      return p;
+    }
   }
   const long tiles = (long)(nt / p.wn) * (kt / p.wk);
   // workgroup target: one per CU (no tail wave), long row ranges.  A/B switch
@@ -414,16 +439,16 @@ inline WavePlan wave_plan(long M, int N, int K) {
   return p;
 }
 
-template <typename T, int NTW, int WN, int WK, int NST>
+template <typename T, int NTW, int WN, int WK, int NST, bool W8 = false>
 void launch_wave(dim3 grid, const bf16_t* dY, const bf16_t* X, float* part, float* dbpart, long M, int N, int K,
                  long mchunk, int ntiles, hipStream_t st) {
-  constexpr int NW = wgrad_nw<WN, WK>();
+  constexpr int NW = wgrad_nw<WN, WK, W8>();
   constexpr int WM = NW / (WN * WK), WT = 16 * NTW, RS = 32 * WM;
   constexpr int SLOTS = RS * ((WN * WT + 8) / 8 + (WK * WT + 8) / 8);
   constexpr int INS = ((SLOTS + 63) / 64 + NW - 1) / NW * NW;
   constexpr size_t lds = (size_t)NST * INS * 64 * 16;
   if constexpr (lds <= 160 * 1024) {  // ring depths the plan never picks are not instantiated
-    auto kern = wgrad_wave_kernel<T, NTW, WN, WK, NST>;
+    auto kern = wgrad_wave_kernel<T, NTW, WN, WK, NST, W8>;
     static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -437,13 +462,20 @@ void launch_wave(dim3 grid, const bf16_t* dY, const bf16_t* X, float* part, floa
 template <typename T>
 int run_wave(const WavePlan& p, const bf16_t* dY, const bf16_t* X, float* part, float* dbpart, long M, int N, int K,
              hipStream_t st) {
-  const int wt = 16 * p.ntw, nw = p.wn * p.wk == 3 ? 3 : 4, wm = nw / (p.wn * p.wk), rs = 32 * wm;
+  const int wt = 16 * p.ntw, nw = p.w8 ? 8 : (p.wn * p.wk == 3 ? 3 : 4), wm = nw / (p.wn * p.wk), rs = 32 * wm;
   long mchunk = (M + p.S - 1) / p.S;
   mchunk = (mchunk + rs - 1) / rs * rs;
   const int ntiles = (N / (p.wn * wt)) * (K / (p.wk * wt));
   const dim3 grid((unsigned)(ntiles * p.S));
+#define MSU_WAVE8(NTW, WN, WK)                                                                                       \
+  if (p.w8 && p.ntw == NTW && p.wn == WN && p.wk == WK) {                                                           \
+    launch_wave<T, NTW, WN, WK, 2, true>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st);                  \
+    return 0;                                                                                                       \
+  }
+  MSU_WAVE8(6, 2, 2) MSU_WAVE8(6, 4, 1) MSU_WAVE8(6, 1, 4)
+#undef MSU_WAVE8
 #define MSU_WAVE(NTW, WN, WK)                                                                                        \
-  if (p.ntw == NTW && p.wn == WN && p.wk == WK) {                                                                   \
+  if (!p.w8 && p.ntw == NTW && p.wn == WN && p.wk == WK) {                                                          \
     switch (p.nst) {                                                                                                \
       case 3: launch_wave<T, NTW, WN, WK, 3>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st); return 0;     \
       case 4: launch_wave<T, NTW, WN, WK, 4>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st); return 0;     \
