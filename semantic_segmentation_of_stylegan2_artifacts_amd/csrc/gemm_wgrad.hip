@@ -408,8 +408,11 @@ inline WavePlan wave_plan(long M, int N, int K) {
     int nst = (int)((160L * 1024) / ((long)ins * 64 * 16));
     return nst > 6 ? 6 : nst;
   };
-  // A/B switch MSU_WGRAD_W8=0: the four-wave form only
-  static const bool w8_on = !(getenv("MSU_WGRAD_W8") && getenv("MSU_WGRAD_W8")[0] == '0');
+  // MSU_WGRAD_W8=1: the eight-wave form where it applies (opt-in).  Alone on the GPU it is
+  // 10-13 % faster (r04m: 50.4 vs 56.3 us at 32768 x 1152 x 384, 61 vs 69 at 32768 x 384 x
+  // 1536), but in the step -- on the side stream, beside the input-gradient kernels -- its
+  // 112 KB of LDS and eight waves per CU crowd them out: 167.1 / 167.3 vs 167.4 / 167.8 img/s
+  static const bool w8_on = getenv("MSU_WGRAD_W8") && getenv("MSU_WGRAD_W8")[0] == '1';
   int rs = 32;
   // (96-wide wave tiles only: the 128-wide ones spill at two waves per SIMD)
   p.w8 = w8_on && p.ntw == 6 && p.wn * p.wk == 4 && ring(true, rs) >= 2;

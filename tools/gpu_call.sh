@@ -168,13 +168,13 @@ for s in "$@"; do
       bash $R/tools/gpu_bench_ab.sh ${TAG}_glds "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gldsb.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gldsb.so" || exit 3 ;;
     w8_ab)
       for v in 1 0 1 0; do
-        echo "MSU_WGRAD_W8=$v" >> $O/${TAG}_w8.log
+        echo "MSU_WGRAD_W8=$v" >> $O/${TAG}_w8.log  # (default 0)
         for shp in "32768 1152 384" "8192 2304 768" "131072 576 192" "32768 384 1536" "8192 768 3072" "131072 192 768"; do
           MSU_WGRAD_W8=$v timeout -k 10 60 python -u $R/tools/wgrad_one.py $shp 30 2>&1 | grep wgrad >> $O/${TAG}_w8.log || exit 3
         done
       done
       cat $O/${TAG}_w8.log
-      bash $R/tools/gpu_bench_ab.sh ${TAG}_w8 "" "MSU_WGRAD_W8=0" "" "MSU_WGRAD_W8=0" || exit 3 ;;
+      bash $R/tools/gpu_bench_ab.sh ${TAG}_w8 "MSU_WGRAD_W8=1" "" "MSU_WGRAD_W8=1" "" || exit 3 ;;
     fused3_ab)
       for r in 1 2; do
         for v in hs 1 0; do
