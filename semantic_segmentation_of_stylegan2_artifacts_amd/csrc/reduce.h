@@ -40,22 +40,15 @@ __global__ void __launch_bounds__(256) colsum_kernel(ColSegs sg, int nparts, int
   const long i = ((long)((int)blockIdx.x - b0) * NC + lx) * V;
   vec s = {};
   if (i < n) {
-    // batches of 8 parts per thread, the last one predicated: all of a batch's loads are in
-    // flight together (a tail of one dependent load per part was latency-bound: the weight-
-    // gradient reductions have 5-85 parts, i.e. mostly tail).  Same summation order as a
-    // sequential walk over p (a missing part adds +0).
-    // (every load is issued -- a missing part re-reads the last one -- and the select is on
-    // the loaded value: a select around the load itself makes hipcc branch and wait per part)
-    for (int p = ly; p < nparts; p += 8 * PL) {
+    int p = ly;
+    for (; p + 7 * PL < nparts; p += 8 * PL) {
       vec v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int q = p + u * PL < nparts ? p + u * PL : nparts - 1;
-        v[u] = *reinterpret_cast<const vec*>(part + (long)q * stride + i);
-      }
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const vec*>(part + (long)(p + u * PL) * stride + i);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += p + u * PL < nparts ? v[u] : vec{};
+      for (int u = 0; u < 8; ++u) s += v[u];
     }
+    for (; p < nparts; p += PL) s += *reinterpret_cast<const vec*>(part + (long)p * stride + i);
   }
   red[ly][lx] = s;
   __syncthreads();

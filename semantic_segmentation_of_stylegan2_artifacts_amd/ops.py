@@ -1096,6 +1096,10 @@ def _wgrad_into(dy, x, dw, db, M, N, K, acc):
               _s(x))
 
 
+# A/B switch MSU_CAT_SIDE=0: linear_cat's weight-gradient halves on the main stream (round 3)
+_CAT_SIDE = os.environ.get("MSU_CAT_SIDE", "1") != "0"
+
+
 def _linear_cat_backward(ctx, dy):
     x, skip = ctx.saved_tensors
     weight, bias = ctx.params
@@ -1111,6 +1115,26 @@ def _linear_cat_backward(ctx, dy):
     # weight gradient per half straight into the column slices of dW (bias with the first):
     # the trainer's flat .grad (accumulate) or a fresh [N, C1 + C2] gradient
     direct = _direct(weight, bias)
+    if direct and _side_enabled and _side_wgrad and _CAT_SIDE:
+        # on the weight-gradient side stream like every other Linear's (the shared skip-fusion
+        # Linears -- concat_back_dim[2 / 3] serve the central decoders too -- then have all
+        # their .grad writers on one stream, in program order)
+        main = torch.cuda.current_stream(x.device)
+        side = _side_stream_for(x.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            _wgrad_into(dy, x, weight.grad[:, :C1], bias.grad, M, N, C1, 1)
+            _wgrad_into(dy, skip, weight.grad[:, C1:], None, M, N, C2, 1)
+        for t in (dy, x, skip):
+            t.record_stream(side)
+            _side_keep.append(t)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        _guard_side_write(weight, ev)
+        _guard_side_write(bias, ev)
+        _join_at_end_of_backward()
+        _notify(weight, bias)
+        return outs[0], outs[1], None, None
     if direct:
         dw, db, acc = weight.grad, bias.grad, 1
     else:

@@ -180,6 +180,7 @@ for s in "$@"; do
       timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d $O/${TAG}_pmcconv -o conv_write --output-format csv -- python3 $R/tools/conv_one.py 0 3 fwd act > /dev/null 2>&1 || exit 3
       python3 $R/tools/pmc_json.py conv3x3_v3_kernel $O/${TAG}_pmcconv/conv_fetch_counter_collection.csv \
         $O/${TAG}_pmcconv/conv_write_counter_collection.csv $O/${TAG}_conv3x3_fwd_pmc.json && cat $O/${TAG}_conv3x3_fwd_pmc.json ;;
+    cat_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_cat "" "MSU_CAT_SIDE=0" "" "MSU_CAT_SIDE=0" "" "MSU_CAT_SIDE=0" || exit 3 ;;
     fused3_ab)
       for r in 1 2; do
         for v in hs 1 0; do
