@@ -45,6 +45,8 @@ def run(steps=3, skip_dead=False):
 
 def configs():
     # (label, side stream, GEMM route, dead branches skipped, wgrad on side, attention tail on side)
+    if len(sys.argv) > 2 and sys.argv[2] == "default":  # the default eager step only
+        return [("side, all parts", True, "", False, True, True)]
     if len(sys.argv) > 2 and sys.argv[2] == "parts":
         return [("side, all parts", True, "", False, True, True),
                 ("side, no dead branches", True, "", True, True, True),

@@ -181,6 +181,7 @@ for s in "$@"; do
       python3 $R/tools/pmc_json.py conv3x3_v3_kernel $O/${TAG}_pmcconv/conv_fetch_counter_collection.csv \
         $O/${TAG}_pmcconv/conv_write_counter_collection.csv $O/${TAG}_conv3x3_fwd_pmc.json && cat $O/${TAG}_conv3x3_fwd_pmc.json ;;
     cat_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_cat "" "MSU_CAT_SIDE=0" "" "MSU_CAT_SIDE=0" "" "MSU_CAT_SIDE=0" || exit 3 ;;
+    determ) step determ 600 python -u $R/tools/determinism_matrix.py 24 default ;;
     fused3_ab)
       for r in 1 2; do
         for v in hs 1 0; do
@@ -197,7 +198,9 @@ for s in "$@"; do
       timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT \
         -d $O/${TAG}_ntpmc2 -o p --output-format csv -- python3 $R/tools/nt_one.py 32768 1152 384 10 >> $O/${TAG}_nt.log 2>&1 || exit 3
       cat $O/${TAG}_nt.log | grep "nt M" ;;
-    prof) step prof 420 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o p --output-format csv -- \
+    # MSU_GRAPH=0: the profiler's per-launch host cost makes the bench's auto policy pick the
+    # single-stream graph replay; the profile must show the eager step the bench line measures
+    prof) MSU_GRAPH=0 step prof 420 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o p --output-format csv -- \
             python3 $R/bench.py --steps 8 --warmup 4 --no-roofline --no-cpu-baseline --no-input-pipeline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
