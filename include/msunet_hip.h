@@ -50,6 +50,10 @@ int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const 
                       int nparts, float* dgamma, float* dbeta, long rows, int C, int H, int W,
                       int Cin, int accumulate, void* stream);
 int msu_ln_part_blocks(long rows, int C);
+/* dgamma == null in msu_layernorm_bwd: only the backward kernel (dx, partials); this reduces the
+ * partials into dgamma / dbeta afterwards, on any stream ordered after it. */
+int msu_ln_param_reduce(const float* part, int nparts, int C, float* dgamma, float* dbeta, int accumulate,
+                        void* stream);
 int msu_reduce_rows(const float* part, int nparts, int n, long stride, float* out,
                     int accumulate, void* stream);
 

@@ -36,6 +36,7 @@ SIGNATURES = {
     "msu_win_attn_qkv_supported": (I, [I, I]),
     "msu_win_attn_qkv_fwd": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P]),
     "msu_win_attn_qkv_fwd2": (I, [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P]),
+    "msu_ln_param_reduce": (I, [P, I, I, P, P, I, P]),
     "msu_win_attn_qkv_hs_fwd": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P]),
     "msu_gelu_fwd": (I, [I, P, P, L, P]),
     "msu_gelu_bwd": (I, [I, P, P, P, L, P]),

@@ -358,6 +358,7 @@ int bwd_dispatch(int dtype, const LnBwdArgs& a, float* dgamma, float* dbeta, int
   int rc = -3;
   MSU_DISPATCH(dtype, T, rc = launch_bwd<T, MODE>(a, st, nparts));
   if (rc) return rc;
+  if (dgamma == nullptr) return MSU_CHECK_LAUNCH();  // partials only: msu_ln_param_reduce later
   if (dbeta == dgamma + a.C) {  // contiguous [dgamma | dbeta]: one reduction launch
     colsum(a.part, nparts, 2L * a.C, 2L * a.C, dgamma, accumulate, st);
   } else {
@@ -718,6 +719,22 @@ int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const 
     case IN_D2S2: return bwd_dispatch<IN_D2S2>(dtype, a, dgamma, dbeta, nparts, accumulate, st);
   }
   return -3;
+}
+
+// The parameter-gradient half of msu_layernorm_bwd (called with dgamma == null): dgamma / dbeta
+// [C] from the nparts x [2C] partials it left, written or accumulated -- on any stream ordered
+// after the backward kernel (the trainer's side stream: off the activation-gradient chain).
+int msu_ln_param_reduce(const float* part, int nparts, int C, float* dgamma, float* dbeta, int accumulate,
+                        void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (nparts <= 0 || C <= 0) return 0;
+  if (dbeta == dgamma + C) {
+    colsum(part, nparts, 2L * C, 2L * C, dgamma, accumulate, st);
+  } else {
+    const ColSeg segs[2] = {{part, C, 2L * C, dgamma}, {part + C, C, 2L * C, dbeta}};
+    colsum_multi(segs, 2, nparts, accumulate, st);
+  }
+  return MSU_CHECK_LAUNCH();
 }
 
 int msu_reduce_rows(const float* part, int nparts, int n, long stride, float* out,

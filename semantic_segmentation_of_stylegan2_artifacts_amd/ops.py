@@ -251,6 +251,32 @@ def _ln_grads(ctx, C, device):
     return dw, db, 0, False
 
 
+# LayerNorm parameter gradients (the partials' reduction into gamma / beta .grad) on the side
+# stream: nothing in backward reads them, and on the main stream the 54 small reductions per
+# step (30 us each, a few dozen workgroups) sat on the activation-gradient chain (r04q eager
+# profile: 1.7 ms/step).  A/B switch MSU_LN_SIDE=0.
+_LN_SIDE = os.environ.get("MSU_LN_SIDE", "1") != "0"
+
+
+def _ln_side(direct):
+    return direct and _LN_SIDE and _side_enabled
+
+
+def _ln_param_tail(ctx, part, n, C, dw, db, device):
+    """dgamma / dbeta of a LayerNorm backward (called with them null) on the side stream."""
+    main = torch.cuda.current_stream(device)
+    side = _side_stream_for(device)
+    side.wait_stream(main)
+    _lib.call("msu_ln_param_reduce", _p(part), n, C, _p(dw), _p(db), 1, side.cuda_stream)
+    part.record_stream(side)
+    _side_keep.append(part)
+    ev = torch.cuda.Event()
+    ev.record(side)
+    for p in ctx.affine:
+        _guard_side_write(p, ev)
+    _join_at_end_of_backward()
+
+
 def _ln_parts(rows, C, device):
     n = _lib.lib().msu_ln_part_blocks(rows, C)
     return n, torch.empty(n * 3 * C, device=device, dtype=torch.float32)
@@ -299,8 +325,12 @@ def _ln_backward(ctx, dy, _dm, _dr):
     dx = torch.empty_like(x)
     dw, db, acc, direct = _ln_grads(ctx, C, x.device)
     n, part = _ln_parts(rows, C, x.device)
+    side = _ln_side(direct)
     _lib.call("msu_layernorm_bwd", _dt(x), IN_PLAIN, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-              _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, C, 0, 0, 0, acc, _s(x))
+              _p(dx), None, None, 1, _p(part), n, None if side else _p(dw), None if side else _p(db), rows, C, 0,
+              0, 0, acc, _s(x))
+    if side:
+        _ln_param_tail(ctx, part, n, C, dw, db, x.device)
     if direct:
         _notify(*ctx.affine)
         return dx, None, None, None
@@ -358,9 +388,12 @@ def _add_ln_backward(ctx, ds, dy, _dm, _dr):
     dbr = torch.empty_like(s) if scale is not None else None
     dw, dbb, acc, direct = _ln_grads(ctx, C, s.device)
     n, part = _ln_parts(rows, C, s.device)
+    side = _ln_side(direct)
     _lib.call("msu_layernorm_bwd", _dt(s), IN_ADD, _p(dy), _p(s), _p(ds), _p(w), _p(mean), _p(rstd),
-              _p(da), _p(dbr), _p(scale), ctx.rps, _p(part), n, _p(dw), _p(dbb), rows, C, 0, 0, 0, acc,
-              _s(s))
+              _p(da), _p(dbr), _p(scale), ctx.rps, _p(part), n, None if side else _p(dw),
+              None if side else _p(dbb), rows, C, 0, 0, 0, acc, _s(s))
+    if side:
+        _ln_param_tail(ctx, part, n, C, dw, dbb, s.device)
     if direct:
         _notify(*ctx.affine)
         dw = dbb = None
@@ -411,8 +444,12 @@ def _merge_ln_backward(ctx, dy, _dm, _dr):
     dx = torch.empty_like(x)
     dw, db, acc, direct = _ln_grads(ctx, 4 * C, x.device)
     n, part = _ln_parts(rows, 4 * C, x.device)
+    side = _ln_side(direct)
     _lib.call("msu_layernorm_bwd", _dt(x), IN_MERGE, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-              _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, 4 * C, H, W, C, acc, _s(x))
+              _p(dx), None, None, 1, _p(part), n, None if side else _p(dw), None if side else _p(db), rows,
+              4 * C, H, W, C, acc, _s(x))
+    if side:
+        _ln_param_tail(ctx, part, n, 4 * C, dw, db, x.device)
     if direct:
         _notify(*ctx.affine)
         return dx, None, None, None
@@ -460,8 +497,12 @@ def _d2s_ln_backward(ctx, dy, _dm, _dr):
     dx = torch.empty_like(x)
     dw, db, acc, direct = _ln_grads(ctx, c, x.device)
     n, part = _ln_parts(rows, c, x.device)
+    side = _ln_side(direct)
     _lib.call("msu_layernorm_bwd", _dt(x), IN_D2S2, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-              _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, c, H, W, 0, acc, _s(x))
+              _p(dx), None, None, 1, _p(part), n, None if side else _p(dw), None if side else _p(db), rows,
+              c, H, W, 0, acc, _s(x))
+    if side:
+        _ln_param_tail(ctx, part, n, c, dw, db, x.device)
     if direct:
         _notify(*ctx.affine)
         return dx, None, None, None

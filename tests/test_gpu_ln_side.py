@@ -1,0 +1,60 @@
+"""GPU: the LayerNorm parameter gradients reduced on the weight-gradient side stream (trainer-style
+direct parameters, ops._ln_param_tail) equal the in-line reduction of the plain autograd path
+bitwise -- the same partials summed in the same order, only on another stream -- for the four
+LayerNorm forms of the path (torchvision block norms, the fused residual + norm, PatchMerging's
+gather + norm, PatchExpand's rearrange + norm; model_parts.py:87-94, :403-405)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    return ops
+
+
+def _params(C, seed, direct):
+    g = torch.Generator().manual_seed(seed)
+    w = torch.nn.Parameter((1 + 0.1 * torch.randn(C, generator=g)).to(DEV))
+    b = torch.nn.Parameter((0.1 * torch.randn(C, generator=g)).to(DEV))
+    if direct:
+        flat = torch.zeros(2 * C, device=DEV)  # contiguous [dgamma | dbeta], like the trainer's
+        w.grad = flat[:C]
+        b.grad = flat[C:]
+        w._msu_direct = b._msu_direct = True
+    return w, b
+
+
+@pytest.mark.parametrize("form", ["plain", "add", "merge", "d2s"])
+def test_ln_param_grads_on_side_stream_equal_inline(form):
+    ops = _ops()
+    assert ops._LN_SIDE
+    g = torch.Generator().manual_seed(3)
+    B, H, W, C = 2, 32, 32, 96
+    x = torch.randn(B, H, W, C, generator=g).to(DEV, torch.bfloat16)
+    br = torch.randn(B, H, W, C, generator=g).to(DEV, torch.bfloat16)
+    res = {}
+    for direct in (False, True):
+        Cn = 4 * C if form == "merge" else (C // 4 if form == "d2s" else C)
+        w, b = _params(Cn, 9, direct)
+        xg = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if form == "plain":
+                y = ops.layer_norm(xg, w, b)
+            elif form == "add":
+                s, y = ops.add_layer_norm(xg, br, None, w, b)
+                y = y + s
+            elif form == "merge":
+                y = ops.merge_layer_norm(xg, w, b)
+            else:
+                y = ops.d2s_layer_norm(xg, w, b)
+        dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).to(DEV, y.dtype)
+        y.backward(dy)
+        ops.join_side_streams()
+        torch.cuda.synchronize()
+        res[direct] = (xg.grad.clone(), w.grad.clone(), b.grad.clone())
+    for name, a, r in zip(("dx", "dgamma", "dbeta"), res[True], res[False]):
+        assert torch.equal(a, r), name
