@@ -58,3 +58,38 @@ def test_ln_param_grads_on_side_stream_equal_inline(form):
         res[direct] = (xg.grad.clone(), w.grad.clone(), b.grad.clone())
     for name, a, r in zip(("dx", "dgamma", "dbeta"), res[True], res[False]):
         assert torch.equal(a, r), name
+
+
+@pytest.mark.parametrize("d2s", [False, True])
+def test_refine_conv_param_grads_on_side_stream_equal_autograd(d2s):
+    """The refine convs' weight / bias gradients added into trainer-style .grad on the side
+    stream (ops._conv_wgrad_param) equal the autograd gradients bitwise (same kernel, added
+    into zeros); the input gradient is unchanged."""
+    ops = _ops()
+    assert ops._CONV_SIDE
+    g = torch.Generator().manual_seed(11)
+    B, H, W, C = 1, 64, 64, 96
+    xin = torch.randn(B, H // 4, W // 4, 16 * C, generator=g) if d2s else torch.randn(B, H, W, C, generator=g)
+    xin = xin.to(DEV, torch.bfloat16)
+    a = torch.nn.functional.gelu(xin.float()).to(torch.bfloat16)
+    w0 = (0.05 * torch.randn(C, C, 3, 3, generator=g)).to(DEV)
+    b0 = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    dz = torch.randn(B, H, W, C, generator=g).to(DEV, torch.bfloat16)
+    res = {}
+    for direct in (False, True):
+        w = torch.nn.Parameter(w0.clone())
+        b = torch.nn.Parameter(b0.clone())
+        if direct:
+            flat = torch.zeros(w.numel() + C, device=DEV)
+            w.grad = flat[:w.numel()].view_as(w)
+            b.grad = flat[w.numel():]
+            w._msu_direct = b._msu_direct = True
+        xg = xin.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            z = ops.refine_conv_act(xg, a, w, b, d2s, (H, W))
+        z.backward(dz)
+        ops.join_side_streams()
+        torch.cuda.synchronize()
+        res[direct] = (xg.grad.clone(), w.grad.clone(), b.grad.clone())
+    for name, u, r in zip(("dx", "dw", "db"), res[True], res[False]):
+        assert torch.equal(u, r), name

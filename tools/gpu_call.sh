@@ -182,6 +182,7 @@ for s in "$@"; do
         $O/${TAG}_pmcconv/conv_write_counter_collection.csv $O/${TAG}_conv3x3_fwd_pmc.json && cat $O/${TAG}_conv3x3_fwd_pmc.json ;;
     cat_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_cat "" "MSU_CAT_SIDE=0" "" "MSU_CAT_SIDE=0" "" "MSU_CAT_SIDE=0" || exit 3 ;;
     determ) step determ 600 python -u $R/tools/determinism_matrix.py 24 default ;;
+    conv_side_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_convside "" "MSU_CONV_SIDE=0" "" "MSU_CONV_SIDE=0" "" "MSU_CONV_SIDE=0" || exit 3 ;;
     ln_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_ln "" "MSU_LN_SIDE=0" "" "MSU_LN_SIDE=0" "" "MSU_LN_SIDE=0" || exit 3 ;;
     fused3_ab)
       for r in 1 2; do
