@@ -251,11 +251,13 @@ def _ln_grads(ctx, C, device):
     return dw, db, 0, False
 
 
-# LayerNorm parameter gradients (the partials' reduction into gamma / beta .grad) on the side
-# stream: nothing in backward reads them, and on the main stream the 54 small reductions per
-# step (30 us each, a few dozen workgroups) sat on the activation-gradient chain (r04q eager
-# profile: 1.7 ms/step).  A/B switch MSU_LN_SIDE=0.
-_LN_SIDE = os.environ.get("MSU_LN_SIDE", "1") != "0"
+# MSU_LN_SIDE=1 (opt-in): LayerNorm parameter gradients (the partials' reduction into gamma /
+# beta .grad) on the side stream.  On the main stream the 54 small reductions per step (30 us
+# each, a few dozen workgroups) sit on the activation-gradient chain (r04q eager profile: 1.7
+# ms/step), but on the side stream each one's wait for the main stream ties the side stream's
+# weight-gradient queue to the main stream's progress: 167.4 / 167.5 / 167.5 vs 170.2 / 170.2 /
+# 170.1 img/s (r04r).
+_LN_SIDE = os.environ.get("MSU_LN_SIDE", "0") == "1"
 
 
 def _ln_side(direct):
