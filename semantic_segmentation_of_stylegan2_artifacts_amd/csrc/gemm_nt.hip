@@ -29,7 +29,7 @@
 
 namespace {
 
-constexpr int BN = 128, BK = 64, CH = BK / 8;  // N tile (KN form), K step, 16-B chunks per row and step
+constexpr int BN = 128, BK = 64;  // N tile and K step of the KN form
 enum { EPI_PLAIN = 0, EPI_GELU_DUAL = 1, EPI_GELU_GRAD = 2 };
 
 struct NtArgs {
@@ -45,15 +45,21 @@ struct NtArgs {
   int prio;            // waves WM.. (the second wave of each SIMD) at s_setprio 1 (A/B MSU_NT_PRIO)
 };
 
-// A ROWS x BK operand tile (K-contiguous rows) staged by NTHR threads.  A 256-B LDS bank row
-// holds 2 tile rows; chunk c of row r is stored at chunk c ^ ((r >> 1) & 7), so a half-wave's 16
-// fragment rows (16 B each) land on 16 distinct bank groups.
-template <int ROWS, int NTHR>
+// A ROWS x KB operand tile (K-contiguous rows, KB = 64 or 32) staged by NTHR threads.  A 256-B
+// LDS bank row holds RPL = 128 / KB tile rows; chunk c of row r is stored at chunk c ^ ((r / RPL)
+// % CH), so a half-wave's 16 fragment rows (16 B each) land on 16 distinct bank groups.  When the
+// tile's 16-B slots are not a whole number of rounds of NTHR (192 rows x 4 chunks over 512
+// threads), the last round is issued by the first FULLW waves only (wave-uniform).
+template <int ROWS, int NTHR, int KB = 64>
 struct RowTile {
-  static constexpr int PER = ROWS * CH / NTHR;  // DMA instructions per thread
-  static_assert(PER * NTHR == ROWS * CH, "whole DMA instructions");
+  static constexpr int CH = KB / 8, RPL = 128 / KB;
+  static constexpr int PER = (ROWS * CH + NTHR - 1) / NTHR;  // DMA instructions per thread (max)
+  static constexpr int FULLW = (ROWS * CH - (PER - 1) * NTHR) / 64;  // waves issuing all PER
+  static_assert((ROWS * CH) % 64 == 0 && KB % 32 == 0, "whole-wave DMA instructions");
+  // DMA instructions of wave w
+  static MSU_DEV constexpr int per_wave(int w) { return w < FULLW ? PER : PER - 1; }
   // LDS element offset of k-chunk `chunk` (8 elements) of tile row `row`
-  static MSU_DEV int off(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
+  static MSU_DEV int off(int row, int chunk) { return row * KB + ((chunk ^ ((row / RPL) % CH)) << 3); }
   // slot p = c * NTHR + tid is row p / CH, LDS chunk p % CH, which holds the global chunk that
   // off() puts there; rows past the tensor re-read its last row (their results are never stored)
   static MSU_DEV void stage(const bf16_t* __restrict__ src, int row0, int rows, int K, int k0, bf16_t* tile,
@@ -61,8 +67,9 @@ struct RowTile {
     const int wave = tid >> 6;
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
+      if (c == PER - 1 && __builtin_amdgcn_readfirstlane(wave) >= FULLW) break;
       const int p = c * NTHR + tid;
-      const int row = p / CH, g = (p % CH) ^ ((row >> 1) & 7);
+      const int row = p / CH, g = (p % CH) ^ ((row / RPL) % CH);
       int r = row0 + row;
       if (r >= rows) r = rows - 1;
       glds16(src + (size_t)r * K + k0 + 8 * g, tile + (c * NTHR + wave * 64) * 8);
@@ -127,20 +134,41 @@ struct KnTile {
 // accumulators).  192 makes the N = 384 / 768 / 1152 / 2304 shapes of Swin-T's stages 2-3 whole
 // rounds of tiles on 256 CUs (N = 384 at M = 32768: 256 tiles of 256 x 192 instead of 384 of
 // 256 x 128, i.e. 1.5 rounds); KN (input-gradient) form: 128 only.
-template <typename T, int EPI, int WM, int NST, bool WKN, int BNT>
+// four-stage ring: wait until at most `younger` later steps' DMAs (D per step) and, if `stores`,
+// one epilogue's E stores are outstanding
+template <int D, int E>
+MSU_DEV void wait_ring4(int younger, bool stores) {
+  if (younger == 2) {
+    if (stores) wait_vmcnt<2 * D + E>();
+    else wait_vmcnt<2 * D>();
+  } else if (younger == 1) {
+    if (stores) wait_vmcnt<D + E>();
+    else wait_vmcnt<D>();
+  } else {
+    if (stores) wait_vmcnt<E>();
+    else wait_vmcnt<0>();
+  }
+}
+
+// KB: K step, 64 (two- or three-stage ring) or 32 (four-stage ring: the same LDS holds three
+// steps in flight instead of one or two).
+template <typename T, int EPI, int WM, int NST, bool WKN, int BNT, int KB>
 __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   constexpr int NTHR = 128 * WM, BM = 64 * WM, NI = BNT / 64;
-  static_assert(!WKN || BNT == BN, "KN tiles are 128 wide");
-  typedef RowTile<BM, NTHR> TA;
-  typedef RowTile<BNT, NTHR> TW;
+  static_assert(!WKN || (BNT == BN && KB == BK), "KN tiles are 128 wide, 64 deep");
+  typedef RowTile<BM, NTHR, KB> TA;
+  typedef RowTile<BNT, NTHR, KB> TW;
   typedef KnTile<NTHR> TK;
-  constexpr int KSL = BK / 16;  // 16-wide k slices per step
-  constexpr int STG = (BM + BNT) * BK;  // elements per ring stage
-  // per thread and step: DMA instructions, and epilogue stores of a tile
+  constexpr int KSL = KB / 16;  // 16-wide k slices per step
+  constexpr int STG = (BM + BNT) * KB;  // elements per ring stage
+  // per thread and step: DMA instructions (waves below DW0 issue D, the others D - 1), and
+  // epilogue stores of a tile
   constexpr int D = TA::PER + (WKN ? TK::PER : TW::PER);
+  static_assert(TA::FULLW * 64 == NTHR, "A rows: whole rounds");
+  constexpr int DW0 = WKN ? 64 : TW::FULLW;
   constexpr int E = (EPI == EPI_GELU_DUAL ? 8 : 4) * NI;
-  static_assert(NST == 2 || NST == 3, "ring depth");
-  static_assert(NST == 2 || (D + E < 64), "vmcnt range");
+  static_assert(NST >= 2 && NST <= 4, "ring depth");
+  static_assert(NST == 2 || ((NST - 2) * D + E < 64), "vmcnt range");
   __shared__ __attribute__((aligned(16))) bf16_t lds[NST * STG];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -148,7 +176,7 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   const int G = gridDim.x;
   const int L = xcd_remap(blockIdx.x, G);
   const int ntiles = a.tiles_m * a.tiles_n;
-  const int nk = a.K / BK;  // K % 64 == 0 (nt_shape_ok)
+  const int nk = a.K / KB;  // K % 64 == 0 (nt_shape_ok)
   const int mine = L < ntiles ? (ntiles - 1 - L) / G + 1 : 0;
   if (WM == 4 && a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int nsteps = mine * nk;
@@ -159,11 +187,11 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     const int t = L + ti * G;
     const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
     bf16_t* dst = lds + st * STG;
-    if (a.A2 == nullptr) TA::stage(a.A, mt * BM, a.M, a.K, kk * BK, dst, tid);
-    else if (kk * BK < a.K1) TA::stage(a.A, mt * BM, a.M, a.K1, kk * BK, dst, tid);  // K1 % BK == 0
-    else TA::stage(a.A2, mt * BM, a.M, a.K - a.K1, kk * BK - a.K1, dst, tid);
-    if constexpr (WKN) TK::stage(a.W, nt * BNT, a.N, kk * BK, dst + BM * BK, tid);
-    else TW::stage(a.W, nt * BNT, a.N, a.K, kk * BK, dst + BM * BK, tid);
+    if (a.A2 == nullptr) TA::stage(a.A, mt * BM, a.M, a.K, kk * KB, dst, tid);
+    else if (kk * KB < a.K1) TA::stage(a.A, mt * BM, a.M, a.K1, kk * KB, dst, tid);  // K1 % 64 == 0
+    else TA::stage(a.A2, mt * BM, a.M, a.K - a.K1, kk * KB - a.K1, dst, tid);
+    if constexpr (WKN) TK::stage(a.W, nt * BNT, a.N, kk * KB, dst + BM * KB, tid);
+    else TW::stage(a.W, nt * BNT, a.N, a.K, kk * KB, dst + BM * KB, tid);
   };
 
   f32x16 acc[NI][2];  // [column tile ni][token tile mi]: C^T, W rows on the accumulator rows
@@ -189,7 +217,7 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     // run-to-run differences of the eager step with the side stream on, round 3)
     if constexpr (NST == 2) {
       wait_vmcnt<0>();
-    } else {
+    } else if constexpr (NST == 3) {
       const bool younger = s + 1 < nsteps;
       const bool stores = epi_age <= 1 && nk >= 3 && epi_full;
       if (nk < 3) wait_vmcnt<0>();
@@ -197,6 +225,14 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
       else if (younger) wait_vmcnt<D>();
       else if (stores) wait_vmcnt<E>();
       else wait_vmcnt<0>();
+    } else {
+      // steps s + 1, s + 2 (those that exist) and the stores of an epilogue in iterations s - 3
+      // .. s - 1 were issued after step s's DMA; a wave's DMA count per step is D or D - 1
+      const int younger = nsteps - 1 - s < 2 ? nsteps - 1 - s : 2;
+      const bool stores = epi_age <= 2 && epi_full;
+      if (nk < 4) wait_vmcnt<0>();
+      else if (wave < DW0) wait_ring4<D, E>(younger, stores);
+      else wait_ring4<D - 1, E>(younger, stores);
     }
     __builtin_amdgcn_s_barrier();   // every wave's DMA of step s has landed, and every wave is
     asm volatile("" ::: "memory");  // done reading step s-1's stage (refilled below)
@@ -232,7 +268,7 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     const bool more = s + NST - 1 < nsteps;
     if (more) issue(s + NST - 1, cst == 0 ? NST - 1 : cst - 1);
     const bf16_t* ta = lds + cst * STG;
-    const bf16_t* tw = ta + BM * BK;
+    const bf16_t* tw = ta + BM * KB;
     cst = cst + 1 == NST ? 0 : cst + 1;
     bf16x8 fw[2][NI], fx[2][2];
     auto rd = [&](int ks, int set) {
@@ -272,8 +308,12 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     epi_full = m0 + 64 * wm + 64 <= a.M && n0 + WNC * wn + WNC <= a.N;
     // the epilogue operands (and every older DMA) have landed; the DMA just issued may stay
     // in flight (NST = 3).  One wait, not one per exec-masked store branch.
-    if (NST == 3 && more) wait_vmcnt<D>();
-    else wait_vmcnt<0>();
+    if (NST >= 3 && more) {
+      if (wave < DW0) wait_vmcnt<D>();
+      else wait_vmcnt<D - 1>();
+    } else {
+      wait_vmcnt<0>();
+    }
     // ---- epilogue of tile t: lane (l & 31) is token m; after the swap, 8 consecutive columns
     // per store
 #pragma unroll
@@ -355,7 +395,7 @@ int num_cus_nt() {
 // KN (input-gradient with the forward weight in place) keeps bn 128.  A/B switches:
 // MSU_NT_TILE = 128 | 192 | 256 (rows; 192 only with 192 columns), MSU_NT_BN = 128 | 192 (columns).
 struct NtCfg {
-  int wm, bn;
+  int wm, bn, kb = 64;
 };
 
 NtCfg nt_cfg(long M, int N, bool wkn) {
@@ -391,19 +431,22 @@ NtCfg nt_cfg(long M, int N, bool wkn) {
       best = c;
     }
   }
+  // MSU_NT_BK=32 (A/B switch): the 192-wide forms with 32-deep K steps and a four-stage ring
+  static const int force_kb = getenv("MSU_NT_BK") ? atoi(getenv("MSU_NT_BK")) : 64;
+  if (force_kb == 32 && best.bn == 192 && best.wm != 3) best.kb = 32;
   return best;
 }
 
-template <typename T, int WM, int NST, bool WKN, int BNT>
+template <typename T, int WM, int NST, bool WKN, int BNT, int KB = 64>
 void launch_nt(int epi, const NtArgs& a, hipStream_t st) {
   const long tiles = (long)a.tiles_m * a.tiles_n;
   const long cap = (long)num_cus_nt() * (WM == 2 ? 2 : 1);
   const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
   const dim3 blk(128 * WM);
   switch (epi) {
-    case EPI_PLAIN: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_PLAIN, WM, NST, WKN, BNT>), dim3(grid), blk, 0, st, a); break;
-    case EPI_GELU_DUAL: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_DUAL, WM, NST, WKN, BNT>), dim3(grid), blk, 0, st, a); break;
-    default: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_GRAD, WM, NST, WKN, BNT>), dim3(grid), blk, 0, st, a); break;
+    case EPI_PLAIN: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_PLAIN, WM, NST, WKN, BNT, KB>), dim3(grid), blk, 0, st, a); break;
+    case EPI_GELU_DUAL: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_DUAL, WM, NST, WKN, BNT, KB>), dim3(grid), blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_GRAD, WM, NST, WKN, BNT, KB>), dim3(grid), blk, 0, st, a); break;
   }
 }
 
@@ -435,7 +478,10 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
   if ((long)a.tiles_m * a.tiles_n >= (1L << 31)) return -2;
   hipStream_t st = (hipStream_t)stream;
   MSU_DISPATCH16(dtype, T,
-    if (cfg.bn == 192) {
+    if (cfg.bn == 192 && cfg.kb == 32) {
+      if (cfg.wm == 4) launch_nt<T, 4, 4, false, 192, 32>(epi, a, st);
+      else launch_nt<T, 2, 4, false, 192, 32>(epi, a, st);
+    } else if (cfg.bn == 192) {
       if (cfg.wm == 4) launch_nt<T, 4, 2, false, 192>(epi, a, st);
       else if (cfg.wm == 3) launch_nt<T, 3, 3, false, 192>(epi, a, st);
       else launch_nt<T, 2, 2, false, 192>(epi, a, st);

@@ -145,6 +145,16 @@ for s in "$@"; do
       done
       for f in $O/${TAG}_mem_nt_one_*/p_counter_collection.csv; do echo "== $f"; python3 $R/tools/pmc_sum.py gemm_nt $f; done
       for f in $O/${TAG}_mem_wgrad_one_*/p_counter_collection.csv; do echo "== $f"; python3 $R/tools/pmc_sum.py wgrad_wave $f; done ;;
+    ntbk_tests) MSU_NT_BK=32 step ntbk_tests 400 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py $R/tests/test_gpu_tok_gemm.py $R/tests/test_gpu_baseline_shapes.py ;;
+    ntbk_kern)
+      for shp in "32768 1152 384" "32768 384 384" "32768 1536 384" "32768 384 1536" "131072 576 192" "131072 192 768" "8192 2304 768" "8192 768 3072"; do
+        for bk in 64 32 64 32; do
+          echo -n "bk=$bk " >> $O/${TAG}_ntbk.log
+          MSU_NT_BK=$bk timeout -k 10 60 python -u $R/tools/nt_one.py $shp 30 2>&1 | grep "nt M" >> $O/${TAG}_ntbk.log || exit 3
+        done
+      done
+      cat $O/${TAG}_ntbk.log ;;
+    ntbk_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_ntbk "" "MSU_NT_BK=32" "" "MSU_NT_BK=32" "" "MSU_NT_BK=32" || exit 3 ;;
     nt192_tests) MSU_NT_TILE=192 MSU_NT_BN=192 step nt192_tests 400 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py -k "not underfilled and not chosen" ;;
     dma_probe) step dma_probe 120 python -u $R/tools/dma_probe.py ;;
     ntsb_ab)
