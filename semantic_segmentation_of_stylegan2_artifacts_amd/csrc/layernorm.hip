@@ -681,10 +681,12 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
 int msu_ln_part_blocks(long rows, int C) {
   // >= 16 rows per block (the per-block parameter-gradient reduction amortises) and enough
   // blocks to fill the CUs at the deep stages (8192 rows x 768: 512 blocks, not 64).  A/B
-  // switch MSU_LN_PARTS_MAX: 512 / 256 vs 1024 = 168.2 / 162.5 vs 170.0 img/s (r04t); a separate
-  // cap for C >= 384 (stages 2-3, whose partials are 2C wide), MSU_LN_PARTS_DEEP
+  // switch MSU_LN_PARTS_MAX: 512 / 256 vs 1024 = 168.2 / 162.5 vs 170.0 img/s (r04t).  C >= 384
+  // (stages 2-3, whose partials are 2C wide and whose reductions run on the main stream): 512
+  // blocks, 170.5 / 170.4 vs 169.8 / 169.8 with 1024 (256: 168.7 / 168.6; r04v), switch
+  // MSU_LN_PARTS_DEEP
   static const long cap = getenv("MSU_LN_PARTS_MAX") ? atol(getenv("MSU_LN_PARTS_MAX")) : 1024;
-  static const long cap_deep = getenv("MSU_LN_PARTS_DEEP") ? atol(getenv("MSU_LN_PARTS_DEEP")) : cap;
+  static const long cap_deep = getenv("MSU_LN_PARTS_DEEP") ? atol(getenv("MSU_LN_PARTS_DEEP")) : (cap < 512 ? cap : 512);
   long nb = (rows + 15) / 16;
   if (nb > cap) nb = cap;
   if (C >= 384 && nb > cap_deep) nb = cap_deep;
