@@ -180,7 +180,17 @@ struct LnBwdArgs {
   long rows_per_sample;
 };
 
-template <typename T, int MODE, int TPR, int KMAX>
+template <typename T>
+MSU_DEV void unpack16(const uint4 q, float (&v)[8]) {
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = Fmt16<T>::lo(w[i]);
+    v[2 * i + 1] = Fmt16<T>::hi(w[i]);
+  }
+}
+
+template <typename T, int MODE, int TPR, int KMAX, bool PFB = true>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
   constexpr int VW = VecW<T>::W;  // elements per 16-B chunk
   const int lane = threadIdx.x % TPR;
@@ -196,12 +206,88 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
     for (int e = 0; e < VW; ++e) { accg[k][e] = 0.f; accb[k][e] = 0.f; }
   LnArgs fa;
   fa.C = a.C; fa.H = a.H; fa.W = a.W; fa.Cin = a.Cin;
+  constexpr bool HAS_RES = MODE == IN_ADD || MODE == IN_PLAIN;
+  // 16-bit rows of one chunk per lane (every C <= 512 of the path): the group's next row is
+  // loaded while this one is reduced and stored, so a group waits one memory round trip per
+  // row only where the prefetch has not landed (the arithmetic, and so the result, is the
+  // plain loop's below).  A/B switch: the plain loop, template-selected by launch_bwd
+  if constexpr (KMAX == 1 && VW == 8 && PFB) {
+    const int ch = lane;
+    const bool act = ch < nchunk;
+    float gg[VW];
+    if (act) load_f32<VW>(a.gamma + ch * VW, gg);
+    const long stride = (long)gridDim.x * GPB;
+    long r = (long)blockIdx.x * GPB + grp;
+    uint4 qx{}, qd{}, qr{};
+    float mu = 0.f, rs = 0.f;
+    auto fetch = [&](long rr) __attribute__((always_inline)) {
+      mu = a.mean[rr];
+      rs = a.rstd[rr];
+      if (act) {
+        const long off = src_off<MODE>(fa, rr, ch * VW);
+        qx = *reinterpret_cast<const uint4*>(X + off);
+        qd = *reinterpret_cast<const uint4*>(DY + rr * (long)a.C + ch * VW);
+        if constexpr (HAS_RES) {
+          if (a.dres) qr = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dres) + off);
+        }
+      }
+    };
+    if (r < a.rows) fetch(r);
+    for (; r < a.rows; r += stride) {
+      const uint4 cx = qx, cd = qd, cr = qr;
+      const float cmu = mu, crs = rs;
+      if (r + stride < a.rows) fetch(r + stride);
+      float xh[VW], g[VW];
+      float s1 = 0.f, s2 = 0.f;
+      if (act) {
+        float xv[VW], dv[VW];
+        unpack16<T>(cx, xv);
+        unpack16<T>(cd, dv);
+#pragma unroll
+        for (int e = 0; e < VW; ++e) {
+          xh[e] = (xv[e] - cmu) * crs;
+          g[e] = dv[e] * gg[e];
+          s1 += g[e];
+          s2 += g[e] * xh[e];
+          accg[0][e] += dv[e] * xh[e];
+          accb[0][e] += dv[e];
+        }
+      }
+      s1 = group_sum<TPR>(s1) / a.C;
+      s2 = group_sum<TPR>(s2) / a.C;
+      float sc = 1.f;
+      if constexpr (MODE == IN_ADD) {
+        if (a.bscale) sc = a.bscale[r / a.rows_per_sample];
+      }
+      if (act) {
+        float o[VW];
+#pragma unroll
+        for (int e = 0; e < VW; ++e) o[e] = crs * (g[e] - s1 - xh[e] * s2);
+        const long off = src_off<MODE>(fa, r, ch * VW);
+        if constexpr (HAS_RES) {
+          if (a.dres) {
+            float dr[VW];
+            unpack16<T>(cr, dr);
+#pragma unroll
+            for (int e = 0; e < VW; ++e) o[e] += dr[e];
+          }
+        }
+        VecW<T>::store(reinterpret_cast<T*>(a.dx) + off, o);
+        if constexpr (MODE == IN_ADD) {
+          if (a.db) {
+#pragma unroll
+            for (int e = 0; e < VW; ++e) o[e] *= sc;
+            VecW<T>::store(reinterpret_cast<T*>(a.db) + off, o);
+          }
+        }
+      }
+    }
+  } else
   for (long r = (long)blockIdx.x * GPB + grp; r < a.rows; r += (long)gridDim.x * GPB) {
     const float mu = a.mean[r], rs = a.rstd[r];
     float xh[KMAX][VW], g[KMAX][VW];
     // the residual gradient is loaded with x and dy: one memory round trip per row, not two
     float dr[KMAX][VW];
-    constexpr bool HAS_RES = MODE == IN_ADD || MODE == IN_PLAIN;
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -328,6 +414,12 @@ int launch_bwd(const LnBwdArgs& a, hipStream_t st, int nblocks) {
     return MSU_CHECK_LAUNCH();
   };
   static const int wide = getenv("MSU_LN_WIDE") ? atoi(getenv("MSU_LN_WIDE")) : 2;  // see launch_fwd
+  static const bool pf = !(getenv("MSU_LN_BWD_PF") && getenv("MSU_LN_BWD_PF")[0] == '0');  // A/B switch
+  if (!pf) {
+    if (wide && nchunk <= 16) return go(ln_bwd_kernel<T, MODE, 16, 1, false>);
+    if (wide >= 2 && nchunk <= 32) return go(ln_bwd_kernel<T, MODE, 32, 1, false>);
+    if (wide >= 2 && nchunk <= 64) return go(ln_bwd_kernel<T, MODE, 64, 1, false>);
+  }
   if (wide && nchunk <= 16) return go(ln_bwd_kernel<T, MODE, 16, 1>);
   if (wide >= 2 && nchunk <= 32) return go(ln_bwd_kernel<T, MODE, 32, 1>);
   if (wide >= 2 && nchunk <= 64) return go(ln_bwd_kernel<T, MODE, 64, 1>);

@@ -1,0 +1,65 @@
+"""LayerNorm backward: the prefetching row loop against the plain one, bitwise.  The kernel
+choice is read once per process (MSU_LN_BWD_PF), so each variant runs in its own process:
+
+    MSU_LN_BWD_PF=0 python tools/ln_pf_check.py save /tmp/ln0.pt
+    python tools/ln_pf_check.py compare /tmp/ln0.pt
+
+Four LayerNorm forms, C = 96 / 192 / 384 (every one-chunk-per-lane width of the path), row
+counts that leave the last block ragged."""
+import sys
+
+import torch
+
+from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+
+
+def run():
+    out = {}
+    for C in (96, 192, 384):
+        for form in ("plain", "add", "merge", "d2s"):
+            g = torch.Generator().manual_seed(C)
+            B, H, W = 2, 34, 30  # 2040 rows: ragged against every block count
+            x = torch.randn(B, H, W, C, generator=g).cuda().to(torch.bfloat16)
+            br = torch.randn(B, H, W, C, generator=g).cuda().to(torch.bfloat16)
+            Cn = 4 * C if form == "merge" else (C // 4 if form == "d2s" else C)
+            w = torch.nn.Parameter((1 + 0.1 * torch.randn(Cn, generator=g)).cuda())
+            b = torch.nn.Parameter((0.1 * torch.randn(Cn, generator=g)).cuda())
+            xg = x.clone().requires_grad_(True)
+            bg = br.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                if form == "plain":
+                    y = ops.layer_norm(xg, w, b)
+                elif form == "add":
+                    s, y = ops.add_layer_norm(xg, bg, None, w, b)
+                    y = y + s
+                elif form == "merge":
+                    y = ops.merge_layer_norm(xg, w, b)
+                else:
+                    y = ops.d2s_layer_norm(xg, w, b)
+            dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).cuda().to(y.dtype)
+            y.backward(dy)
+            torch.cuda.synchronize()
+            key = f"{form}_{C}"
+            out[key + "_dx"] = xg.grad.cpu()
+            out[key + "_dw"] = w.grad.cpu()
+            out[key + "_db"] = b.grad.cpu()
+            if bg.grad is not None:
+                out[key + "_dbr"] = bg.grad.cpu()
+    return out
+
+
+def main():
+    mode, path = sys.argv[1], sys.argv[2]
+    res = run()
+    if mode == "save":
+        torch.save(res, path)
+        print(f"saved {len(res)} tensors")
+        return
+    ref = torch.load(path, weights_only=True)
+    bad = [k for k in ref if not torch.equal(ref[k], res[k])]
+    print(f"compared {len(ref)} tensors: {len(bad)} differ {bad[:8]}")
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
