@@ -95,7 +95,17 @@ MSU_DEV long src_off(const LnArgs& a, long r, int col) {
   }
 }
 
-template <typename T, int MODE, int TPR, int KMAX>
+template <typename T>
+MSU_DEV void unpack16(const uint4 q, float (&v)[8]) {
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = Fmt16<T>::lo(w[i]);
+    v[2 * i + 1] = Fmt16<T>::hi(w[i]);
+  }
+}
+
+template <typename T, int MODE, int TPR, int KMAX, bool PFF = true>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs a) {
   constexpr int VW = VecW<T>::W;  // elements per 16-B chunk
   const int lane = threadIdx.x % TPR;
@@ -104,6 +114,73 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs a) {
   const int nchunk = a.C / VW;
   const T* X = reinterpret_cast<const T*>(a.x);
   const T* Bv = reinterpret_cast<const T*>(a.b);
+  // 16-bit rows of one chunk per lane: the group's next row is loaded while this one is
+  // normalised (same arithmetic as the plain loop below; see ln_bwd_kernel)
+  if constexpr (KMAX == 1 && VW == 8 && PFF) {
+    const int ch = lane;
+    const bool act = ch < nchunk;
+    float g[VW], bt[VW];
+    if (act) {
+      load_f32<VW>(a.gamma + ch * VW, g);
+      load_f32<VW>(a.beta + ch * VW, bt);
+    }
+    const long stride = (long)gridDim.x * GPB;
+    long r = (long)blockIdx.x * GPB + grp;
+    uint4 qx{}, qb{};
+    float qsc = 1.f;
+    auto fetch = [&](long rr) __attribute__((always_inline)) {
+      if constexpr (MODE == IN_ADD) {
+        if (a.bscale) qsc = a.bscale[rr / a.rows_per_sample];
+      }
+      if (act) {
+        const long off = src_off<MODE>(a, rr, ch * VW);
+        qx = *reinterpret_cast<const uint4*>(X + off);
+        if constexpr (MODE == IN_ADD) {
+          if (Bv) qb = *reinterpret_cast<const uint4*>(Bv + off);
+        }
+      }
+    };
+    if (r < a.rows) fetch(r);
+    for (; r < a.rows; r += stride) {
+      const uint4 cx = qx, cb = qb;
+      const float sc = qsc;
+      if (r + stride < a.rows) fetch(r + stride);
+      float v[VW];
+      float sum = 0.f;
+      if (act) {
+        unpack16<T>(cx, v);
+        if constexpr (MODE == IN_ADD) {
+          if (Bv) {
+            float w[VW];
+            unpack16<T>(cb, w);
+#pragma unroll
+            for (int e = 0; e < VW; ++e) v[e] += sc * w[e];
+          }
+#pragma unroll
+          for (int e = 0; e < VW; ++e) v[e] = to_f32(from_f32<T>(v[e]));
+          if (a.s_out) VecW<T>::store(reinterpret_cast<T*>(a.s_out) + src_off<MODE>(a, r, ch * VW), v);
+        }
+#pragma unroll
+        for (int e = 0; e < VW; ++e) sum += v[e];
+      }
+      sum = group_sum<TPR>(sum);
+      const float mu = sum / a.C;
+      float var = 0.f;
+      if (act) {
+#pragma unroll
+        for (int e = 0; e < VW; ++e) { const float d = v[e] - mu; var += d * d; }
+      }
+      var = group_sum<TPR>(var);
+      const float rs = rsqrtf(var / a.C + a.eps);
+      if (act) {
+        float o[VW];
+#pragma unroll
+        for (int e = 0; e < VW; ++e) o[e] = (v[e] - mu) * rs * g[e] + bt[e];
+        VecW<T>::store(reinterpret_cast<T*>(a.y) + r * (long)a.C + ch * VW, o);
+      }
+      if (lane == 0) { a.mean[r] = mu; a.rstd[r] = rs; }
+    }
+  } else
   for (long r = (long)blockIdx.x * GPB + grp; r < a.rows; r += (long)gridDim.x * GPB) {
     float v[KMAX][VW];
     float sum = 0.f;
@@ -179,16 +256,6 @@ struct LnBwdArgs {
   int C, H, W, Cin;
   long rows_per_sample;
 };
-
-template <typename T>
-MSU_DEV void unpack16(const uint4 q, float (&v)[8]) {
-  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = Fmt16<T>::lo(w[i]);
-    v[2 * i + 1] = Fmt16<T>::hi(w[i]);
-  }
-}
 
 template <typename T, int MODE, int TPR, int KMAX, bool PFB = true>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
@@ -394,6 +461,12 @@ int launch_fwd(const LnArgs& a, hipStream_t st, int max_blocks) {
   // and the same up to C <= 512 on 32 / 64 lanes: +0.25 % more (3 of 3 pairs).  A/B switch
   // MSU_LN_WIDE: 0 = 4-lane rows, 1 = one chunk per lane up to C = 128 only)
   static const int wide = getenv("MSU_LN_WIDE") ? atoi(getenv("MSU_LN_WIDE")) : 2;
+  static const bool pf = !(getenv("MSU_LN_FWD_PF") && getenv("MSU_LN_FWD_PF")[0] == '0');  // A/B switch
+  if (!pf) {
+    if (wide && nchunk <= 16) return go(ln_fwd_kernel<T, MODE, 16, 1, false>, 16);
+    if (wide >= 2 && nchunk <= 32) return go(ln_fwd_kernel<T, MODE, 32, 1, false>, 32);
+    if (wide >= 2 && nchunk <= 64) return go(ln_fwd_kernel<T, MODE, 64, 1, false>, 64);
+  }
   if (wide && nchunk <= 16) return go(ln_fwd_kernel<T, MODE, 16, 1>, 16);
   if (wide >= 2 && nchunk <= 32) return go(ln_fwd_kernel<T, MODE, 32, 1>, 32);
   if (wide >= 2 && nchunk <= 64) return go(ln_fwd_kernel<T, MODE, 64, 1>, 64);

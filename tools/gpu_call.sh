@@ -193,10 +193,11 @@ for s in "$@"; do
     cat_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_cat "" "MSU_CAT_SIDE=0" "" "MSU_CAT_SIDE=0" "" "MSU_CAT_SIDE=0" || exit 3 ;;
     determ) step determ 600 python -u $R/tools/determinism_matrix.py 24 default ;;
     conv_side_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_convside "" "MSU_CONV_SIDE=0" "" "MSU_CONV_SIDE=0" "" "MSU_CONV_SIDE=0" || exit 3 ;;
-    lnpf_check) MSU_LN_BWD_PF=0 step lnpf_save 120 python -u $R/tools/ln_pf_check.py save $O/${TAG}_ln0.pt && \
+    lnpf_check) MSU_LN_FWD_PF=0 MSU_LN_BWD_PF=0 step lnpf_save 120 python -u $R/tools/ln_pf_check.py save $O/${TAG}_ln0.pt && \
                 step lnpf_check 120 python -u $R/tools/ln_pf_check.py compare $O/${TAG}_ln0.pt && \
                 step lnpf_tests 300 $PYT -m gpu $R/tests/test_gpu_ops.py -k "norm" $R/tests/test_gpu_ln_side.py ;;
     lnpf_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_lnpf "" "MSU_LN_BWD_PF=0" "" "MSU_LN_BWD_PF=0" "" "MSU_LN_BWD_PF=0" || exit 3 ;;
+    lnfpf_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_lnfpf "" "MSU_LN_FWD_PF=0" "" "MSU_LN_FWD_PF=0" "" "MSU_LN_FWD_PF=0" || exit 3 ;;
     lndeep_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_lndeep "" "MSU_LN_PARTS_DEEP=512" "MSU_LN_PARTS_DEEP=256" "" "MSU_LN_PARTS_DEEP=512" "MSU_LN_PARTS_DEEP=256" || exit 3 ;;
     lnparts_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_lnparts "" "MSU_LN_PARTS_MAX=512" "MSU_LN_PARTS_MAX=256" "" "MSU_LN_PARTS_MAX=512" "MSU_LN_PARTS_MAX=256" || exit 3 ;;
     ln_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_ln "MSU_LN_SIDE=1" "" "MSU_LN_SIDE=1" "" "MSU_LN_SIDE=1" "" || exit 3 ;;

@@ -1,15 +1,18 @@
-"""LayerNorm backward: the prefetching row loop against the plain one, bitwise.  The kernel
-choice is read once per process (MSU_LN_BWD_PF), so each variant runs in its own process:
+"""LayerNorm forward and backward: the prefetching row loops against the plain ones, bitwise.
+The kernel choice is read once per process (MSU_LN_FWD_PF / MSU_LN_BWD_PF), so each variant
+runs in its own process:
 
-    MSU_LN_BWD_PF=0 python tools/ln_pf_check.py save /tmp/ln0.pt
+    MSU_LN_FWD_PF=0 MSU_LN_BWD_PF=0 python tools/ln_pf_check.py save /tmp/ln0.pt
     python tools/ln_pf_check.py compare /tmp/ln0.pt
 
 Four LayerNorm forms, C = 96 / 192 / 384 (every one-chunk-per-lane width of the path), row
 counts that leave the last block ragged."""
+import os
 import sys
 
 import torch
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from semantic_segmentation_of_stylegan2_artifacts_amd import ops
 
 
@@ -37,6 +40,7 @@ def run():
                 else:
                     y = ops.d2s_layer_norm(xg, w, b)
             dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).cuda().to(y.dtype)
+            out[f"{form}_{C}_y"] = y.detach().float().cpu()
             y.backward(dy)
             torch.cuda.synchronize()
             key = f"{form}_{C}"
