@@ -162,7 +162,22 @@ def side_stream(device):
     return _side_streams.get(device.index if device.index is not None else torch.cuda.current_device())
 
 
+# Side-stream launches held back to the next side-stream fork (or the end of backward): the
+# refine convs' weight gradients (MSU_CONV_DEFER=1), so they overlap the HBM-bound stage-0
+# decoder backward instead of the MFMA-bound conv input gradients of the stacks after them.
+_deferred_side = []
+
+
+def _flush_deferred_side():
+    if _deferred_side:
+        work = _deferred_side[:]
+        _deferred_side.clear()
+        for fn in work:
+            fn()
+
+
 def _side_stream_for(device):
+    _flush_deferred_side()
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _side_streams.get(idx)
     if st is None:
@@ -215,6 +230,7 @@ _side_event_params = []
 def _end_of_backward():
     global _join_queued
     _join_queued = False
+    _flush_deferred_side()
     join_side_streams()
     _side_keep.clear()  # the main stream now waits for every side-stream read
     for p in _side_event_params:
@@ -1441,6 +1457,8 @@ def _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout):
 
 # A/B switch MSU_CONV_SIDE=0: the refine convs' weight gradients on the main stream
 _CONV_SIDE = os.environ.get("MSU_CONV_SIDE", "1") != "0"
+# MSU_CONV_DEFER=1: ... and issued at the next side-stream fork (_deferred_side)
+_CONV_DEFER = os.environ.get("MSU_CONV_DEFER", "0") == "1"
 
 
 def _conv_wgrad_param(a, dz, mode, B, H, W, Cin, Cout, weight, bias):
@@ -1449,22 +1467,30 @@ def _conv_wgrad_param(a, dz, mode, B, H, W, Cin, Cout, weight, bias):
     them: off the activation-gradient chain, 2 x 1.3 ms per step on the main stream before)."""
     if not (_CONV_SIDE and _side_enabled and _direct(weight, bias)):
         return _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout)
-    main = torch.cuda.current_stream(a.device)
-    side = _side_stream_for(a.device)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        dw, db = _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout)
-        weight.grad.add_(dw)
-        bias.grad.add_(db)
-    for t in (a, dz):
-        t.record_stream(side)
-        _side_keep.append(t)
-    ev = torch.cuda.Event()
-    ev.record(side)
-    _guard_side_write(weight, ev)
-    _guard_side_write(bias, ev)
+
+    def launch():
+        main = torch.cuda.current_stream(a.device)
+        side = _side_stream_for(a.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            dw, db = _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout)
+            weight.grad.add_(dw)
+            bias.grad.add_(db)
+        for t in (a, dz):
+            t.record_stream(side)
+            _side_keep.append(t)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        _guard_side_write(weight, ev)
+        _guard_side_write(bias, ev)
+        _notify(weight, bias)
+
+    if _CONV_DEFER:
+        # the closure holds a and dz (autograd cannot steal them for an in-place add meanwhile)
+        _deferred_side.append(launch)
+    else:
+        launch()
     _join_at_end_of_backward()
-    _notify(weight, bias)
     return None, None
 
 

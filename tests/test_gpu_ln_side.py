@@ -60,13 +60,16 @@ def test_ln_param_grads_on_side_stream_equal_inline(form, monkeypatch):
         assert torch.equal(a, r), name
 
 
+@pytest.mark.parametrize("defer", [False, True])
 @pytest.mark.parametrize("d2s", [False, True])
-def test_refine_conv_param_grads_on_side_stream_equal_autograd(d2s):
+def test_refine_conv_param_grads_on_side_stream_equal_autograd(d2s, defer, monkeypatch):
     """The refine convs' weight / bias gradients added into trainer-style .grad on the side
     stream (ops._conv_wgrad_param) equal the autograd gradients bitwise (same kernel, added
-    into zeros); the input gradient is unchanged."""
+    into zeros); the input gradient is unchanged.  defer: the launch held back to the end of
+    backward (MSU_CONV_DEFER)."""
     ops = _ops()
     assert ops._CONV_SIDE
+    monkeypatch.setattr(ops, "_CONV_DEFER", defer)
     g = torch.Generator().manual_seed(11)
     B, H, W, C = 1, 64, 64, 96
     xin = torch.randn(B, H // 4, W // 4, 16 * C, generator=g) if d2s else torch.randn(B, H, W, C, generator=g)

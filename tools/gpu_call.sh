@@ -193,6 +193,14 @@ for s in "$@"; do
     cat_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_cat "" "MSU_CAT_SIDE=0" "" "MSU_CAT_SIDE=0" "" "MSU_CAT_SIDE=0" || exit 3 ;;
     determ) step determ 600 python -u $R/tools/determinism_matrix.py 24 default ;;
     conv_side_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_convside "" "MSU_CONV_SIDE=0" "" "MSU_CONV_SIDE=0" "" "MSU_CONV_SIDE=0" || exit 3 ;;
+    defer_tests) step defer_tests 300 $PYT -m gpu $R/tests/test_gpu_ln_side.py $R/tests/test_gpu_trainer.py $R/tests/test_gpu_rccl.py $R/tests/test_gpu_graph.py ;;
+    defer_tests1) MSU_CONV_DEFER=1 step defer_tests1 300 $PYT -m gpu $R/tests/test_gpu_trainer.py $R/tests/test_gpu_rccl.py $R/tests/test_gpu_graph.py $R/tests/test_gpu_bench_dp.py ;;
+    defer_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_defer "MSU_CONV_DEFER=1" "" "MSU_CONV_DEFER=1" "" "MSU_CONV_DEFER=1" "" || exit 3 ;;
+    lnpf_iso) MSU_LN_FWD_PF=0 MSU_LN_BWD_PF=0 step lnpf_save 120 python -u $R/tools/ln_pf_check.py save $O/${TAG}_ln0.pt && \
+              MSU_LN_FWD_PF=0 MSU_LN_BWD_PF=0 step lnpf_same 120 python -u $R/tools/ln_pf_check.py compare $O/${TAG}_ln0.pt && \
+              MSU_LN_BWD_PF=0 step lnpf_fwdonly 120 python -u $R/tools/ln_pf_check.py compare $O/${TAG}_ln0.pt && \
+              MSU_LN_FWD_PF=0 step lnpf_bwdonly 120 python -u $R/tools/ln_pf_check.py compare $O/${TAG}_ln0.pt && \
+              step lnpf_both 120 python -u $R/tools/ln_pf_check.py compare $O/${TAG}_ln0.pt ;;
     lnpf_check) MSU_LN_FWD_PF=0 MSU_LN_BWD_PF=0 step lnpf_save 120 python -u $R/tools/ln_pf_check.py save $O/${TAG}_ln0.pt && \
                 step lnpf_check 120 python -u $R/tools/ln_pf_check.py compare $O/${TAG}_ln0.pt && \
                 step lnpf_tests 300 $PYT -m gpu $R/tests/test_gpu_ops.py -k "norm" $R/tests/test_gpu_ln_side.py ;;

@@ -62,6 +62,9 @@ def main():
     ref = torch.load(path, weights_only=True)
     bad = [k for k in ref if not torch.equal(ref[k], res[k])]
     print(f"compared {len(ref)} tensors: {len(bad)} differ {bad[:8]}")
+    for k in bad[:8]:
+        d = (ref[k].float() - res[k].float()).abs()
+        print(f"  {k}: max |diff| {d.max().item():.3e} at {d.argmax().item()}, {int((d > 0).sum())} of {d.numel()} elements")
     sys.exit(1 if bad else 0)
 
 
