@@ -259,6 +259,9 @@ struct LnBwdArgs {
 
 template <typename T, int MODE, int TPR, int KMAX, bool PFB = true>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
+  // no implicit contraction: the two row loops below (prefetching / plain) fuse exactly the
+  // multiply-adds written as fmaf, so they agree bitwise (tools/ln_pf_check.py)
+#pragma clang fp contract(off)
   constexpr int VW = VecW<T>::W;  // elements per 16-B chunk
   const int lane = threadIdx.x % TPR;
   const int grp = threadIdx.x / TPR;
@@ -315,8 +318,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
           xh[e] = (xv[e] - cmu) * crs;
           g[e] = dv[e] * gg[e];
           s1 += g[e];
-          s2 += g[e] * xh[e];
-          accg[0][e] += dv[e] * xh[e];
+          s2 = __builtin_fmaf(g[e], xh[e], s2);
+          accg[0][e] = __builtin_fmaf(dv[e], xh[e], accg[0][e]);
           accb[0][e] += dv[e];
         }
       }
@@ -329,15 +332,18 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
       if (act) {
         float o[VW];
 #pragma unroll
-        for (int e = 0; e < VW; ++e) o[e] = crs * (g[e] - s1 - xh[e] * s2);
+        for (int e = 0; e < VW; ++e) o[e] = __builtin_fmaf(-xh[e], s2, g[e] - s1);
         const long off = src_off<MODE>(fa, r, ch * VW);
-        if constexpr (HAS_RES) {
-          if (a.dres) {
-            float dr[VW];
-            unpack16<T>(cr, dr);
+        bool res = false;
+        if constexpr (HAS_RES) res = a.dres != nullptr;
+        if (res) {
+          float dr[VW];
+          unpack16<T>(cr, dr);
 #pragma unroll
-            for (int e = 0; e < VW; ++e) o[e] += dr[e];
-          }
+          for (int e = 0; e < VW; ++e) o[e] = __builtin_fmaf(crs, o[e], dr[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < VW; ++e) o[e] *= crs;
         }
         VecW<T>::store(reinterpret_cast<T*>(a.dx) + off, o);
         if constexpr (MODE == IN_ADD) {
@@ -373,8 +379,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
           xh[k][e] = (xv[e] - mu) * rs;
           g[k][e] = dv[e] * gg[e];
           s1 += g[k][e];
-          s2 += g[k][e] * xh[k][e];
-          accg[k][e] += dv[e] * xh[k][e];
+          s2 = __builtin_fmaf(g[k][e], xh[k][e], s2);
+          accg[k][e] = __builtin_fmaf(dv[e], xh[k][e], accg[k][e]);
           accb[k][e] += dv[e];
         }
       }
@@ -391,13 +397,16 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
       if (ch < nchunk) {
         float o[VW];
 #pragma unroll
-        for (int e = 0; e < VW; ++e) o[e] = rs * (g[k][e] - s1 - xh[k][e] * s2);
+        for (int e = 0; e < VW; ++e) o[e] = __builtin_fmaf(-xh[k][e], s2, g[k][e] - s1);
         const long off = src_off<MODE>(fa, r, ch * VW);
-        if constexpr (HAS_RES) {
-          if (a.dres) {
+        bool res = false;
+        if constexpr (HAS_RES) res = a.dres != nullptr;
+        if (res) {
 #pragma unroll
-            for (int e = 0; e < VW; ++e) o[e] += dr[k][e];
-          }
+          for (int e = 0; e < VW; ++e) o[e] = __builtin_fmaf(rs, o[e], dr[k][e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < VW; ++e) o[e] *= rs;
         }
         VecW<T>::store(reinterpret_cast<T*>(a.dx) + off, o);
         if constexpr (MODE == IN_ADD) {
