@@ -732,11 +732,15 @@ __global__ void __launch_bounds__(256) head_fwd16_kernel(const T* z, const float
 // dgamma_c = w_c A_c, dbeta_c = w_c D, dw_c = gamma_c A_c + beta_c D with A_c = sum_r dl xh_c,
 // D = sum_r dl: per block only A (per channel) and D are accumulated, reduced over the
 // block's 64 row groups in fixed order through LDS, and expanded into the [3][C] partial.
-template <typename T, int KC>
+// PF: the group's next row (z chunks, mean, rstd, dlogit) is loaded while this one is reduced
+// and stored -- a group walks ~128 rows per launch at 1024^2; the arithmetic is the plain loop's
+// (no implicit contraction; A/B switch MSU_HEAD_BWD_PF=0)
+template <typename T, int KC, bool PF = true>
 __global__ void __launch_bounds__(256) head_bwd16_kernel(const float* dlogit, const T* z, const float* gamma,
                                                          const float* beta, const float* w, const float* mean,
                                                          const float* rstd, T* dz,
                                                          float* part /* [grid, 3, C] */, long rows) {
+#pragma clang fp contract(off)
   constexpr int TPR = 4, C = 32 * KC, RPB = 256 / TPR;
   __shared__ float redA[RPB][C + 1];
   __shared__ float redD[RPB];
@@ -751,13 +755,32 @@ __global__ void __launch_bounds__(256) head_bwd16_kernel(const float* dlogit, co
       gw[k][e] = gamma[c] * w[c];
       acc[k][e] = 0.f;
     }
-  for (long r = (long)blockIdx.x * RPB + grp; r < rows; r += (long)gridDim.x * RPB) {
-    const float mu = mean[r], rs = rstd[r], dl = dlogit[r];
+  const long stride = (long)gridDim.x * RPB;
+  long r = (long)blockIdx.x * RPB + grp;
+  u32x4 nq[KC];
+  float nmu = 0.f, nrs = 0.f, ndl = 0.f;
+  auto fetch = [&](long rr) __attribute__((always_inline)) {
+    nmu = mean[rr];
+    nrs = rstd[rr];
+    ndl = dlogit[rr];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) nq[k] = *reinterpret_cast<const u32x4*>(z + rr * C + (lane + TPR * k) * 8);
+  };
+  if (PF && r < rows) fetch(r);
+  for (; r < rows; r += stride) {
+    if constexpr (!PF) fetch(r);
+    const float mu = nmu, rs = nrs, dl = ndl;
+    u32x4 cq[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) cq[k] = nq[k];
+    if constexpr (PF) {
+      if (r + stride < rows) fetch(r + stride);
+    }
     float xh[KC][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
-      const u32x4 q = *reinterpret_cast<const u32x4*>(z + r * C + (lane + TPR * k) * 8);
+      const u32x4 q = cq[k];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         xh[k][2 * i] = (Fmt16<T>::lo(q[i]) - mu) * rs;
@@ -767,8 +790,8 @@ __global__ void __launch_bounds__(256) head_bwd16_kernel(const float* dlogit, co
       for (int e = 0; e < 8; ++e) {
         const float g = dl * gw[k][e];
         s1 += g;
-        s2 += g * xh[k][e];
-        acc[k][e] += dl * xh[k][e];
+        s2 = __builtin_fmaf(g, xh[k][e], s2);
+        acc[k][e] = __builtin_fmaf(dl, xh[k][e], acc[k][e]);
       }
     }
     adl += dl;
@@ -778,7 +801,7 @@ __global__ void __launch_bounds__(256) head_bwd16_kernel(const float* dlogit, co
     for (int k = 0; k < KC; ++k) {
       float o[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = rs * (dl * gw[k][e] - s1 - xh[k][e] * s2);
+      for (int e = 0; e < 8; ++e) o[e] = rs * __builtin_fmaf(-xh[k][e], s2, dl * gw[k][e] - s1);
       *reinterpret_cast<u32x4*>(dz + r * C + (lane + TPR * k) * 8) =
           u32x4{pack2<T>(o[0], o[1]), pack2<T>(o[2], o[3]), pack2<T>(o[4], o[5]), pack2<T>(o[6], o[7])};
     }
@@ -834,10 +857,13 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
   if (C % 4 || C > 256) return -2;
   if (rows == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  static const bool head_pf = !(getenv("MSU_HEAD_BWD_PF") && getenv("MSU_HEAD_BWD_PF")[0] == '0');  // A/B switch
   if (msu_is16(dtype) && (C == 96 || C == 128)) {
     MSU_DISPATCH16(dtype, T,
-      if (C == 96) hipLaunchKernelGGL((head_bwd16_kernel<T, 3>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows);
-      else hipLaunchKernelGGL((head_bwd16_kernel<T, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows));
+      if (C == 96 && head_pf) hipLaunchKernelGGL((head_bwd16_kernel<T, 3>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows);
+      else if (C == 96) hipLaunchKernelGGL((head_bwd16_kernel<T, 3, false>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows);
+      else if (head_pf) hipLaunchKernelGGL((head_bwd16_kernel<T, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows);
+      else hipLaunchKernelGGL((head_bwd16_kernel<T, 4, false>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows));
   } else {
     MSU_DISPATCH(dtype, T,
       if (C <= 128) hipLaunchKernelGGL((head_bwd_kernel<T, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows, C);

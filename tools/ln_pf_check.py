@@ -1,6 +1,6 @@
 """LayerNorm forward and backward: the prefetching row loops against the plain ones, bitwise.
-The kernel choice is read once per process (MSU_LN_FWD_PF / MSU_LN_BWD_PF), so each variant
-runs in its own process:
+The kernel choice is read once per process (MSU_LN_FWD_PF / MSU_LN_BWD_PF / MSU_HEAD_BWD_PF),
+so each variant runs in its own process:
 
     MSU_LN_FWD_PF=0 MSU_LN_BWD_PF=0 python tools/ln_pf_check.py save /tmp/ln0.pt
     python tools/ln_pf_check.py compare /tmp/ln0.pt
@@ -49,6 +49,20 @@ def run():
             out[key + "_db"] = b.grad.cpu()
             if bg.grad is not None:
                 out[key + "_dbr"] = bg.grad.cpu()
+    # the decoder head (LayerNorm + 1x1 output conv, head_bwd16_kernel: MSU_HEAD_BWD_PF)
+    for C in (96, 128):
+        g = torch.Generator().manual_seed(7 + C)
+        z = torch.randn(2, 66, 62, C, generator=g).cuda().to(torch.bfloat16).requires_grad_(True)
+        gm = (1 + 0.1 * torch.randn(C, generator=g)).cuda().requires_grad_(True)
+        bt = (0.1 * torch.randn(C, generator=g)).cuda().requires_grad_(True)
+        wo = (torch.randn(1, C, 1, 1, generator=g) / C ** 0.5).cuda().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = ops.head_norm_output(z, gm, bt, wo)
+        dl = torch.randn(y.shape, generator=torch.Generator().manual_seed(3)).cuda()
+        y.backward(dl.to(y.dtype))
+        torch.cuda.synchronize()
+        for name, t in (("y", y.detach().float()), ("dz", z.grad), ("dg", gm.grad), ("db", bt.grad), ("dw", wo.grad)):
+            out[f"head_{C}_{name}"] = t.cpu()
     return out
 
 
