@@ -1444,9 +1444,14 @@ def _pad_to(t, dim, mult):
     return torch.cat([t, t.new_zeros(shape)], dim)
 
 
+# persistent workgroups of the refine-conv weight gradient (one 139 KB / 12-wave workgroup per
+# CU: while it runs on the side stream nothing else fits on its CUs).  A/B switch
+_CONV_WGRAD_BLOCKS = int(os.environ.get("MSU_CONV_WGRAD_BLOCKS", "256"))
+
+
 def _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout):
     L = _lib.lib()
-    nchunk = 256
+    nchunk = _CONV_WGRAD_BLOCKS
     ws = torch.empty(L.msu_conv3x3_wgrad_workspace(nchunk, Cin, Cout, 0, 0), device=a.device, dtype=torch.float32)
     dw = torch.empty(Cout, Cin, 3, 3, device=a.device, dtype=torch.float32)
     db = torch.empty(Cout, device=a.device, dtype=torch.float32)

@@ -205,6 +205,8 @@ for s in "$@"; do
             step headpf_check 120 python -u $R/tools/ln_pf_check.py compare $O/${TAG}_h0.pt && \
             step headpf_tests 300 $PYT -m gpu $R/tests/test_gpu_ops.py -k "head or norm" ;;
     headpf_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_headpf "" "MSU_HEAD_BWD_PF=0" "" "MSU_HEAD_BWD_PF=0" "" "MSU_HEAD_BWD_PF=0" || exit 3 ;;
+    convblk_ab) bash $R/tools/gpu_bench_ab.sh ${TAG}_convblk "" "MSU_CONV_WGRAD_BLOCKS=192" "MSU_CONV_WGRAD_BLOCKS=128" "" "MSU_CONV_WGRAD_BLOCKS=192" "MSU_CONV_WGRAD_BLOCKS=128" || exit 3 ;;
+    convblk_tests) MSU_CONV_WGRAD_BLOCKS=128 step convblk_tests 300 $PYT -m gpu $R/tests/test_gpu_ln_side.py $R/tests/test_gpu_ops.py -k "refine or conv" ;;
     lnpf_check) MSU_LN_FWD_PF=0 MSU_LN_BWD_PF=0 step lnpf_save 120 python -u $R/tools/ln_pf_check.py save $O/${TAG}_ln0.pt && \
                 step lnpf_check 120 python -u $R/tools/ln_pf_check.py compare $O/${TAG}_ln0.pt && \
                 step lnpf_tests 300 $PYT -m gpu $R/tests/test_gpu_ops.py -k "norm" $R/tests/test_gpu_ln_side.py ;;
