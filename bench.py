@@ -140,8 +140,8 @@ def conv_roofline(device, batch, img, C):
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
-    # the C-ABI dispatches C = 96 to the 16-row-tile v3 kernel unless MSU_CONV_V=2 (csrc/conv3x3.h)
-    kname = "conv3x3_v3_kernel" if C == 96 and os.environ.get("MSU_CONV_V", "") != "2" else "conv3x3_v2_kernel"
+    # the C-ABI dispatches C = 96 to the 16-row-tile v3 kernel (csrc/conv3x3.h)
+    kname = "conv3x3_v3_kernel" if C == 96 else "conv3x3_v2_kernel"
     return {"kernel": f"{kname} (refine2 fwd, bf16 MFMA implicit GEMM)", "bound": "mfma",
             "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
@@ -218,9 +218,8 @@ def attention_roofline(device, batch, img, C, heads, p_drop):
 
 
 def fused_unit_roofline(device, batch, img, C, heads, p_drop):
-    """The stage-0 fused unit (qkv Linear -> window attention -> proj Linear: by default the
-    head-stationary msu_win_attn_qkv_hs_fwd + the proj Linear's GEMM, MSU_ATTN_QKV=1 all three in
-    msu_win_attn_qkv_fwd2) at the bench shape: inference (no qkv / o written) and the training
+    """The stage-0 fused unit (qkv Linear -> window attention -> proj Linear, all three in one
+    kernel, msu_win_attn_qkv_fwd2 = attn_qkv_fwd_mfma<PROJ>) at the bench shape: inference (no qkv / o written) and the training
     forward (qkv and o kept for the backward, dropout keep bits), HIP events on the launching
     stream.  Algorithmic FLOP per launch = 2 M C 3C (qkv) + 4 49^2 32 per window x head (QK^T, PV
     over the padded window grid) + 2 M C C (proj); bytes = x in + y out (+ qkv and o kept in
@@ -258,8 +257,7 @@ def fused_unit_roofline(device, batch, img, C, heads, p_drop):
 
     nwin = batch * ((res + 6) // 7) ** 2
     flops = 2.0 * M * C * 3 * C + 4.0 * 49 * 49 * 32 * nwin * heads + 2.0 * M * C * C
-    kern = ("attn_qkv_hs_mfma (qkv Linear + window attention) + proj GEMM" if ops._ATTN_QKV_MODE == "hs" else
-            "attn_qkv_fwd_mfma<PROJ> (qkv Linear + window attention + proj, one kernel)")
+    kern = "attn_qkv_fwd_mfma<PROJ> (qkv Linear + window attention + proj, one kernel)"
     out = {"kernel": kern,
            "flops_per_launch": flops}
     for name, store, byts in (("inference", False, 2 * M * C * 2), ("training_fwd", True, (2 * C + 3 * C + C) * M * 2)):
@@ -575,7 +573,7 @@ def main():
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     device = torch.device("cuda", local)
 
-    from semantic_segmentation_of_stylegan2_artifacts_amd import load_config
+    from semantic_segmentation_of_stylegan2_artifacts_amd import load_config, switches
     from semantic_segmentation_of_stylegan2_artifacts_amd.network import MSUNet
     from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import Trainer
     from semantic_segmentation_of_stylegan2_artifacts_amd.data import batch_pool
@@ -639,7 +637,10 @@ def main():
                        "dead_branches": "skipped" if args.skip_dead else "executed (no grad)",
                        "step_execution": "hip_graph_replay" if trainer._graph is not None else "eager",
                        "graph_probe": getattr(trainer, "graph_probe", None),
-                       "params": trainer.num_params(), "final_loss": round(loss_val, 6)},
+                       "params": trainer.num_params(), "final_loss": round(loss_val, 6),
+                       # environment switches away from their defaults (+ unknown MSU_* names):
+                       # empty for the product configuration (switches.py)
+                       "switches": switches.report()},
         }
         if not args.no_roofline:
             res["roofline"] = conv_roofline(device, args.batch, args.img, cfg.MODEL.SWIN.EMBED_DIM)

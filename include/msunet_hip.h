@@ -50,10 +50,6 @@ int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const 
                       int nparts, float* dgamma, float* dbeta, long rows, int C, int H, int W,
                       int Cin, int accumulate, void* stream);
 int msu_ln_part_blocks(long rows, int C);
-/* dgamma == null in msu_layernorm_bwd: only the backward kernel (dx, partials); this reduces the
- * partials into dgamma / dbeta afterwards, on any stream ordered after it. */
-int msu_ln_param_reduce(const float* part, int nparts, int C, float* dgamma, float* dbeta, int accumulate,
-                        void* stream);
 int msu_reduce_rows(const float* part, int nparts, int n, long stride, float* out,
                     int accumulate, void* stream);
 
@@ -150,12 +146,6 @@ int msu_win_attn_qkv_fwd2(int dtype, const void* x, const void* w_qkv, const flo
                           const void* w_proj, const float* b_proj, void* out, void* o_out, void* qkv_out, void* keep,
                           float* workspace, int B, int H, int W, int C, int nh, int shift, float p_drop,
                           unsigned long long seed, const unsigned long long* seed_dev, void* stream);
-/* msu_win_attn_qkv_fwd's contract, head-stationary kernel (one wave per (window, head) item, the
- * head's W_qkv rows resident in LDS); opt-in (MSU_ATTN_QKV=hs) form of ops.window_attention_qkv. */
-int msu_win_attn_qkv_hs_fwd(int dtype, const void* x, const void* w_qkv, const float* b_qkv, const float* table,
-                            void* out, void* qkv_out, void* keep, float* workspace, int B, int H, int W, int C, int nh,
-                            int shift, float p_drop, unsigned long long seed, const unsigned long long* seed_dev,
-                            void* stream);
 
 /* ---------------------------------------------------------------- Linear weight gradient
  * Every nn.Linear on the path (torchvision block qkv / proj / mlp.0 / mlp.3,

@@ -5,10 +5,12 @@ There is no CPU fallback: if the library is missing or fails to load, every op r
 import ctypes
 import os
 
+from . import switches
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # MSU_LIB_OVERRIDE: an alternative build of the same library (kernel ablation builds made by
 # tools/build_exp.sh); the product path never sets it
-LIB_PATH = os.environ.get("MSU_LIB_OVERRIDE") or os.path.join(_HERE, "libmsunet_hip.so")
+LIB_PATH = switches.get("MSU_LIB_OVERRIDE") or os.path.join(_HERE, "libmsunet_hip.so")
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -36,8 +38,6 @@ SIGNATURES = {
     "msu_win_attn_qkv_supported": (I, [I, I]),
     "msu_win_attn_qkv_fwd": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P]),
     "msu_win_attn_qkv_fwd2": (I, [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P]),
-    "msu_ln_param_reduce": (I, [P, I, I, P, P, I, P]),
-    "msu_win_attn_qkv_hs_fwd": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P]),
     "msu_gelu_fwd": (I, [I, P, P, L, P]),
     "msu_gelu_bwd": (I, [I, P, P, P, L, P]),
     "msu_residual": (I, [I, P, P, P, P, L, L, P]),

@@ -232,25 +232,10 @@ MSU_DEV int xcd_remap(int b, int nb) {
 // wave-uniform); counted by vmcnt like any global load.
 typedef __attribute__((address_space(3))) void msu_lds_void;
 typedef __attribute__((address_space(1))) void msu_glb_void;
-// MSU_GLDS_ASM (experiment): issue it as inline asm.  While a builtin LDS-DMA is in flight
-// hipcc waits lgkmcnt(0) before every compiler-visible ds_read (it cannot order them against
-// the DMA's LDS write), so no LDS read overlaps the MFMAs before it; the asm form is invisible to
-// hipcc's counters and gets counted lgkmcnt(N) waits instead (every consumer of DMA'd data
-// waits by hand: wait_vmcnt<N> + raw barrier; __syncthreads() would NOT drain it).  Measured
-// neutral at two waves per SIMD (r04l: NT / conv launches within +-3 %, bench 168.6 / 168.6 vs
-// 168.2 / 169.0 img/s): the partner wave already hides those waits.
+// (Issuing it as inline asm, invisible to hipcc's lgkmcnt tracking, measured neutral at two
+// waves per SIMD: r04l, not kept.)
 MSU_DEV void glds16(const void* src, void* lds_base) {
-#ifndef MSU_GLDS_ASM
   __builtin_amdgcn_global_load_lds((msu_glb_void*)src, (msu_lds_void*)lds_base, 16, 0, 0);
-#else
-  const uint32_t dst = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)(lds_base));
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(dst)
-               : "memory");
-#endif
 }
 // s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0], expcnt[6:4], lgkmcnt[11:8], vmcnt_hi[15:14])
 template <int N> MSU_DEV void wait_vmcnt() {

@@ -35,7 +35,6 @@ struct ConvGeom {
   int PS;          // LDS pixel stride (elements) of the input image
   int PSW;         // LDS row stride of the weight tile (fwd/dgrad)
   int PSD;         // LDS pixel stride of the dY tile (wgrad)
-  int prio;        // v3: waves 4-7 (the second wave of each SIMD) at s_setprio 1 (A/B MSU_CONV_PRIO)
 };
 
 // element offset of channel 0 of pixel (b, y, x) of the logical [B,H,W,C] image
@@ -648,10 +647,6 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
 
   int tile = blockIdx.x;
   if (tile >= ntiles) return;
-  // the second-dispatched wave of each SIMD (waves w and w + 4 share one) loses every issue
-  // arbitration by age; static priority lets it keep pace, so fewer waves idle at the per-tap
-  // barrier (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if (g.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   load_halo(tile, IC<0>{}, IC<NHC>{});
   store_halo();
   dma_w(0, 0);
@@ -955,273 +950,6 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
       // the next tile's halo (stored after tap 8) visible to every wave before its tap 0
       __syncthreads();
     }
-  }
-}
-
-// ------------------------------------------------------------------ 16-bit fwd, v4 (C = 96)
-// v3 with one wave per SIMD: 4 waves x 4 output rows.  v3's 8 waves read 5 fragments per 6
-// MFMAs (every weight fragment is read by all 8 waves), which at the MFMA rate is ~80 % of the
-// LDS read bandwidth, and its two waves per SIMD reach every per-tap barrier in lockstep.  Here
-// each X fragment feeds 3 MFMAs and each weight fragment 4: 7 reads per 12 MFMAs (0.58 per
-// MFMA), half the LDS read traffic per output, and a wave owns its SIMD's matrix pipe (up to
-// 512 registers: 192 accumulators + the next tile's halo in 116 + fragments).  Same tile
-// (16 rows x 32 pixels x 96 channels), halo / weight images, swizzle and epilogue as v3; the
-// GELU' operands (dgrad) are loaded at tap 8.
-constexpr int V4_SPRE = 24;  // GELU' operand loads per lane (4 rows x 3 co tiles x 2)
-
-template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-conv3x3_v4_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt, const float* __restrict__ bias,
-                  const bf16_t* __restrict__ S, bf16_t* __restrict__ Y, bf16_t* __restrict__ Y2, ConvGeom g,
-                  int ntiles) {
-  constexpr int C = 96, CH = 12, NW = 4, MT = 4, TH = NW * MT, TWV = 32, HWD = TWV + 2;
-  constexpr int HPIX = (TH + 2) * HWD;  // 612 halo pixels
-  (void)HPIX;
-  constexpr int NTHR = 64 * NW;
-  constexpr int PSTEP = NTHR / CH;                // halo pixels per staging round (one channel
-                                                  // chunk per thread: thread t stages chunk t % 12)
-  constexpr int NHC = (HPIX + PSTEP - 1) / PSTEP;  // staging rounds
-  constexpr int WIMG = C * C;
-  constexpr int WINS = WIMG * 2 / 1024;         // 18 DMA wave-instructions per tap
-  constexpr int WPER = (WINS + NW - 1) / NW;    // <= 5 per wave
-  static_assert(WINS * 1024 == WIMG * 2, "weight image in whole DMA instructions");
-
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  bf16_t* sX = reinterpret_cast<bf16_t*>(smem_raw);
-  bf16_t* sW = sX + HPIX * C;  // [2][96][96]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles_x = (g.W + TWV - 1) / TWV, tiles_y = (g.H + TH - 1) / TH;
-  const int per_img = tiles_x * tiles_y;
-
-  auto coords = [&](int tile, int& b, int& y0, int& x0) {
-    b = tile / per_img;
-    const int r = tile - b * per_img;
-    y0 = (r / tiles_x) * TH;
-    x0 = (r - (r / tiles_x) * tiles_x) * TWV;
-  };
-  u32x4 hr[NHC];
-  // Halo staging: thread t < 12 * PSTEP owns channel chunk t % 12 of pixels t / 12 + PSTEP * c
-  // (c = 0 .. NHC-1); the pixel's (row, col) advance incrementally, so a chunk costs a few adds
-  // and one address multiply instead of the divisions of a flat chunk index
-  // rounds [c0, c1) of this thread's share of tile `tile`'s halo -> registers
-  auto load_halo = [&](int tile, auto C0, auto C1) {
-    constexpr int c0 = decltype(C0)::value, c1 = decltype(C1)::value;
-    int b, y0, x0;
-    coords(tile, b, y0, x0);
-    const int t = opaque(tid);  // recomputed per call: nothing pinned across the tile loop
-    const bool hact = t < PSTEP * CH;
-    int p = t / CH + PSTEP * c0;
-    int row = p / HWD, col = p - (p / HWD) * HWD;
-    const bf16_t* xc = X + (t % CH) * 8;
-#pragma unroll
-    for (int c = c0; c < c1; ++c) {
-      const int y = y0 - 1 + row, x = x0 - 1 + col;
-      const bool ok = hact && p < HPIX && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
-      // out-of-image chunks read the zero region: no select on the loaded value, so the load
-      // stays in flight until the halo is stored (address select, no branch)
-      const bf16_t* src = ok ? xc + pix_off32<IN_D2S>(b, y, x, g.H, g.W, C)
-                             : reinterpret_cast<const bf16_t*>(zero_src(tid));
-      hr[c] = *reinterpret_cast<const u32x4*>(src);
-      p += PSTEP;
-      col += PSTEP % HWD;
-      row += PSTEP / HWD;
-      if (col >= HWD) {
-        col -= HWD;
-        ++row;
-      }
-    }
-  };
-  auto store_halo = [&]() {
-    const int t = opaque(tid);
-    const bool hact = t < PSTEP * CH;
-    const int hch = t % CH;
-    int p = t / CH;
-#pragma unroll
-    for (int c = 0; c < NHC; ++c) {
-      if (hact && p < HPIX) *reinterpret_cast<u32x4*>(sX + p * C + ((hch ^ swz(p)) << 3)) = hr[c];
-      p += PSTEP;
-    }
-  };
-  // this wave's share of the DMA of tap `tap`'s weight image into buffer `buf`
-  auto dma_w = [&](int tap, int buf) {
-    const bf16_t* src = Wt + (long)tap * WIMG;
-    bf16_t* dst = sW + buf * WIMG;
-    // piece r of this wave is slot q = 64 (wave + NW r) + lane: row q / 12, chunk q % 12,
-    // advanced incrementally from r = 0 (one division per call)
-    const int q0 = 64 * wave + opaque(lane);
-    int row = q0 / CH, pos = q0 - (q0 / CH) * CH;
-#pragma unroll
-    for (int r = 0; r < WPER; ++r) {
-      const int k = wave + NW * r;
-      if (WINS % NW == 0 || k < WINS) glds16(src + row * C + ((pos ^ swz(row)) << 3), dst + 512 * k);
-      pos += (64 * NW) % CH;
-      row += (64 * NW) / CH;
-      if (pos >= CH) {
-        pos -= CH;
-        ++row;
-      }
-    }
-  };
-
-  int tile = blockIdx.x;
-  if (tile >= ntiles) return;
-  load_halo(tile, IC<0>{}, IC<NHC>{});
-  store_halo();
-  dma_w(0, 0);
-  __syncthreads();
-  int wbuf = 0;
-
-  const int xl = lane & 31, h = lane >> 5;
-  auto koff = [&](int sw, int odd) { return ((2 * odd + h) ^ sw) << 3; };
-  const int wsw = swz(xl);
-  const int wk0 = xl * C + koff(wsw, 0), wk1 = xl * C + koff(wsw, 1);
-
-  for (; tile < ntiles; tile += gridDim.x) {
-    const int next = tile + gridDim.x;
-    int b, y0, x0;
-    coords(tile, b, y0, x0);
-    const int xo = x0 + xl;
-    f32x16 acc[MT][3];
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int n = 0; n < 3; ++n) acc[m][n] = f32x16{0};
-    u32x4 sp[OUT_GGRAD ? MT : 1][OUT_GGRAD ? 3 : 1][2];
-
-    static_for([&](auto TAP) {
-      constexpr int tap = decltype(TAP)::value;
-      constexpr int dy = tap / 3, dx = tap % 3;
-      // W(tap) landed: this wave's DMAs (issued at tap - 1, before that tap's halo part and,
-      // at tap 8, the GELU' operands, which may stay in flight), then every wave's (barrier)
-      constexpr int hprev = tap >= 2 ? halo_part_lo(tap, NHC) - halo_part_lo(tap - 1, NHC) : 0;
-      constexpr int sprev = (OUT_GGRAD && tap == 8) ? V4_SPRE : 0;
-      if constexpr (hprev > 0) {
-        if (next < ntiles) wait_vmcnt<hprev + sprev>();
-        else wait_vmcnt<sprev>();
-      } else {
-        wait_vmcnt<sprev>();
-      }
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      const bf16_t* wcur = sW + wbuf * WIMG;
-      if constexpr (tap < 8) {
-        dma_w(tap + 1, wbuf ^ 1);
-      } else {
-        if (next < ntiles) dma_w(0, wbuf ^ 1);
-      }
-      if constexpr (tap >= 1 && tap <= 7) {
-        if (next < ntiles) load_halo(next, IC<halo_part_lo(tap, NHC)>{}, IC<halo_part_lo(tap + 1, NHC)>{});
-      }
-      if constexpr (OUT_GGRAD && tap == 7) {
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          const int y = min(y0 + MT * wave + m, g.H - 1), xs = min(xo, g.W - 1);
-#pragma unroll
-          for (int n = 0; n < 3; ++n)
-#pragma unroll
-            for (int pp = 0; pp < 2; ++pp)
-              sp[m][n][pp] = *reinterpret_cast<const u32x4*>(S + pix_off32<OUT_D2S>(b, y, xs, g.H, g.W, C) + 32 * n +
-                                                             16 * pp + 8 * h);
-        }
-      }
-      int xo0[MT], xo1[MT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const int p = opaque((MT * wave + m + dy) * HWD + dx) + xl;
-        xo0[m] = p * C + koff(swz(p), 0);
-        xo1[m] = p * C + koff(swz(p), 1);
-      }
-      bf16x8 xa[2][MT], wf[3];
-      auto read_x = [&](auto KSI, int set) __attribute__((always_inline)) {
-        constexpr int ks = decltype(KSI)::value;
-        constexpr int kb = 32 * (ks >> 1);
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-          xa[set][m] = *reinterpret_cast<const bf16x8*>(sX + ((ks & 1) ? xo1[m] : xo0[m]) + kb);
-      };
-      auto read_w = [&](auto KSI, int n) __attribute__((always_inline)) -> bf16x8 {
-        constexpr int ks = decltype(KSI)::value;
-        constexpr int kb = 32 * (ks >> 1);
-        return *reinterpret_cast<const bf16x8*>(wcur + 32 * n * C + ((ks & 1) ? wk1 : wk0) + kb);
-      };
-      read_x(IC<0>{}, 0);
-      wf[0] = read_w(IC<0>{}, 0);
-      wf[1] = read_w(IC<0>{}, 1);
-      static_for([&](auto KSI) {
-        constexpr int ks = decltype(KSI)::value;
-        constexpr int cur = ks & 1;
-        if constexpr (ks + 1 < 6) read_x(IC<ks + 1>{}, cur ^ 1);
-        static_for([&](auto NI) {
-          constexpr int n = decltype(NI)::value;
-          constexpr int jn = 3 * ks + n + 2;  // ring of three, as v3
-          if constexpr (jn < 18) wf[jn % 3] = read_w(IC<jn / 3>{}, jn % 3);
-#pragma unroll
-          for (int m = 0; m < MT; ++m) acc[m][n] = Fmt16<T>::mma32(wf[n], xa[cur][m], acc[m][n]);
-        }, std::make_integer_sequence<int, 3>{});
-        __builtin_amdgcn_sched_barrier(0);
-      }, std::make_integer_sequence<int, 6>{});
-      if constexpr (tap == 8) {
-        if (next < ntiles) {
-          __syncthreads();
-          store_halo();
-        }
-      }
-      wbuf ^= 1;
-    }, std::make_integer_sequence<int, 9>{});
-
-    float4 bq[3][2][2];
-    if constexpr (BIAS) {
-#pragma unroll
-      for (int n = 0; n < 3; ++n)
-#pragma unroll
-        for (int pp = 0; pp < 2; ++pp) {
-          const int co = 32 * n + 16 * pp + 8 * h;
-          bq[n][pp][0] = *reinterpret_cast<const float4*>(bias + co);
-          bq[n][pp][1] = *reinterpret_cast<const float4*>(bias + co + 4);
-        }
-    }
-    if constexpr (BIAS || OUT_GGRAD) wait_vmcnt<0>();
-    if (xo < g.W) {
-#pragma unroll
-      for (int n = 0; n < 3; ++n)
-#pragma unroll
-        for (int pp = 0; pp < 2; ++pp) {
-          float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-          if constexpr (BIAS) {
-            const float4 t0 = bq[n][pp][0], t1 = bq[n][pp][1];
-            bv[0] = t0.x; bv[1] = t0.y; bv[2] = t0.z; bv[3] = t0.w;
-            bv[4] = t1.x; bv[5] = t1.y; bv[6] = t1.z; bv[7] = t1.w;
-          }
-          const int co = 32 * n + 16 * pp + 8 * h;
-#pragma unroll
-          for (int m = 0; m < MT; ++m) {
-            const int y = y0 + MT * wave + m;
-            float v[8];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[m][n][8 * pp + i]),
-                                                              __float_as_uint(acc[m][n][8 * pp + 4 + i]), false, false);
-              v[i] = __uint_as_float(r[0]) + bv[i];
-              v[4 + i] = __uint_as_float(r[1]) + bv[4 + i];
-            }
-            if (y >= g.H) continue;
-            if constexpr (OUT_GGRAD) {
-              const u32x4 t = sp[m][n][pp];
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                v[2 * i] *= gelu_grad_fast(Fmt16<T>::lo(t[i]));
-                v[2 * i + 1] *= gelu_grad_fast(Fmt16<T>::hi(t[i]));
-              }
-            }
-            const u32x4 pk = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
-            const int off = pix_off32<OUT_D2S>(b, y, xo, g.H, g.W, C) + co;
-            *reinterpret_cast<u32x4*>(Y + off) = pk;
-            if constexpr (DUAL) *reinterpret_cast<u32x4*>(Y2 + off) = gelu8<T>(pk);
-          }
-        }
-    }
-    if (next < ntiles) __syncthreads();
   }
 }
 
@@ -1535,7 +1263,6 @@ ConvGeom make_geom(int B, int H, int W, int Cin, int Cout, int elem_bytes) {
   g.PS = g.CinP + pad;
   g.PSW = g.CinP + pad;
   g.PSD = Cout + pad;
-  g.prio = 0;
   return g;
 }
 
@@ -1592,24 +1319,6 @@ int launch_v2(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float*
   return MSU_CHECK_LAUNCH();
 }
 
-// v3 forward (A/B switch MSU_CONV_V=2: every launch on v2)
-inline bool conv_v3_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("MSU_CONV_V");
-    return !(e && e[0] == '2');
-  }();
-  return on;
-}
-
-// halo load schedule of v3 (A/B switch MSU_CONV_HALO=1: the whole halo at tap 1)
-inline bool conv_v3_spread() {
-  static const bool on = [] {
-    const char* e = getenv("MSU_CONV_HALO");
-    return !(e && e[0] == '1');
-  }();
-  return on;
-}
-
 template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL, bool SPREAD, bool M16>
 int launch_v3s(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S, bf16_t* Y,
                bf16_t* Y2, hipStream_t st) {
@@ -1625,66 +1334,23 @@ int launch_v3s(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float
   if (ntiles == 0) return 0;
   if ((long)g.B * g.H * g.W * 96 >= (1L << 31)) return -2;
   const int grid = (int)(ntiles < num_cus() ? ntiles : num_cus());
-  static const int prio = getenv("MSU_CONV_PRIO") ? atoi(getenv("MSU_CONV_PRIO")) : 0;
-  ConvGeom gp = g;
-  gp.prio = prio;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, X, Wt, bias, S, Y, Y2, gp, (int)ntiles);
-  return MSU_CHECK_LAUNCH();
-}
-
-// v3 on 16x16x32 MFMA (same tile, LDS images and schedule; (p >> 1) & 3 swizzle), the default
-// for the forward launches since round 4: same-box kbench (r04b) conv1 2.22-2.28 vs 2.44 ms, conv2
-// 1.48 vs 1.55 ms (bare MFMA loops of this shape run at ~1.12-1.15x the FLOP/s of 32x32x16 on
-// MI355X at equal cycles: the clock it holds, MI355X_MICROARCH.md).  A/B switch MSU_CONV_MFMA=32.
-inline bool conv_v3_m16() {
-  static const bool on = [] {
-    const char* e = getenv("MSU_CONV_MFMA");
-    return !(e && e[0] == '3' && e[1] == '2');
-  }();
-  return on;
-}
-
-// v4 (one wave per SIMD, 4 rows per wave): opt-in A/B switch MSU_CONV_V=4 (measured 7-10 %
-// slower than v3 on every launch: DESIGN.md section 7, round 3)
-inline int conv_v4_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("MSU_CONV_V");
-    return e && e[0] == '4';
-  }();
-  return on;
-}
-
-template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL>
-int launch_v4(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S, bf16_t* Y,
-              bf16_t* Y2, hipStream_t st) {
-  constexpr size_t lds = sizeof(bf16_t) * ((size_t)18 * 34 * 96 + 2 * 96 * 96);
-  static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = conv3x3_v4_kernel<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
-  const long ntiles = (long)g.B * ((g.W + 31) / 32) * ((g.H + 15) / 16);
-  if (ntiles == 0) return 0;
-  if ((long)g.B * g.H * g.W * 96 >= (1L << 31)) return -2;
-  const int grid = (int)(ntiles < num_cus() ? ntiles : num_cus());
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, X, Wt, bias, S, Y, Y2, g, (int)ntiles);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, X, Wt, bias, S, Y, Y2, g, (int)ntiles);
   return MSU_CHECK_LAUNCH();
 }
 
 template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL>
 int launch_v3(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S, bf16_t* Y,
               bf16_t* Y2, hipStream_t st) {
-  if (conv_v4_enabled()) return launch_v4<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL>(g, X, Wt, bias, S, Y, Y2, st);
-  // (forward launches only: with the dgrad's GELU' operands held from tap 7 the 16x16 form
-  // spills 260 B per lane)
+  // Forward launches on 16x16x32 MFMA (same tile, LDS images and schedule; (p >> 1) & 3
+  // swizzle), since round 4: same-box kbench (r04b) conv1 2.22-2.28 vs 2.44 ms, conv2 1.48 vs
+  // 1.55 ms (bare MFMA loops of this shape run at ~1.12-1.15x the FLOP/s of 32x32x16 on MI355X at
+  // equal cycles: the clock it holds, MI355X_MICROARCH.md).  The dgrad keeps 32x32x16: with its
+  // GELU' operands held from tap 7 the 16x16 form spills 260 B per lane.  Halo loads spread over
+  // taps 1..7 (SPREAD; all at tap 1 measured equal, r03).  v4 (one wave per SIMD, 4 rows per
+  // wave) was 7-10 % slower on every launch (r03l/m) and is gone.
   if constexpr (!OUT_GGRAD)
-    if (conv_v3_m16())
-      return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, true, true>(g, X, Wt, bias, S, Y, Y2, st);
-  if (conv_v3_spread())
-    return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, true, false>(g, X, Wt, bias, S, Y, Y2, st);
-  return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, false, false>(g, X, Wt, bias, S, Y, Y2, st);
+    return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, true, true>(g, X, Wt, bias, S, Y, Y2, st);
+  return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, true, false>(g, X, Wt, bias, S, Y, Y2, st);
 }
 
 template <typename T, bool IN_D2S, bool IN_GELU, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL = false>
@@ -1692,7 +1358,7 @@ int conv_nt(const ConvGeom& g, const void* X, const void* Wt, const float* bias,
             void* Y, void* Y2, hipStream_t st) {
   const T* x = (const T*)X; const T* w = (const T*)Wt; const T* s = (const T*)S; T* y = (T*)Y; T* y2 = (T*)Y2;
   if constexpr (sizeof(T) == 2 && !IN_GELU) {
-    if (g.Cout == 96 && g.CinP == 96 && g.Cin == 96 && conv_v3_enabled())
+    if (g.Cout == 96 && g.CinP == 96 && g.Cin == 96)
       return launch_v3<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL>(g, (const bf16_t*)x, (const bf16_t*)w, bias,
                                                                   (const bf16_t*)s, (bf16_t*)y, (bf16_t*)y2, st);
   }

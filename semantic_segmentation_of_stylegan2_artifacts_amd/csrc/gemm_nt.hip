@@ -42,7 +42,6 @@ struct NtArgs {
   const bf16_t* H;     // [M][N] (GELU_GRAD: pre-activation)
   int M, N, K, K1;
   int tiles_m, tiles_n;
-  int prio;            // waves WM.. (the second wave of each SIMD) at s_setprio 1 (A/B MSU_NT_PRIO)
 };
 
 // A ROWS x KB operand tile (K-contiguous rows, KB = 64 or 32) staged by NTHR threads.  A 256-B
@@ -134,24 +133,8 @@ struct KnTile {
 // accumulators).  192 makes the N = 384 / 768 / 1152 / 2304 shapes of Swin-T's stages 2-3 whole
 // rounds of tiles on 256 CUs (N = 384 at M = 32768: 256 tiles of 256 x 192 instead of 384 of
 // 256 x 128, i.e. 1.5 rounds); KN (input-gradient) form: 128 only.
-// four-stage ring: wait until at most `younger` later steps' DMAs (D per step) and, if `stores`,
-// one epilogue's E stores are outstanding
-template <int D, int E>
-MSU_DEV void wait_ring4(int younger, bool stores) {
-  if (younger == 2) {
-    if (stores) wait_vmcnt<2 * D + E>();
-    else wait_vmcnt<2 * D>();
-  } else if (younger == 1) {
-    if (stores) wait_vmcnt<D + E>();
-    else wait_vmcnt<D>();
-  } else {
-    if (stores) wait_vmcnt<E>();
-    else wait_vmcnt<0>();
-  }
-}
-
-// KB: K step, 64 (two- or three-stage ring) or 32 (four-stage ring: the same LDS holds three
-// steps in flight instead of one or two).
+// KB: K step (64).  A 32-deep step with a four-stage ring (three steps in flight in the same LDS)
+// was 25-50 % slower on every stage 1-3 shape (r04u) and is gone.
 template <typename T, int EPI, int WM, int NST, bool WKN, int BNT, int KB>
 __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   constexpr int NTHR = 128 * WM, BM = 64 * WM, NI = BNT / 64;
@@ -167,7 +150,7 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   static_assert(TA::FULLW * 64 == NTHR, "A rows: whole rounds");
   constexpr int DW0 = WKN ? 64 : TW::FULLW;
   constexpr int E = (EPI == EPI_GELU_DUAL ? 8 : 4) * NI;
-  static_assert(NST >= 2 && NST <= 4, "ring depth");
+  static_assert(NST >= 2 && NST <= 3, "ring depth");
   static_assert(NST == 2 || ((NST - 2) * D + E < 64), "vmcnt range");
   __shared__ __attribute__((aligned(16))) bf16_t lds[NST * STG];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -178,7 +161,6 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   const int ntiles = a.tiles_m * a.tiles_n;
   const int nk = a.K / KB;  // K % 64 == 0 (nt_shape_ok)
   const int mine = L < ntiles ? (ntiles - 1 - L) / G + 1 : 0;
-  if (WM == 4 && a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int nsteps = mine * nk;
 
   // K step s of this workgroup's sequence -> LDS stage `st`
@@ -225,14 +207,6 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
       else if (younger) wait_vmcnt<D>();
       else if (stores) wait_vmcnt<E>();
       else wait_vmcnt<0>();
-    } else {
-      // steps s + 1, s + 2 (those that exist) and the stores of an epilogue in iterations s - 3
-      // .. s - 1 were issued after step s's DMA; a wave's DMA count per step is D or D - 1
-      const int younger = nsteps - 1 - s < 2 ? nsteps - 1 - s : 2;
-      const bool stores = epi_age <= 2 && epi_full;
-      if (nk < 4) wait_vmcnt<0>();
-      else if (wave < DW0) wait_ring4<D, E>(younger, stores);
-      else wait_ring4<D - 1, E>(younger, stores);
     }
     __builtin_amdgcn_s_barrier();   // every wave's DMA of step s has landed, and every wave is
     asm volatile("" ::: "memory");  // done reading step s-1's stage (refilled below)
@@ -285,12 +259,10 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     for (int ks = 0; ks < KSL; ++ks) {
       const int cur = ks & 1;
       if (ks + 1 < KSL) rd(ks + 1, cur ^ 1);
-#ifndef MSU_NT_NOSB
       // all of slice ks + 1's fragment reads go out before slice ks's MFMAs (the wait before
       // those is then lgkmcnt(reads of ks + 1)); left alone, the scheduler sank some reads
       // between the MFMAs into registers freed by them and waited lgkmcnt(0) two MFMAs later
       __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
         acc[ni][0] = Fmt16<T>::mma32(fw[cur][ni], fx[cur][0], acc[ni][0]);
@@ -392,30 +364,19 @@ int num_cus_nt() {
 //   wm 2, bn 128: 128 x 128, two-stage ring, two workgroups per CU;
 //   wm 4, bn 192: 256 x 192, two-stage ring (3 x 56 KB does not fit), one workgroup per CU;
 //   wm 2, bn 192: 128 x 192, two-stage ring, two workgroups per CU (2 x 80 KB of LDS).
-// KN (input-gradient with the forward weight in place) keeps bn 128.  A/B switches:
-// MSU_NT_TILE = 128 | 192 | 256 (rows; 192 only with 192 columns), MSU_NT_BN = 128 | 192 (columns).
+// KN (input-gradient with the forward weight in place) keeps bn 128.  (A 192 x 192 tile with a
+// three-stage ring, 6 waves, was slower on every shape, r04j: gone.)
 struct NtCfg {
-  int wm, bn, kb = 64;
+  int wm, bn;
 };
 
 NtCfg nt_cfg(long M, int N, bool wkn) {
-  static const int force_m = [] {
-    const char* e = getenv("MSU_NT_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  static const int force_n = [] {
-    const char* e = getenv("MSU_NT_BN");
-    return e ? atoi(e) : 0;
-  }();
   const long cus = num_cus_nt();
-  // {3, 192}: 192 x 192 tiles, 6 waves, three-stage ring (144 KB) -- opt-in (MSU_NT_TILE=192)
-  const NtCfg cands[5] = {{4, 128}, {2, 128}, {4, 192}, {2, 192}, {3, 192}};
+  const NtCfg cands[4] = {{4, 128}, {2, 128}, {4, 192}, {2, 192}};
   NtCfg best = cands[0];
   double best_cost = -1.0;
   for (const NtCfg& c : cands) {
     if (c.bn == 192 && (wkn || N % 192 != 0)) continue;
-    if (force_m ? force_m != 64 * c.wm : c.wm == 3) continue;
-    if (force_n && force_n != c.bn) continue;
     // rounds of resident tiles x the output area a CU computes per round (x 0.78 for the
     // 192-wide form).  A 128-row (two-per-CU) form with no more tiles than CUs has ONE tile per
     // CU, at a per-area cost of 1.57 (it shares the CU with nobody): r04h sweep, 8192 x 768 x
@@ -431,9 +392,6 @@ NtCfg nt_cfg(long M, int N, bool wkn) {
       best = c;
     }
   }
-  // MSU_NT_BK=32 (A/B switch): the 192-wide forms with 32-deep K steps and a four-stage ring
-  static const int force_kb = getenv("MSU_NT_BK") ? atoi(getenv("MSU_NT_BK")) : 64;
-  if (force_kb == 32 && best.bn == 192 && best.wm != 3) best.kb = 32;
   return best;
 }
 
@@ -470,20 +428,14 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
   a.M = (int)M;
   a.N = N;
   a.K = K;
-  static const int prio = getenv("MSU_NT_PRIO") ? atoi(getenv("MSU_NT_PRIO")) : 0;
-  a.prio = prio;
   const NtCfg cfg = nt_cfg(M, N, wkn);
   a.tiles_n = (N + cfg.bn - 1) / cfg.bn;
   a.tiles_m = (int)((M + 64 * cfg.wm - 1) / (64 * cfg.wm));
   if ((long)a.tiles_m * a.tiles_n >= (1L << 31)) return -2;
   hipStream_t st = (hipStream_t)stream;
   MSU_DISPATCH16(dtype, T,
-    if (cfg.bn == 192 && cfg.kb == 32) {
-      if (cfg.wm == 4) launch_nt<T, 4, 4, false, 192, 32>(epi, a, st);
-      else launch_nt<T, 2, 4, false, 192, 32>(epi, a, st);
-    } else if (cfg.bn == 192) {
+    if (cfg.bn == 192) {
       if (cfg.wm == 4) launch_nt<T, 4, 2, false, 192>(epi, a, st);
-      else if (cfg.wm == 3) launch_nt<T, 3, 3, false, 192>(epi, a, st);
       else launch_nt<T, 2, 2, false, 192>(epi, a, st);
     } else if (cfg.wm == 4) {
       if (wkn) launch_nt<T, 4, 3, true, 128>(epi, a, st);

@@ -17,29 +17,26 @@ TokPlan tok_plan(long M, int N, int K, int epi = EPI_PLAIN) {
   if (!p.kc) return p;
   static const int ncs[] = {384, 288, 256, 192, 128, 96, 64};
   int best[2] = {0, 0};
-  static const int max_nc = getenv("MSU_TOK_MAXNC") ? atoi(getenv("MSU_TOK_MAXNC")) : 1 << 20;  // A/B switch
   for (int i = 0; i < 2; ++i) {
     const int nst = 3 - i;
     for (int nc : ncs) {
       if (N % nc) continue;
       if (epi != EPI_PLAIN && nc > 192) continue;  // GELU epilogue registers
-      if (nc > max_nc) continue;
       if (plan_lds(p.kc, nc, nst, K) > LDS_MAX) continue;
       best[i] = nc;
       break;
     }
   }
-  static const int force_nst = getenv("MSU_TOK_NST") ? atoi(getenv("MSU_TOK_NST")) : 0;  // A/B switch
   int nst = 3;
-  if (force_nst == 2 || (force_nst != 3 && best[1] >= 2 * best[0])) nst = 2;
+  if (best[1] >= 2 * best[0]) nst = 2;
   p.nc = best[3 - nst];
   if (!p.nc) { nst = 2; p.nc = best[1]; }
   if (!p.nc) return p;
   p.nst = nst;
   p.lds = plan_lds(p.kc, p.nc, nst, K);
-  // eight waves with 2-deep rings when the W chunk leaves room (A/B switch: MSU_TOK_NW=4)
-  static const int force_nw = getenv("MSU_TOK_NW") ? atoi(getenv("MSU_TOK_NW")) : 0;
-  if (force_nw != 4 && plan_lds(p.kc, p.nc, 2, K, 8) <= LDS_MAX) {
+  // eight waves with 2-deep rings when the W chunk leaves room (8 vs 4 waves measured equal
+  // within noise on two boxes, r02c: kept)
+  if (plan_lds(p.kc, p.nc, 2, K, 8) <= LDS_MAX) {
     p.nst = 2;
     p.nw = 8;
     p.lds = plan_lds(p.kc, p.nc, 2, K, 8);

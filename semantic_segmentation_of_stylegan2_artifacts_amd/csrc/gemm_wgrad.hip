@@ -141,16 +141,15 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const T* __restrict__ dY, co
 // global_load_lds_dwordx4 (pad slots re-read chunk 0 of their row; rows past the block's
 // range read the spread zero region); a ring of NST stages keeps NST-1 in flight; raw
 // s_barrier + counted vmcnt keep the prefetch alive across barriers.
-// W8: a second row group of four waves (eight waves, two per SIMD, 64-row stages; the MFMA-bound
-// one-wave-per-SIMD form waited 37 % of its cycles on DMA / LDS latency with nothing to fill the
-// SIMD, r04i counters); the two groups' partial tiles are summed in LDS before the slab store.
-template <int WN, int WK, bool W8 = false> constexpr int wgrad_nw() { return W8 ? 8 : (WN * WK == 3 ? 3 : 4); }
+// (An eight-wave form, two row groups at two waves per SIMD, was 10-13 % faster alone but slower
+// in the step, where its LDS and waves crowd the input-gradient kernels it overlaps: r04m, gone.)
+template <int WN, int WK> constexpr int wgrad_nw() { return WN * WK == 3 ? 3 : 4; }
 
-template <typename T, int NTW, int WN, int WK, int NST, bool W8>
-__global__ void __launch_bounds__(W8 ? 512 : 256) wgrad_wave_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
+template <typename T, int NTW, int WN, int WK, int NST>
+__global__ void __launch_bounds__(256) wgrad_wave_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X,
                                                          float* __restrict__ part, float* __restrict__ dbpart,
-                                                         long M, int N, int K, long mchunk, int ntiles, int xcd) {
-  constexpr int NW = wgrad_nw<WN, WK, W8>();
+                                                         long M, int N, int K, long mchunk, int ntiles) {
+  constexpr int NW = wgrad_nw<WN, WK>();
   constexpr int WM = NW / (WN * WK), WT = 16 * NTW, BN = WN * WT, BK = WK * WT, RS = 32 * WM;
   static_assert(WM * WN * WK == NW, "wave split");
   constexpr int SA = (BN + 8) / 8, SB = (BK + 8) / 8;  // 16-B slots per row
@@ -166,12 +165,11 @@ __global__ void __launch_bounds__(W8 ? 512 : 256) wgrad_wave_kernel(const bf16_t
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wni = wave % WN, wki = (wave / WN) % WK, wmi = wave / (WN * WK);
   const int ntk = K / BK;
-  // 1-D grid of ntiles x splits work items.  xcd: consecutive items (the output tiles of one
-  // row split, which stream the same dY / X rows) go to one XCD (dispatch is round-robin over
-  // the 8 XCDs by block id), so the rows a split's tiles share are fetched from HBM once and
-  // re-read from that XCD's L2; otherwise item = block id (the tiles of a split spread over
-  // all XCDs and each XCD fetches the rows again)
-  const int item = xcd ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  // 1-D grid of ntiles x splits work items: consecutive items (the output tiles of one row
+  // split, which stream the same dY / X rows) go to one XCD (dispatch is round-robin over the 8
+  // XCDs by block id), so the rows a split's tiles share are fetched from HBM once and re-read
+  // from that XCD's L2 (r04c: 252 -> 109 MB read per 32768 x 1152 x 384 launch)
+  const int item = xcd_remap(blockIdx.x, gridDim.x);
   const int split = item / ntiles, tile = item - split * ntiles;
   const int tn = tile / ntk, tk = tile - (tile / ntk) * ntk;
   const int n0 = tn * BN, k0 = tk * BK;
@@ -349,35 +347,13 @@ __global__ void __launch_bounds__(W8 ? 512 : 256) wgrad_wave_kernel(const bf16_t
 // bf16 plan: wave tile, waves along N and K, ring depth, splits
 struct WavePlan {
   int ntw = 0, wn = 1, wk = 1, nst = 3, S = 1;
-  bool w8 = false;  // eight waves (two row groups), see wgrad_nw
   int slabs() const { return S; }
 };
 
 // the (WN, WK) split of a workgroup's waves over the N x K tiles: least operand traffic
-// M (N kt / WK + K nt / WN) (dY re-read per K group, X per N group), more waves on ties;
-// MSU_WGRAD_WK=0: the round-2 plan (waves along N only)
+// M (N kt / WK + K nt / WN) (dY re-read per K group, X per N group), more waves on ties
+// (round 3: +1.5 % over the round-2 plan of waves along N only)
 inline void pick_wave_split(int nt, int kt, int& wn, int& wk) {
-  static const bool k_split = !(getenv("MSU_WGRAD_WK") && getenv("MSU_WGRAD_WK")[0] == '0');
-  if (!k_split) {
-    wn = nt % 4 == 0 ? 4 : (nt % 2 == 0 ? 2 : 1);
-    wk = 1;
-    return;
-  }
-  // A/B switch MSU_WGRAD_SPLIT=WN,WK forces a split where the tile counts allow it
-  static const int forced = [] {
-    const char* e = getenv("MSU_WGRAD_SPLIT");
-    return e && e[0] >= '1' && e[0] <= '4' && e[1] == ',' && e[2] >= '1' && e[2] <= '4' ? (e[0] - '0') * 8 + (e[2] - '0')
-                                                                                          : 0;
-  }();
-  if (forced) {
-    const int fw = forced / 8, fk = forced % 8;
-    const bool instantiated = fw * fk <= 4 && (fw == 1 || fk == 1 || (fw == 2 && fk == 2));
-    if (instantiated && nt % fw == 0 && kt % fk == 0) {
-      wn = fw;
-      wk = fk;
-      return;
-    }
-  }
   static const int cand[8][2] = {{4, 1}, {2, 2}, {1, 4}, {3, 1}, {1, 3}, {2, 1}, {1, 2}, {1, 1}};
   long best = -1;
   for (const auto& c : cand) {
@@ -398,43 +374,25 @@ inline WavePlan wave_plan(long M, int N, int K) {
   else return p;  // not supported: generic kernel
   const int wt = 16 * p.ntw, nt = N / wt, kt = K / wt;
   pick_wave_split(nt, kt, p.wn, p.wk);
-  // ring depth that fits 160 KB for the four- or eight-wave form
-  auto ring = [&](bool w8, int& rs) {
-    const int nw = w8 ? 8 : (p.wn * p.wk == 3 ? 3 : 4);
-    const int wm = nw / (p.wn * p.wk);
-    rs = 32 * wm;
+  // ring depth that fits 160 KB, capped at 3 stages: the depth does not change the stage-0
+  // streaming rate (measured 3-6 flat, r04d), and the smaller LDS footprint (<= 96 KB) lets the
+  // kernel share CUs with the input-gradient kernels it overlaps on the side stream (+0.8 %)
+  const int nw = p.wn * p.wk == 3 ? 3 : 4;
+  const int rs = 32 * (nw / (p.wn * p.wk));
+  {
     const int sa = (p.wn * wt + 8) / 8, sb = (p.wk * wt + 8) / 8;
     const int ins = ((rs * (sa + sb) + 63) / 64 + nw - 1) / nw * nw;
-    int nst = (int)((160L * 1024) / ((long)ins * 64 * 16));
-    return nst > 6 ? 6 : nst;
-  };
-  // MSU_WGRAD_W8=1: the eight-wave form where it applies (opt-in).  Alone on the GPU it is
-  // 10-13 % faster (r04m: 50.4 vs 56.3 us at 32768 x 1152 x 384, 61 vs 69 at 32768 x 384 x
-  // 1536), but in the step -- on the side stream, beside the input-gradient kernels -- its
-  // 112 KB of LDS and eight waves per CU crowd them out: 167.1 / 167.3 vs 167.4 / 167.8 img/s
-  static const bool w8_on = getenv("MSU_WGRAD_W8") && getenv("MSU_WGRAD_W8")[0] == '1';
-  int rs = 32;
-  // (96-wide wave tiles only: the 128-wide ones spill at two waves per SIMD)
-  p.w8 = w8_on && p.ntw == 6 && p.wn * p.wk == 4 && ring(true, rs) >= 2;
-  if (p.w8) {
-    p.nst = 2;  // 2 x 56 KB (Swin-T/S widths): the second row group hides what the ring depth did
-  } else {
-    p.nst = ring(false, rs);
-    // 3 stages: the ring depth does not change the stage-0 streaming rate (measured), and the
-    // smaller LDS footprint (<= 96 KB) lets the kernel share CUs with the input-gradient
-    // kernels it overlaps on the side stream (+0.8 % per step).  MSU_WGRAD_NST: A/B switch.
-    static const int nst_cap = getenv("MSU_WGRAD_NST") ? atoi(getenv("MSU_WGRAD_NST")) : 3;
-    if (nst_cap >= 3 && p.nst > nst_cap) p.nst = nst_cap;
-    if (p.nst < 3) {  // ring too shallow: generic kernel
+    const int nst = (int)((160L * 1024) / ((long)ins * 64 * 16));
+    if (nst < 3) {  // ring too shallow: generic kernel
       p.ntw = 0;
       return p;
     }
+    p.nst = 3;
   }
   const long tiles = (long)(nt / p.wn) * (kt / p.wk);
-  // workgroup target: one per CU (no tail wave), long row ranges.  A/B switch
-  // MSU_WGRAD_TARGET_S23: the target for the stage 2-3 shapes (M <= 32768 at the bench)
-  static const long tgt23 = getenv("MSU_WGRAD_TARGET_S23") ? atol(getenv("MSU_WGRAD_TARGET_S23")) : 256;
-  long s = (M <= 32768 ? tgt23 : 256) / tiles;
+  // workgroup target: one per CU (no tail wave), long row ranges (128 / 512 measured no better
+  // for the stage 2-3 shapes, r03x)
+  long s = 256 / tiles;
   const long max_s = (M + 8 * rs - 1) / (8 * rs);  // at least 8 stages per split
   if (s > max_s) s = max_s;
   if (s < 1) s = 1;
@@ -442,49 +400,37 @@ inline WavePlan wave_plan(long M, int N, int K) {
   return p;
 }
 
-template <typename T, int NTW, int WN, int WK, int NST, bool W8 = false>
+template <typename T, int NTW, int WN, int WK, int NST>
 void launch_wave(dim3 grid, const bf16_t* dY, const bf16_t* X, float* part, float* dbpart, long M, int N, int K,
                  long mchunk, int ntiles, hipStream_t st) {
-  constexpr int NW = wgrad_nw<WN, WK, W8>();
+  constexpr int NW = wgrad_nw<WN, WK>();
   constexpr int WM = NW / (WN * WK), WT = 16 * NTW, RS = 32 * WM;
   constexpr int SLOTS = RS * ((WN * WT + 8) / 8 + (WK * WT + 8) / 8);
   constexpr int INS = ((SLOTS + 63) / 64 + NW - 1) / NW * NW;
   constexpr size_t lds = (size_t)NST * INS * 64 * 16;
   if constexpr (lds <= 160 * 1024) {  // ring depths the plan never picks are not instantiated
-    auto kern = wgrad_wave_kernel<T, NTW, WN, WK, NST, W8>;
+    auto kern = wgrad_wave_kernel<T, NTW, WN, WK, NST>;
     static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
-    static const int xcd = !(getenv("MSU_WGRAD_XCD") && getenv("MSU_WGRAD_XCD")[0] == '0');  // A/B switch
-    hipLaunchKernelGGL(kern, grid, dim3(64 * NW), lds, st, dY, X, part, dbpart, M, N, K, mchunk, ntiles, xcd);
+    hipLaunchKernelGGL(kern, grid, dim3(64 * NW), lds, st, dY, X, part, dbpart, M, N, K, mchunk, ntiles);
   }
 }
 
 template <typename T>
 int run_wave(const WavePlan& p, const bf16_t* dY, const bf16_t* X, float* part, float* dbpart, long M, int N, int K,
              hipStream_t st) {
-  const int wt = 16 * p.ntw, nw = p.w8 ? 8 : (p.wn * p.wk == 3 ? 3 : 4), wm = nw / (p.wn * p.wk), rs = 32 * wm;
+  const int wt = 16 * p.ntw, nw = p.wn * p.wk == 3 ? 3 : 4, wm = nw / (p.wn * p.wk), rs = 32 * wm;
   long mchunk = (M + p.S - 1) / p.S;
   mchunk = (mchunk + rs - 1) / rs * rs;
   const int ntiles = (N / (p.wn * wt)) * (K / (p.wk * wt));
   const dim3 grid((unsigned)(ntiles * p.S));
-#define MSU_WAVE8(NTW, WN, WK)                                                                                       \
-  if (p.w8 && p.ntw == NTW && p.wn == WN && p.wk == WK) {                                                           \
-    launch_wave<T, NTW, WN, WK, 2, true>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st);                  \
-    return 0;                                                                                                       \
-  }
-  MSU_WAVE8(6, 2, 2) MSU_WAVE8(6, 4, 1) MSU_WAVE8(6, 1, 4)
-#undef MSU_WAVE8
 #define MSU_WAVE(NTW, WN, WK)                                                                                        \
-  if (!p.w8 && p.ntw == NTW && p.wn == WN && p.wk == WK) {                                                          \
-    switch (p.nst) {                                                                                                \
-      case 3: launch_wave<T, NTW, WN, WK, 3>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st); return 0;     \
-      case 4: launch_wave<T, NTW, WN, WK, 4>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st); return 0;     \
-      case 5: launch_wave<T, NTW, WN, WK, 5>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st); return 0;     \
-      case 6: launch_wave<T, NTW, WN, WK, 6>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st); return 0;     \
-    }                                                                                                               \
+  if (p.ntw == NTW && p.wn == WN && p.wk == WK) {                                                                   \
+    launch_wave<T, NTW, WN, WK, 3>(grid, dY, X, part, dbpart, M, N, K, mchunk, ntiles, st);                         \
+    return 0;                                                                                                       \
   }
   MSU_WAVE(6, 1, 1) MSU_WAVE(6, 2, 1) MSU_WAVE(6, 4, 1) MSU_WAVE(6, 1, 2) MSU_WAVE(6, 2, 2) MSU_WAVE(6, 1, 4)
   MSU_WAVE(6, 3, 1) MSU_WAVE(6, 1, 3)
@@ -538,8 +484,7 @@ int msu_linear_wgrad_ld(int dtype, const void* dY, const void* X, float* dW, lon
     if (db && !accumulate) hipMemsetAsync(db, 0, sizeof(float) * N, st);
     return MSU_CHECK_LAUNCH();
   }
-  static const bool generic_only = getenv("MSU_WGRAD_GENERIC") != nullptr;  // A/B timing switch
-  if (msu_is16(dtype) && !generic_only) {
+  if (msu_is16(dtype)) {
     const WavePlan p = wave_plan(M, N, K);
     if (p.ntw) {
       float* part = workspace;

@@ -465,20 +465,13 @@ int launch_fwd(const LnArgs& a, hipStream_t st, int max_blocks) {
     hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), 0, st, a);
     return MSU_CHECK_LAUNCH();
   };
-  // rows of <= 16 chunks (C <= 128 bf16) read by 16 lanes each (one 16-B chunk per lane, whole
-  // rows per load instruction) instead of 4 lanes x 4 chunks: bench 153.5 vs 152.8 img/s
-  // and the same up to C <= 512 on 32 / 64 lanes: +0.25 % more (3 of 3 pairs).  A/B switch
-  // MSU_LN_WIDE: 0 = 4-lane rows, 1 = one chunk per lane up to C = 128 only)
-  static const int wide = getenv("MSU_LN_WIDE") ? atoi(getenv("MSU_LN_WIDE")) : 2;
-  static const bool pf = !(getenv("MSU_LN_FWD_PF") && getenv("MSU_LN_FWD_PF")[0] == '0');  // A/B switch
-  if (!pf) {
-    if (wide && nchunk <= 16) return go(ln_fwd_kernel<T, MODE, 16, 1, false>, 16);
-    if (wide >= 2 && nchunk <= 32) return go(ln_fwd_kernel<T, MODE, 32, 1, false>, 32);
-    if (wide >= 2 && nchunk <= 64) return go(ln_fwd_kernel<T, MODE, 64, 1, false>, 64);
-  }
-  if (wide && nchunk <= 16) return go(ln_fwd_kernel<T, MODE, 16, 1>, 16);
-  if (wide >= 2 && nchunk <= 32) return go(ln_fwd_kernel<T, MODE, 32, 1>, 32);
-  if (wide >= 2 && nchunk <= 64) return go(ln_fwd_kernel<T, MODE, 64, 1>, 64);
+  // rows of <= 64 chunks (C <= 512 bf16) read by 16 / 32 / 64 lanes (one 16-B chunk per lane,
+  // whole rows per load instruction) instead of 4 lanes x 4 chunks: bench 153.5 vs 152.8 img/s
+  // up to C = 128, +0.25 % more up to C = 512 (r01, 3 of 3 pairs); the next row of a group
+  // prefetched (r04y: +0.2 %)
+  if (nchunk <= 16) return go(ln_fwd_kernel<T, MODE, 16, 1>, 16);
+  if (nchunk <= 32) return go(ln_fwd_kernel<T, MODE, 32, 1>, 32);
+  if (nchunk <= 64) return go(ln_fwd_kernel<T, MODE, 64, 1>, 64);
   if (nchunk <= 4 * 4) return go(ln_fwd_kernel<T, MODE, 4, 4>, 4);
   if (nchunk <= 8 * 4) return go(ln_fwd_kernel<T, MODE, 8, 4>, 8);
   if (nchunk <= 16 * 4) return go(ln_fwd_kernel<T, MODE, 16, 4>, 16);
@@ -495,16 +488,10 @@ int launch_bwd(const LnBwdArgs& a, hipStream_t st, int nblocks) {
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(256), 0, st, a);
     return MSU_CHECK_LAUNCH();
   };
-  static const int wide = getenv("MSU_LN_WIDE") ? atoi(getenv("MSU_LN_WIDE")) : 2;  // see launch_fwd
-  static const bool pf = !(getenv("MSU_LN_BWD_PF") && getenv("MSU_LN_BWD_PF")[0] == '0');  // A/B switch
-  if (!pf) {
-    if (wide && nchunk <= 16) return go(ln_bwd_kernel<T, MODE, 16, 1, false>);
-    if (wide >= 2 && nchunk <= 32) return go(ln_bwd_kernel<T, MODE, 32, 1, false>);
-    if (wide >= 2 && nchunk <= 64) return go(ln_bwd_kernel<T, MODE, 64, 1, false>);
-  }
-  if (wide && nchunk <= 16) return go(ln_bwd_kernel<T, MODE, 16, 1>);
-  if (wide >= 2 && nchunk <= 32) return go(ln_bwd_kernel<T, MODE, 32, 1>);
-  if (wide >= 2 && nchunk <= 64) return go(ln_bwd_kernel<T, MODE, 64, 1>);
+  // one chunk per lane up to C = 512 (see launch_fwd), next row prefetched (r04x: +0.45 %)
+  if (nchunk <= 16) return go(ln_bwd_kernel<T, MODE, 16, 1>);
+  if (nchunk <= 32) return go(ln_bwd_kernel<T, MODE, 32, 1>);
+  if (nchunk <= 64) return go(ln_bwd_kernel<T, MODE, 64, 1>);
   if (nchunk <= 4 * 3) return go(ln_bwd_kernel<T, MODE, 4, 3>);  // C = 96 bf16: no idle slot
   if (nchunk <= 4 * 4) return go(ln_bwd_kernel<T, MODE, 4, 4>);
   if (nchunk <= 8 * 4) return go(ln_bwd_kernel<T, MODE, 8, 4>);
@@ -519,8 +506,8 @@ template <int MODE>
 int fwd_dispatch(int dtype, const LnArgs& a, hipStream_t st) {
   if (a.C % (msu_is16(dtype) ? 8 : 4) != 0 || a.C > 2048) return -2;
   if (a.rows == 0) return 0;
-  static const int maxb = getenv("MSU_LN_FWD_BLOCKS") ? atoi(getenv("MSU_LN_FWD_BLOCKS")) : 16384;  // A/B switch: 16384 vs 4096 vs 2048 = 154.06 / 153.82 / 152.78 img/s
-  MSU_DISPATCH(dtype, T, return launch_fwd<T, MODE>(a, st, maxb));
+  // grid cap 16384 blocks (vs 4096 / 2048: 154.06 vs 153.82 / 152.78 img/s, r01)
+  MSU_DISPATCH(dtype, T, return launch_fwd<T, MODE>(a, st, 16384));
   return -3;
 }
 
@@ -532,7 +519,6 @@ int bwd_dispatch(int dtype, const LnBwdArgs& a, float* dgamma, float* dbeta, int
   int rc = -3;
   MSU_DISPATCH(dtype, T, rc = launch_bwd<T, MODE>(a, st, nparts));
   if (rc) return rc;
-  if (dgamma == nullptr) return MSU_CHECK_LAUNCH();  // partials only: msu_ln_param_reduce later
   if (dbeta == dgamma + a.C) {  // contiguous [dgamma | dbeta]: one reduction launch
     colsum(a.part, nparts, 2L * a.C, 2L * a.C, dgamma, accumulate, st);
   } else {
@@ -734,7 +720,7 @@ __global__ void __launch_bounds__(256) head_fwd16_kernel(const T* z, const float
 // block's 64 row groups in fixed order through LDS, and expanded into the [3][C] partial.
 // PF: the group's next row (z chunks, mean, rstd, dlogit) is loaded while this one is reduced
 // and stored -- a group walks ~128 rows per launch at 1024^2; the arithmetic is the plain loop's
-// (no implicit contraction; A/B switch MSU_HEAD_BWD_PF=0)
+// (no implicit contraction; 0 of 61 tensors differ from the plain loop, r04ab)
 template <typename T, int KC, bool PF = true>
 __global__ void __launch_bounds__(256) head_bwd16_kernel(const float* dlogit, const T* z, const float* gamma,
                                                          const float* beta, const float* w, const float* mean,
@@ -857,13 +843,10 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
   if (C % 4 || C > 256) return -2;
   if (rows == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  static const bool head_pf = !(getenv("MSU_HEAD_BWD_PF") && getenv("MSU_HEAD_BWD_PF")[0] == '0');  // A/B switch
   if (msu_is16(dtype) && (C == 96 || C == 128)) {
     MSU_DISPATCH16(dtype, T,
-      if (C == 96 && head_pf) hipLaunchKernelGGL((head_bwd16_kernel<T, 3>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows);
-      else if (C == 96) hipLaunchKernelGGL((head_bwd16_kernel<T, 3, false>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows);
-      else if (head_pf) hipLaunchKernelGGL((head_bwd16_kernel<T, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows);
-      else hipLaunchKernelGGL((head_bwd16_kernel<T, 4, false>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows));
+      if (C == 96) hipLaunchKernelGGL((head_bwd16_kernel<T, 3>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows);
+      else hipLaunchKernelGGL((head_bwd16_kernel<T, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows));
   } else {
     MSU_DISPATCH(dtype, T,
       if (C <= 128) hipLaunchKernelGGL((head_bwd_kernel<T, 4>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows, C);
@@ -880,13 +863,11 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
 
 int msu_ln_part_blocks(long rows, int C) {
   // >= 16 rows per block (the per-block parameter-gradient reduction amortises) and enough
-  // blocks to fill the CUs at the deep stages (8192 rows x 768: 512 blocks, not 64).  A/B
-  // switch MSU_LN_PARTS_MAX: 512 / 256 vs 1024 = 168.2 / 162.5 vs 170.0 img/s (r04t).  C >= 384
-  // (stages 2-3, whose partials are 2C wide and whose reductions run on the main stream): 512
-  // blocks, 170.5 / 170.4 vs 169.8 / 169.8 with 1024 (256: 168.7 / 168.6; r04v), switch
-  // MSU_LN_PARTS_DEEP
-  static const long cap = getenv("MSU_LN_PARTS_MAX") ? atol(getenv("MSU_LN_PARTS_MAX")) : 1024;
-  static const long cap_deep = getenv("MSU_LN_PARTS_DEEP") ? atol(getenv("MSU_LN_PARTS_DEEP")) : (cap < 512 ? cap : 512);
+  // blocks to fill the CUs at the deep stages (8192 rows x 768: 512 blocks, not 64).  Cap 1024
+  // (512 / 256: 168.2 / 162.5 vs 170.0 img/s, r04t); C >= 384 (stages 2-3, whose partials are 2C
+  // wide and whose reductions run on the main stream): 512 (170.5 / 170.4 vs 169.8 / 169.8 with
+  // 1024, 256: 168.7 / 168.6; r04v)
+  constexpr long cap = 1024, cap_deep = 512;
   long nb = (rows + 15) / 16;
   if (nb > cap) nb = cap;
   if (C >= 384 && nb > cap_deep) nb = cap_deep;
@@ -924,22 +905,6 @@ int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const 
     case IN_D2S2: return bwd_dispatch<IN_D2S2>(dtype, a, dgamma, dbeta, nparts, accumulate, st);
   }
   return -3;
-}
-
-// The parameter-gradient half of msu_layernorm_bwd (called with dgamma == null): dgamma / dbeta
-// [C] from the nparts x [2C] partials it left, written or accumulated -- on any stream ordered
-// after the backward kernel (the trainer's side stream: off the activation-gradient chain).
-int msu_ln_param_reduce(const float* part, int nparts, int C, float* dgamma, float* dbeta, int accumulate,
-                        void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-  if (nparts <= 0 || C <= 0) return 0;
-  if (dbeta == dgamma + C) {
-    colsum(part, nparts, 2L * C, 2L * C, dgamma, accumulate, st);
-  } else {
-    const ColSeg segs[2] = {{part, C, 2L * C, dgamma}, {part + C, C, 2L * C, dbeta}};
-    colsum_multi(segs, 2, nparts, accumulate, st);
-  }
-  return MSU_CHECK_LAUNCH();
 }
 
 int msu_reduce_rows(const float* part, int nparts, int n, long stride, float* out,

@@ -792,20 +792,14 @@ long head_blocks(long need, long cap) {
 }
 
 // heads per backward workgroup: pairs for even nh (a 128-B line holds two heads' slices; the
-// LDS still allows two 4-wave workgroups per CU), else one.  All three heads at nh = 3 (stage 0
-// of Swin-T/S) cut the fetched bytes by a third (r04g counters: 431 vs 649 MB per stage-0
-// backward, 1.03x the algorithmic 420 MB) but fit one 6-wave workgroup per CU instead of four
-// 2-wave ones, and ran 300 vs 267 us: opt-in.  A/B switch MSU_ATTN_BWD_HPW=1|2|3 (where nh
-// allows it).
-int bwd_hpw(int nh) {
-  static const int forced = getenv("MSU_ATTN_BWD_HPW") ? atoi(getenv("MSU_ATTN_BWD_HPW")) : 0;
-  if (forced >= 1 && forced <= 3 && nh % forced == 0) return forced;
-  return nh % 2 == 0 ? 2 : 1;
-}
+// LDS still allows two 4-wave workgroups per CU), else one.  (All three heads at nh = 3 cut the
+// stage-0 fetched bytes by a third, r04g: 431 vs 649 MB, but fit one 6-wave workgroup per CU
+// instead of four 2-wave ones and ran 300 vs 267 us: not kept.)
+int bwd_hpw(int nh) { return nh % 2 == 0 ? 2 : 1; }
 
 // backward workgroups per head group: the LDS (40 KB per head) allows four heads per CU
 // (three at nh = 3), i.e. 1024 / nh workgroups of 2 HPW waves (768 / nh at HPW = 3)
-int bwd_blocks(long nwin, int nh) { return (int)head_blocks(nwin, (bwd_hpw(nh) == 3 ? 768 : 1024) / nh); }
+int bwd_blocks(long nwin, int nh) { return (int)head_blocks(nwin, 1024 / nh); }
 
 template <typename T, int HPW>
 void launch_bwd(dim3 grid, hipStream_t st, const void* qkv, const Aux& aux, const void* dout, void* dqkv,
@@ -880,8 +874,7 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
   MSU_DISPATCH16(dtype, T,
     hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
                        1.0f / scale, img, brow, zrow);
-    if (hpw == 3) launch_bwd<T, 3>(grid, st, qkv, aux, dout, dqkv, dB_part, qb_part, g, scale, p_drop, seed, seed_dev, keep, nblk);
-    else if (hpw == 2) launch_bwd<T, 2>(grid, st, qkv, aux, dout, dqkv, dB_part, qb_part, g, scale, p_drop, seed, seed_dev, keep, nblk);
+    if (hpw == 2) launch_bwd<T, 2>(grid, st, qkv, aux, dout, dqkv, dB_part, qb_part, g, scale, p_drop, seed, seed_dev, keep, nblk);
     else launch_bwd<T, 1>(grid, st, qkv, aux, dout, dqkv, dB_part, qb_part, g, scale, p_drop, seed, seed_dev, keep, nblk));
   if (pst == (hipStream_t)(intptr_t)-1) return MSU_CHECK_LAUNCH();  // tail issued by the caller
   // parameter-gradient reductions: on pst (after the backward kernel) when given
@@ -1239,269 +1232,6 @@ int msu_win_attn_qkv_fwd(int dtype, const void* x, const void* w_qkv, const floa
                          void* stream) {
   return msu_win_attn_qkv_fwd2(dtype, x, w_qkv, b_qkv, table, nullptr, nullptr, out, nullptr, qkv_out, keep, workspace,
                                B, H, W, C, nh, shift, p_drop, seed, seed_dev, stream);
-}
-
-}  // extern "C"
-
-// =====================================================================================
-// Fused qkv Linear + window attention, head-stationary (round 4, second form).  The six-wave
-// window-per-workgroup form above keeps 1.5 waves per SIMD and puts three barriers per window
-// between the phases, so its VALU-bound attention phases serialise on the SIMDs that carry two
-// waves (r04b: 0.245 ms per stage-0 launch, no faster than the unfused pair).  Here the
-// structure of attn_fwd_mfma is kept -- independent waves, one (window, head) item each, the
-// next item's operands loaded during the current one, no workgroup barrier in the loop -- and
-// the q / k / v rows an item needs are computed by the wave itself: the next window's 64 LN1
-// rows are loaded straight into MFMA B-operand registers (12 x 16 B per lane), and the head's
-// W_qkv rows (96 x 96, 18 KB) stay in LDS for the workgroup's life.  36 extra 32x32x16 MFMAs
-// per item, on a kernel whose MFMA pipe was ~90 % idle.  proj stays a separate Linear.
-namespace {
-
-template <int WAVES>
-struct HsLds {
-  float4 bimg[4 * 4 * 64];  // the head's bias image, [tile][q][lane]
-  bf16_t w[FQ_C * FQ_C];    // the head's q / k / v rows of W_qkv (local row 32 m + r), swizzled chunks
-  float bias[FQ_C];
-  FwdLds wave[WAVES];
-};
-
-template <typename T, int WAVES, bool DROP, bool STORE_QKV>
-__global__ void __launch_bounds__(64 * WAVES, 1) attn_qkv_hs_mfma(const bf16_t* __restrict__ xin,
-                                                                 const bf16_t* __restrict__ wqkv,
-                                                                 const float* __restrict__ bqkv, Aux aux,
-                                                                 bf16_t* __restrict__ out,
-                                                                 bf16_t* __restrict__ qkv_out, Geom g, float scale,
-                                                                 float p_drop, uint64_t seed0,
-                                                                 const unsigned long long* seed_dev,
-                                                                 uint32_t* __restrict__ keep_out) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  HsLds<WAVES>& S = *reinterpret_cast<HsLds<WAVES>*>(smem_raw);
-  const uint64_t seed = launch_seed(seed0, seed_dev);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  FwdLds& L = S.wave[wave];
-  const int h = blockIdx.y;
-  {
-    const float4* src = reinterpret_cast<const float4*>(aux.bimg + (long)h * 4096);
-    for (int e = threadIdx.x; e < 1024; e += 64 * WAVES) {
-      const int t = e >> 8, q = (e >> 6) & 3, ln = e & 63;
-      S.bimg[e] = src[(t * 64 + ln) * 4 + q];
-    }
-    for (int s = threadIdx.x; s < FQ_C * FQ_CH; s += 64 * WAVES) {
-      const int lr = s / FQ_CH, c = s - (s / FQ_CH) * FQ_CH;
-      const int gr = (lr >> 5) * FQ_C + h * HD + (lr & 31);  // q, k, v row of head h
-      *reinterpret_cast<u32x4*>(S.w + lr * FQ_C + ((c ^ fq_swz(lr)) << 3)) =
-          *reinterpret_cast<const u32x4*>(wqkv + gr * FQ_C + 8 * c);
-    }
-    for (int s = threadIdx.x; s < FQ_C; s += 64 * WAVES) S.bias[s] = bqkv[(s >> 5) * FQ_C + h * HD + (s & 31)];
-  }
-  __syncthreads();
-  const long nitems = g.nwin;
-  const long stride = (long)gridDim.x * WAVES;
-  const int hh = lane >> 5;
-  long item = (long)xcd_remap(blockIdx.x, gridDim.x) * WAVES + wave;
-  if (item >= nitems) return;  // no block-wide barriers after this point: waves are independent
-
-  // the item's LN1 rows as B fragments: [buf][tt * 6 + ks] -> token 32 tt + (lane & 31),
-  // k = 16 ks + 8 (lane >> 5) .. + 7 (zero rows for padded / filler tokens: qkv = bias there)
-  u32x4 xr[2][12];
-  bool bnd[2] = {false, false};
-  auto prep = [&](long it, auto BUF) __attribute__((always_inline)) {
-    constexpr int buf = decltype(BUF)::value;
-    bnd[buf] = window_tokens(g, (int)it, L.tok[buf], L.reg[buf], lane);
-    lds_sync();
-    static_for([&](auto TT) {
-      constexpr int tt = decltype(TT)::value;
-      const int tok = L.tok[buf][32 * tt + (lane & 31)];
-      const bf16_t* rb = tok >= 0 ? xin + (size_t)((unsigned)tok * (unsigned)FQ_C) : aux.zrow;
-      static_for([&](auto KS) {
-        constexpr int ks = decltype(KS)::value;
-        xr[buf][tt * 6 + ks] = *reinterpret_cast<const u32x4*>(rb + 16 * ks + 8 * hh);
-      }, std::make_integer_sequence<int, 6>{});
-    }, std::make_integer_sequence<int, 2>{});
-  };
-
-  auto step = [&](auto BUF, long it_cur) __attribute__((always_inline)) -> bool {
-    constexpr int buf = decltype(BUF)::value;
-    const int win = (int)it_cur;
-    // ---- q, k, v rows of this item (the previous item's LDS reads are complete: lds_sync below)
-    static_for([&](auto TT) {
-      constexpr int tt = decltype(TT)::value;
-      f32x16 acc[3];
-#pragma unroll
-      for (int m = 0; m < 3; ++m) acc[m] = f32x16{0};
-      static_for([&](auto KS) {
-        constexpr int ks = decltype(KS)::value;
-        const bf16x8 xf = __builtin_bit_cast(bf16x8, xr[buf][tt * 6 + ks]);
-#pragma unroll
-        for (int m = 0; m < 3; ++m) acc[m] = mfma32<T>(fq_frag(S.w, 32 * m, ks, lane), xf, acc[m]);
-      }, std::make_integer_sequence<int, 6>{});
-      const int tk = 32 * tt + (lane & 31);
-#pragma unroll
-      for (int m = 0; m < 3; ++m) {
-        bf16_t* img = m == 0 ? L.q : (m == 1 ? L.k : L.v);
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const float4 b = *reinterpret_cast<const float4*>(S.bias + 32 * m + 8 * gq + 4 * hh);
-          uint2 wv;
-          wv.x = pack2<T>(acc[m][4 * gq] + b.x, acc[m][4 * gq + 1] + b.y);
-          wv.y = pack2<T>(acc[m][4 * gq + 2] + b.z, acc[m][4 * gq + 3] + b.w);
-          *reinterpret_cast<uint2*>(img + tk * LD + 8 * gq + 4 * hh) = wv;
-        }
-      }
-    }, std::make_integer_sequence<int, 2>{});
-    uint32_t kmasks[2] = {~0u, ~0u};
-    if constexpr (DROP) {
-#pragma unroll
-      for (int it = 0; it < 2; ++it)
-        kmasks[it] = drop_bits<false>(drop_seed32(seed), (uint32_t)win * g.nh + h, it * 32 + (lane & 31), hh,
-                                      drop_thresh16(p_drop));
-    }
-    const long nxt = it_cur + stride;
-    const bool more = nxt < nitems;
-    if (more) prep(nxt, std::integral_constant<int, buf ^ 1>{});
-    lds_sync();
-    if constexpr (STORE_QKV) {
-      // the training path keeps qkv for the backward: head h's three 64-B slices of every real
-      // token, 4 lanes per slice
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int t = (lane >> 2) + 16 * c;
-        const int tok = L.tok[buf][t];
-#pragma unroll
-        for (int m = 0; m < 3; ++m) {
-          const bf16_t* img = m == 0 ? L.q : (m == 1 ? L.k : L.v);
-          const u32x4 v = *reinterpret_cast<const u32x4*>(img + t * LD + 8 * (lane & 3));
-          if (tok >= 0)
-            *reinterpret_cast<u32x4*>(qkv_out + (size_t)((unsigned)tok * (unsigned)FQ_C3) + m * FQ_C + h * HD +
-                                      8 * (lane & 3)) = v;
-        }
-      }
-    }
-    bf16x8 ka[2][2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) ka[t][ks] = frag_rows(L.k, LD, 32 * t, 16 * ks, lane);
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      f32x16 P[2];
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt) {
-        const float4* bp = S.bimg + (jt * 2 + it) * 256 + lane;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v = bp[64 * q];
-          P[jt][4 * q] = v.x; P[jt][4 * q + 1] = v.y; P[jt][4 * q + 2] = v.z; P[jt][4 * q + 3] = v.w;
-        }
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 qf = frag_rows(L.q, LD, 32 * it, 16 * ks, lane);
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt) P[jt] = mfma32<T>(ka[jt][ks], qf, P[jt]);
-      }
-      if (bnd[buf]) mask_col(P, L.reg[buf], it, scale, lane);
-      softmax_col(P, scale);
-      if constexpr (DROP) {
-        const float kscale = 1.0f / (1.0f - p_drop);
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (live_key(jt, r)) P[jt][r] = (kmasks[it] >> (jt * 16 + r)) & 1u ? P[jt][r] * kscale : 0.f;
-      }
-      f32x16 O = f32x16{0};
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-        for (int sb = 0; sb < 2; ++sb)
-          O = mfma32<T>(frag_tr_perm(L.v, LD, jt * 32 + 16 * sb, 0, lane), pack8<T>(P[jt], sb), O);
-      const int i = it * 32 + (lane & 31);
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        uint2 w;
-        w.x = pack2<T>(O[4 * gq], O[4 * gq + 1]);
-        w.y = pack2<T>(O[4 * gq + 2], O[4 * gq + 3]);
-        *reinterpret_cast<uint2*>(L.q + i * LD + 8 * gq + 4 * hh) = w;
-      }
-    }
-    lds_sync();
-    u32x4 ov[4];
-    int otok[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int t = (lane >> 2) + 16 * c;
-      otok[c] = L.tok[buf][t];
-      ov[c] = *reinterpret_cast<const u32x4*>(L.q + t * LD + 8 * (lane & 3));
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (otok[c] >= 0)
-        *reinterpret_cast<u32x4*>(out + (size_t)((unsigned)otok[c] * (unsigned)g.C) + h * HD + 8 * (lane & 3)) = ov[c];
-    if (DROP && keep_out) {
-      uint32_t* kp = keep_out + ((size_t)win * g.nh + h) * 128 + lane;
-      kp[0] = kmasks[0];
-      kp[64] = kmasks[1];
-    }
-    lds_sync();  // LDS reads of this item done before they are overwritten
-    return more;
-  };
-
-  prep(item, std::integral_constant<int, 0>{});
-  for (;;) {
-    if (!step(std::integral_constant<int, 0>{}, item)) break;
-    item += stride;
-    if (!step(std::integral_constant<int, 1>{}, item)) break;
-    item += stride;
-  }
-}
-
-constexpr int HS_WAVES = 4;
-
-template <typename T, bool DROP, bool STORE_QKV>
-void launch_hs(dim3 grid, const void* x, const void* w, const float* b, const Aux& aux, void* out, void* qkv, Geom g,
-               float scale, float p_drop, unsigned long long seed, const unsigned long long* seed_dev, void* keep,
-               hipStream_t st) {
-  auto kern = attn_qkv_hs_mfma<T, HS_WAVES, DROP, STORE_QKV>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sizeof(HsLds<HS_WAVES>));
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(kern, grid, dim3(64 * HS_WAVES), sizeof(HsLds<HS_WAVES>), st, (const bf16_t*)x, (const bf16_t*)w,
-                     b, aux, (bf16_t*)out, (bf16_t*)qkv, g, scale, p_drop, (uint64_t)seed, seed_dev, (uint32_t*)keep);
-}
-
-}  // namespace
-
-extern "C" {
-
-// Fused qkv Linear + window attention, head-stationary form (no proj): same contract as
-// msu_win_attn_qkv_fwd.
-int msu_win_attn_qkv_hs_fwd(int dtype, const void* x, const void* w_qkv, const float* b_qkv, const float* table,
-                            void* out, void* qkv_out, void* keep, float* workspace, int B, int H, int W, int C, int nh,
-                            int shift, float p_drop, unsigned long long seed, const unsigned long long* seed_dev,
-                            void* stream) {
-  if (!msu_is16(dtype) || !msu_win_attn_qkv_supported(C, nh)) return -2;
-  if ((long)B * H * W * 3 * C >= (1L << 32)) return -2;
-  const Geom g = make_geom(B, H, W, C, nh, shift);
-  if (g.nwin == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  const float scale = 1.0f / sqrtf((float)HD);
-  float* img; bf16_t* brow; bf16_t* zrow;
-  const Aux aux = carve_aux(workspace, C, nh, &img, &brow, &zrow);
-  // one 4-wave workgroup per CU (100 KB of LDS), split over the heads (XCD-consistent grid)
-  const long nb = head_blocks((g.nwin + HS_WAVES - 1) / HS_WAVES, num_cus_fq() / nh);
-  const dim3 grid((unsigned)nb, (unsigned)nh);
-  const bool drop = p_drop > 0.f;
-  MSU_DISPATCH16(dtype, T,
-    hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, b_qkv, nh, 3 * C,
-                       1.0f / scale, img, brow, zrow);
-    if (drop && qkv_out) launch_hs<T, true, true>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st);
-    else if (drop) launch_hs<T, true, false>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st);
-    else if (qkv_out) launch_hs<T, false, true>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st);
-    else launch_hs<T, false, false>(grid, x, w_qkv, b_qkv, aux, out, qkv_out, g, scale, p_drop, seed, seed_dev, keep, st));
-  return MSU_CHECK_LAUNCH();
 }
 
 }  // extern "C"

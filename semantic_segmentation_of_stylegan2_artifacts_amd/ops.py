@@ -13,16 +13,12 @@ autocast state of the caller; statistics, parameters and parameter gradients are
 
 The public functions below (``layer_norm``, ``linear``, ``window_attention`` ...) are what the
 modules in ``network/`` call.  They cast the activation to the autocast dtype and invoke the
-registered op.  ``set_dispatch("fast")`` routes the same implementations through a plain
-``autograd.Function`` built from the very same forward / setup / backward functions (no
-dispatcher round trip: ~15 us less host time per call), for launch-bound eager loops; the
-numerics are identical by construction.
+registered op.  (A plain ``autograd.Function`` route around the dispatcher measured equal on
+the GPU-bound 1024^2 step, r02c 50.50 vs 50.57 ms: gone.)
 """
-import os
-
 import torch
 
-from . import _lib
+from . import _lib, switches
 
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 _LOW = (torch.bfloat16, torch.float16)
@@ -74,53 +70,18 @@ def _as(t, dtype):
 
 # ----------------------------------------------------------------------------- registration
 _LIB = torch.library.Library("msunet", "DEF")
-_DISPATCH = os.environ.get("MSU_DISPATCH", "torch_ops")  # "torch_ops" | "fast"
 _OPS = {}
 
 
-class _Op:
-    """One registered operator: the ``torch.ops.msunet`` overload and the equivalent direct
-    autograd.Function built from the same forward / setup_context / backward."""
-
-    __slots__ = ("op", "fast")
-
-    def __call__(self, *args):
-        return (self.op if _DISPATCH == "torch_ops" else self.fast)(*args)
-
-
-def set_dispatch(mode):
-    """'torch_ops': call through torch.ops.msunet (dispatcher + register_autograd);
-    'fast': the same implementation as a plain autograd.Function."""
-    global _DISPATCH
-    if mode not in ("torch_ops", "fast"):
-        raise ValueError(mode)
-    _DISPATCH = mode
-
-
-def _fast_function(name, impl, setup, backward):
-    def fwd(ctx, *args):
-        out = impl(*args)
-        setup(ctx, args, out)
-        return out
-
-    def bwd(ctx, *grads):
-        return backward(ctx, *grads)
-
-    return type("_" + name, (torch.autograd.Function,), {"forward": staticmethod(fwd),
-                                                          "backward": staticmethod(bwd)}).apply
-
-
 def _define(name, schema, impl, fake, setup=None, backward=None):
+    """Register ``torch.ops.msunet.<name>``: CUDA kernel, fake kernel, autograd formula."""
     _LIB.define(name + schema)
     _LIB.impl(name, impl, "CUDA")
     torch.library.register_fake("msunet::" + name, fake, lib=_LIB)
     if backward is not None:
         torch.library.register_autograd("msunet::" + name, backward, setup_context=setup, lib=_LIB)
-    o = _Op()
-    o.op = getattr(torch.ops.msunet, name).default
-    o.fast = _fast_function(name, impl, setup, backward) if backward is not None else o.op
-    _OPS[name] = o
-    return o
+    op = _OPS[name] = getattr(torch.ops.msunet, name).default
+    return op
 
 
 def registered_ops():
@@ -145,8 +106,7 @@ def set_grad_ready_callback(fn):
 # later in backward reads them, so they overlap the input-gradient chain (which is often
 # latency-bound at stages 1-3) instead of sitting on it.  The trainer joins the side stream
 # before the optimizer (join_side_streams) and the bucketed all-reduce is issued from it.
-_side_enabled = os.environ.get("MSU_WGRAD_SIDE", "1") != "0"
-_SIDE_PRIORITY = int(os.environ.get("MSU_SIDE_PRIORITY", "1"))  # A/B switch (0: same as main)
+_side_enabled = switches.on("MSU_WGRAD_SIDE")
 _side_streams = {}
 # per-use switches of the side stream (tools/graph_side_probe.py bisects the forked capture)
 _side_wgrad = True      # Linear weight gradients
@@ -162,28 +122,14 @@ def side_stream(device):
     return _side_streams.get(device.index if device.index is not None else torch.cuda.current_device())
 
 
-# Side-stream launches held back to the next side-stream fork (or the end of backward): the
-# refine convs' weight gradients (MSU_CONV_DEFER=1), so they overlap the HBM-bound stage-0
-# decoder backward instead of the MFMA-bound conv input gradients of the stacks after them.
-_deferred_side = []
-
-
-def _flush_deferred_side():
-    if _deferred_side:
-        work = _deferred_side[:]
-        _deferred_side.clear()
-        for fn in work:
-            fn()
-
-
 def _side_stream_for(device):
-    _flush_deferred_side()
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _side_streams.get(idx)
     if st is None:
         # lowest priority: when both streams have work queued, the dispatcher serves the
         # main (critical-path) stream's workgroups first
-        st = _side_streams[idx] = torch.cuda.Stream(device=idx, priority=_SIDE_PRIORITY)
+        # (low / equal priority measured equal, r02c; a high-priority main stream -0.4 %)
+        st = _side_streams[idx] = torch.cuda.Stream(device=idx, priority=1)
     return st
 
 
@@ -230,7 +176,6 @@ _side_event_params = []
 def _end_of_backward():
     global _join_queued
     _join_queued = False
-    _flush_deferred_side()
     join_side_streams()
     _side_keep.clear()  # the main stream now waits for every side-stream read
     for p in _side_event_params:
@@ -265,34 +210,6 @@ def _ln_grads(ctx, C, device):
         return w.grad, b.grad, 1, True
     dw, db = torch.empty(2, C, device=device, dtype=torch.float32)  # contiguous: one reduction
     return dw, db, 0, False
-
-
-# MSU_LN_SIDE=1 (opt-in): LayerNorm parameter gradients (the partials' reduction into gamma /
-# beta .grad) on the side stream.  On the main stream the 54 small reductions per step (30 us
-# each, a few dozen workgroups) sit on the activation-gradient chain (r04q eager profile: 1.7
-# ms/step), but on the side stream each one's wait for the main stream ties the side stream's
-# weight-gradient queue to the main stream's progress: 167.4 / 167.5 / 167.5 vs 170.2 / 170.2 /
-# 170.1 img/s (r04r).
-_LN_SIDE = os.environ.get("MSU_LN_SIDE", "0") == "1"
-
-
-def _ln_side(direct):
-    return direct and _LN_SIDE and _side_enabled
-
-
-def _ln_param_tail(ctx, part, n, C, dw, db, device):
-    """dgamma / dbeta of a LayerNorm backward (called with them null) on the side stream."""
-    main = torch.cuda.current_stream(device)
-    side = _side_stream_for(device)
-    side.wait_stream(main)
-    _lib.call("msu_ln_param_reduce", _p(part), n, C, _p(dw), _p(db), 1, side.cuda_stream)
-    part.record_stream(side)
-    _side_keep.append(part)
-    ev = torch.cuda.Event()
-    ev.record(side)
-    for p in ctx.affine:
-        _guard_side_write(p, ev)
-    _join_at_end_of_backward()
 
 
 def _ln_parts(rows, C, device):
@@ -343,12 +260,8 @@ def _ln_backward(ctx, dy, _dm, _dr):
     dx = torch.empty_like(x)
     dw, db, acc, direct = _ln_grads(ctx, C, x.device)
     n, part = _ln_parts(rows, C, x.device)
-    side = _ln_side(direct)
     _lib.call("msu_layernorm_bwd", _dt(x), IN_PLAIN, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-              _p(dx), None, None, 1, _p(part), n, None if side else _p(dw), None if side else _p(db), rows, C, 0,
-              0, 0, acc, _s(x))
-    if side:
-        _ln_param_tail(ctx, part, n, C, dw, db, x.device)
+              _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, C, 0, 0, 0, acc, _s(x))
     if direct:
         _notify(*ctx.affine)
         return dx, None, None, None
@@ -406,12 +319,8 @@ def _add_ln_backward(ctx, ds, dy, _dm, _dr):
     dbr = torch.empty_like(s) if scale is not None else None
     dw, dbb, acc, direct = _ln_grads(ctx, C, s.device)
     n, part = _ln_parts(rows, C, s.device)
-    side = _ln_side(direct)
     _lib.call("msu_layernorm_bwd", _dt(s), IN_ADD, _p(dy), _p(s), _p(ds), _p(w), _p(mean), _p(rstd),
-              _p(da), _p(dbr), _p(scale), ctx.rps, _p(part), n, None if side else _p(dw),
-              None if side else _p(dbb), rows, C, 0, 0, 0, acc, _s(s))
-    if side:
-        _ln_param_tail(ctx, part, n, C, dw, dbb, s.device)
+              _p(da), _p(dbr), _p(scale), ctx.rps, _p(part), n, _p(dw), _p(dbb), rows, C, 0, 0, 0, acc, _s(s))
     if direct:
         _notify(*ctx.affine)
         dw = dbb = None
@@ -462,12 +371,8 @@ def _merge_ln_backward(ctx, dy, _dm, _dr):
     dx = torch.empty_like(x)
     dw, db, acc, direct = _ln_grads(ctx, 4 * C, x.device)
     n, part = _ln_parts(rows, 4 * C, x.device)
-    side = _ln_side(direct)
     _lib.call("msu_layernorm_bwd", _dt(x), IN_MERGE, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-              _p(dx), None, None, 1, _p(part), n, None if side else _p(dw), None if side else _p(db), rows,
-              4 * C, H, W, C, acc, _s(x))
-    if side:
-        _ln_param_tail(ctx, part, n, 4 * C, dw, db, x.device)
+              _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, 4 * C, H, W, C, acc, _s(x))
     if direct:
         _notify(*ctx.affine)
         return dx, None, None, None
@@ -515,12 +420,8 @@ def _d2s_ln_backward(ctx, dy, _dm, _dr):
     dx = torch.empty_like(x)
     dw, db, acc, direct = _ln_grads(ctx, c, x.device)
     n, part = _ln_parts(rows, c, x.device)
-    side = _ln_side(direct)
     _lib.call("msu_layernorm_bwd", _dt(x), IN_D2S2, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-              _p(dx), None, None, 1, _p(part), n, None if side else _p(dw), None if side else _p(db), rows,
-              c, H, W, 0, acc, _s(x))
-    if side:
-        _ln_param_tail(ctx, part, n, c, dw, db, x.device)
+              _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, c, H, W, 0, acc, _s(x))
     if direct:
         _notify(*ctx.affine)
         return dx, None, None, None
@@ -538,9 +439,10 @@ def d2s_layer_norm(x, weight, bias, eps=1e-5):
 
 
 # ----------------------------------------------------------------------------- attention
-# dropout keep bits stored by the forward for the backward (A/B switch MSU_ATTN_KEEP=0: the
-# backward re-hashes the mask from the seed, as the f32 parity kernels always do)
-_ATTN_KEEP = os.environ.get("MSU_ATTN_KEEP", "1") != "0"
+# dropout keep bits stored by the forward for the backward (False: the backward re-hashes the
+# mask from the seed, as the f32 parity kernels always do; bit-identical, equal speed since the
+# xorshift streams, r02c -- the stored form is the default, the re-hash stays for the tests)
+_ATTN_KEEP = True
 
 def _attn_impl(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
     _need_cuda(qkv)
@@ -653,14 +555,14 @@ def window_attention(qkv, qkv_bias, table, num_heads, shift, p_drop=0.0, seed=0,
 # ----------------------------------------------------------------------------- fused qkv + attention
 # Stage-0 fused unit (csrc/window_attention_mfma.hip attn_qkv_fwd_mfma): the qkv Linear and the
 # window attention in one kernel, qkv never read back (in inference never written).  The backward
-# is the two existing ones in sequence: the attention backward (dqkv, relative table, padded-token
-# bias share) then the qkv Linear's (one-pass msu_linear_bwd at stage 0).  Two kernels:
-# MSU_ATTN_QKV=1 (default) the window-per-workgroup one with proj inside
-# (msu_win_attn_qkv_fwd2), =hs the head-stationary one (msu_win_attn_qkv_hs_fwd: independent
-# waves, one (window, head) item each, proj a separate Linear; r04d same-box benches 165.6 /
-# 165.8 vs 166.4 / 166.5 img/s), =0 the unfused qkv Linear + window_attention path.
-_ATTN_QKV_MODE = os.environ.get("MSU_ATTN_QKV", "1")
-_ATTN_QKV = _ATTN_QKV_MODE != "0"
+# is the existing ones in sequence: the proj Linear's, the attention backward (dqkv, relative
+# table, padded-token bias share), then the qkv Linear's (one-pass msu_linear_bwd at stage 0).
+# The kernel is the window-per-workgroup one with proj inside (msu_win_attn_qkv_fwd2);
+# MSU_ATTN_QKV=0: the unfused qkv Linear + window_attention + proj path.  (A head-stationary
+# form with independent waves, proj a separate Linear, was slower: r04d 165.6 / 165.8 vs 166.4 /
+# 166.5 img/s, gone.)
+_ATTN_QKV = switches.on("MSU_ATTN_QKV")
+fused_qkv_calls = 0  # fused-unit launches (tests assert which path a forward took)
 
 
 class _Ctx:
@@ -675,6 +577,7 @@ def _attn_qkv_impl(x, weight, bias, table, proj_weight, proj_bias, num_heads, sh
                    store):
     """(y, o, qkv, keep): y = proj(o) when proj_weight is given (else y = o and o is empty),
     o = attention(x W^T + b); o / qkv are kept (written) only when ``store`` (training)."""
+    global fused_qkv_calls
     _need_cuda(x)
     x = x.contiguous()
     B, H, W, C = x.shape
@@ -689,16 +592,7 @@ def _attn_qkv_impl(x, weight, bias, table, proj_weight, proj_bias, num_heads, sh
     ws = torch.empty(L.msu_win_attn_fwd_workspace(_dt(x), C, num_heads), device=x.device, dtype=torch.float32)
     keep = torch.empty(L.msu_win_attn_keep_words(_dt(x), B, H, W, num_heads) if p_drop > 0 and _ATTN_KEEP else 0,
                        device=x.device, dtype=torch.int32)
-    if _ATTN_QKV_MODE == "hs":
-        a = torch.empty(B, H, W, C, device=x.device, dtype=dt) if proj else y
-        _lib.call("msu_win_attn_qkv_hs_fwd", _dt(x), _p(x), _p(w), _p(bias), _p(table), _p(a),
-                  _p(qkv) if store else None, _p(keep) if keep.numel() else None, _p(ws), B, H, W, C, num_heads,
-                  shift, float(p_drop), seed, _p(seed_dev), _s(x))
-        if proj:
-            y = _linear_impl(a, proj_weight, proj_bias)
-            if store:
-                o = a
-        return y, o, qkv, keep
+    fused_qkv_calls += 1
     _lib.call("msu_win_attn_qkv_fwd2", _dt(x), _p(x), _p(w), _p(bias), _p(table), _p(wp),
               _p(proj_bias) if proj else None, _p(y), _p(o) if o.numel() else None, _p(qkv) if store else None,
               _p(keep) if keep.numel() else None, _p(ws), B, H, W, C, num_heads, shift, float(p_drop), seed,
@@ -737,14 +631,15 @@ def _attn_qkv_backward(ctx, dy, _do, _dqkv, _dkeep):
     dwp = dbp = None
     if wp is not None:
         # proj Linear first: do = dy . W_proj, dW_proj / db_proj from (dy, o)
-        pctx = _Ctx((o,), params=(wp, bp), needs_input_grad=(True, True, True))
+        pctx = _Ctx((o,), params=(wp, bp), needs_input_grad=(True, ctx.needs_input_grad[4], ctx.needs_input_grad[5]))
         dout, dwp, dbp = _linear_backward(pctx, dy)
     else:
         dout = dy
     actx = _Ctx((qkv, bias, table, seed_dev, keep), cfg=ctx.cfg, bias_param=ctx.bias_param,
                 table_param=ctx.table_param)
     dqkv, dbias_pad, dtable = _attn_backward(actx, dout, None)[:3]
-    lctx = _Ctx((x,), params=(weight, bias), needs_input_grad=(ctx.needs_input_grad[0], True, True))
+    lctx = _Ctx((x,), params=(weight, bias),
+                needs_input_grad=(ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]))
     dx, dw, db = _linear_backward(lctx, dqkv)
     if db is not None and dbias_pad is not None:
         db = db + dbias_pad
@@ -768,10 +663,6 @@ def window_attention_qkv_fusable(x, num_heads, bias):
     return bool(_lib.lib().msu_win_attn_qkv_supported(C, num_heads))
 
 
-def _param_or_f32(t):
-    return t if isinstance(t, torch.nn.Parameter) else _f32(t)
-
-
 def window_attention_qkv(x, weight, bias, table, num_heads, shift, p_drop=0.0, seed=0, seed_dev=None,
                          proj_weight=None, proj_bias=None):
     """window_attention(linear(x, weight, bias), bias, table, ...) with the qkv Linear fused in
@@ -784,8 +675,10 @@ def window_attention_qkv(x, weight, bias, table, num_heads, shift, p_drop=0.0, s
         raise ValueError("the fused proj needs its bias")
     params = [weight, bias, table] + ([proj_weight, proj_bias] if proj else [])
     store = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
-    return _window_attention_qkv(x, weight, _param_or_f32(bias), _param_or_f32(table),
-                                 proj_weight if proj else None, _param_or_f32(proj_bias) if proj else None,
+    # _f32 hands an f32 contiguous Parameter through as the same object (direct .grad in the
+    # backward), and converts anything else: the kernel reads the biases and the table as f32
+    return _window_attention_qkv(x, weight, _f32(bias), _f32(table),
+                                 proj_weight if proj else None, _f32(proj_bias) if proj else None,
                                  int(num_heads), int(shift), float(p_drop), int(seed) & ((1 << 63) - 1), seed_dev,
                                  bool(store))[0]
 
@@ -925,9 +818,10 @@ def _shadow(param, dt):
     return param.to(dt)
 
 
-# A/B switch: the trainer's transposed weight shadow for the input-gradient GEMMs (0: W^T is
-# read in place by the NT GEMM's KN variant / copied per call for the token GEMM)
-_SHADOW_T = os.environ.get("MSU_SHADOW_T", "1") != "0"
+# the trainer's transposed weight shadow for the input-gradient GEMMs (r03i: +2.1 %); False (the
+# tests' second arm): W^T read in place by the NT GEMM's KN variant / copied per call for the
+# token GEMM, as under fp16 autocast over the bf16 shadow
+_SHADOW_T = True
 
 
 def _shadow_t(param, dt):
@@ -953,7 +847,7 @@ def transpose16_multi(src, dst, table, ntiles):
 # the library GEMM (hipBLASLt) wherever the epilogue allows it, "ntmlp" = the NT GEMM only for
 # the GELU-epilogue MLP GEMMs (library elsewhere), "nt" = the NT GEMM before the narrow-K token
 # GEMM plans.
-_ROUTE_FORCE = os.environ.get("MSU_GEMM_ROUTE", "")
+_ROUTE_FORCE = switches.get("MSU_GEMM_ROUTE")
 
 
 def gemm_route(M, N, K, epi=TOK_PLAIN):
@@ -1029,7 +923,7 @@ def _linear_setup(ctx, inputs, output):
 # One-pass Linear backward (csrc/gemm_linbwd.hip) for the stage-0 block Linears: dX, dW and db
 # from one read of dY on the main stream, instead of the input-gradient GEMM plus a side-stream
 # weight gradient that reads dY again.  A/B switch MSU_LINBWD=0: the two-kernel path.
-_LINBWD = os.environ.get("MSU_LINBWD", "1") != "0"
+_LINBWD = switches.on("MSU_LINBWD")
 _LINBWD_MIN_M = 65536
 
 
@@ -1040,7 +934,7 @@ def _linbwd(dy, x, weight, bias, M, N, K, h=None):
     """dX = dy . W (* GELU'(h)) with dW / db accumulated into the trainer's .grad in the same
     pass; None when the shape, dtype or parameters are not covered (caller: two-kernel path).
     W^T is the trainer's transposed shadow when it has one in x's dtype, else a per-call
-    transpose of the 16-bit weight (fp16 autocast over a bf16 shadow, MSU_SHADOW_T=0)."""
+    transpose of the 16-bit weight (fp16 autocast over a bf16 shadow, or _SHADOW_T off)."""
     global linbwd_calls
     if not _LINBWD or x.dtype not in _LOW or M < _LINBWD_MIN_M:
         return None
@@ -1085,6 +979,8 @@ def _linear_backward(ctx, dy):
         else:
             with torch.autocast("cuda", enabled=False):
                 dx = dy.matmul(w)
+    if not (ctx.needs_input_grad[1] or (bias is not None and ctx.needs_input_grad[2])):
+        return dx, None, None  # frozen weight and bias: no weight-gradient work at all
     dw, db = _wgrad(dy, x, weight, bias, M, N, K)
     return dx, dw, db
 
@@ -1155,8 +1051,6 @@ def _wgrad_into(dy, x, dw, db, M, N, K, acc):
               _s(x))
 
 
-# A/B switch MSU_CAT_SIDE=0: linear_cat's weight-gradient halves on the main stream (round 3)
-_CAT_SIDE = os.environ.get("MSU_CAT_SIDE", "1") != "0"
 
 
 def _linear_cat_backward(ctx, dy):
@@ -1174,7 +1068,7 @@ def _linear_cat_backward(ctx, dy):
     # weight gradient per half straight into the column slices of dW (bias with the first):
     # the trainer's flat .grad (accumulate) or a fresh [N, C1 + C2] gradient
     direct = _direct(weight, bias)
-    if direct and _side_enabled and _side_wgrad and _CAT_SIDE:
+    if direct and _side_enabled and _side_wgrad:
         # on the weight-gradient side stream like every other Linear's (the shared skip-fusion
         # Linears -- concat_back_dim[2 / 3] serve the central decoders too -- then have all
         # their .grad writers on one stream, in program order)
@@ -1445,8 +1339,8 @@ def _pad_to(t, dim, mult):
 
 
 # persistent workgroups of the refine-conv weight gradient (one 139 KB / 12-wave workgroup per
-# CU: while it runs on the side stream nothing else fits on its CUs).  A/B switch
-_CONV_WGRAD_BLOCKS = int(os.environ.get("MSU_CONV_WGRAD_BLOCKS", "256"))
+# CU; 192 / 128 measured slower, r04ac)
+_CONV_WGRAD_BLOCKS = 256
 
 
 def _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout):
@@ -1460,10 +1354,9 @@ def _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout):
     return dw, db
 
 
-# A/B switch MSU_CONV_SIDE=0: the refine convs' weight gradients on the main stream
-_CONV_SIDE = os.environ.get("MSU_CONV_SIDE", "1") != "0"
-# MSU_CONV_DEFER=1: ... and issued at the next side-stream fork (_deferred_side)
-_CONV_DEFER = os.environ.get("MSU_CONV_DEFER", "0") == "1"
+# A/B switch MSU_CONV_SIDE=0: the refine convs' weight gradients on the main stream.  (Holding
+# them back to the next side-stream fork measured equal, r04z: gone.)
+_CONV_SIDE = switches.on("MSU_CONV_SIDE")
 
 
 def _conv_wgrad_param(a, dz, mode, B, H, W, Cin, Cout, weight, bias):
@@ -1490,11 +1383,7 @@ def _conv_wgrad_param(a, dz, mode, B, H, W, Cin, Cout, weight, bias):
         _guard_side_write(bias, ev)
         _notify(weight, bias)
 
-    if _CONV_DEFER:
-        # the closure holds a and dz (autograd cannot steal them for an in-place add meanwhile)
-        _deferred_side.append(launch)
-    else:
-        launch()
+    launch()
     _join_at_end_of_backward()
     return None, None
 

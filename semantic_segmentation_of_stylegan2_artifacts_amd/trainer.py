@@ -27,18 +27,16 @@ Here:
 """
 import math
 import os
+import threading
 import time
 
 import torch
 import torch.distributed as dist
 
-from . import ops
+from . import ops, switches
 from .loss import DynamicLoss
 from .network import model_parts
 
-# A/B switch: mark the bf16 shadow's parameter versions before AdamW (host-only work while
-# the GPU is still busy) instead of after the step's last launch
-_EARLY_MARK = os.environ.get("MSU_EARLY_SHADOW_MARK", "1") != "0"
 
 
 def is_no_decay(name, param):
@@ -192,6 +190,11 @@ class GradBucketer:
         self.pending = [0] * len(self.buckets)
         self.launched = [False] * len(self.buckets)
         self.works = []
+        # (bucket, thread id, "hook" | "finish", capturing) of every launch of the current step;
+        # ``last_launches`` keeps the previous step's (tests/test_capture_guard.py checks that a
+        # capture issues every bucket from finish() on the capturing thread)
+        self.launches = []
+        self.last_launches = []
         self.handles = []
         for g in groups:
             for p in g.params:
@@ -210,9 +213,10 @@ class GradBucketer:
             buf.copy_(g.grad[s:e])
         return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.pg, async_op=True), buf
 
-    def _launch(self, b):
+    def _launch(self, b, via):
         g, s, e = self.buckets[b]
         self.launched[b] = True
+        self.launches.append((b, threading.get_ident(), via, self.capturing))
         if self.comm is None:
             self.works.append((b,) + self._reduce(b, g, s, e))
             return
@@ -242,7 +246,7 @@ class GradBucketer:
         b = self.param_bucket[id(p)]
         self.pending[b] += 1
         if self.expected is not None and self.pending[b] == self.expected[b] and not self.capturing:
-            self._launch(b)
+            self._launch(b, "hook")
 
     def _unwire(self, b, buf):
         g, s, e = self.buckets[b]
@@ -258,7 +262,7 @@ class GradBucketer:
             self.expected = list(self.pending)
         for b in range(len(self.buckets)):
             if not self.launched[b]:
-                self._launch(b)
+                self._launch(b, "finish")
         if self.comm is None or self.capturing or torch.cuda.is_current_stream_capturing():
             for b, w, buf in self.works:  # (the current stream waits for each collective)
                 w.wait()
@@ -275,6 +279,7 @@ class GradBucketer:
         self.works = []
         self.pending = [0] * len(self.buckets)
         self.launched = [False] * len(self.buckets)
+        self.last_launches, self.launches = self.launches, []
 
     def reset(self):
         """Forget a step that did not finish (e.g. an aborted HIP-graph capture): no pending
@@ -282,6 +287,7 @@ class GradBucketer:
         self.works = []
         self.pending = [0] * len(self.buckets)
         self.launched = [False] * len(self.buckets)
+        self.launches = []
 
     def update_scale(self, found_inf):
         """GradScaler's dynamic-scale rule for the f16 wire (no-op otherwise), on the device:
@@ -312,8 +318,9 @@ def rccl_capture_blocker(process_group):
     work's HIP events to new works; after a capture its watchdog thread can query an event last
     recorded inside the capture, HIP refuses the query (hipErrorCapturedEvent) and the watchdog
     terminates the process (round-3 record).  The variable must be 0 before the
-    process group is created; gloo groups never capture (their collectives run on the host)."""
-    if process_group is None:
+    process group is created; gloo groups never capture (their collectives run on the host).
+    ``process_group=None`` is the default (WORLD) group, as for the collectives themselves."""
+    if not (dist.is_available() and dist.is_initialized()):
         return None
     try:
         backend = dist.get_backend(process_group)
@@ -377,12 +384,12 @@ class Trainer:
         # GPU time, measured on the last warmup step): the replay removes the host from the
         # critical path, but costs ~1-2 % of GPU time where the host is not on it
         on_gpu = torch.device(device).type == "cuda"
-        mode = use_graph if use_graph is not None else os.environ.get("MSU_GRAPH", "auto")
+        mode = use_graph if use_graph is not None else switches.get("MSU_GRAPH")
         mode = {True: "1", False: "0"}.get(mode, str(mode))
         self.graph_mode = mode if on_gpu else "0"
         if self.graph_mode != "0" and self.reducer is not None and dist.get_backend(process_group) != "nccl":
             self.graph_mode = "0"  # gloo collectives run on the host: not capturable
-        blocker = rccl_capture_blocker(process_group if self.reducer is not None else None)
+        blocker = rccl_capture_blocker(self.reducer.pg) if self.reducer is not None else None
         if self.graph_mode != "0" and blocker:
             # never capture into a process group whose watchdog can abort the process;
             # every rank sees the same environment, so every rank stays eager together
@@ -531,9 +538,10 @@ class Trainer:
         ops.join_side_streams()  # weight gradients issued on the side stream
         inv = self.inv_world if self.world_size > 1 else None
         bf16 = self.amp_dtype == torch.bfloat16
-        if bf16 and _EARLY_MARK:
-            # the per-parameter Python loop runs now, while the GPU still has backward work
-            # queued, not after the last launch of the step (it left the GPU idle there)
+        if bf16:
+            # the bf16 shadow's parameter versions are marked now, while the GPU still has
+            # backward work queued, not after the last launch of the step (it left the GPU idle
+            # there); the shadow itself is refreshed after AdamW below
             for g in self.groups:
                 g.mark_shadow()
         found = None
@@ -552,10 +560,7 @@ class Trainer:
                            self.eps, g.weight_decay, inv_scale=inv, found_inf=found)
             g.grad.zero_()
             if bf16:  # keeps evaluation between steps on the updated weights
-                if _EARLY_MARK:
-                    g.copy_shadow()
-                else:
-                    g.refresh_shadow()
+                g.copy_shadow()
         return loss.detach()
 
     GRAPH_HOST_FRACTION = 0.9
@@ -600,7 +605,7 @@ class Trainer:
 
     def _capture(self, images, labels):
         """Capture _device_step into a HIP graph (nothing executes during capture)."""
-        blocker = rccl_capture_blocker(self.reducer.pg if self.reducer is not None else None)
+        blocker = rccl_capture_blocker(self.reducer.pg) if self.reducer is not None else None
         if blocker:  # use_graph forced on after construction: refuse instead of aborting later
             raise RuntimeError(f"cannot capture the training step: {blocker}")
         if self.amp_dtype == torch.bfloat16 and not self._shadow_fresh:
@@ -617,7 +622,7 @@ class Trainer:
         # when the step is launch-bound, where the side-stream overlap matters least.
         # MSU_GRAPH_SIDE=1 keeps the side stream (A/B switch).
         side_prev = ops._side_enabled
-        if os.environ.get("MSU_GRAPH_SIDE", "0") != "1":
+        if switches.get("MSU_GRAPH_SIDE") != "1":
             ops._side_enabled = False
         try:
             # thread_local: the process group's watchdog thread keeps querying its events while
@@ -648,6 +653,9 @@ class Trainer:
             return
         if self.reducer is not None:
             self.reducer.capturing = False
+            # (bucket, thread, "hook" | "finish", capturing) of the captured collectives: every one
+            # from finish() on this thread (tests/test_gpu_rccl.py checks it)
+            self.capture_launches = list(self.reducer.last_launches)
         ops._side_enabled = side_prev
         self._graph = graph
         self._graph_loss_fn = self.loss_fn

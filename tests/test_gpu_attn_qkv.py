@@ -1,7 +1,6 @@
 """GPU: the fused stage-0 unit qkv Linear -> window attention -> proj Linear (ops.window_attention_qkv,
-csrc/window_attention_mfma.hip: attn_qkv_hs_mfma, the default head-stationary form, and
-attn_qkv_fwd_mfma, the window-per-workgroup form with proj inside) against fp32 PyTorch and against the unfused
-path it replaces (ops.linear -> ops.window_attention -> ops.linear; reference
+csrc/window_attention_mfma.hip attn_qkv_fwd_mfma, one window per workgroup step with proj inside)
+against fp32 PyTorch and against the unfused path it replaces (ops.linear -> ops.window_attention -> ops.linear; reference
 network/model_parts.py:166-170 -> torchvision qkv Linear + shifted_window_attention + proj).
 
 * forward vs fp32: attention(x W^T + b) on the same 16-bit operands (tests/_parity_refs.py), at
@@ -12,7 +11,9 @@ network/model_parts.py:166-170 -> torchvision qkv Linear + shifted_window_attent
   and the keep bits equal the unfused forward's (same dropout streams);
 * backward (dx, dW, db, d table) equals the unfused path's to 16-bit rounding, and the trainer's
   direct-.grad parameters take the same values;
-* inference (no grad) writes no qkv.
+* inference (no grad) writes no qkv;
+* parameters in 16 bits (a model cast with .to(bfloat16)) are converted, not read as f32, and
+  frozen ones get no gradient.
 """
 import math
 
@@ -62,19 +63,13 @@ def low(request):
     return request.param
 
 
-@pytest.fixture(params=["hs", "1"], ids=["head_stationary", "window_wg"])
-def kernel(request, monkeypatch):
-    monkeypatch.setattr(_ops(), "_ATTN_QKV_MODE", request.param)
-    return request.param
-
-
 CASES = [(2, 8, 8, 3), (1, 14, 14, 0), (2, 28, 28, 3), (1, 10, 12, 3), (1, 256, 256, 3), (1, 256, 256, 0)]
 
 
 @pytest.mark.parametrize("proj", [False, True], ids=["attn", "attn_proj"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.05])
 @pytest.mark.parametrize("B,H,W,shift", CASES)
-def test_fused_forward_matches_fp32(B, H, W, shift, p_drop, proj, low, kernel):
+def test_fused_forward_matches_fp32(B, H, W, shift, p_drop, proj, low):
     ops = _ops()
     x, w, b, table, _ = _inputs(B, H, W, B * H + W + shift, low)
     wp, bp = _proj(B + H) if proj else (None, None)
@@ -95,7 +90,7 @@ def test_fused_forward_matches_fp32(B, H, W, shift, p_drop, proj, low, kernel):
 
 
 @pytest.mark.parametrize("B,H,W,shift", [(2, 28, 28, 3), (1, 256, 256, 3)])
-def test_fused_equals_unfused_including_backward(B, H, W, shift, low, kernel):
+def test_fused_equals_unfused_including_backward(B, H, W, shift, low):
     """Same keep bits and qkv as the unfused forward; the outputs and all gradients agree to
     16-bit rounding (the backward kernels are the unfused path's own)."""
     ops = _ops()
@@ -123,7 +118,7 @@ def test_fused_equals_unfused_including_backward(B, H, W, shift, low, kernel):
             _check(a, r, t, name)
 
 
-def test_fused_direct_params_match_autograd_params(kernel):
+def test_fused_direct_params_match_autograd_params():
     """Trainer-style parameters (flat .grad, bf16 shadow, direct accumulation: the one-pass Linear
     backward and the side-stream attention tail) give the plain autograd gradients."""
     ops = _ops()
@@ -153,7 +148,7 @@ def test_fused_direct_params_match_autograd_params(kernel):
         _check(a, r, 1e-2, name)
 
 
-def test_fused_inference_keeps_no_qkv(kernel):
+def test_fused_inference_keeps_no_qkv():
     ops = _ops()
     x, w, b, table, _ = _inputs(1, 28, 28, 3, torch.bfloat16)
     wp, bp = _proj(5)
@@ -163,3 +158,43 @@ def test_fused_inference_keeps_no_qkv(kernel):
         y2 = ops.linear(ops.window_attention(ops.linear(x, w, b), b, table, NH, 3), wp, bp)
     assert qkv.numel() == 0 and o.numel() == 0
     _check(y1, y2, 1.5e-2, "no-grad fused vs unfused")
+
+
+def test_fused_16bit_params_are_converted():
+    """a model cast to bf16 hands the fused unit bf16 biases and table; they must be
+    read as their values (converted to f32), exactly as the f32 parameters' rounded values."""
+    ops = _ops()
+    B, H, W, shift = 1, 28, 28, 3
+    x, w, b, table, _ = _inputs(B, H, W, 21, torch.bfloat16)
+    wp, bp = _proj(9)
+    p16 = [torch.nn.Parameter(t.to(torch.bfloat16)) for t in (w, b, table, wp, bp)]
+    p32 = [t.detach().float() for t in p16]  # the same values in f32
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y16 = ops.window_attention_qkv(x, p16[0], p16[1], p16[2], NH, shift, proj_weight=p16[3], proj_bias=p16[4])
+        y32 = ops.window_attention_qkv(x, p32[0], p32[1], p32[2], NH, shift, proj_weight=p32[3], proj_bias=p32[4])
+    torch.cuda.synchronize()
+    assert torch.equal(y16, y32)
+
+
+def test_fused_frozen_params_get_no_grad():
+    """Frozen qkv / proj weights and biases: no gradient for them (no weight-gradient
+    work for parameters that need none), the input gradient equals the unfrozen run's."""
+    ops = _ops()
+    B, H, W, shift = 1, 28, 28, 3
+    x, w, b, table, dy = _inputs(B, H, W, 23, torch.bfloat16)
+    wp0, bp0 = _proj(13)
+    res = {}
+    for frozen in (False, True):
+        xg = x.clone().requires_grad_(True)
+        ps = [torch.nn.Parameter(t.clone(), requires_grad=not frozen) for t in (w, b, wp0, bp0)]
+        pt = torch.nn.Parameter(table.clone())
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = ops.window_attention_qkv(xg, ps[0], ps[1], pt, NH, shift, 0.0, 0, None, ps[2], ps[3])
+        y.backward(dy)
+        ops.join_side_streams()
+        torch.cuda.synchronize()
+        res[frozen] = (xg.grad.clone(), pt.grad.clone(), [p.grad for p in ps])
+    assert all(g is None for g in res[True][2])
+    assert all(g is not None for g in res[False][2])
+    assert torch.equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][1], res[False][1])

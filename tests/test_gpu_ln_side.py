@@ -1,8 +1,11 @@
-"""GPU: the LayerNorm parameter gradients reduced on the weight-gradient side stream (trainer-style
-direct parameters, ops._ln_param_tail) equal the in-line reduction of the plain autograd path
-bitwise -- the same partials summed in the same order, only on another stream -- for the four
-LayerNorm forms of the path (torchvision block norms, the fused residual + norm, PatchMerging's
-gather + norm, PatchExpand's rearrange + norm; model_parts.py:87-94, :403-405)."""
+"""GPU: parameter gradients written straight into trainer-style ``.grad`` (direct parameters) equal
+the plain autograd gradients bitwise -- the same partials summed in the same order:
+
+* the LayerNorm parameter gradients accumulated into ``.grad`` by the backward's reduction, for
+  the four LayerNorm forms of the path (torchvision block norms, the fused residual + norm,
+  PatchMerging's gather + norm, PatchExpand's rearrange + norm; model_parts.py:87-94, :403-405);
+* the refine convs' weight / bias gradients added into ``.grad`` on the side stream
+  (ops._conv_wgrad_param; model_parts.py:447-448, :468-471)."""
 import pytest
 import torch
 
@@ -29,9 +32,8 @@ def _params(C, seed, direct):
 
 
 @pytest.mark.parametrize("form", ["plain", "add", "merge", "d2s"])
-def test_ln_param_grads_on_side_stream_equal_inline(form, monkeypatch):
+def test_ln_param_grads_direct_equal_autograd(form):
     ops = _ops()
-    monkeypatch.setattr(ops, "_LN_SIDE", True)  # opt-in path
     g = torch.Generator().manual_seed(3)
     B, H, W, C = 2, 32, 32, 96
     x = torch.randn(B, H, W, C, generator=g).to(DEV, torch.bfloat16)
@@ -60,16 +62,13 @@ def test_ln_param_grads_on_side_stream_equal_inline(form, monkeypatch):
         assert torch.equal(a, r), name
 
 
-@pytest.mark.parametrize("defer", [False, True])
 @pytest.mark.parametrize("d2s", [False, True])
-def test_refine_conv_param_grads_on_side_stream_equal_autograd(d2s, defer, monkeypatch):
+def test_refine_conv_param_grads_on_side_stream_equal_autograd(d2s):
     """The refine convs' weight / bias gradients added into trainer-style .grad on the side
     stream (ops._conv_wgrad_param) equal the autograd gradients bitwise (same kernel, added
-    into zeros); the input gradient is unchanged.  defer: the launch held back to the end of
-    backward (MSU_CONV_DEFER)."""
+    into zeros); the input gradient is unchanged."""
     ops = _ops()
     assert ops._CONV_SIDE
-    monkeypatch.setattr(ops, "_CONV_DEFER", defer)
     g = torch.Generator().manual_seed(11)
     B, H, W, C = 1, 64, 64, 96
     xin = torch.randn(B, H // 4, W // 4, 16 * C, generator=g) if d2s else torch.randn(B, H, W, C, generator=g)

@@ -20,6 +20,7 @@ process (r03j: the whole pytest run; r03p: the child, log attached to the failur
 """
 import os
 import socket
+import threading
 
 import pytest
 import torch
@@ -63,7 +64,11 @@ def _run(pg, graph, reduce, wire=None, steps=5, bucket_mb=1.0, lr=1e-3):
     ops.set_grad_ready_callback(None)
     info = {"captured": tr._graph is not None, "skipped": tr.skipped_steps(),
             "buckets": len(tr.reducer.buckets) if tr.reducer is not None else 0,
-            "comm": tr.reducer.comm is not None if tr.reducer is not None else None}
+            "comm": tr.reducer.comm is not None if tr.reducer is not None else None,
+            # (bucket, thread, "hook" | "finish", capturing) of the captured collectives, and
+            # the thread that captured (all from finish() on the capturing thread)
+            "capture_launches": getattr(tr, "capture_launches", None),
+            "thread": threading.get_ident()}
     _KEEP.append(tr)  # see _child
     return losses, [torch.cat([g.data, g.exp_avg, g.exp_avg_sq]) for g in tr.groups], info
 
@@ -178,6 +183,9 @@ def test_rccl_bucketer_graph_replay_equals_eager(rccl_runs):
     lg, sg, info = _get(rccl_runs, "graph_lr0")
     assert info["buckets"] > 10
     assert info["captured"], "the step with RCCL all-reduces was not captured"
+    log = info["capture_launches"]
+    assert sorted(b for b, *_ in log) == list(range(info["buckets"]))
+    assert all(via == "finish" and tid == info["thread"] and cap for _, tid, via, cap in log), log
     assert lg == pytest.approx(le, rel=1e-6, abs=1e-7), (le, lg)
     for a, b in zip(se, sg):
         torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-9)

@@ -1,0 +1,223 @@
+"""GPU: the BENCHMARKED training step, end to end, against the fp32 parity mode.
+
+Swin-T MS-UNet at 1024^2, batch 4 (stage-0 M = 4 x 256^2 = 262 144 tokens), dropout and drop-path
+off, identical weights and inputs in three arms, all in one spawned child process (so a fault
+ends these tests, not the suite, and the 1-rank RCCL group is this process's own):
+
+* ``fp32`` -- the parity mode of the same modules (f32 kernels, library GEMMs), plain autograd:
+  the reference.  It is pinned against the CPU oracle at this resolution by
+  ``test_gpu_baseline_shapes.py::test_swinT_1024_bs1_fp32_backward_matches_oracle`` (every
+  gradient norm within 2e-3, the refine-conv / relative-table / qkv / expand gradients in full).
+* ``bf16`` -- the production ``Trainer`` step exactly as bench.py runs it (reference
+  trainer.py:308-316 -> ``Trainer.step``: bf16 shadow weights, direct ``.grad`` accumulation,
+  side-stream weight gradients, eager), with the RCCL gradient bucketer forced on over a
+  1-rank group (``always_reduce``: the all-reduce path of the 8-GPU run, identity at one
+  rank).  Two steps at lr 0; the gradients AdamW receives in the second step (the one whose
+  buckets launch from backward's hooks) are recorded.  The routes are asserted: the one-pass
+  stage-0 Linear backward (``ops.linbwd_calls``), the fused stage-0 qkv -> attention -> proj
+  unit (``ops.fused_qkv_calls``), no library GEMM route, bucket launches from hooks.  At this
+  size the token GEMM (M >= 262 144), ``msu_linear_bwd``, conv v3, the looping persistent
+  attention kernels (5476 stage-0 windows) and the side-stream ``.grad`` writers all fire.
+* ``f16`` -- the reference's own fp16 autocast + GradScaler + torch AdamW step
+  (``test_gpu_reference_step.reference_step``, trainer.py:299-316 unchanged) on these modules.
+
+Checked against fp32: logits relative L2, the loss, every per-parameter gradient norm, and the
+full gradient tensors of both 1024^2 refine convs and a stage-0 relative-position table.
+Tolerances (16-bit activations through ~80 layers; the f16 reference test's norm rule,
+test_gpu_reference_step.py:98-108): logits rel. L2 <= 5e-2 (bf16) / 2e-2 (f16); loss within 1e-2
+relative; norms within 5e-2 n + 1e-3 max-norm; full tensors rel. L2 <= 1e-1 (bf16) / 5e-2 (f16).
+The measured values are printed (run with -s) and attached to a failure.
+"""
+import json
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+BS, IMG = 4, 1024
+FULL = ("ms_unet.up.refine1.weight", "ms_unet.up.refine2.weight",
+        "ms_unet.layers.0.blocks.1.attn.relative_position_bias_table")
+TOL = {"bf16": {"logits": 5e-2, "full": 1e-1}, "f16": {"logits": 2e-2, "full": 5e-2}}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _summary(logits, loss, grads):
+    """What the parent compares: logits (CPU f32), loss, gradient norms, full selected grads."""
+    return {"logits": logits.detach().float().cpu(), "loss": float(loss),
+            "norms": {k: g.float().norm().item() for k, g in grads.items()},
+            "full": {k: grads[k].detach().float().cpu() for k in FULL}}
+
+
+def _child(port, outdir):
+    fd = os.open(os.path.join(outdir, "child.log"), os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    os.dup2(fd, 1)
+    os.dup2(fd, 2)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] = "0"
+    import torch.distributed as dist
+    from semantic_segmentation_of_stylegan2_artifacts_amd import load_config, ops
+    from semantic_segmentation_of_stylegan2_artifacts_amd.data import synthetic_batch
+    from semantic_segmentation_of_stylegan2_artifacts_amd.loss import DynamicLoss
+    from semantic_segmentation_of_stylegan2_artifacts_amd.network import MSUNet
+    from semantic_segmentation_of_stylegan2_artifacts_amd.trainer import Trainer
+    from test_gpu_reference_step import make_optimizer, reference_step
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    cfg = load_config(None, "swin_t", **{"DATA.IMG_SIZE": IMG, "DATA.BATCH_SIZE": BS, "MODEL.DROP_RATE": 0.0,
+                                         "MODEL.DROP_PATH_RATE": 0.0, "MODEL.ATTN_DROP_RATE": 0.0})
+    torch.manual_seed(cfg.SEED)
+    sd = MSUNet(cfg, img_size=IMG, num_classes=1).state_dict()
+    x, y = synthetic_batch(BS, IMG, DEV, 131)
+    t = cfg.TRAIN
+    loss_args = dict(alpha=t.TVERSKY_LOSS_ALPHA, beta=t.TVERSKY_LOSS_BETA, tversky_bce_mix=t.LOSS_TVERSKY_BCE_MIX)
+
+    def fresh():
+        m = MSUNet(cfg, img_size=IMG, num_classes=1)
+        m.load_state_dict(sd, strict=True)
+        return m.to(DEV).train()
+
+    # ---- fp32 parity mode, plain autograd
+    m = fresh()
+    logits = m(x)
+    loss = DynamicLoss(**loss_args)(logits, y)
+    loss.backward()
+    torch.cuda.synchronize()
+    out = {"fp32": _summary(logits, loss.item(), {k: p.grad for k, p in m.named_parameters() if p.grad is not None})}
+    del m, logits, loss
+    torch.cuda.empty_cache()
+
+    # ---- bf16: the production Trainer step with the RCCL bucketer
+    m = fresh()
+    names = {id(p): k for k, p in m.named_parameters()}
+    tr = Trainer(m, cfg, DEV, lr=0.0, process_group=dist.group.WORLD, always_reduce=True, use_graph=False)
+    seen = {}
+
+    class _Capture(torch.nn.Module):  # the logits the step's loss sees
+        def __init__(self, f):
+            super().__init__()
+            self.f = f
+
+        def forward(self, o, lab):
+            seen["logits"] = o.detach().float().clone()
+            return self.f(o, lab)
+
+    tr.loss_fn = _Capture(tr.loss_fn)
+    adamw = ops.adamw_dev_
+    grads = {}
+
+    def snap(param, grad, *a, **kw):  # the gradient AdamW receives, before it and the zeroing
+        for g in tr.groups:
+            if g.grad is grad:
+                for p, off in zip(g.params, g.offsets):
+                    grads[names[id(p)]] = grad[off:off + p.numel()].view_as(p).clone()
+        return adamw(param, grad, *a, **kw)
+
+    ops.adamw_dev_ = snap
+    counts = {}
+    try:
+        for i in range(2):
+            lb0, fq0 = ops.linbwd_calls, ops.fused_qkv_calls
+            grads.clear()
+            loss = tr.step(x, y)
+            torch.cuda.synchronize()
+            counts[i] = {"linbwd": ops.linbwd_calls - lb0, "fused_qkv": ops.fused_qkv_calls - fq0,
+                         "hook_launches": sum(v == "hook" for _, _, v, _ in tr.reducer.last_launches),
+                         "buckets": len(tr.reducer.buckets)}
+    finally:
+        ops.adamw_dev_ = adamw
+    assert not tr.use_graph and tr._graph is None
+    out["bf16"] = _summary(seen["logits"], loss.item(), grads)
+    out["bf16"]["counts"] = counts
+    out["bf16"]["lib_routes"] = [list(k) for k, v in ops._tok_cache.items()
+                                 if isinstance(k, tuple) and k[0] == "route" and v == "lib"]
+    ops.set_grad_ready_callback(None)
+    del m, tr, grads, seen
+    torch.cuda.empty_cache()
+
+    # ---- f16: the reference's fp16 autocast + GradScaler step on these modules
+    m = fresh()
+    opt = make_optimizer(m, 0.0, 1e-3, (0.9, 0.999), 1e-8)
+    scaler = torch.amp.GradScaler("cuda")
+    rec = {}
+
+    def probe(model, outputs, loss, sc):
+        s = sc.get_scale()
+        rec["logits"] = outputs.detach().float()
+        rec["loss"] = loss.item()
+        rec["grads"] = {k: p.grad.float() / s for k, p in model.named_parameters() if p.grad is not None}
+
+    reference_step(m, DynamicLoss(**loss_args), opt, scaler, x, y, DEV, probe)
+    out["f16"] = _summary(rec["logits"], rec["loss"], rec["grads"])
+    torch.save(out, os.path.join(outdir, "arms.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def arms(tmp_path_factory):
+    import torch.multiprocessing as mp
+    out = tmp_path_factory.mktemp("step_parity")
+    p = mp.get_context("spawn").Process(target=_child, args=(_free_port(), str(out)))
+    p.start()
+    p.join(900)
+    if p.is_alive():
+        p.kill()
+        p.join()
+    f = os.path.join(out, "arms.pt")
+    log = os.path.join(out, "child.log")
+    assert os.path.exists(f), (f"child exited with {p.exitcode}; its log ends:\n"
+                               + (open(log).read()[-4000:] if os.path.exists(log) else ""))
+    return torch.load(f, weights_only=True)
+
+
+def _rel(a, b):
+    return ((a - b).norm() / b.norm()).item()
+
+
+@pytest.mark.parametrize("arm", ["bf16", "f16"])
+def test_step_matches_fp32_parity_mode(arms, arm):
+    ref, got = arms["fp32"], arms[arm]
+    rec = {"arm": arm, "logits_rel_l2": _rel(got["logits"], ref["logits"]),
+           "loss": got["loss"], "loss_fp32": ref["loss"]}
+    assert set(got["norms"]) == set(ref["norms"]), sorted(set(got["norms"]) ^ set(ref["norms"]))
+    gmax = max(ref["norms"].values())
+    worst, bad = 0.0, []
+    for k, n in ref["norms"].items():
+        d = abs(got["norms"][k] - n)
+        worst = max(worst, d / (5e-2 * n + 1e-3 * gmax))
+        if d > 5e-2 * n + 1e-3 * gmax:
+            bad.append((k, got["norms"][k], n))
+    rec["norm_worst_fraction_of_tol"] = worst
+    rec["n_params"] = len(ref["norms"])
+    rec["full_rel_l2"] = {k: _rel(got["full"][k], ref["full"][k]) for k in FULL}
+    print(json.dumps(rec))
+    assert rec["logits_rel_l2"] <= TOL[arm]["logits"], rec
+    assert abs(got["loss"] - ref["loss"]) <= 1e-2 * abs(ref["loss"]), rec
+    assert not bad, (bad[:10], rec)
+    assert rec["n_params"] > 300
+    for k, r in rec["full_rel_l2"].items():
+        assert r <= TOL[arm]["full"], (k, rec)
+    agree = ((got["logits"] > 0) == (ref["logits"] > 0)).float().mean().item()
+    assert agree >= 0.98, (agree, rec)
+
+
+def test_bf16_step_took_the_production_routes(arms):
+    b = arms["bf16"]
+    print(json.dumps({"counts": b["counts"], "lib_routes": b["lib_routes"]}))
+    for i, c in b["counts"].items():
+        assert c["linbwd"] >= 4 * 2, c  # stage 0: qkv / proj / mlp.0 / mlp.3 of every block
+        assert c["fused_qkv"] >= 4, c   # the four stage-0 blocks of the live encoder / decoder
+    assert b["counts"][1]["hook_launches"] > 0, b["counts"]  # buckets overlapped backward
+    assert not b["lib_routes"], b["lib_routes"]
