@@ -197,8 +197,12 @@ int msu_tok_gemm_plan(long M, int N, int K, long* out6);
  * workgroup) for the stage 1-3 Linears, whose wide weights do not fit the token GEMM's LDS: same
  * Y / epi semantics as msu_tok_gemm.  Covered: N % 32 == 0, K % 64 == 0. */
 int msu_nt_gemm_supported(long M, int N, int K);
-/* Tile msu_nt_gemm picks for an M x N output (rows * 1000 + columns; 128/256 x 128/192). */
+/* Tile msu_nt_gemm picks for an M x N output (rows * 1000 + columns; 128/256 x 128/192/256),
+ * + 1000000 when the ping-pong kernel (gemm_pp.h) takes it. */
 int msu_nt_gemm_plan(long M, int N);
+/* 1: the ping-pong kernel where the shape tiles exactly (default); 0: the persistent 2-barrier
+ * kernel everywhere (A/B switch MSU_NT_PP).  Returns the previous mode. */
+int msu_nt_gemm_mode(int mode);
 int msu_nt_gemm(int dtype, const void* A, const void* W, const float* bias, void* Y, void* Y2, const void* H,
                 long M, int N, int K, int epi, void* stream);
 /* Plain epilogue with the split-A input of msu_tok_gemm: A's columns [K1, K) from A2 (K1 % 64 == 0):

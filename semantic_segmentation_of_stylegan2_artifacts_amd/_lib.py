@@ -70,6 +70,7 @@ SIGNATURES = {
     "msu_tok_gemm_plan": (I, [L, I, I, P]),
     "msu_nt_gemm_supported": (I, [L, I, I]),
     "msu_nt_gemm_plan": (I, [L, I]),
+    "msu_nt_gemm_mode": (I, [I]),
     "msu_nt_gemm": (I, [I, P, P, P, P, P, P, L, I, I, I, P]),
     "msu_nt_gemm_kn": (I, [I, P, P, P, P, P, P, L, I, I, I, P]),
     "msu_nt_gemm_cat": (I, [I, P, P, I, P, P, P, L, I, I, P]),
@@ -99,14 +100,16 @@ def lib():
         fn = getattr(h, name)
         fn.restype = res
         fn.argtypes = args
+    # the library-side A/B switches (the C code reads no environment; switches.py does)
+    h.msu_nt_gemm_mode(1 if switches.on("MSU_NT_PP") else 0)
     _lib = h
     return _lib
 
 
 def plan_nt(M, N):
-    """(tile rows, tile columns) msu_nt_gemm uses for an M x N output."""
+    """(tile rows, tile columns, ping-pong kernel?) msu_nt_gemm uses for an M x N output."""
     v = lib().msu_nt_gemm_plan(M, N)
-    return v // 1000, v % 1000
+    return (v % 1000000) // 1000, v % 1000, v >= 1000000
 
 
 def call(name, *args):

@@ -24,8 +24,10 @@
 // ops.gemm_route for the stage 1-3 shapes the token GEMM does not take.
 #include <cstdlib>
 #include <cstring>
+#include <utility>
 
 #include "common.h"
+#include "mfma_frag.h"
 
 namespace {
 
@@ -340,6 +342,34 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   }
 }
 
+}  // namespace
+
+#include "gemm_pp.h"
+
+namespace {
+
+// ping-pong kernel (gemm_pp.h) where the shape tiles exactly; msu_nt_gemm_mode(0): the persistent
+// 2-barrier kernel everywhere (A/B switch MSU_NT_PP, set by the Python side at import)
+int g_nt_pp = 1;
+
+int num_cus_nt();
+
+// BN of the ping-pong kernel for this shape, or 0 (gemm_nt_kernel takes it): exact tiling, and
+// rounds of tiles at least 3/4 full (the stage-3 shapes, 96-288 tiles of 256 rows on 256 CUs,
+// keep the persistent kernel's 128-row tiles)
+int pp_bn(long M, int N, int K, int epi, bool wkn) {
+  if (!g_nt_pp || wkn || M % pp::BM != 0 || K % 64 != 0 || K < 128) return 0;
+  // 256-wide tiles hold 128 accumulator registers per wave: the GELU' operands of the GELU_GRAD
+  // epilogue do not fit beside them, that form takes the 192-wide tile
+  int bn = 0;
+  if (N % 256 == 0 && epi != EPI_GELU_GRAD) bn = 256;
+  else if (N % 192 == 0) bn = 192;
+  if (!bn) return 0;
+  const long tiles = (M / pp::BM) * (N / bn), cus = num_cus_nt();
+  const long rounds = (tiles + cus - 1) / cus;
+  return 4 * tiles >= 3 * rounds * cus ? bn : 0;
+}
+
 bool nt_shape_ok(long M, int N, int K) {
   return M > 0 && M < (1L << 31) && N > 0 && N % 32 == 0 && K > 0 && K % 64 == 0 && (long)M * N < (1L << 40);
 }
@@ -433,6 +463,23 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
   a.tiles_m = (int)((M + 64 * cfg.wm - 1) / (64 * cfg.wm));
   if ((long)a.tiles_m * a.tiles_n >= (1L << 31)) return -2;
   hipStream_t st = (hipStream_t)stream;
+  const int pbn = pp_bn(M, N, K, epi, wkn);
+  if (pbn) {
+    a.tiles_n = N / pbn;
+    a.tiles_m = (int)(M / pp::BM);
+    const long tiles = (long)a.tiles_m * a.tiles_n;
+    const unsigned grid = (unsigned)(tiles < num_cus_nt() ? tiles : num_cus_nt());
+    MSU_DISPATCH16(dtype, T,
+      if (pbn == 256) {
+        if (epi == EPI_PLAIN) hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_PLAIN, 256>), dim3(grid), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_GELU_DUAL, 256>), dim3(grid), dim3(512), 0, st, a);
+      } else {
+        if (epi == EPI_PLAIN) hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_PLAIN, 192>), dim3(grid), dim3(512), 0, st, a);
+        else if (epi == EPI_GELU_DUAL) hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_GELU_DUAL, 192>), dim3(grid), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_GELU_GRAD, 192>), dim3(grid), dim3(512), 0, st, a);
+      });
+    return MSU_CHECK_LAUNCH();
+  }
   MSU_DISPATCH16(dtype, T,
     if (cfg.bn == 192) {
       if (cfg.wm == 4) launch_nt<T, 4, 2, false, 192>(epi, a, st);
@@ -454,10 +501,21 @@ extern "C" {
 // Whether msu_nt_gemm covers this shape (K % 64, N % 32).
 int msu_nt_gemm_supported(long M, int N, int K) { return nt_shape_ok(M, N, K) ? 1 : 0; }
 
-// The tile msu_nt_gemm picks for M x N (the [N, K] weight form): rows * 1000 + columns.
+// The tile msu_nt_gemm picks for M x N (the [N, K] weight form, plain epilogue, K = 384):
+// rows * 1000 + columns, + 1000000 for the ping-pong kernel.
 int msu_nt_gemm_plan(long M, int N) {
+  const int pbn = pp_bn(M, N, 384, EPI_PLAIN, false);
+  if (pbn) return 1000000 + pp::BM * 1000 + pbn;
   const NtCfg c = nt_cfg(M, N, false);
   return 64 * c.wm * 1000 + c.bn;
+}
+
+// 1: the ping-pong kernel where the shape tiles exactly (default), 0: the persistent 2-barrier
+// kernel everywhere.  Returns the previous mode.
+int msu_nt_gemm_mode(int mode) {
+  const int prev = g_nt_pp;
+  g_nt_pp = mode ? 1 : 0;
+  return prev;
 }
 
 // Y[M][N] = epi(A . W^T + bias), 16-bit in / out (dtype 1 bf16, 2 f16), f32 accumulation.

@@ -29,6 +29,16 @@ def _ops():
     return ops
 
 
+@pytest.fixture(params=[1, 0], ids=["pingpong", "persistent"], autouse=True)
+def nt_mode(request):
+    """Every test runs with both NT kernels: the ping-pong one (gemm_pp.h, default where the shape
+    tiles exactly) and the persistent 2-barrier one (MSU_NT_PP=0)."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
+    prev = _lib.lib().msu_nt_gemm_mode(request.param)
+    yield request.param
+    _lib.lib().msu_nt_gemm_mode(prev)
+
+
 @pytest.fixture(params=[torch.bfloat16, torch.float16], ids=["bf16", "f16"])
 def low(request):
     return request.param
@@ -109,13 +119,15 @@ def test_nt_gemm_kn_gelu_grad(M, N, K, low):
 
 
 @pytest.mark.parametrize("M,N,K", WIDE)
-def test_nt_gemm_wide_tile_is_chosen_and_exact(M, N, K):
+def test_nt_gemm_wide_tile_is_chosen_and_exact(M, N, K, nt_mode):
     """The shapes the round-4 tile model sends to the 192-column tile (a launch with that tile is
-    told apart by the whole-round tile count; msu_nt_gemm_plan reports the choice), bias epilogue."""
+    told apart by the whole-round tile count; msu_nt_gemm_plan reports the choice), bias epilogue;
+    with the ping-pong kernel where it tiles exactly (N % 192, M % 256), the 2-barrier one else."""
     from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
     ops = _ops()
-    wm, bn = _lib.plan_nt(M, N)
+    wm, bn, pp = _lib.plan_nt(M, N)
     assert bn == 192, (M, N, wm, bn)
+    assert pp == (nt_mode == 1 and M % 256 == 0), (M, N, pp)
     a, w, b = _inputs(M, N, K, 11 * M + N, torch.bfloat16)
     y = ops.nt_gemm(a, w, b)
     _check(y, F.linear(a.float(), w.float(), b), "y")
@@ -127,11 +139,56 @@ def test_nt_gemm_underfilled_shape_takes_all_cus(M, N, K):
     tiles, one per CU (r04h: 59 vs 65-75 us at 8192 x 768 x 3072); the result is unchanged."""
     from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
     ops = _ops()
-    rows, cols = _lib.plan_nt(M, N)
-    assert rows == 128 and cols == 192, (M, N, rows, cols)
+    rows, cols, pp = _lib.plan_nt(M, N)
+    assert rows == 128 and cols == 192 and not pp, (M, N, rows, cols, pp)
     a, w, b = _inputs(M, N, K, 5 * M + N, torch.bfloat16)
     y = ops.nt_gemm(a, w, b)
     _check(y, F.linear(a.float(), w.float(), b), "y")
+
+
+# every stage 1-3 shape of the Swin-T 8 x 1024^2 step the ping-pong kernel takes (forward and input
+# gradient, both tile widths), the three epilogues and the skip concatenation's split A
+PP = [(131072, 576, 192), (131072, 192, 192), (131072, 768, 192), (131072, 192, 768), (131072, 384, 192),
+      (32768, 1152, 384), (32768, 384, 384), (32768, 1536, 384), (32768, 384, 1536), (32768, 768, 384),
+      (32768, 384, 768)]
+
+
+@pytest.mark.parametrize("M,N,K", PP)
+def test_nt_gemm_production_shapes(M, N, K, nt_mode, low):
+    from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
+    ops = _ops()
+    _, bn, pp = _lib.plan_nt(M, N)
+    if nt_mode == 1:
+        assert pp, (M, N)
+    a, w, b = _inputs(M, N, K, 13 * M + N + K, low)
+    y = ops.nt_gemm(a, w, b)
+    _check(y, F.linear(a.float(), w.float(), b), "y")
+    if N % 192 == 0 or N % 256 == 0:
+        h, g = ops.nt_gemm(a, w, b, ops.TOK_GELU_DUAL)
+        _check(h, F.linear(a.float(), w.float(), b), "h")
+        _check(g, F.gelu(h.float()), "gelu(h)")
+        hf = h.float().requires_grad_(True)
+        F.gelu(hf).backward(torch.ones_like(hf))
+        dh = ops.nt_gemm(a, w, None, ops.TOK_GELU_GRAD, h=h)
+        _check(dh, F.linear(a.float(), w.float()) * hf.grad, "dh")
+    if K % 128 == 0:  # [x | skip] . W^T with K1 = K / 2 (concat_back_dim)
+        K1 = K // 2
+        y2 = ops.nt_gemm_cat(a[:, :K1].contiguous(), a[:, K1:].contiguous(), w, b)
+        _check(y2, F.linear(a.float(), w.float(), b), "cat")
+
+
+def test_nt_gemm_pingpong_matches_persistent():
+    """Both kernels on the same operands agree to rounding (different summation order only)."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
+    ops = _ops()
+    a, w, b = _inputs(32768, 1152, 384, 5, torch.bfloat16)
+    prev = _lib.lib().msu_nt_gemm_mode(1)
+    y1 = ops.nt_gemm(a, w, b)
+    _lib.lib().msu_nt_gemm_mode(0)
+    y0 = ops.nt_gemm(a, w, b)
+    _lib.lib().msu_nt_gemm_mode(prev)
+    d = (y1.float() - y0.float()).abs().max().item()
+    assert d <= 2e-2 * y0.float().abs().max().item(), d
 
 
 def test_nt_gemm_rejects_uncovered_shapes():

@@ -24,8 +24,10 @@ ends these tests, not the suite, and the 1-rank RCCL group is this process's own
 Checked against fp32: logits relative L2, the loss, every per-parameter gradient norm, and the
 full gradient tensors of both 1024^2 refine convs and a stage-0 relative-position table.
 Tolerances (16-bit activations through ~80 layers; the f16 reference test's norm rule,
-test_gpu_reference_step.py:98-108): logits rel. L2 <= 5e-2 (bf16) / 2e-2 (f16); loss within 1e-2
-relative; norms within 5e-2 n + 1e-3 max-norm; full tensors rel. L2 <= 1e-1 (bf16) / 5e-2 (f16).
+test_gpu_reference_step.py:98-108): logits rel. L2 <= 2.5e-2 (bf16) / 5e-3 (f16); loss within 1e-2
+relative; norms within 5e-2 n + 1e-3 max-norm; full tensors rel. L2 <= 5e-2 (bf16) / 1e-2 (f16).
+Measured on the GPU (r05c): bf16 logits 8.9e-3, worst norm 1.6 % of its tolerance, refine1 / refine2
+/ stage-0 table gradients 2.6e-3 / 1.1e-3 / 1.4e-2; f16 1.1e-3, 0.24 %, 3.1e-4 / 1.2e-4 / 1.8e-3.
 The measured values are printed (run with -s) and attached to a failure.
 """
 import json
@@ -41,7 +43,7 @@ DEV = "cuda"
 BS, IMG = 4, 1024
 FULL = ("ms_unet.up.refine1.weight", "ms_unet.up.refine2.weight",
         "ms_unet.layers.0.blocks.1.attn.relative_position_bias_table")
-TOL = {"bf16": {"logits": 5e-2, "full": 1e-1}, "f16": {"logits": 2e-2, "full": 5e-2}}
+TOL = {"bf16": {"logits": 2.5e-2, "full": 5e-2}, "f16": {"logits": 5e-3, "full": 1e-2}}
 
 
 def _free_port():

@@ -25,6 +25,8 @@ for s in "$@"; do
     tests_new) step tests_new 600 $PYT -m gpu $R/tests/test_gpu_attn_qkv.py $R/tests/test_gpu_ln_side.py \
                  $R/tests/test_gpu_rccl.py ;;
     parity) step parity 900 $PYT -s -m gpu $R/tests/test_gpu_step_parity.py ;;
+    nt_tests) step nt_tests 600 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py $R/tests/test_routing.py ;;
+    nt_ab) step nt_ab 300 python -u $R/tools/nt_ab.py 3 20 ;;
     tests) step tests 1000 python -u -m pytest $R/tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     smoke) step smoke 300 python -u -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 480 python -u $R/bench.py
