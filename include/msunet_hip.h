@@ -200,7 +200,7 @@ int msu_nt_gemm_supported(long M, int N, int K);
 /* Tile msu_nt_gemm picks for an M x N output (rows * 1000 + columns; 128/256 x 128/192/256),
  * + 1000000 when the ping-pong kernel (gemm_pp.h) takes it. */
 int msu_nt_gemm_plan(long M, int N);
-/* 1: the ping-pong kernel where the shape tiles exactly (default); 0: the persistent 2-barrier
+/* 1: the ping-pong kernel where the shape tiles exactly; 0 (default): the persistent 2-barrier
  * kernel everywhere (A/B switch MSU_NT_PP).  Returns the previous mode. */
 int msu_nt_gemm_mode(int mode);
 int msu_nt_gemm(int dtype, const void* A, const void* W, const float* bias, void* Y, void* Y2, const void* H,

@@ -348,9 +348,10 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
 
 namespace {
 
-// ping-pong kernel (gemm_pp.h) where the shape tiles exactly; msu_nt_gemm_mode(0): the persistent
-// 2-barrier kernel everywhere (A/B switch MSU_NT_PP, set by the Python side at import)
-int g_nt_pp = 1;
+// msu_nt_gemm_mode(1): the ping-pong kernel (gemm_pp.h) where the shape tiles exactly; 0 (the
+// default): the persistent 2-barrier kernel everywhere.  A/B switch MSU_NT_PP, set by the Python
+// side at import: the ping-pong kernel measured 0.72-0.98x of the persistent one (r05g)
+int g_nt_pp = 0;
 
 int num_cus_nt();
 
@@ -358,12 +359,12 @@ int num_cus_nt();
 // rounds of tiles at least 3/4 full (the stage-3 shapes, 96-288 tiles of 256 rows on 256 CUs,
 // keep the persistent kernel's 128-row tiles)
 int pp_bn(long M, int N, int K, int epi, bool wkn) {
-  if (!g_nt_pp || wkn || M % pp::BM != 0 || K % 64 != 0 || K < 128) return 0;
-  // 256-wide tiles hold 128 accumulator registers per wave: the GELU' operands of the GELU_GRAD
-  // epilogue do not fit beside them, that form takes the 192-wide tile
+  // (the GELU' epilogue's operands, 16-bit pre-activations of the whole tile, would be global
+  // loads the compiler drains the DMA ring for: that form stays on gemm_nt_kernel)
+  // (K >= 192: a tile's output stores are spread over the next tile's first four load slots)
+  if (!g_nt_pp || wkn || epi == EPI_GELU_GRAD || M % pp::BM != 0 || K % 64 != 0 || K < 192) return 0;
   int bn = 0;
-  if (N % 256 == 0 && epi != EPI_GELU_GRAD) bn = 256;
-  else if (N % 192 == 0) bn = 192;
+  if (N % 192 == 0) bn = 192;
   if (!bn) return 0;
   const long tiles = (M / pp::BM) * (N / bn), cus = num_cus_nt();
   const long rounds = (tiles + cus - 1) / cus;
@@ -470,14 +471,8 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
     const long tiles = (long)a.tiles_m * a.tiles_n;
     const unsigned grid = (unsigned)(tiles < num_cus_nt() ? tiles : num_cus_nt());
     MSU_DISPATCH16(dtype, T,
-      if (pbn == 256) {
-        if (epi == EPI_PLAIN) hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_PLAIN, 256>), dim3(grid), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_GELU_DUAL, 256>), dim3(grid), dim3(512), 0, st, a);
-      } else {
-        if (epi == EPI_PLAIN) hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_PLAIN, 192>), dim3(grid), dim3(512), 0, st, a);
-        else if (epi == EPI_GELU_DUAL) hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_GELU_DUAL, 192>), dim3(grid), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_GELU_GRAD, 192>), dim3(grid), dim3(512), 0, st, a);
-      });
+      if (epi == EPI_PLAIN) hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_PLAIN, 192>), dim3(grid), dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((pp::gemm_pp_kernel<T, EPI_GELU_DUAL, 192>), dim3(grid), dim3(512), 0, st, a));
     return MSU_CHECK_LAUNCH();
   }
   MSU_DISPATCH16(dtype, T,

@@ -19,8 +19,8 @@ SWITCHES = {
                      "DESIGN 4d (r04c: +0.8 %)"),
     "MSU_GEMM_ROUTE": ("", "force a GEMM route: lib (hipBLASLt) / tok / nt",
                        "DESIGN 7 (r03c: hand-written +2.7 % over hipBLASLt)"),
-    "MSU_NT_PP": ("1", "0: the persistent 2-barrier NT GEMM for every stage 1-3 shape (no ping-pong kernel)",
-                  "DESIGN 7 (round 5)"),
+    "MSU_NT_PP": ("0", "1: the ping-pong NT GEMM (gemm_pp.h) where it tiles exactly, else the persistent one",
+                  "DESIGN 7 (r05g: 0.72-0.98x of the persistent kernel; no-store ablation 1.07-1.66x)"),
     "MSU_LINBWD": ("1", "0: stage-0 Linear backward as input-gradient GEMM + side-stream weight gradient",
                    "DESIGN 7 (r03af: one-pass +1.4 %)"),
     "MSU_CONV_SIDE": ("1", "0: the refine-conv weight gradients on the main stream",

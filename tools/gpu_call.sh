@@ -27,6 +27,12 @@ for s in "$@"; do
     parity) step parity 900 $PYT -s -m gpu $R/tests/test_gpu_step_parity.py ;;
     nt_tests) step nt_tests 600 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py $R/tests/test_routing.py ;;
     nt_ab) step nt_ab 300 python -u $R/tools/nt_ab.py 3 20 ;;
+    nt_exp)
+      for X in 4 8; do
+        echo "== MSU_EXP=$X (1: no DMA, 2: no fragment reads, 4: no MFMA, 8: no epilogue)" >> $O/${TAG}_nt_exp.log
+        MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_nt_$X.so timeout -k 10 200 python -u $R/tools/nt_ab.py 1 20 >> $O/${TAG}_nt_exp.log 2>&1 || exit 3
+      done
+      cat $O/${TAG}_nt_exp.log ;;
     tests) step tests 1000 python -u -m pytest $R/tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     smoke) step smoke 300 python -u -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 480 python -u $R/bench.py
