@@ -50,6 +50,10 @@ int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const 
                       int nparts, float* dgamma, float* dbeta, long rows, int C, int H, int W,
                       int Cin, int accumulate, void* stream);
 int msu_ln_part_blocks(long rows, int C);
+/* 1 (default): the partial-row reductions of msu_layernorm_bwd / msu_head_bwd run inside the
+ * kernel (its last blocks, in a fixed order); 0: a separate column-sum launch after it (A/B switch
+ * MSU_TAIL).  Returns the previous mode. */
+int msu_tail_reduce_mode(int mode);
 int msu_reduce_rows(const float* part, int nparts, int n, long stride, float* out,
                     int accumulate, void* stream);
 

@@ -255,6 +255,12 @@ struct LnBwdArgs {
   long rows;
   int C, H, W, Cin;
   long rows_per_sample;
+  // the partials summed in the kernel (reduce.h tail_reduce) into dgamma / dbeta (+= when
+  // accumulate): the counter region of the launch stream, or -1 (a colsum launch after it)
+  int tail = -1;
+  int accumulate = 0;
+  float* dgamma = nullptr;
+  float* dbeta = nullptr;
 };
 
 template <typename T, int MODE, int TPR, int KMAX, bool PFB = true>
@@ -449,8 +455,15 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
   __syncthreads();
   float* P = a.part + (long)blockIdx.x * 2 * a.C;
   for (int i = threadIdx.x; i < a.C; i += 256) {
-    P[i] = ((red[0][0][i] + red[0][1][i]) + red[0][2][i]) + red[0][3][i];
-    P[a.C + i] = ((red[1][0][i] + red[1][1][i]) + red[1][2][i]) + red[1][3][i];
+    tail_st(P + i, ((red[0][0][i] + red[0][1][i]) + red[0][2][i]) + red[0][3][i]);
+    tail_st(P + a.C + i, ((red[1][0][i] + red[1][1][i]) + red[1][2][i]) + red[1][3][i]);
+  }
+  if (a.tail >= 0) {
+    __shared__ int tail_flag;
+    tail_reduce(a.part, blockIdx.x, gridDim.x, 2 * a.C, 2L * a.C, g_tail_cnt + a.tail * TAIL_WORDS, &tail_flag,
+                [&](int i, float4 v) {
+                  acc_store4(i < a.C ? a.dgamma + i : a.dbeta + (i - a.C), v, a.accumulate);
+                });
   }
 }
 
@@ -517,8 +530,16 @@ int bwd_dispatch(int dtype, const LnBwdArgs& a, float* dgamma, float* dbeta, int
   if (a.C % (msu_is16(dtype) ? 8 : 4) != 0 || a.C > 2048) return -2;
   if (a.rows == 0) return 0;
   int rc = -3;
-  MSU_DISPATCH(dtype, T, rc = launch_bwd<T, MODE>(a, st, nparts));
-  if (rc) return rc;
+  // the parameter-gradient partials summed by the kernel's last blocks (16-B aligned rows and
+  // outputs), else by a colsum launch after it
+  const bool al = ((uintptr_t)a.part & 15) == 0 && ((uintptr_t)dgamma & 15) == 0 && ((uintptr_t)dbeta & 15) == 0;
+  LnBwdArgs b = a;
+  b.tail = al && nparts <= TAIL_GS * (TAIL_WORDS - 1) ? tail_slot(st) : -1;
+  b.accumulate = accumulate;
+  b.dgamma = dgamma;
+  b.dbeta = dbeta;
+  MSU_DISPATCH(dtype, T, rc = launch_bwd<T, MODE>(b, st, nparts));
+  if (rc || b.tail >= 0) return rc;
   if (dbeta == dgamma + a.C) {  // contiguous [dgamma | dbeta]: one reduction launch
     colsum(a.part, nparts, 2L * a.C, 2L * a.C, dgamma, accumulate, st);
   } else {
@@ -812,6 +833,8 @@ __global__ void __launch_bounds__(256) head_bwd16_kernel(const float* dlogit, co
 
 }  // namespace
 
+int g_msu_tail_on = 1;
+
 extern "C" {
 
 int msu_head_fwd(int dtype, const void* z, const float* gamma, const float* beta, const float* w,
@@ -905,6 +928,12 @@ int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const 
     case IN_D2S2: return bwd_dispatch<IN_D2S2>(dtype, a, dgamma, dbeta, nparts, accumulate, st);
   }
   return -3;
+}
+
+int msu_tail_reduce_mode(int mode) {
+  const int prev = g_msu_tail_on;
+  g_msu_tail_on = mode ? 1 : 0;
+  return prev;
 }
 
 int msu_reduce_rows(const float* part, int nparts, int n, long stride, float* out,

@@ -8,7 +8,12 @@
 // flight; wide ones (weight-gradient slabs) 8 part-lanes.  Several reductions over the same
 // parts (a weight slab and its bias) share one launch.
 #pragma once
+#include <mutex>
+
 #include "common.h"
+
+// in-kernel tail reductions on (1, default) / off (0: colsum launches); msu_tail_reduce_mode
+extern int g_msu_tail_on;
 
 namespace {
 
@@ -117,6 +122,110 @@ inline void colsum(const float* part, int nparts, long n, long stride, float* ou
                    hipStream_t st) {
   const ColSeg s{part, n, stride, out};
   colsum_multi(&s, 1, nparts, accumulate, st);
+}
+
+// ------------------------------------------------------------------ in-kernel tail reduction
+// The partial rows a kernel's blocks write, summed by the kernel itself instead of a colsum
+// launch.  A colsum launch queued behind the other stream's kernels waited for free CUs: the
+// LayerNorm parameter reductions took 15-43 us each on the main stream in the step for ~5 us of
+// work, the weight-gradient slab reductions up to 1 ms on the side stream (r05a profile).
+// Two levels, in a fixed order (deterministic, whatever the arrival order): part rows form groups
+// of TAIL_GS consecutive indices; the block drawing the last ticket of its group sums the group's
+// rows in index order into the group's first row; the block finishing the last group sums those
+// rows in group order and emits the result.
+// Hand-off (cdna_hip_programming.md "In-launch split-K reduction", its write-through form): the
+// partial rows are stored write-through (sc1: tail_st), every wave drains its stores (vmcnt(0)),
+// barrier, lane 0 draws a relaxed agent-scope ticket; the last arriver: lane 0 agent-scope acquire
+// + vmcnt(0), barrier, plain loads.  (An agent-scope release fence in every block instead wrote
+// back the whole L2 -- the kernel's dx too -- per block: the step ran 2.7 % slower, r05h.)
+// Counters: one region per stream (launches on one stream never overlap; a captured graph keeps
+// the regions of its capture streams), zero at load and left zero by every launch: the block
+// drawing a counter's last ticket resets it.
+constexpr int TAIL_GS = 32, TAIL_SLOTS = 64, TAIL_WORDS = 2048;
+__device__ int g_tail_cnt[TAIL_SLOTS * TAIL_WORDS];
+
+// the counter region of stream st (-1: every region taken; the caller falls back to colsum)
+inline int tail_slot(hipStream_t st) {
+  static std::mutex mu;
+  static hipStream_t owner[TAIL_SLOTS];
+  static int used = 0;
+  if (!g_msu_tail_on) return -1;
+  std::lock_guard<std::mutex> lk(mu);
+  for (int i = 0; i < used; ++i)
+    if (owner[i] == st) return i;
+  if (used == TAIL_SLOTS) return -1;
+  owner[used] = st;
+  return used++;
+}
+
+// write-through store of a partial-row value (4 B per lane: the natural width of these writers)
+MSU_DEV void tail_st(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+MSU_DEV void tail_st4(float* p, float4 v) {
+  tail_st(p, v.x);
+  tail_st(p + 1, v.y);
+  tail_st(p + 2, v.z);
+  tail_st(p + 3, v.w);
+}
+
+// true (in every thread) in the block that drew the last of `total` tickets at *cnt, after the
+// acquire; the block's partial rows stored by tail_st; flag: one int of the kernel's LDS
+// (kernels staging by LDS-DMA keep one LDS array)
+MSU_DEV bool tail_ticket(int* cnt, int total, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == total - 1;
+    if (last) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every ticket drawn
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+// Sum rows part[q * stride + i] (i < n) over q in [0, nparts), this block having written row p:
+// emit(i, float4) receives columns i .. i + 3 of the total in the block that finishes it.
+// n % 4 == 0, stride % 4 == 0, part 16-B aligned; cnt = g_tail_cnt + slot * TAIL_WORDS,
+// nparts <= TAIL_GS * (TAIL_WORDS - 1).
+template <typename Emit>
+MSU_DEV void tail_reduce(float* part, int p, int nparts, int n, long stride, int* cnt, int* flag, Emit&& emit) {
+  const int g = p / TAIL_GS, ng = (nparts + TAIL_GS - 1) / TAIL_GS;
+  const int q0 = g * TAIL_GS, q1 = min(nparts, q0 + TAIL_GS);
+  if (!tail_ticket(cnt + g, q1 - q0, flag)) return;
+  for (int i = 4 * (int)threadIdx.x; i < n; i += 4 * (int)blockDim.x) {
+    const float* r = part + (long)q0 * stride + i;
+    float4 s = *reinterpret_cast<const float4*>(r);
+#pragma unroll 8
+    for (int q = 1; q < q1 - q0; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(r + (long)q * stride);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    if (ng == 1) emit(i, s);
+    else tail_st4(part + (long)q0 * stride + i, s);
+  }
+  if (ng == 1 || !tail_ticket(cnt + ng, ng, flag)) return;
+  for (int i = 4 * (int)threadIdx.x; i < n; i += 4 * (int)blockDim.x) {
+    const float* r = part + i;
+    float4 s = *reinterpret_cast<const float4*>(r);
+#pragma unroll 8
+    for (int h = 1; h < ng; ++h) {
+      const float4 v = *reinterpret_cast<const float4*>(r + (long)h * TAIL_GS * stride);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    emit(i, s);
+  }
+}
+
+MSU_DEV void acc_store4(float* o, float4 s, int accumulate) {
+  if (accumulate) {
+    const float4 v = *reinterpret_cast<const float4*>(o);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  *reinterpret_cast<float4*>(o) = s;
 }
 
 }  // namespace
