@@ -68,6 +68,29 @@ for s in "$@"; do
       done
       cat $O/${TAG}_kern.log ;;
     ab_conv_side) bash $R/tools/gpu_bench_ab.sh ${TAG}_convside "" "MSU_CONV_SIDE=0" "" "MSU_CONV_SIDE=0" "" "MSU_CONV_SIDE=0" || exit 3 ;;
+    conv_exp)
+      # refine-conv kernel times with ablation builds (tools/build_exp.sh conv3x3 64 128 256 512)
+      for X in ${CONV_EXP:-0 64 128 256 512}; do
+        L=""; [ $X != 0 ] && L=$R/tools/exp/libmsunet_conv3x3_$X.so
+        for args in "1 6 bwd" "0 6 fwd act"; do
+          d=$O/${TAG}_convexp_${X}_${args// /_}
+          MSU_LIB_OVERRIDE=$L timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $d -o p --output-format csv -- python3 $R/tools/conv_one.py $args > /dev/null 2>&1 || exit 3
+          python3 $R/tools/kstats.py $d/p_kernel_stats.csv conv3x3 $X >> $O/${TAG}_conv_exp.log
+        done
+      done
+      cat $O/${TAG}_conv_exp.log ;;
+    conv_tests) step conv_tests 900 $PYT -m gpu $R/tests/test_gpu_ops.py $R/tests/test_gpu_ln_side.py $R/tests/test_gpu_production_parity.py ;;
+    conv_kern)
+      # refine-conv kernel times, this build vs an override library (CONV_B)
+      for L in "" "$CONV_B"; do
+        for args in "1 6 bwd" "0 6 fwd act" "1 6 fwd"; do
+          d=$O/${TAG}_convk_$(basename "${L:-cur}" .so)_${args// /_}
+          MSU_LIB_OVERRIDE=$L timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $d -o p --output-format csv -- python3 $R/tools/conv_one.py $args > /dev/null 2>&1 || exit 3
+          python3 $R/tools/kstats.py $d/p_kernel_stats.csv conv3x3 "${L:+B}" >> $O/${TAG}_conv_kern.log
+        done
+      done
+      cat $O/${TAG}_conv_kern.log ;;
+    ab_lib) bash $R/tools/gpu_bench_ab.sh ${TAG}_lib "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" || exit 3 ;;
     tail_tests) step tail_tests 600 $PYT -m gpu $R/tests/test_gpu_tail_reduce.py $R/tests/test_gpu_ln_side.py ;;
     ab_tail) bash $R/tools/gpu_bench_ab.sh ${TAG}_tail "" "MSU_TAIL=0" "" "MSU_TAIL=0" "" "MSU_TAIL=0" || exit 3 ;;
     ab_fused) bash $R/tools/gpu_bench_ab.sh ${TAG}_fused "" "MSU_ATTN_QKV=0" "" "MSU_ATTN_QKV=0" "" "MSU_ATTN_QKV=0" || exit 3 ;;
