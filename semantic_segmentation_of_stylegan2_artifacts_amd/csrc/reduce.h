@@ -187,14 +187,15 @@ MSU_DEV bool tail_ticket(int* cnt, int total, int* flag) {
   return *flag != 0;
 }
 
-// Sum rows part[q * stride + i] (i < n) over q in [0, nparts), this block having written row p:
-// emit(i, float4) receives columns i .. i + 3 of the total in the block that finishes it.
-// n % 4 == 0, stride % 4 == 0, part 16-B aligned; cnt = g_tail_cnt + slot * TAIL_WORDS,
-// nparts <= TAIL_GS * (TAIL_WORDS - 1).
+// Sum rows part[q * stride + i] (i < n) over q in [0, nparts), this block having written row p
+// (by tail_st): emit(i, float4) receives columns i .. i + 3 of the total in the block that
+// finishes it.  n % 4 == 0, stride % 4 == 0, part 16-B aligned; groups of gs rows; cnt: the
+// ceil(nparts / gs) + 1 counters of this reduction (in g_tail_cnt + slot * TAIL_WORDS).
 template <typename Emit>
-MSU_DEV void tail_reduce(float* part, int p, int nparts, int n, long stride, int* cnt, int* flag, Emit&& emit) {
-  const int g = p / TAIL_GS, ng = (nparts + TAIL_GS - 1) / TAIL_GS;
-  const int q0 = g * TAIL_GS, q1 = min(nparts, q0 + TAIL_GS);
+MSU_DEV void tail_reduce(float* part, int p, int nparts, int n, long stride, int* cnt, int* flag, Emit&& emit,
+                         int gs = TAIL_GS) {
+  const int g = p / gs, ng = (nparts + gs - 1) / gs;
+  const int q0 = g * gs, q1 = min(nparts, q0 + gs);
   if (!tail_ticket(cnt + g, q1 - q0, flag)) return;
   for (int i = 4 * (int)threadIdx.x; i < n; i += 4 * (int)blockDim.x) {
     const float* r = part + (long)q0 * stride + i;
@@ -213,7 +214,7 @@ MSU_DEV void tail_reduce(float* part, int p, int nparts, int n, long stride, int
     float4 s = *reinterpret_cast<const float4*>(r);
 #pragma unroll 8
     for (int h = 1; h < ng; ++h) {
-      const float4 v = *reinterpret_cast<const float4*>(r + (long)h * TAIL_GS * stride);
+      const float4 v = *reinterpret_cast<const float4*>(r + (long)h * gs * stride);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     emit(i, s);

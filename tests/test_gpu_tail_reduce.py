@@ -1,6 +1,6 @@
 """GPU: the LayerNorm parameter-gradient partials summed inside the backward kernel (reduce.h
-tail_reduce: the last block of each group of 32 partial rows sums its group, the last group
-sums the groups, in a fixed order) against the separate colsum launch (msu_tail_reduce_mode(0)).
+tail_reduce: the last block of each group of 32 partial rows sums its group, the last group sums
+the groups, in a fixed order) against the separate colsum launch (msu_tail_reduce_mode(0)):
 
 * dgamma / dbeta agree with the colsum path to f32 rounding (a different but fixed summation
   order) and with an f64 sum of the LayerNorm gradient definition; dx is untouched (bitwise);
@@ -146,3 +146,4 @@ def test_misaligned_output_falls_back_to_colsum():
             torch.cuda.synchronize()
             res[mode] = (wp.grad.clone(), bp.grad.clone())
     assert torch.equal(res[1][0], res[0][0]) and torch.equal(res[1][1], res[0][1])
+

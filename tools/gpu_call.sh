@@ -91,7 +91,8 @@ for s in "$@"; do
       done
       cat $O/${TAG}_conv_kern.log ;;
     ab_lib) bash $R/tools/gpu_bench_ab.sh ${TAG}_lib "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" || exit 3 ;;
-    tail_tests) step tail_tests 600 $PYT -m gpu $R/tests/test_gpu_tail_reduce.py $R/tests/test_gpu_ln_side.py ;;
+    tail_tests) step tail_tests 600 $PYT -m gpu $R/tests/test_gpu_tail_reduce.py $R/tests/test_gpu_ln_side.py \
+                  $R/tests/test_gpu_tok_gemm.py $R/tests/test_gpu_linbwd.py ;;
     ab_tail) bash $R/tools/gpu_bench_ab.sh ${TAG}_tail "" "MSU_TAIL=0" "" "MSU_TAIL=0" "" "MSU_TAIL=0" || exit 3 ;;
     ab_fused) bash $R/tools/gpu_bench_ab.sh ${TAG}_fused "" "MSU_ATTN_QKV=0" "" "MSU_ATTN_QKV=0" "" "MSU_ATTN_QKV=0" || exit 3 ;;
     determ) step determ 600 python -u $R/tools/determinism_matrix.py 24 default ;;
