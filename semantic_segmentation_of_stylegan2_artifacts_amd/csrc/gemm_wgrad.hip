@@ -392,7 +392,7 @@ inline WavePlan wave_plan(long M, int N, int K) {
   const long tiles = (long)(nt / p.wn) * (kt / p.wk);
   // workgroup target: one per CU (no tail wave), long row ranges (128 / 512 measured no better
   // for the stage 2-3 shapes, r03x)
-  long s = 256 / tiles;
+  long s = ((MSU_EXP & 512) ? 128 : 256) / tiles;  // (ablation 512: half the splits)
   const long max_s = (M + 8 * rs - 1) / (8 * rs);  // at least 8 stages per split
   if (s > max_s) s = max_s;
   if (s < 1) s = 1;

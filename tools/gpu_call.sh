@@ -90,6 +90,9 @@ for s in "$@"; do
         done
       done
       cat $O/${TAG}_conv_kern.log ;;
+    ab_wgrad) bash $R/tools/gpu_bench_ab.sh ${TAG}_wgrad "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_256.so" \
+                "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_512.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_256.so" \
+                "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_512.so" || exit 3 ;;
     ab_lib) bash $R/tools/gpu_bench_ab.sh ${TAG}_lib "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" || exit 3 ;;
     tail_tests) step tail_tests 600 $PYT -m gpu $R/tests/test_gpu_tail_reduce.py $R/tests/test_gpu_ln_side.py \
                   $R/tests/test_gpu_tok_gemm.py $R/tests/test_gpu_linbwd.py ;;
