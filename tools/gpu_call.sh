@@ -93,6 +93,17 @@ for s in "$@"; do
     ab_wgrad) bash $R/tools/gpu_bench_ab.sh ${TAG}_wgrad "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_256.so" \
                 "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_512.so" "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_256.so" \
                 "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_gemm_wgrad_512.so" || exit 3 ;;
+    conv_env)
+      # refine-conv kernel times under two environments (CONV_ENV_B, e.g. MSU_CONV_V5=0)
+      for E in "NOENV=1" "$CONV_ENV_B"; do
+        for args in "1 6 fwd act" "0 6 fwd act" "1 6 bwd"; do
+          d=$O/${TAG}_conve_${E%%=*}_${args// /_}
+          env $E timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $d -o p --output-format csv -- python3 $R/tools/conv_one.py $args > /dev/null 2>&1 || exit 3
+          python3 $R/tools/kstats.py $d/p_kernel_stats.csv conv3x3 "${E%%=*}" >> $O/${TAG}_conv_env.log
+        done
+      done
+      cat $O/${TAG}_conv_env.log ;;
+    ab_env) bash $R/tools/gpu_bench_ab.sh ${TAG}_env "" "$AB_ENV" "" "$AB_ENV" "" "$AB_ENV" || exit 3 ;;
     ab_lib) bash $R/tools/gpu_bench_ab.sh ${TAG}_lib "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" || exit 3 ;;
     tail_tests) step tail_tests 600 $PYT -m gpu $R/tests/test_gpu_tail_reduce.py $R/tests/test_gpu_ln_side.py \
                   $R/tests/test_gpu_tok_gemm.py $R/tests/test_gpu_linbwd.py ;;
