@@ -118,9 +118,6 @@ int msu_win_attn_bwd_tail(int dtype, float* workspace, float* dtable, float* dqk
  * (model_parts.py:464-465).  Wt: [9][Cout][roundup(Cin,32)] in the activation dtype. */
 int msu_conv3x3_fwd(int dtype, int in_mode, const void* X, const void* Wt, const float* bias,
                     void* Y, int B, int H, int W, int Cin, int Cout, void* stream);
-/* 1 (default): the C = 96 refine-conv forward launches run the v5 kernel (output-channel halves
- * with resident weights); 0: the v3 kernel (A/B switch MSU_CONV_V5).  Returns the previous mode. */
-int msu_conv_mode(int v5);
 /* As msu_conv3x3_fwd; Y2 (may be null; only with in_mode bit0 clear) receives GELU(Y) from
  * the same epilogue, so the next refine conv loads its activation instead of converting its
  * halo (model_parts.py:469: refine2(act(refine1(.)))). */

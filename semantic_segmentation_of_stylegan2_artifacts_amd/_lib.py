@@ -26,7 +26,6 @@ SIGNATURES = {
     "msu_layernorm_bwd": (I, [I, I, P, P, P, P, P, P, P, P, P, L, P, I, P, P, L, I, I, I, I, I, P]),
     "msu_reduce_rows": (I, [P, I, I, L, P, I, P]),
     "msu_tail_reduce_mode": (I, [I]),
-    "msu_conv_mode": (I, [I]),
     "msu_head_fwd": (I, [I, P, P, P, P, P, P, P, L, I, F, P]),
     "msu_head_bwd": (I, [I, P, P, P, P, P, P, P, P, P, I, P, P, P, L, I, P]),
     "msu_win_count": (L, [I, I, I]),
@@ -105,7 +104,6 @@ def lib():
     # the library-side A/B switches (the C code reads no environment; switches.py does)
     h.msu_nt_gemm_mode(1 if switches.on("MSU_NT_PP") else 0)
     h.msu_tail_reduce_mode(1 if switches.on("MSU_TAIL") else 0)
-    h.msu_conv_mode(1 if switches.on("MSU_CONV_V5") else 0)
     _lib = h
     return _lib
 

@@ -24,10 +24,6 @@
 #define MSU_EXP 0
 #endif
 
-// 1 (default): the refine-conv forward / backward-data launches on the v5 kernel (resident
-// weights per channel half); 0: v3.  Set through msu_conv_mode (A/B switch MSU_CONV_V5).
-extern int g_msu_conv_v5;
-
 namespace {
 
 constexpr int TW = 16;  // output tile width (pixels) = one MFMA M tile
@@ -1387,12 +1383,9 @@ int launch_v3s(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float
   return MSU_CHECK_LAUNCH();
 }
 
-#include "conv3x3_v5.h"
-
 template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL>
 int launch_v3(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S, bf16_t* Y,
               bf16_t* Y2, hipStream_t st) {
-  if (g_msu_conv_v5) return launch_v5<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL>(g, X, Wt, bias, S, Y, Y2, st);
   // Forward launches on 16x16x32 MFMA (same tile, LDS images and schedule; (p >> 1) & 3
   // swizzle), since round 4: same-box kbench (r04b) conv1 2.22-2.28 vs 2.44 ms, conv2 1.48 vs
   // 1.55 ms (bare MFMA loops of this shape run at ~1.12-1.15x the FLOP/s of 32x32x16 on MI355X at

@@ -1,15 +1,7 @@
 // Refine-conv forward and backward-data entry points (kernels: conv3x3.h).
 #include "conv3x3.h"
 
-int g_msu_conv_v5 = 1;
-
 extern "C" {
-
-int msu_conv_mode(int v5) {
-  const int prev = g_msu_conv_v5;
-  g_msu_conv_v5 = v5 ? 1 : 0;
-  return prev;
-}
 
 // in_mode bit 0: GELU on the loaded input, bit 1: input is the pre-d2s [B,H/4,W/4,16*Cin]
 // tensor.  Wt: [9][Cout][CinP] (CinP = roundup(Cin, 32), zero padded), dtype of X.

@@ -27,8 +27,6 @@ SWITCHES = {
                       "DESIGN 7 (r04s: side +0.2 %)"),
     "MSU_TAIL": ("1", "0: LayerNorm parameter-gradient partials summed by a colsum launch, not in the kernel",
                  "DESIGN 7 (r05i: +0.5 %, host -4 ms/step)"),
-    "MSU_CONV_V5": ("1", "0: the refine-conv forward on the v3 kernel (weights re-staged per tap)",
-                    "DESIGN 7 (round 5)"),
     "MSU_GRAPH": ("auto", "HIP-graph replay of the step: 1 / 0 / auto (replay when launch-bound)",
                   "DESIGN 4b (512^2: 401 vs 249-307 img/s)"),
     "MSU_GRAPH_SIDE": ("0", "1: fork the side stream into the captured graph (nondeterministic on ROCm 7.2)",
