@@ -13,6 +13,11 @@
 #include "common.h"
 #include "reduce.h"
 
+// MSU_EXP: ablation bits for timing experiments only (tools/build_exp.sh); 0 in every real build
+#ifndef MSU_EXP
+#define MSU_EXP 0
+#endif
+
 namespace {
 
 enum InMode { IN_PLAIN = 0, IN_ADD = 1, IN_MERGE = 2, IN_D2S2 = 3 };
@@ -483,6 +488,9 @@ int launch_fwd(const LnArgs& a, hipStream_t st, int max_blocks) {
   // up to C = 128, +0.25 % more up to C = 512 (r01, 3 of 3 pairs); the next row of a group
   // prefetched (r04y: +0.2 %)
   if (nchunk <= 16) return go(ln_fwd_kernel<T, MODE, 16, 1>, 16);
+  if constexpr ((MSU_EXP & 8) != 0) {  // ablation: C = 192 rows as 8 lanes x 3 chunks
+    if (nchunk <= 24 && nchunk > 16) return go(ln_fwd_kernel<T, MODE, 8, 3>, 8);
+  }
   if (nchunk <= 32) return go(ln_fwd_kernel<T, MODE, 32, 1>, 32);
   if (nchunk <= 64) return go(ln_fwd_kernel<T, MODE, 64, 1>, 64);
   if (nchunk <= 4 * 4) return go(ln_fwd_kernel<T, MODE, 4, 4>, 4);
@@ -890,7 +898,8 @@ int msu_ln_part_blocks(long rows, int C) {
   // (512 / 256: 168.2 / 162.5 vs 170.0 img/s, r04t); C >= 384 (stages 2-3, whose partials are 2C
   // wide and whose reductions run on the main stream): 512 (170.5 / 170.4 vs 169.8 / 169.8 with
   // 1024, 256: 168.7 / 168.6; r04v)
-  constexpr long cap = 1024, cap_deep = 512;
+  constexpr long cap = (MSU_EXP & 2) ? 4096 : ((MSU_EXP & 1) ? 2048 : 1024);
+  constexpr long cap_deep = (MSU_EXP & 2) ? 2048 : ((MSU_EXP & 1) ? 1024 : 512);
   long nb = (rows + 15) / 16;
   if (nb > cap) nb = cap;
   if (C >= 384 && nb > cap_deep) nb = cap_deep;

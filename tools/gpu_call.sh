@@ -104,6 +104,19 @@ for s in "$@"; do
       done
       cat $O/${TAG}_conv_env.log ;;
     ab_env) bash $R/tools/gpu_bench_ab.sh ${TAG}_env "" "$AB_ENV" "" "$AB_ENV" "" "$AB_ENV" || exit 3 ;;
+    ln_exp)
+      for X in ${LN_EXP:-0 1 2 8}; do
+        L=""; [ $X != 0 ] && L=$R/tools/exp/libmsunet_layernorm_$X.so
+        echo "== MSU_EXP=$X" >> $O/${TAG}_ln_exp.log
+        for K in ln lnadd; do
+          MSU_LIB_OVERRIDE=$L timeout -k 10 200 python -u $R/tools/kbench.py $K >> $O/${TAG}_ln_exp.log 2>&1 || exit 3
+        done
+      done
+      cat $O/${TAG}_ln_exp.log ;;
+    ab_ln) bash $R/tools/gpu_bench_ab.sh ${TAG}_ln "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_1.so" \
+             "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_2.so" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_8.so" \
+             "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_1.so" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_2.so" \
+             "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_8.so" || exit 3 ;;
     ab_lib) bash $R/tools/gpu_bench_ab.sh ${TAG}_lib "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" || exit 3 ;;
     tail_tests) step tail_tests 600 $PYT -m gpu $R/tests/test_gpu_tail_reduce.py $R/tests/test_gpu_ln_side.py \
                   $R/tests/test_gpu_tok_gemm.py $R/tests/test_gpu_linbwd.py ;;
