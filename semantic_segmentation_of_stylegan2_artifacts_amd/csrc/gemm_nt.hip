@@ -29,6 +29,11 @@
 #include "common.h"
 #include "mfma_frag.h"
 
+// MSU_EXP: ablation bits for timing experiments only (tools/build_exp.sh); 0 in every real build
+#ifndef MSU_EXP
+#define MSU_EXP 0
+#endif
+
 namespace {
 
 constexpr int BN = 128, BK = 64;  // N tile and K step of the KN form
@@ -322,6 +327,10 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
             }
           }
           const u32x4 pk = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
+          // ablation 16: no output stores (results wrong; the never-true test keeps the MFMAs).
+          // These 16-B stores cover 32 tokens x 32 B per instruction; an epilogue staged through
+          // the consumed ring stage and stored as 192-B row pieces was neutral (r05z).
+          if constexpr ((MSU_EXP & 16) != 0) if (v[0] != 1.2345e-30f) continue;
           *reinterpret_cast<u32x4*>(a.Y + off) = pk;
           if constexpr (EPI == EPI_GELU_DUAL) {
             // GELU of the rounded pre-activation, as the unfused GELU kernel would see it

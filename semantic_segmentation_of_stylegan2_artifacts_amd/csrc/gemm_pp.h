@@ -235,7 +235,9 @@ __global__ void __launch_bounds__(512) gemm_pp_kernel(NtArgs a) {
   constexpr int D = EPI == EPI_GELU_DUAL ? 2 : 1;    // stores per put
   auto put = [&](auto II) __attribute__((always_inline)) {
     constexpr int m = decltype(II)::value / (NT / 2), q = decltype(II)::value % (NT / 2);
-    if constexpr (MSU_EXP & 8) return;  // ablation: no output stores (results wrong)
+    // ablation: no output stores (results wrong; this also leaves the MFMAs dead code, so it
+    // times neither stores nor MFMAs: r05g's "no-store" numbers are no-store-no-MFMA ones)
+    if constexpr (MSU_EXP & 8) return;
     const size_t off = (size_t)(o_m0 + 64 * wq + 16 * m + l15) * a.N + o_n0 + grp * HB + 32 * q + cofs;
     *reinterpret_cast<u32x4*>(a.Y + off) = outp[m][q];
     if constexpr (EPI == EPI_GELU_DUAL) {

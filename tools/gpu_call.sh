@@ -117,6 +117,7 @@ for s in "$@"; do
              "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_2.so" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_8.so" \
              "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_1.so" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_2.so" \
              "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_8.so" || exit 3 ;;
+    nt_store) step nt_store 400 bash $R/tools/nt_store_ab.sh ;;
     ab_lib) bash $R/tools/gpu_bench_ab.sh ${TAG}_lib "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" || exit 3 ;;
     tail_tests) step tail_tests 600 $PYT -m gpu $R/tests/test_gpu_tail_reduce.py $R/tests/test_gpu_ln_side.py \
                   $R/tests/test_gpu_tok_gemm.py $R/tests/test_gpu_linbwd.py ;;
