@@ -22,6 +22,7 @@
 // columns so that every lane stores whole 16-B pieces of its token's rows; relative-bias
 // gradients accumulate in registers in the bias-image layout; padded tokens' dq/dk/dv go
 // to the qkv-bias partial.
+#include <type_traits>
 #include <utility>
 
 #include "common.h"
@@ -96,6 +97,28 @@ MSU_DEV bf16x8 frag_tr_q4(const bf16_t* img, int ld, int r0, int col0, int lane)
   return *reinterpret_cast<bf16x8*>(both);
 }
 
+// Row of a 16-row block staged by lane quad qd = lane >> 2 (4 lanes x 16 B per 64-B row).
+// ds_write_b128 banks 8 consecutive lanes (two quads) on (a/4) mod 32: at the 20-dword row
+// stride rows r and r + 4 fill disjoint banks, r and r + 1 overlap (2-way), so quads 2k, 2k + 1
+// take rows k', k' + 4.
+MSU_DEV constexpr int stage_row(int qd) { return ((qd & 1) << 2) | ((qd >> 1) & 3) | (qd & 8); }
+// Same for ds_read_b128 of staged rows (lane groups {0-3, 12-15, 20-27}, ... on (a/4) mod 64):
+// a group's four quads take rows a, a + 4, a + 8, a + 12.
+MSU_DEV int read_row(int qd) { return (int)((0xfeab6732dc894510ull >> (4 * qd)) & 15); }
+
+// frag_tr_q4 on an image whose rows with bit 3 set hold their 8-B column granules (4
+// values) pairwise swapped (granule ^ 1): the Pd image, written by 16-lane groups of 16
+// consecutive rows (ds_write_b64 banks on (a/4) mod 32: rows i and i + 8 collide at a
+// 36-dword stride; the swap moves i + 8 onto the other granule of the pair)
+MSU_DEV int pswz(int i) { return (i >> 3) & 1; }
+MSU_DEV bf16x8 frag_tr_q4_swz(const bf16_t* img, int ld, int r0, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3, h = lane >> 5;
+  const int row = r0 + 4 * q + 2 * h;
+  const int col = ((((col0 + 16 * (g & 1)) >> 2) + p) ^ pswz(row)) << 2;  // rows row, row + 1: same bit 3
+  v4s both[2] = {tr_read(img + row * ld + col), tr_read(img + (row + 1) * ld + col)};
+  return *reinterpret_cast<bf16x8*>(both);
+}
+
 // accumulator registers 8s..8s+7 -> 16-bit fragment
 template <typename T>
 MSU_DEV bf16x8 pack8(const f32x16& a, int s) {
@@ -130,9 +153,33 @@ MSU_DEV bool window_tokens(const Geom& g, long win_l, int* sTok, int* sReg, int 
   return (g.sh + g.sw) > 0 && (wy == g.nWy - 1 || wx == g.nWx - 1);
 }
 
-// x where bit n of m is set, else +0 (the bit shifted into the sign, spread, ANDed: no VCC)
-MSU_DEV float keep_sel(uint32_t m, int n, float x) {
-  return __int_as_float(((int)(m << (31 - n)) >> 31) & __float_as_int(x));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2_v __attribute__((ext_vector_type(2)));
+
+// keep factor of bit N of m: s where the bit is set, +0 where clear.  v_bfe_i32 spreads the
+// bit over the word and an AND keeps s's bits: two VALU ops and no lane mask (the compiler's
+// select form kept one SGPR-pair compare mask per key live and spilled SGPRs to VGPR lanes)
+template <int N>
+MSU_DEV float keep_factor(uint32_t m, float s) {
+  int b;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(b) : "v"(m), "n"(N));
+  return __int_as_float(b & __float_as_int(s));
+}
+
+// two values -> one packed 16-bit pair with one v_cvt_pk_{bf16,f16}_f32 (RNE, as pack2)
+template <typename T>
+MSU_DEV uint32_t pack2v(f32x2 v) {
+  if constexpr (std::is_same<T, f16_t>::value)
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2_v));
+  else
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_v));
+}
+
+MSU_DEV f32x2 pair(const f32x16& a, int r) { return f32x2{a[r], a[r + 1]}; }
+MSU_DEV void set_pair(f32x16& a, int r, f32x2 v) {
+  a[r] = v.x;
+  a[r + 1] = v.y;
 }
 
 // Accumulator register r of key tile jt holds key jt*32 + crow(r, hh): for jt = 1 and r >= 9
@@ -176,25 +223,54 @@ MSU_DEV void softmax_col(f32x16 (&P)[2], float scale) {
   m = fmaxf(m, __shfl_xor(m, 32, 64));
   const float c = scale * 1.44269504088896341f;
   const float mc = m * c;
-  float sum = 0.f;
+  // pairs of registers on the packed f32 ops (v_pk_fma / v_pk_add / v_pk_mul)
+  const f32x2 c2 = {c, c}, nmc2 = {-mc, -mc};
+  f32x2 sum2 = {0.f, 0.f};
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if (live_key(jt, r)) {
+    for (int r = 0; r < 16; r += 2) {
+      if (live_key(jt, r + 1)) {
+        const f32x2 x = __builtin_elementwise_fma(pair(P[jt], r), c2, nmc2);
+        const f32x2 e = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+        set_pair(P[jt], r, e);
+        sum2 += e;
+      } else if (live_key(jt, r)) {
         P[jt][r] = __builtin_amdgcn_exp2f(fmaf(P[jt][r], c, -mc));
-        sum += P[jt][r];
+        P[jt][r + 1] = 0.f;
+        sum2.x += P[jt][r];
       } else {
-        P[jt][r] = 0.f;
+        P[jt][r] = P[jt][r + 1] = 0.f;
       }
     }
+  float sum = sum2.x + sum2.y;
   sum += __shfl_xor(sum, 32, 64);
   const float inv = 1.0f / sum;
+  const f32x2 inv2 = {inv, inv};
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      if (live_key(jt, r)) P[jt][r] *= inv;
+    for (int r = 0; r < 16; r += 2) {
+      if (live_key(jt, r + 1)) set_pair(P[jt], r, pair(P[jt], r) * inv2);
+      else if (live_key(jt, r)) P[jt][r] *= inv;
+    }
+}
+
+// dropout of one query-column tile: P * keep / (1 - p) on register pairs (keep_factor + one
+// v_pk_mul_f32 per pair; keep bit jt*16 + r as drop_bits lays them out)
+MSU_DEV void drop_scale(f32x16 (&P)[2], uint32_t kmask, float kscale) {
+  static_for([&](auto JT) {
+    constexpr int jt = decltype(JT)::value;
+    static_for([&](auto RP) {
+      constexpr int r = 2 * decltype(RP)::value;
+      if constexpr (live_key(jt, r + 1)) {
+        const f32x2 kf = {keep_factor<jt * 16 + r>(kmask, kscale), keep_factor<jt * 16 + r + 1>(kmask, kscale)};
+        set_pair(P[jt], r, pair(P[jt], r) * kf);
+      } else if constexpr (live_key(jt, r)) {
+        P[jt][r] *= keep_factor<jt * 16 + r>(kmask, kscale);
+      }
+    }, std::make_integer_sequence<int, 8>{});
+  }, std::make_integer_sequence<int, 2>{});
 }
 
 // shifted-window mask of one query-column tile: -100/scale where query and key regions differ
@@ -272,7 +348,7 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
     const int cq = h * HD + 8 * (lane & 3), ck = g.C + cq, cv = 2 * g.C + cq;
     static_for([&](auto CI) {
       constexpr int c = decltype(CI)::value;
-      const bf16_t* rb = rowbase(L.tok[buf][(lane >> 2) + 16 * c]);
+      const bf16_t* rb = rowbase(L.tok[buf][stage_row(lane >> 2) + 16 * c]);
       if constexpr ((MSU_EXP & 16) != 0) {  // ablation: no q / k / v loads (compute-side time)
         const uint32_t f = 0x3c003c00u + (uint32_t)(lane & 7) + (uint32_t)c;
         kr[buf][c] = u32x4{f, f + 1, f + 2, f + 3};
@@ -294,7 +370,7 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
     // K / Q / V rows of this item -> LDS (the previous item's reads are complete: lds_sync below)
     static_for([&](auto CI) {
       constexpr int c = decltype(CI)::value;
-      const int o = ((lane >> 2) + 16 * c) * LD + (lane & 3) * 8;
+      const int o = (stage_row(lane >> 2) + 16 * c) * LD + (lane & 3) * 8;
       *reinterpret_cast<u32x4*>(L.k + o) = kr[buf][c];
       *reinterpret_cast<u32x4*>(L.q + o) = qr[buf][c];
       *reinterpret_cast<u32x4*>(L.v + o) = vr[buf][c];
@@ -341,16 +417,9 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
       }
       if (bnd[buf]) mask_col(P, L.reg[buf], it, scale, lane);
       softmax_col(P, scale);
-      if constexpr (DROP) {
-        // select-and-scale per element: measured 17 % faster here than folding 1/(1-p) into the
-        // normaliser and masking with keep_sel (150 vs 180 us at stage 0)
-        const float kscale = 1.0f / (1.0f - p_drop);
-#pragma unroll
-        for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (live_key(jt, r)) P[jt][r] = (kmasks[it] >> (jt * 16 + r)) & 1u ? P[jt][r] * kscale : 0.f;
-      }
+      // (a per-element select-and-scale measured 17 % faster here than folding 1/(1-p) into the
+      // normaliser and masking with keep_sel, 150 vs 180 us at stage 0)
+      if constexpr (DROP) drop_scale(P, kmasks[it], 1.0f / (1.0f - p_drop));
       // O^T[d][i] = sum_j V[j][d] P^T[j][i]: P^T is the B operand straight from the registers
       f32x16 O = f32x16{0};
 #pragma unroll
@@ -374,7 +443,7 @@ __global__ void __launch_bounds__(64 * WAVES, 2) attn_fwd_mfma(const bf16_t* __r
     int otok[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const int t = (lane >> 2) + 16 * c;
+      const int t = read_row(lane >> 2) + 16 * c;
       otok[c] = L.tok[buf][t];
       ov[c] = *reinterpret_cast<const u32x4*>(L.q + t * LD + 8 * (lane & 3));
     }
@@ -525,7 +594,7 @@ __global__ void __launch_bounds__(128 * HPW, HPW == 3 ? 1 : 2) attn_bwd_mfma(
     static_for([&](auto CI) {
       constexpr int c = decltype(CI)::value;
       int rg;  // (a __shfl of tokt from lane (lane>>2) + 16c measured no faster)
-      const int tok = token_of(g, win, 32 * w + (lane >> 2) + 16 * c, &rg);
+      const int tok = token_of(g, win, 32 * w + stage_row(lane >> 2) + 16 * c, &rg);
       const bf16_t* rb = rowbase(tok);
       rq[buf][c] = *reinterpret_cast<const u32x4*>(rb + cq + o);
       rk[buf][c] = *reinterpret_cast<const u32x4*>(rb + ck + o);
@@ -538,7 +607,7 @@ __global__ void __launch_bounds__(128 * HPW, HPW == 3 ? 1 : 2) attn_bwd_mfma(
     constexpr int buf = decltype(BUF)::value;
     static_for([&](auto CI) {
       constexpr int c = decltype(CI)::value;
-      const int off = (32 * w + (lane >> 2) + 16 * c) * LD + 8 * (lane & 3);
+      const int off = (32 * w + stage_row(lane >> 2) + 16 * c) * LD + 8 * (lane & 3);
       *reinterpret_cast<u32x4*>(L.q + off) = rq[buf][c];
       *reinterpret_cast<u32x4*>(L.k + off) = rk[buf][c];
       *reinterpret_cast<u32x4*>(L.v + off) = rv[buf][c];
@@ -601,44 +670,66 @@ __global__ void __launch_bounds__(128 * HPW, HPW == 3 ? 1 : 2) attn_bwd_mfma(
     }
     if (boundary) mask_col(P, sReg, it, scale, lane);
     softmax_col(P, scale);
-    float delta = 0.f;
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (!live_key(jt, r)) continue;  // P = 0: no share of delta, dS = 0
-        if constexpr (DROP)  // dP = dPd * keep/(1-p)
-          D[jt][r] = keep_sel(kmask, jt * 16 + r, D[jt][r] * kscale);
-        delta += P[jt][r] * D[jt][r];
-      }
-    delta += __shfl_xor(delta, 32, 64);
-    // Pd and dS images [i][j], 4 consecutive j per 8-byte store
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        float pd[4], ds[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = 4 * gq + e;
-          if (!live_key(jt, r)) {
-            ds[e] = pd[e] = 0.f;
-            continue;
-          }
-          const float p = P[jt][r];
-          ds[e] = p * (D[jt][r] - delta);
-          pd[e] = DROP ? keep_sel(kmask, jt * 16 + r, p * kscale) : p;
-          dB[jt][r] += ds[e];
+    // Pd and dS images [i][j], 4 consecutive j (registers 4gq .. 4gq + 3) per 8-byte store, on
+    // register pairs (packed f32 ops).  Pass 1: dP = dPd keep / (1 - p), Pd = P keep / (1 - p)
+    // (-> the Pd image) and delta = sum_j P dP; pass 2: dS = P (dP - delta) (-> the dS image,
+    // dB).  Group gq = 3 of key tile 1 (keys 56 .. 63) is padding in every window: its image
+    // words were zeroed once before the window loop.
+    f32x2 dl = {0.f, 0.f};
+    static_for([&](auto JT) {
+      constexpr int jt = decltype(JT)::value;
+      static_for([&](auto GQ) {
+        constexpr int gq = decltype(GQ)::value;
+        if constexpr (jt == 0 || gq < 3) {
+          f32x2 pd[2];
+          static_for([&](auto E2) {
+            constexpr int r = 4 * gq + 2 * decltype(E2)::value;
+            if constexpr (live_key(jt, r)) {
+              f32x2 p = pair(P[jt], r), d = pair(D[jt], r);
+              if constexpr (!live_key(jt, r + 1)) p.y = d.y = 0.f;  // key 49 .. (P = 0)
+              if constexpr (DROP) {
+                const f32x2 kf = {keep_factor<jt * 16 + r>(kmask, kscale), keep_factor<jt * 16 + r + 1>(kmask, kscale)};
+                d *= kf;
+                pd[decltype(E2)::value] = p * kf;
+              } else {
+                pd[decltype(E2)::value] = p;
+              }
+              dl = __builtin_elementwise_fma(p, d, dl);
+              set_pair(D[jt], r, d);
+            } else {
+              pd[decltype(E2)::value] = f32x2{0.f, 0.f};
+            }
+          }, std::make_integer_sequence<int, 2>{});
+          const uint2 wp = {pack2v<T>(pd[0]), pack2v<T>(pd[1])};
+          *reinterpret_cast<uint2*>(L.P + i * LDP + jt * 32 + 8 * gq + 4 * (hh ^ pswz(i))) = wp;
         }
-        const int j0 = jt * 32 + 8 * gq + 4 * hh;
-        uint2 wp, wd;
-        wp.x = pack2<T>(pd[0], pd[1]);
-        wp.y = pack2<T>(pd[2], pd[3]);
-        wd.x = pack2<T>(ds[0], ds[1]);
-        wd.y = pack2<T>(ds[2], ds[3]);
-        *reinterpret_cast<uint2*>(L.P + i * LDP + j0) = wp;
-        *reinterpret_cast<uint2*>(L.dS + i * LDP + j0) = wd;
-      }
+      }, std::make_integer_sequence<int, 4>{});
+    }, std::make_integer_sequence<int, 2>{});
+    float delta = dl.x + dl.y;
+    delta += __shfl_xor(delta, 32, 64);
+    const f32x2 delta2 = {delta, delta};
+    static_for([&](auto JT) {
+      constexpr int jt = decltype(JT)::value;
+      static_for([&](auto GQ) {
+        constexpr int gq = decltype(GQ)::value;
+        if constexpr (jt == 0 || gq < 3) {
+          f32x2 ds[2];
+          static_for([&](auto E2) {
+            constexpr int r = 4 * gq + 2 * decltype(E2)::value;
+            if constexpr (live_key(jt, r)) {
+              f32x2 v = pair(P[jt], r) * (pair(D[jt], r) - delta2);
+              if constexpr (!live_key(jt, r + 1)) v.y = 0.f;
+              ds[decltype(E2)::value] = v;
+              set_pair(dB[jt], r, pair(dB[jt], r) + v);
+            } else {
+              ds[decltype(E2)::value] = f32x2{0.f, 0.f};
+            }
+          }, std::make_integer_sequence<int, 2>{});
+          const uint2 wd = {pack2v<T>(ds[0]), pack2v<T>(ds[1])};
+          *reinterpret_cast<uint2*>(L.dS + i * LDP + jt * 32 + 8 * gq + 4 * hh) = wd;
+        }
+      }, std::make_integer_sequence<int, 4>{});
+    }, std::make_integer_sequence<int, 2>{});
     __syncthreads();  // both halves of the images written
     // ---- gradient pass: key tile mt = w (dV, dK) and query tile mt (dQ)
     // dV^T[d][j] = sum_i dO[i][d] Pd[i][j]; dK^T[d][j] = scale sum_i Q[i][d] dS[i][j];
@@ -653,7 +744,7 @@ __global__ void __launch_bounds__(128 * HPW, HPW == 3 ? 1 : 2) attn_bwd_mfma(
       f32x16 av = f32x16{0}, ak = f32x16{0};
 #pragma unroll 1  // unrolled, the fragment reads of all four k steps were hoisted: 17 VGPRs spilled
       for (int ks = 0; ks < 64; ks += 16) {
-        av = mfma32<T>(frag_tr_q4(L.dO, LD, ks, 0, lane), frag_tr_q4(L.P, LDP, ks, mt * 32, lane), av);
+        av = mfma32<T>(frag_tr_q4(L.dO, LD, ks, 0, lane), frag_tr_q4_swz(L.P, LDP, ks, mt * 32, lane), av);
         ak = mfma32<T>(frag_tr_q4(L.q, LD, ks, 0, lane), frag_tr_q4(L.dS, LDP, ks, mt * 32, lane), ak);
       }
       store_slice<T>(row + g.C, ak, scale, hh, st_ok);
@@ -678,6 +769,11 @@ __global__ void __launch_bounds__(128 * HPW, HPW == 3 ? 1 : 2) attn_bwd_mfma(
   const long win0 = blockIdx.x;
   if (win0 < g.nwin) {  // block-uniform
     long win = win0;
+    {  // the padded keys 56 .. 63 of this wave's query rows: zero in both images for good
+      const int zi = w * 32 + (lane & 31), zo = zi * LDP + 56;
+      *reinterpret_cast<uint2*>(L.P + zo + 4 * (hh ^ pswz(zi))) = uint2{0u, 0u};
+      *reinterpret_cast<uint2*>(L.dS + zo + 4 * hh) = uint2{0u, 0u};
+    }
     prep(win, std::integral_constant<int, 0>{});
     for (;;) {
       if (!step(std::integral_constant<int, 0>{}, win)) break;
@@ -1081,13 +1177,7 @@ __global__ void __launch_bounds__(64 * FQ_WAVES) attn_qkv_fwd_mfma(const bf16_t*
     }
     if (bnd) mask_col(P, L.reg, t, scale, lane);
     softmax_col(P, scale);
-    if constexpr (DROP) {
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (live_key(jt, r)) P[jt][r] = (kmask >> (jt * 16 + r)) & 1u ? P[jt][r] * kscale : 0.f;
-    }
+    if constexpr (DROP) drop_scale(P, kmask, kscale);
     f32x16 O = f32x16{0};
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)

@@ -67,6 +67,19 @@ for s in "$@"; do
         timeout -k 10 60 python -u $R/tools/nt_one.py $shp 30 2>&1 | grep "nt M" >> $O/${TAG}_kern.log || exit 3
       done
       cat $O/${TAG}_kern.log ;;
+    attn_tests) step attn_tests 900 $PYT -m gpu $R/tests/test_gpu_attn_qkv.py $R/tests/test_gpu_production_parity.py \
+                  $R/tests/test_gpu_ops.py -k "attn or attention or window" ;;
+    attn_kern)
+      # window-attention kernel times per stage shape (8 x res^2, nh heads, shift 3, dropout 0.05),
+      # this build vs an override library (AB_LIB)
+      for L in "" "$AB_LIB"; do
+        for shp in "256 3" "128 6" "64 12" "32 24"; do
+          d=$O/${TAG}_attnk_$(basename "${L:-cur}" .so)_${shp// /_}
+          MSU_LIB_OVERRIDE=$L timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $d -o p --output-format csv -- python3 $R/tools/attn_one.py $shp 3 1 6 0.05 > /dev/null 2>&1 || exit 3
+          python3 $R/tools/kstats.py $d/p_kernel_stats.csv attn "${L:+B}${shp// /x}" >> $O/${TAG}_attn_kern.log
+        done
+      done
+      cat $O/${TAG}_attn_kern.log ;;
     ab_conv_side) bash $R/tools/gpu_bench_ab.sh ${TAG}_convside "" "MSU_CONV_SIDE=0" "" "MSU_CONV_SIDE=0" "" "MSU_CONV_SIDE=0" || exit 3 ;;
     conv_exp)
       # refine-conv kernel times with ablation builds (tools/build_exp.sh conv3x3 64 128 256 512)
