@@ -527,8 +527,12 @@ template <int MODE>
 int fwd_dispatch(int dtype, const LnArgs& a, hipStream_t st) {
   if (a.C % (msu_is16(dtype) ? 8 : 4) != 0 || a.C > 2048) return -2;
   if (a.rows == 0) return 0;
-  // grid cap 16384 blocks (vs 4096 / 2048: 154.06 vs 153.82 / 152.78 img/s, r01)
-  MSU_DISPATCH(dtype, T, return launch_fwd<T, MODE>(a, st, 16384));
+  // grid cap 4096 blocks: with the next row prefetched (r04y) a group needs several rows to
+  // overlap loads with the normalisation; at 16384 the C >= 192 launches ran one row per group
+  // (r05af alone: 131072 x 192 add-LN 43.3 vs 51.5 us, 32768 x 384 22.9 vs 25.0; step 172.3 vs
+  // 171.8 img/s, 3 of 3 pairs, r05ag; r01, before the prefetch, had 16384 ahead of 4096)
+  constexpr int cap = (MSU_EXP & 16) ? 2048 : ((MSU_EXP & 64) ? 1024 : ((MSU_EXP & 32) ? 16384 : 4096));
+  MSU_DISPATCH(dtype, T, return launch_fwd<T, MODE>(a, st, cap));
   return -3;
 }
 

@@ -1153,7 +1153,7 @@ __global__ void __launch_bounds__(64 * FQ_WAVES) attn_qkv_fwd_mfma(const bf16_t*
       for (int m = 0; m < 3; ++m)
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-          const int r = 32 * t + (lane >> 2) + 16 * c;
+          const int r = 32 * t + read_row(lane >> 2) + 16 * c;
           const int tok = L.tok[r];
           const u32x4 v = *reinterpret_cast<const u32x4*>(L.qkv[h][m] + r * LD + 8 * (lane & 3));
           if (tok >= 0)
@@ -1198,7 +1198,7 @@ __global__ void __launch_bounds__(64 * FQ_WAVES) attn_qkv_fwd_mfma(const bf16_t*
     if (!PROJ || o_out != nullptr) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const int r = 32 * t + (lane >> 2) + 16 * c;
+        const int r = 32 * t + read_row(lane >> 2) + 16 * c;
         const int tok = L.tok[r];
         const u32x4 v = *reinterpret_cast<const u32x4*>(Lo + r * LD + 8 * (lane & 3));
         if (tok >= 0)

@@ -47,6 +47,7 @@ for s in "$@"; do
       python3 $R/tools/pmc_json.py conv3x3_v3_kernel $O/${TAG}_pmcconv/conv_fetch_counter_collection.csv \
         $O/${TAG}_pmcconv/conv_write_counter_collection.csv $O/${TAG}_conv3x3_fwd_pmc.json && cat $O/${TAG}_conv3x3_fwd_pmc.json ;;
     attn_pmc) step attn_pmc 400 bash $R/tools/pmc_attn.sh $TAG 256 3 3 0.05 ;;
+    fused_pmc) step fused_pmc 400 bash $R/tools/pmc_attn.sh ${TAG}_fused fused 0.05 ;;
     gemm_mem)
       # memory-side counters of the NT GEMM and the weight gradient at a stage-2 shape: HBM bytes
       # (FETCH_SIZE x2 / WRITE_SIZE) and the L2 hit rate, one counter group per pass
@@ -126,6 +127,15 @@ for s in "$@"; do
         done
       done
       cat $O/${TAG}_ln_exp.log ;;
+    ln_kern)
+      # LayerNorm kernel times at the step's shapes per ablation build (LN_EXP masks, 0 = this build)
+      for X in ${LN_EXP:-0 16 32 64}; do
+        L=""; [ $X != 0 ] && L=$R/tools/exp/libmsunet_layernorm_$X.so
+        d=$O/${TAG}_lnk_$X
+        MSU_LIB_OVERRIDE=$L timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $d -o p --output-format csv -- python3 $R/tools/ln_one.py 5 > /dev/null 2>&1 || exit 3
+        python3 $R/tools/kstats.py $d/p_kernel_stats.csv ln_ X$X >> $O/${TAG}_ln_kern.log
+      done
+      cat $O/${TAG}_ln_kern.log ;;
     ab_ln) bash $R/tools/gpu_bench_ab.sh ${TAG}_ln "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_1.so" \
              "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_2.so" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_8.so" \
              "" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_1.so" "MSU_LIB_OVERRIDE=$R/tools/exp/libmsunet_layernorm_2.so" \
