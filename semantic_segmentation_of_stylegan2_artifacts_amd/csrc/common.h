@@ -16,6 +16,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // register-resident 16-B chunk
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));  // a register pair (v_pk_*_f32 operands)
 typedef uint16_t bf16_t;  // storage type of a bf16 activation
 typedef _Float16 f16_t;   // storage type of an f16 activation
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));

@@ -153,7 +153,6 @@ MSU_DEV bool window_tokens(const Geom& g, long win_l, int* sTok, int* sReg, int 
   return (g.sh + g.sw) > 0 && (wy == g.nWy - 1 || wx == g.nWx - 1);
 }
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x2_v __attribute__((ext_vector_type(2)));
 

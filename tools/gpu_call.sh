@@ -68,6 +68,8 @@ for s in "$@"; do
         timeout -k 10 60 python -u $R/tools/nt_one.py $shp 30 2>&1 | grep "nt M" >> $O/${TAG}_kern.log || exit 3
       done
       cat $O/${TAG}_kern.log ;;
+    gelu_tests) step gelu_tests 900 $PYT -m gpu $R/tests/test_gpu_tok_gemm.py $R/tests/test_gpu_nt_gemm.py \
+                  $R/tests/test_gpu_linbwd.py $R/tests/test_gpu_ln_side.py $R/tests/test_gpu_ops.py ;;
     attn_tests) step attn_tests 900 $PYT -m gpu $R/tests/test_gpu_attn_qkv.py $R/tests/test_gpu_production_parity.py \
                   $R/tests/test_gpu_ops.py -k "attn or attention or window" ;;
     attn_kern)
