@@ -1137,15 +1137,42 @@ def mlp_fusable(x, fc1_weight, fc2_weight):
             gemm_route(M, Hd, C, TOK_GELU_GRAD) != "lib")
 
 
+# MSU_MLP_INFER=0: the no-grad MLPs on the token-GEMM pair (A/B switch)
+_MLP_INFER = switches.on("MSU_MLP_INFER")
+mlp_infer_calls = 0  # fused inference-MLP launches (tests assert which path a no-grad forward took)
+_mlp_infer_cache = {}
+
+
+def _mlp_infer_ok(C, Hd):
+    key = (int(C), int(Hd))
+    r = _mlp_infer_cache.get(key)
+    if r is None:
+        r = _mlp_infer_cache[key] = bool(_lib.lib().msu_mlp_infer_supported(*key))
+    return r
+
+
 def _mlp_impl(x, w1, b1, w2, b2, keep):
     """y = mlp.3(GELU(mlp.0(x))) (torchvision ops.misc.MLP without dropout): mlp.0's epilogue
     stores H and GELU(H) (returned for backward); mlp.3's input gradient applies GELU'(H) in
     its epilogue.  keep = False (no backward will run: the reference's discarded branches,
     inference): H is not kept -- the GELU store overwrites it in one buffer -- and H / G come
     back empty."""
+    global mlp_infer_calls
     _need_cuda(x)
     W1 = _shadow(w1, x.dtype)
     W2 = _shadow(w2, x.dtype)
+    Hd, C = W1.shape
+    if not keep and _MLP_INFER and x.dtype in _LOW and _mlp_infer_ok(C, Hd):
+        # one kernel, the hidden activation on chip (csrc/mlp_fused.hip); its operands 16-B
+        # aligned (weight shadows are views into one flat buffer)
+        x = x.contiguous()
+        B1, B2 = _f32(b1), _f32(b2)
+        if all(t.data_ptr() % 16 == 0 for t in (x, W1, W2, B1, B2)) and W1.is_contiguous() and W2.is_contiguous():
+            y = torch.empty(*x.shape[:-1], C, device=x.device, dtype=x.dtype)
+            mlp_infer_calls += 1
+            _lib.call("msu_mlp_infer", _dt(x), _p(x), _p(W1), _p(B1), _p(W2), _p(B2), _p(y), x.numel() // C, C, Hd,
+                      _s(x))
+            return y, x.new_empty(0), x.new_empty(0)
     h, g = _gemm(x, W1, _f32(b1), TOK_GELU_DUAL, gelu_only=not keep)
     y = _gemm(g, W2, _f32(b2))
     if not keep:

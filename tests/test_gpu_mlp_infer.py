@@ -1,0 +1,119 @@
+"""GPU: the fused inference MLP (csrc/mlp_fused.hip, ops.mlp without autograd) against plain fp32
+PyTorch and against the training path's token-GEMM pair.
+
+Reference: fp32 of the same 16-bit operands with the kernel's two roundings (the pre-activation
+and GELU(H) stored in 16 bits, as the unfused epilogues do), exact erf GELU.  Tolerance as the
+token-GEMM tests: |y - ref| <= 1e-2 |ref| + 4e-3 max|ref| (one f32 -> 16-bit rounding of the
+output, different summation order; A&S 7.1.26 erf |err| <= 1.5e-7).  Against the training path
+(same roundings, bias added in f32 instead of as a hi / lo k-block): rel. L2 <= 2e-3.
+Every case runs for both 16-bit formats.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    return ops
+
+
+@pytest.fixture(params=[torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+def low(request):
+    return request.param
+
+
+def _params(seed, low):
+    g = torch.Generator().manual_seed(seed)
+    w1 = torch.nn.Parameter((torch.randn(384, 96, generator=g) / 96 ** 0.5).to(DEV))
+    b1 = torch.nn.Parameter((torch.randn(384, generator=g) * 0.1).to(DEV))
+    w2 = torch.nn.Parameter((torch.randn(96, 384, generator=g) / 384 ** 0.5).to(DEV))
+    b2 = torch.nn.Parameter((torch.randn(96, generator=g) * 0.1).to(DEV))
+    return w1, b1, w2, b2
+
+
+def _ref(x, w1, b1, w2, b2, low):
+    h = (x.float() @ w1.detach().to(low).float().t() + b1.detach()).to(low).float()
+    g = F.gelu(h).to(low).float()
+    return g @ w2.detach().to(low).float().t() + b2.detach()
+
+
+# M: ragged tails (tile 32), one wave's worth, several tiles per wave, production (8 x 256^2)
+@pytest.mark.parametrize("M", [1, 33, 1000, 8192 + 17, 524288])
+def test_mlp_infer_matches_fp32(M, low):
+    ops = _ops()
+    w1, b1, w2, b2 = _params(M, low)
+    x = torch.randn(M, 96, generator=torch.Generator().manual_seed(M + 1)).to(DEV, low)
+    n0 = ops.mlp_infer_calls
+    with torch.no_grad(), torch.autocast("cuda", dtype=low):
+        y = ops.mlp(x, w1, b1, w2, b2)
+    assert ops.mlp_infer_calls == n0 + 1, "the no-grad MLP did not take the fused kernel"
+    assert y.dtype == low and y.shape == (M, 96)
+    ref = _ref(x, w1, b1, w2, b2, low)
+    scale = ref.abs().max().item()
+    err = (y.float() - ref).abs() - 1e-2 * ref.abs()
+    assert err.max().item() <= 4e-3 * scale, f"M={M}: excess err {err.max().item():.3e} vs scale {scale:.3e}"
+
+
+def test_mlp_infer_matches_training_path(low):
+    """The same block forward with autograd on (token-GEMM pair, H / GELU(H) kept) and off."""
+    ops = _ops()
+    w1, b1, w2, b2 = _params(7, low)
+    x = torch.randn(4, 64, 64, 96, generator=torch.Generator().manual_seed(8)).to(DEV, low)
+    with torch.autocast("cuda", dtype=low):
+        y_train = ops.mlp(x.clone().requires_grad_(True), w1, b1, w2, b2).detach().float()
+    n0 = ops.mlp_infer_calls
+    with torch.no_grad(), torch.autocast("cuda", dtype=low):
+        y_inf = ops.mlp(x, w1, b1, w2, b2).float()
+    assert ops.mlp_infer_calls == n0 + 1
+    rel = ((y_inf - y_train).norm() / y_train.norm()).item()
+    assert rel <= 2e-3, rel
+
+
+def test_mlp_infer_other_widths_keep_token_gemm_pair():
+    """Stage-1 widths (192 -> 768) are not covered: the no-grad MLP keeps the GEMM pair."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(5)
+    w1 = torch.nn.Parameter((torch.randn(768, 192, generator=g) / 192 ** 0.5).to(DEV))
+    b1 = torch.nn.Parameter((torch.randn(768, generator=g) * 0.1).to(DEV))
+    w2 = torch.nn.Parameter((torch.randn(192, 768, generator=g) / 768 ** 0.5).to(DEV))
+    b2 = torch.nn.Parameter((torch.randn(192, generator=g) * 0.1).to(DEV))
+    x = torch.randn(4096, 192, generator=g).to(DEV, torch.bfloat16)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        fusable = ops.mlp_fusable(x, w1, w2)
+    if not fusable:
+        pytest.skip("stage-1 MLP not on the fused GEMM pair")
+    n0 = ops.mlp_infer_calls
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.mlp(x, w1, b1, w2, b2)
+    assert ops.mlp_infer_calls == n0
+    ref = _ref(x, w1, b1, w2, b2, torch.bfloat16)
+    scale = ref.abs().max().item()
+    assert ((y.float() - ref).abs() - 1e-2 * ref.abs()).max().item() <= 4e-3 * scale
+
+
+def test_dead_branches_take_fused_mlp():
+    """The reference's discarded branches (layers_cent1[-1], layers_cent2[-1]: stage-0 Swin
+    blocks run without autograd) go through the fused inference MLP."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import load_config, ops
+    from semantic_segmentation_of_stylegan2_artifacts_amd.network import MSUNet
+    cfg = load_config(None, "swin_t", **{"DATA.IMG_SIZE": 1024, "DATA.BATCH_SIZE": 1})
+    torch.manual_seed(0)
+    model = MSUNet(cfg, img_size=1024, num_classes=1).to(DEV).train()
+    x = torch.randn(1, 3, 1024, 1024, device=DEV)
+    probe = torch.empty(65536, 96, device=DEV, dtype=torch.bfloat16)
+    blk = model.ms_unet.layers[0].blocks[0]
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        fusable = ops.mlp_fusable(probe, blk.mlp[0].weight, blk.mlp[3].weight)
+    if blk.dropout > 0 or not fusable:
+        pytest.skip("stage-0 MLP not on the fused path in this configuration")
+    n0 = ops.mlp_infer_calls
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = model(x)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y.float()).all()
+    assert ops.mlp_infer_calls - n0 == 4, ops.mlp_infer_calls - n0  # 2 + 2 dead stage-0 blocks

@@ -70,6 +70,7 @@ for s in "$@"; do
       cat $O/${TAG}_kern.log ;;
     gelu_tests) step gelu_tests 900 $PYT -m gpu $R/tests/test_gpu_tok_gemm.py $R/tests/test_gpu_nt_gemm.py \
                   $R/tests/test_gpu_linbwd.py $R/tests/test_gpu_ln_side.py $R/tests/test_gpu_ops.py ;;
+    mlp_tests) step mlp_tests 600 $PYT -m gpu $R/tests/test_gpu_mlp_infer.py $R/tests/test_gpu_tok_gemm.py ;;
     attn_tests) step attn_tests 900 $PYT -m gpu $R/tests/test_gpu_attn_qkv.py $R/tests/test_gpu_production_parity.py \
                   $R/tests/test_gpu_ops.py -k "attn or attention or window" ;;
     attn_kern)
@@ -146,6 +147,16 @@ for s in "$@"; do
     ab_lib) bash $R/tools/gpu_bench_ab.sh ${TAG}_lib "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" "" "MSU_LIB_OVERRIDE=$AB_LIB" || exit 3 ;;
     tail_tests) step tail_tests 600 $PYT -m gpu $R/tests/test_gpu_tail_reduce.py $R/tests/test_gpu_ln_side.py \
                   $R/tests/test_gpu_tok_gemm.py $R/tests/test_gpu_linbwd.py ;;
+    mlp_kern)
+      # stage-0 no-grad MLP kernels: fused (MSU_MLP_INFER=1) vs the token-GEMM pair
+      for X in 1 0; do
+        d=$O/${TAG}_mlpk_$X
+        MSU_MLP_INFER=$X timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $d -o p --output-format csv -- python3 $R/tools/mlp_one.py 5 > /dev/null 2>&1 || exit 3
+        python3 $R/tools/kstats.py $d/p_kernel_stats.csv gemm I$X >> $O/${TAG}_mlp_kern.log
+        python3 $R/tools/kstats.py $d/p_kernel_stats.csv mlp I$X >> $O/${TAG}_mlp_kern.log
+      done
+      cat $O/${TAG}_mlp_kern.log ;;
+    ab_mlp) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlp "" "MSU_MLP_INFER=0" "" "MSU_MLP_INFER=0" "" "MSU_MLP_INFER=0" || exit 3 ;;
     ab_tail) bash $R/tools/gpu_bench_ab.sh ${TAG}_tail "" "MSU_TAIL=0" "" "MSU_TAIL=0" "" "MSU_TAIL=0" || exit 3 ;;
     ab_fused) bash $R/tools/gpu_bench_ab.sh ${TAG}_fused "" "MSU_ATTN_QKV=0" "" "MSU_ATTN_QKV=0" "" "MSU_ATTN_QKV=0" || exit 3 ;;
     determ) step determ 600 python -u $R/tools/determinism_matrix.py 24 default ;;
