@@ -222,15 +222,17 @@ int msu_nt_gemm_kn(int dtype, const void* A, const void* Wk, const float* bias, 
 
 /* ---------------------------------------------------------------- streaming ops
  * nn.GELU() (exact erf): torchvision MLP activation, FinalPatchExpand_X4_V2.act. */
-/* Stage-0 Swin MLP in inference, fused (csrc/mlp_fused.hip; replaces mlp.0 -> GELU -> mlp.3 of
- * torchvision's block, model_parts.py:538, on the no-grad path: the reference's discarded
- * branches layers_cent1[-1] / layers_cent2[-1], model_parts.py:795 / :807, and evaluation):
- * y = W2 GELU(W1 x + b1) + b2 with the hidden activation kept on chip.  x, y [M][96] and
+/* Stage-0 Swin MLP forward, fused (csrc/mlp_fused.hip; replaces mlp.0 -> GELU -> mlp.3 of
+ * torchvision's block, model_parts.py:538): y = W2 GELU(W1 x + b1) + b2 with the hidden
+ * activation kept on chip; h (nullable) receives the 16-bit pre-activation W1 x + b1 [M][384]
+ * for the backward (training; null on the no-grad path: the reference's discarded branches
+ * layers_cent1[-1] / layers_cent2[-1], model_parts.py:795 / :807, and evaluation).  x, y [M][96],
  * w1 [384][96], w2 [96][384] in the 16-bit format dtype, b1 / b2 f32, all 16-B aligned.
- * msu_mlp_infer_supported(C, Hd): 1 for C = 96, Hd = 384.  Returns 0, -2 (unsupported). */
-int msu_mlp_infer_supported(int C, int Hd);
-int msu_mlp_infer(int dtype, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
-                  long M, int C, int Hd, void* stream);
+ * msu_mlp_fused_supported(C, Hd): 1 for C = 96, Hd = 384.  Returns 0, -2 (unsupported).
+ * The backward's mlp.3 step is msu_linear_bwd with X = null and H = h. */
+int msu_mlp_fused_supported(int C, int Hd);
+int msu_mlp_fused_fwd(int dtype, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                      void* y, void* h, long M, int C, int Hd, void* stream);
 int msu_gelu_fwd(int dtype, const void* x, void* y, long n, void* stream);
 int msu_gelu_bwd(int dtype, const void* x, const void* dy, void* dx, long n, void* stream);
 /* PatchEmbed.proj im2col (model_parts.py:211, :222): img [B,Cin,H,W] f32 ->

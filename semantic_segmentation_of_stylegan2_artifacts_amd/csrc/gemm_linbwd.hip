@@ -179,7 +179,9 @@ MSU_DEV int wg_tile(int w, int i) {
   return jt;
 }
 
-template <typename T, int K, int N, bool GG>
+// GX: X is GELU(H) re-derived from H while the rows are staged (X = H in the arguments): mlp.3
+// after the fused MLP forward (csrc/mlp_fused.hip), which keeps H only
+template <typename T, int K, int N, bool GG, bool GX = false>
 __global__ void __launch_bounds__(NTHR, 1)
 linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
               const bf16_t* __restrict__ H, bf16_t* __restrict__ dX, float* __restrict__ part, long M) {
@@ -278,6 +280,19 @@ linbwd_kernel(const bf16_t* __restrict__ dY, const bf16_t* __restrict__ X, const
   // retire more, never less)
   auto store = [&](long step, auto SET) __attribute__((always_inline)) {
     constexpr int set = decltype(SET)::value;
+    if constexpr (GX) {
+      // X chunks: GELU of the staged H (the forward's arithmetic: gelu_fast of the 16-bit H,
+      // rounded to 16 bits), so the image holds exactly the activation the forward fed mlp.3
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        if (kind(j) == 1) {
+          u32x4& q = st[set][j];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            q[i] = pack2<T>(gelu_fast(Fmt16<T>::lo(q[i])), gelu_fast(Fmt16<T>::hi(q[i])));
+        }
+      }
+    }
     // every path passes one wait (the last D - 1 steps of a workgroup drain fully)
     bf16_t* y = sS + (int)(step & 1) * STAGE;
     const long m0 = (b + step * G) * TM;
@@ -467,12 +482,12 @@ long grid_of(long M, int K, int N) {
   return ntiles < g ? ntiles : g;
 }
 
-template <typename T, int K, int N, bool GG>
+template <typename T, int K, int N, bool GG, bool GX = false>
 int launch_lb(const void* dY, const void* X, const void* Wt, const void* H, void* dX, float* part, long M,
               hipStream_t st) {
   constexpr size_t lds = linbwd_lds<K, N>();
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = linbwd_kernel<T, K, N, GG>;
+  auto kern = linbwd_kernel<T, K, N, GG, GX>;
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
@@ -501,14 +516,19 @@ long msu_linear_bwd_workspace(long M, int K, int N) { return grid_of(M, K, N) * 
 // One pass over the tokens of y = x . W^T + b (x [M][K], W [N][K], 16-bit dtype 1 bf16 / 2 f16):
 //   dX = dY . W (times GELU'(H) when H != null: mlp.3's input gradient into mlp.0's output),
 //   dW (+)= dY^T X and db (+)= column sums of dY (f32, accumulate != 0 adds to dW / db; db may
-//   be null).  Wt is W^T [K][N] (16-bit).  Stream: `stream`.
+//   be null).  Wt is W^T [K][N] (16-bit).  X null with H given (mlp.3 only): X = GELU(H),
+//   derived from H in the kernel.  Stream: `stream`.
 int msu_linear_bwd(int dtype, const void* dY, const void* X, const void* Wt, const void* H, void* dX, float* dW,
                    float* db, float* workspace, long M, int K, int N, int accumulate, void* stream) {
   if (!msu_is16(dtype)) return -3;
   if (M <= 0 || !lb_shape(K, N)) return -2;
   if (H != nullptr && !(K == 384 && N == 96)) return -3;  // the GELU' epilogue: mlp.3 only
+  if (X == nullptr && H == nullptr) return -2;
   hipStream_t st = (hipStream_t)stream;
   int rc = -3;
+  if (X == nullptr) {
+    MSU_DISPATCH16(dtype, T, rc = (launch_lb<T, 384, 96, true, true>(dY, H, Wt, H, dX, workspace, M, st)));
+  } else {
 #define MSU_LB(KK, NN, GG)                                                                   \
   if (K == KK && N == NN && (H != nullptr) == GG) {                                          \
     MSU_DISPATCH16(dtype, T, rc = launch_lb<T, KK, NN, GG>(dY, X, Wt, H, dX, workspace, M, st)); \
@@ -518,6 +538,7 @@ int msu_linear_bwd(int dtype, const void* dY, const void* X, const void* Wt, con
   MSU_LB(96, 384, false)
   MSU_LB(384, 96, false)
   MSU_LB(384, 96, true)
+  }
 #undef MSU_LB
   if (rc) return rc;
   const int parts = (int)grid_of(M, K, N);

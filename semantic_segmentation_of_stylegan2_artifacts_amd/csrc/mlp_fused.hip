@@ -1,11 +1,14 @@
-// Stage-0 Swin MLP in inference (no backward will run: the reference's discarded branches,
-// layers_cent1[-1] / layers_cent2[-1] at model_parts.py:795 / :807, and evaluation):
+// Stage-0 Swin MLP forward in ONE kernel (torchvision MLP, model_parts.py:538):
 //
-//   y = mlp.3(GELU(mlp.0(x)))      x, y: [M][96], hidden 384 (torchvision MLP, model_parts.py:538)
+//   y = mlp.3(GELU(mlp.0(x)))      x, y: [M][96], hidden 384
 //
-// in ONE kernel: the 384-wide hidden activation never leaves the chip.  The unfused inference
-// path writes GELU(H) (403 MB at 8 x 256^2 tokens) and reads it back; here a wave runs, per
-// 32-token tile and per 32-wide hidden chunk,
+// Without autograd (the reference's discarded branches layers_cent1[-1] / layers_cent2[-1] at
+// model_parts.py:795 / :807, and evaluation) the 384-wide hidden activation never leaves the
+// chip: the GEMM pair wrote GELU(H) (403 MB at 8 x 256^2 tokens) and read it back.  In training
+// (H_OUT) the kernel also stores the pre-activation H -- the one tensor the backward needs (mlp.3's
+// input gradient applies GELU'(H), its weight gradient re-derives GELU(H) from H while staging:
+// msu_linear_bwd with X = null); the pair wrote H and GELU(H) and read GELU(H) back.
+// Per 32-token tile and per 32-wide hidden chunk a wave runs
 //   * fc1 on MFMA with W1 as the A operand and the tile's token rows as B (the tokens end up on
 //     the accumulator columns, the hidden units on its rows), + b1, rounded to 16 bits, GELU
 //     (the unfused epilogue's arithmetic: gelu_fast of the rounded pre-activation), rounded
@@ -36,10 +39,11 @@ MSU_DEV int w1_swz(int r) { return (r >> 2) & 3; }
 // accumulator row of register r for lane half h (32x32 C layout)
 MSU_DEV constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-template <typename T>
-__global__ void __launch_bounds__(64 * MW) mlp_infer_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
+template <typename T, bool H_OUT>
+__global__ void __launch_bounds__(64 * MW) mlp_fused_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
                                                           const float* __restrict__ b1, const bf16_t* __restrict__ w2,
-                                                          const float* __restrict__ b2, bf16_t* __restrict__ y, long M) {
+                                                          const float* __restrict__ b2, bf16_t* __restrict__ y,
+                                                          bf16_t* __restrict__ hout, long M) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   MlpLds& L = *reinterpret_cast<MlpLds*>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
@@ -87,7 +91,10 @@ __global__ void __launch_bounds__(64 * MW) mlp_infer_kernel(const bf16_t* __rest
     f32x16 yacc[3];
 #pragma unroll
     for (int ct = 0; ct < 3; ++ct) yacc[ct] = f32x16{0};
-#pragma unroll 2
+    const long hrow_i = tile * MT + tl;
+    const bool hok = hrow_i < M;
+    bf16_t* hrow = H_OUT ? hout + (hok ? hrow_i : 0) * MH : nullptr;
+#pragma unroll(H_OUT ? 1 : 2)
     for (int nc = 0; nc < MH / 32; ++nc) {
       // fc1: C1^T[n][t] for hidden n in chunk nc
       f32x16 h = f32x16{0};
@@ -98,16 +105,29 @@ __global__ void __launch_bounds__(64 * MW) mlp_infer_kernel(const bf16_t* __rest
         h = Fmt16<T>::mma32(wf, __builtin_bit_cast(bf16x8, xc[ks]), h);
       }
       // + b1, 16-bit pre-activation, GELU, 16-bit activation (the unfused epilogues' roundings)
-      uint32_t g[8];
+      uint32_t g[8], hw[8];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 bq = *reinterpret_cast<const float4*>(L.b1 + nc * 32 + 8 * q + 4 * hh);
-        const float v0 = gelu_fast(round16<T>(h[4 * q] + bq.x));
-        const float v1 = gelu_fast(round16<T>(h[4 * q + 1] + bq.y));
-        const float v2 = gelu_fast(round16<T>(h[4 * q + 2] + bq.z));
-        const float v3 = gelu_fast(round16<T>(h[4 * q + 3] + bq.w));
-        g[2 * q] = pack2<T>(v0, v1);
-        g[2 * q + 1] = pack2<T>(v2, v3);
+        const float u0 = round16<T>(h[4 * q] + bq.x), u1 = round16<T>(h[4 * q + 1] + bq.y);
+        const float u2 = round16<T>(h[4 * q + 2] + bq.z), u3 = round16<T>(h[4 * q + 3] + bq.w);
+        if constexpr (H_OUT) {
+          hw[2 * q] = pack2<T>(u0, u1);
+          hw[2 * q + 1] = pack2<T>(u2, u3);
+        }
+        g[2 * q] = pack2<T>(gelu_fast(u0), gelu_fast(u1));
+        g[2 * q + 1] = pack2<T>(gelu_fast(u2), gelu_fast(u3));
+      }
+      if constexpr (H_OUT) {
+        // H row piece: a permlane32 swap pairs the halves' 4-unit groups into 8 consecutive
+        // hidden units per lane (hidden nc*32 + 16p + 8hh .. + 7), one 16-B store each
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const auto s0 = __builtin_amdgcn_permlane32_swap(hw[4 * p], hw[4 * p + 2], false, false);
+          const auto s1 = __builtin_amdgcn_permlane32_swap(hw[4 * p + 1], hw[4 * p + 3], false, false);
+          const u32x4 v = {s0[0], s1[0], s0[1], s1[1]};
+          if (hok) *reinterpret_cast<u32x4*>(hrow + nc * 32 + 16 * p + 8 * hh) = v;
+        }
       }
       // fc2: two 16-deep k steps over the chunk (registers 8s .. 8s + 7 of the fc1 accumulator)
 #pragma unroll
@@ -164,10 +184,10 @@ int num_cus_mlp() {
   return cus;
 }
 
-template <typename T>
-int launch_mlp(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y, long M,
-               hipStream_t st) {
-  auto kern = mlp_infer_kernel<T>;
+template <typename T, bool H_OUT>
+int launch_mlp(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y, void* h,
+               long M, hipStream_t st) {
+  auto kern = mlp_fused_kernel<T, H_OUT>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(MlpLds)) !=
@@ -179,7 +199,7 @@ int launch_mlp(const void* x, const void* w1, const float* b1, const void* w2, c
   long grid = num_cus_mlp();
   if (grid * MW > ntiles) grid = (ntiles + MW - 1) / MW;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * MW), sizeof(MlpLds), st, (const bf16_t*)x,
-                     (const bf16_t*)w1, b1, (const bf16_t*)w2, b2, (bf16_t*)y, M);
+                     (const bf16_t*)w1, b1, (const bf16_t*)w2, b2, (bf16_t*)y, (bf16_t*)h, M);
   return MSU_CHECK_LAUNCH();
 }
 
@@ -187,19 +207,25 @@ int launch_mlp(const void* x, const void* w1, const float* b1, const void* w2, c
 
 extern "C" {
 
-// Whether msu_mlp_infer covers a (channels, hidden) shape: the stage-0 MLP, 96 -> 384 -> 96.
-int msu_mlp_infer_supported(int C, int Hd) { return C == MC && Hd == MH ? 1 : 0; }
+// Whether msu_mlp_fused_fwd covers a (channels, hidden) shape: the stage-0 MLP, 96 -> 384 -> 96.
+int msu_mlp_fused_supported(int C, int Hd) { return C == MC && Hd == MH ? 1 : 0; }
 
-// y = fc2(GELU(fc1(x))) without the hidden activation in HBM.  dtype bf16 / f16; x, y [M][96]
+// y = fc2(GELU(fc1(x))) with the hidden activation kept on chip; h (nullable) receives the
+// 16-bit pre-activation fc1(x) [M][384] for the backward.  dtype bf16 / f16; x, y [M][96]
 // (16-B aligned rows), w1 [384][96], w2 [96][384] in x's format, b1 [384] / b2 [96] f32.
-int msu_mlp_infer(int dtype, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y,
-                  long M, int C, int Hd, void* stream) {
-  if (!msu_is16(dtype) || !msu_mlp_infer_supported(C, Hd) || M < 0) return -2;
-  if ((((uintptr_t)x | (uintptr_t)y | (uintptr_t)w1 | (uintptr_t)w2 | (uintptr_t)b1 | (uintptr_t)b2) & 15) != 0)
+int msu_mlp_fused_fwd(int dtype, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                      void* y, void* h, long M, int C, int Hd, void* stream) {
+  if (!msu_is16(dtype) || !msu_mlp_fused_supported(C, Hd) || M < 0) return -2;
+  if ((((uintptr_t)x | (uintptr_t)y | (uintptr_t)h | (uintptr_t)w1 | (uintptr_t)w2 | (uintptr_t)b1 | (uintptr_t)b2) &
+       15) != 0)
     return -2;
   if (M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  MSU_DISPATCH16(dtype, T, return launch_mlp<T>(x, w1, b1, w2, b2, y, M, st));
+  if (h != nullptr) {
+    MSU_DISPATCH16(dtype, T, return launch_mlp<T, true>(x, w1, b1, w2, b2, y, h, M, st));
+  } else {
+    MSU_DISPATCH16(dtype, T, return launch_mlp<T, false>(x, w1, b1, w2, b2, y, h, M, st));
+  }
   return -3;
 }
 

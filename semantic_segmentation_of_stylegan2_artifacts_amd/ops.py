@@ -930,7 +930,7 @@ _LINBWD_MIN_M = 65536
 linbwd_calls = 0  # one-pass backward launches (tests assert which path a backward took)
 
 
-def _linbwd(dy, x, weight, bias, M, N, K, h=None):
+def _linbwd(dy, x, weight, bias, M, N, K, h=None, gelu_x=False):
     """dX = dy . W (* GELU'(h)) with dW / db accumulated into the trainer's .grad in the same
     pass; None when the shape, dtype or parameters are not covered (caller: two-kernel path).
     W^T is the trainer's transposed shadow when it has one in x's dtype, else a per-call
@@ -954,7 +954,9 @@ def _linbwd(dy, x, weight, bias, M, N, K, h=None):
             torch.cuda.current_stream(x.device).wait_event(ev)
     dx = torch.empty(*dy.shape[:-1], K, device=dy.device, dtype=dy.dtype)
     ws = torch.empty(L.msu_linear_bwd_workspace(M, K, N), device=x.device, dtype=torch.float32)
-    _lib.call("msu_linear_bwd", _dt(x), _p(dy), _p(x.contiguous()), _p(wt), _p(h), _p(dx), _p(weight.grad),
+    # gelu_x: x is H and the kernel stages GELU(H) as the input (msu_linear_bwd with X = null)
+    _lib.call("msu_linear_bwd", _dt(x), _p(dy), _p(None if gelu_x else x.contiguous()), _p(wt), _p(h), _p(dx),
+              _p(weight.grad),
               _p(None if bias is None else bias.grad), _p(ws), M, K, N, 1, _s(x))
     linbwd_calls += 1
     _notify(weight, bias)
@@ -1137,17 +1139,20 @@ def mlp_fusable(x, fc1_weight, fc2_weight):
             gemm_route(M, Hd, C, TOK_GELU_GRAD) != "lib")
 
 
-# MSU_MLP_INFER=0: the no-grad MLPs on the token-GEMM pair (A/B switch)
+# MSU_MLP_INFER=0 / MSU_MLP_TRAIN=0: the no-grad / training stage-0 MLPs on the token-GEMM pair
+# (A/B switches)
 _MLP_INFER = switches.on("MSU_MLP_INFER")
-mlp_infer_calls = 0  # fused inference-MLP launches (tests assert which path a no-grad forward took)
-_mlp_infer_cache = {}
+_MLP_TRAIN = switches.on("MSU_MLP_TRAIN")
+mlp_infer_calls = 0  # fused MLP launches without H (tests assert which path a no-grad forward took)
+mlp_train_calls = 0  # fused MLP launches storing H
+_mlp_fused_cache = {}
 
 
-def _mlp_infer_ok(C, Hd):
+def _mlp_fused_ok(C, Hd):
     key = (int(C), int(Hd))
-    r = _mlp_infer_cache.get(key)
+    r = _mlp_fused_cache.get(key)
     if r is None:
-        r = _mlp_infer_cache[key] = bool(_lib.lib().msu_mlp_infer_supported(*key))
+        r = _mlp_fused_cache[key] = bool(_lib.lib().msu_mlp_fused_supported(*key))
     return r
 
 
@@ -1157,22 +1162,27 @@ def _mlp_impl(x, w1, b1, w2, b2, keep):
     its epilogue.  keep = False (no backward will run: the reference's discarded branches,
     inference): H is not kept -- the GELU store overwrites it in one buffer -- and H / G come
     back empty."""
-    global mlp_infer_calls
+    global mlp_infer_calls, mlp_train_calls
     _need_cuda(x)
     W1 = _shadow(w1, x.dtype)
     W2 = _shadow(w2, x.dtype)
     Hd, C = W1.shape
-    if not keep and _MLP_INFER and x.dtype in _LOW and _mlp_infer_ok(C, Hd):
-        # one kernel, the hidden activation on chip (csrc/mlp_fused.hip); its operands 16-B
-        # aligned (weight shadows are views into one flat buffer)
+    if (_MLP_TRAIN if keep else _MLP_INFER) and x.dtype in _LOW and _mlp_fused_ok(C, Hd):
+        # one kernel, the hidden activation on chip (csrc/mlp_fused.hip); training keeps H only
+        # (the backward re-derives GELU(H)).  Operands 16-B aligned (weight shadows are views
+        # into one flat buffer).
         x = x.contiguous()
         B1, B2 = _f32(b1), _f32(b2)
         if all(t.data_ptr() % 16 == 0 for t in (x, W1, W2, B1, B2)) and W1.is_contiguous() and W2.is_contiguous():
             y = torch.empty(*x.shape[:-1], C, device=x.device, dtype=x.dtype)
-            mlp_infer_calls += 1
-            _lib.call("msu_mlp_infer", _dt(x), _p(x), _p(W1), _p(B1), _p(W2), _p(B2), _p(y), x.numel() // C, C, Hd,
-                      _s(x))
-            return y, x.new_empty(0), x.new_empty(0)
+            h = torch.empty(*x.shape[:-1], Hd, device=x.device, dtype=x.dtype) if keep else None
+            if keep:
+                mlp_train_calls += 1
+            else:
+                mlp_infer_calls += 1
+            _lib.call("msu_mlp_fused_fwd", _dt(x), _p(x), _p(W1), _p(B1), _p(W2), _p(B2), _p(y), _p(h),
+                      x.numel() // C, C, Hd, _s(x))
+            return y, (h if keep else x.new_empty(0)), x.new_empty(0)
     h, g = _gemm(x, W1, _f32(b1), TOK_GELU_DUAL, gelu_only=not keep)
     y = _gemm(g, W2, _f32(b2))
     if not keep:
@@ -1207,7 +1217,13 @@ def _mlp_backward(ctx, dy, _dh, _dg):
     Hd, C = W1.shape
     M = x.numel() // C
     dy = dy.contiguous()
-    dh = _linbwd(dy, g, w2, b2, M, C, Hd, h=h)  # mlp.3 in one pass (dh through GELU')
+    if g.numel() == 0:  # fused forward: H only; mlp.3's pass re-derives GELU(H) while staging
+        dh = _linbwd(dy, h, w2, b2, M, C, Hd, h=h, gelu_x=True)
+        if dh is None:  # the two-kernel path reads GELU(H): derive it in H's 16-bit format
+            g = torch.empty_like(h)
+            _lib.call("msu_gelu_fwd", _dt(h), _p(h), _p(g), h.numel(), _s(h))
+    else:
+        dh = _linbwd(dy, g, w2, b2, M, C, Hd, h=h)  # mlp.3 in one pass (dh through GELU')
     if dh is None:
         dw2, db2 = _wgrad(dy, g, w2, b2, M, C, Hd)
         dh = _gemm_dx(dy, W2, TOK_GELU_GRAD, h=h, param=w2)

@@ -28,7 +28,9 @@ SWITCHES = {
     "MSU_TAIL": ("1", "0: LayerNorm parameter-gradient partials summed by a colsum launch, not in the kernel",
                  "DESIGN 7 (r05i: +0.5 %, host -4 ms/step)"),
     "MSU_MLP_INFER": ("1", "0: no-grad stage-0 MLPs on the token-GEMM pair instead of the fused kernel",
-                      "DESIGN 7 (r05am)"),
+                      "DESIGN 7 (r05am: +1.3 %)"),
+    "MSU_MLP_TRAIN": ("1", "0: training stage-0 MLPs on the token-GEMM pair (H and GELU(H) stored) instead of "
+                      "the fused kernel storing H only", "DESIGN 7 (r05ao)"),
     "MSU_GRAPH": ("auto", "HIP-graph replay of the step: 1 / 0 / auto (replay when launch-bound)",
                   "DESIGN 4b (512^2: 401 vs 249-307 img/s)"),
     "MSU_GRAPH_SIDE": ("0", "1: fork the side stream into the captured graph (nondeterministic on ROCm 7.2)",

@@ -117,3 +117,35 @@ def test_dead_branches_take_fused_mlp():
     torch.cuda.synchronize()
     assert torch.isfinite(y.float()).all()
     assert ops.mlp_infer_calls - n0 == 4, ops.mlp_infer_calls - n0  # 2 + 2 dead stage-0 blocks
+
+
+def test_linbwd_gelu_from_h_matches_explicit_gelu(low):
+    """mlp.3's one-pass backward with X = null re-derives GELU(H) while staging: bitwise the same
+    dX / dW / db as with the GELU(H) tensor the token-GEMM pair stored (same gelu_fast, same
+    16-bit rounding)."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
+    ops = _ops()
+    L = _lib.lib()
+    M, K, N = 4096 + 17, 384, 96
+    g = torch.Generator().manual_seed(11)
+    dy = torch.randn(M, N, generator=g).to(DEV, low)
+    h = torch.randn(M, K, generator=g).to(DEV, low)
+    wt = (torch.randn(K, N, generator=g) / K ** 0.5).to(DEV, low)
+    with torch.no_grad(), torch.autocast("cuda", dtype=low):
+        gx = ops.gelu(h)
+    assert gx.dtype == low and gx.is_contiguous()
+    s = torch.cuda.current_stream().cuda_stream
+    out = []
+    for X in (gx, None):
+        dx = torch.empty(M, K, device=DEV, dtype=low)
+        dw = torch.zeros(N, K, device=DEV)
+        db = torch.zeros(N, device=DEV)
+        ws = torch.empty(L.msu_linear_bwd_workspace(M, K, N), device=DEV)
+        _lib.call("msu_linear_bwd", ops._dt(h), dy.data_ptr(), None if X is None else X.data_ptr(), wt.data_ptr(),
+                  h.data_ptr(), dx.data_ptr(), dw.data_ptr(), db.data_ptr(), ws.data_ptr(), M, K, N, 1, s)
+        out.append((dx, dw, db))
+    torch.cuda.synchronize()
+    for a, b, name in zip(out[0], out[1], ("dx", "dW", "db")):
+        assert torch.equal(a, b), name
+    ref_dw = dy.float().t() @ F.gelu(h.float()).to(low).float()
+    assert ((out[1][1] - ref_dw).norm() / ref_dw.norm()).item() < 1e-2

@@ -131,11 +131,12 @@ def _child(port, outdir):
     counts = {}
     try:
         for i in range(2):
-            lb0, fq0 = ops.linbwd_calls, ops.fused_qkv_calls
+            lb0, fq0, mt0 = ops.linbwd_calls, ops.fused_qkv_calls, ops.mlp_train_calls
             grads.clear()
             loss = tr.step(x, y)
             torch.cuda.synchronize()
             counts[i] = {"linbwd": ops.linbwd_calls - lb0, "fused_qkv": ops.fused_qkv_calls - fq0,
+                         "fused_mlp": ops.mlp_train_calls - mt0,
                          "hook_launches": sum(v == "hook" for _, _, v, _ in tr.reducer.last_launches),
                          "buckets": len(tr.reducer.buckets)}
     finally:
@@ -215,11 +216,18 @@ def test_step_matches_fp32_parity_mode(arms, arm):
     assert agree >= 0.98, (agree, rec)
 
 
+def _ops_module():
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    return ops
+
+
 def test_bf16_step_took_the_production_routes(arms):
     b = arms["bf16"]
     print(json.dumps({"counts": b["counts"], "lib_routes": b["lib_routes"]}))
     for i, c in b["counts"].items():
         assert c["linbwd"] >= 4 * 2, c  # stage 0: qkv / proj / mlp.0 / mlp.3 of every block
         assert c["fused_qkv"] >= 4, c   # the four stage-0 blocks of the live encoder / decoder
+        if _ops_module()._MLP_TRAIN:
+            assert c["fused_mlp"] >= 4, c  # their MLPs: fused forward (H kept), GELU(H) re-derived in mlp.3's pass
     assert b["counts"][1]["hook_launches"] > 0, b["counts"]  # buckets overlapped backward
     assert not b["lib_routes"], b["lib_routes"]
