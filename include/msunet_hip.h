@@ -231,6 +231,12 @@ int msu_nt_gemm_kn(int dtype, const void* A, const void* Wk, const float* bias, 
  * msu_mlp_fused_supported(C, Hd): 1 for C = 96, Hd = 384.  Returns 0, -2 (unsupported).
  * The backward's mlp.3 step is msu_linear_bwd with X = null and H = h. */
 int msu_mlp_fused_supported(int C, int Hd);
+/* No-grad second half of a stage-0 block: s_out = a + bscale[sample] * br (16-bit; bscale null = 1,
+ * rows_per_sample rows per sample), y = mlp(LN(s) with gamma / beta / eps) -- the residual-add
+ * LayerNorm (norm2) and the fused MLP above in one kernel, the normalised rows on chip. */
+int msu_add_ln_mlp_fwd(int dtype, const void* a, const void* br, const float* bscale, long rows_per_sample,
+                       const float* gamma, const float* beta, float eps, const void* w1, const float* b1,
+                       const void* w2, const float* b2, void* s_out, void* y, long M, int C, int Hd, void* stream);
 int msu_mlp_fused_fwd(int dtype, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
                       void* y, void* h, long M, int C, int Hd, void* stream);
 int msu_gelu_fwd(int dtype, const void* x, void* y, long n, void* stream);

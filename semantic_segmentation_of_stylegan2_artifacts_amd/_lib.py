@@ -41,6 +41,7 @@ SIGNATURES = {
     "msu_win_attn_qkv_fwd2": (I, [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P]),
     "msu_mlp_fused_supported": (I, [I, I]),
     "msu_mlp_fused_fwd": (I, [I, P, P, P, P, P, P, P, L, I, I, P]),
+    "msu_add_ln_mlp_fwd": (I, [I, P, P, P, L, P, P, F, P, P, P, P, P, P, L, I, I, P]),
     "msu_gelu_fwd": (I, [I, P, P, L, P]),
     "msu_gelu_bwd": (I, [I, P, P, P, L, P]),
     "msu_residual": (I, [I, P, P, P, P, L, L, P]),

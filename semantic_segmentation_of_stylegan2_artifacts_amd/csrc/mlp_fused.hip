@@ -32,6 +32,25 @@ struct MlpLds {
   bf16_t w2[MC * LW2];
   float b1[MH];
   float b2[MC];
+  float g2[MC], be2[MC];  // LN_IN: norm2's weight / bias
+};
+
+struct MlpArgs {
+  const bf16_t* x;      // the MLP input rows; LN_IN: the residual stream a
+  const bf16_t* br;     // LN_IN: the branch added to it, scaled per sample
+  const float* bscale;  // LN_IN: per-sample scale (StochasticDepth 'row'), null = 1
+  long rps;             // LN_IN: rows per sample
+  const float* g2;      // LN_IN: norm2 weight / bias, eps
+  const float* be2;
+  float eps;
+  bf16_t* s_out;        // LN_IN: s = a + scale * br (the residual stream the block passes on)
+  const bf16_t* w1;
+  const float* b1;
+  const bf16_t* w2;
+  const float* b2;
+  bf16_t* y;
+  bf16_t* hout;         // H_OUT: the pre-activation
+  long M;
 };
 
 MSU_DEV int w1_swz(int r) { return (r >> 2) & 3; }
@@ -39,11 +58,19 @@ MSU_DEV int w1_swz(int r) { return (r >> 2) & 3; }
 // accumulator row of register r for lane half h (32x32 C layout)
 MSU_DEV constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-template <typename T, bool H_OUT>
-__global__ void __launch_bounds__(64 * MW) mlp_fused_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w1,
-                                                          const float* __restrict__ b1, const bf16_t* __restrict__ w2,
-                                                          const float* __restrict__ b2, bf16_t* __restrict__ y,
-                                                          bf16_t* __restrict__ hout, long M) {
+// LN_IN (no-grad blocks): the input rows are LN2(a + scale * br), computed here as the residual-add
+// LayerNorm kernel does (the sum rounded to 16 bits and stored as s, two-pass variance), so the
+// normalised rows never reach HBM either
+template <typename T, bool H_OUT, bool LN_IN>
+__global__ void __launch_bounds__(64 * MW) mlp_fused_kernel(MlpArgs A) {
+  const bf16_t* __restrict__ x = A.x;
+  const bf16_t* __restrict__ w1 = A.w1;
+  const float* __restrict__ b1 = A.b1;
+  const bf16_t* __restrict__ w2 = A.w2;
+  const float* __restrict__ b2 = A.b2;
+  bf16_t* __restrict__ y = A.y;
+  bf16_t* __restrict__ hout = A.hout;
+  const long M = A.M;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   MlpLds& L = *reinterpret_cast<MlpLds*>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5;
@@ -61,6 +88,12 @@ __global__ void __launch_bounds__(64 * MW) mlp_fused_kernel(const bf16_t* __rest
   }
   for (int s = tid; s < MH; s += 64 * MW) L.b1[s] = b1[s];
   for (int s = tid; s < MC; s += 64 * MW) L.b2[s] = b2[s];
+  if constexpr (LN_IN) {
+    for (int s = tid; s < MC; s += 64 * MW) {
+      L.g2[s] = A.g2[s];
+      L.be2[s] = A.be2[s];
+    }
+  }
   __syncthreads();
 
   const long ntiles = (M + MT - 1) / MT;
@@ -79,7 +112,70 @@ __global__ void __launch_bounds__(64 * MW) mlp_fused_kernel(const bf16_t* __rest
       xr[ks] = ok ? v : u32x4{0u, 0u, 0u, 0u};
     }
   };
-  u32x4 xc[6], xn[6];
+  // LN_IN: the branch rows of a tile and their per-sample scale (loaded at the tile's start, not
+  // a tile ahead: the registers for a second prefetched set spilled)
+  auto load_br = [&](long t, u32x4 (&ar)[6], float& sc) __attribute__((always_inline)) {
+    const long row = t * MT + tl;
+    const bool ok = row < M;
+    const bf16_t* q = A.br + (ok ? row : 0) * MC + 8 * hh;
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(q + 16 * ks);
+      ar[ks] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+    }
+    sc = A.bscale ? A.bscale[(ok ? row : 0) / A.rps] : 1.f;
+  };
+  // LN_IN: s = round16(a + sc br) (stored), rows normalised over the token's 96 channels (this
+  // lane's 48 and its xor-32 partner's) -> the fc1 B operand
+  auto ln_rows = [&](long t, u32x4 (&xr)[6], const u32x4 (&ar)[6], float sc) __attribute__((always_inline)) {
+    const long row = t * MT + tl;
+    const bool ok = row < M;
+    // s = round16(a + sc br), kept packed in xr (the 16-bit values the sums and the output use)
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        xr[ks][i] = pack2<T>(fmaf(sc, Fmt16<T>::lo(ar[ks][i]), Fmt16<T>::lo(xr[ks][i])),
+                             fmaf(sc, Fmt16<T>::hi(ar[ks][i]), Fmt16<T>::hi(xr[ks][i])));
+    float sum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sum += Fmt16<T>::lo(xr[ks][i]) + Fmt16<T>::hi(xr[ks][i]);
+    sum += __shfl_xor(sum, 32, 64);
+    const float mu = sum / MC;
+    float var = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float d0 = Fmt16<T>::lo(xr[ks][i]) - mu, d1 = Fmt16<T>::hi(xr[ks][i]) - mu;
+        var += d0 * d0;
+        var += d1 * d1;
+      }
+    var += __shfl_xor(var, 32, 64);
+    const float rs = rsqrtf(var / MC + A.eps);
+    bf16_t* srow = A.s_out + (ok ? row : 0) * MC + 8 * hh;
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) {
+      if (ok) *reinterpret_cast<u32x4*>(srow + 16 * ks) = xr[ks];
+      const float4 g0 = *reinterpret_cast<const float4*>(L.g2 + 16 * ks + 8 * hh);
+      const float4 g1 = *reinterpret_cast<const float4*>(L.g2 + 16 * ks + 8 * hh + 4);
+      const float4 c0 = *reinterpret_cast<const float4*>(L.be2 + 16 * ks + 8 * hh);
+      const float4 c1 = *reinterpret_cast<const float4*>(L.be2 + 16 * ks + 8 * hh + 4);
+      const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        o[i] = pack2<T>((Fmt16<T>::lo(xr[ks][i]) - mu) * rs * g[2 * i] + bb[2 * i],
+                        (Fmt16<T>::hi(xr[ks][i]) - mu) * rs * g[2 * i + 1] + bb[2 * i + 1]);
+      xr[ks] = u32x4{o[0], o[1], o[2], o[3]};
+      __builtin_amdgcn_sched_barrier(0);  // gamma / beta reads one chunk at a time (hoisted, they spilled)
+    }
+  };
+  u32x4 xc[6], xn[6], ac[6];
+  float scc = 1.f;
   load_x(tile, xc);
   // fc2 A fragment of output tile ct, hidden k step n0 .. n0 + 15 in the accumulator row order:
   // element e of half hh <-> hidden n0 + 8 (e >> 2) + 4 hh + (e & 3)
@@ -87,14 +183,16 @@ __global__ void __launch_bounds__(64 * MW) mlp_fused_kernel(const bf16_t* __rest
   for (;;) {
     const long nxt = tile + stride;
     const bool more = nxt < ntiles;
+    if constexpr (LN_IN) load_br(tile, ac, scc);
     if (more) load_x(nxt, xn);
+    if constexpr (LN_IN) ln_rows(tile, xc, ac, scc);
     f32x16 yacc[3];
 #pragma unroll
     for (int ct = 0; ct < 3; ++ct) yacc[ct] = f32x16{0};
     const long hrow_i = tile * MT + tl;
     const bool hok = hrow_i < M;
     bf16_t* hrow = H_OUT ? hout + (hok ? hrow_i : 0) * MH : nullptr;
-#pragma unroll(H_OUT ? 1 : 2)
+#pragma unroll((H_OUT || LN_IN) ? 1 : 2)
     for (int nc = 0; nc < MH / 32; ++nc) {
       // fc1: C1^T[n][t] for hidden n in chunk nc
       f32x16 h = f32x16{0};
@@ -184,10 +282,10 @@ int num_cus_mlp() {
   return cus;
 }
 
-template <typename T, bool H_OUT>
-int launch_mlp(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* y, void* h,
-               long M, hipStream_t st) {
-  auto kern = mlp_fused_kernel<T, H_OUT>;
+template <typename T, bool H_OUT, bool LN_IN = false>
+int launch_mlp(const MlpArgs& a, hipStream_t st) {
+  auto kern = mlp_fused_kernel<T, H_OUT, LN_IN>;
+  const long M = a.M;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(MlpLds)) !=
@@ -198,8 +296,7 @@ int launch_mlp(const void* x, const void* w1, const float* b1, const void* w2, c
   const long ntiles = (M + MT - 1) / MT;
   long grid = num_cus_mlp();
   if (grid * MW > ntiles) grid = (ntiles + MW - 1) / MW;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * MW), sizeof(MlpLds), st, (const bf16_t*)x,
-                     (const bf16_t*)w1, b1, (const bf16_t*)w2, b2, (bf16_t*)y, (bf16_t*)h, M);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * MW), sizeof(MlpLds), st, a);
   return MSU_CHECK_LAUNCH();
 }
 
@@ -221,11 +318,52 @@ int msu_mlp_fused_fwd(int dtype, const void* x, const void* w1, const float* b1,
     return -2;
   if (M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  MlpArgs a{};
+  a.x = (const bf16_t*)x;
+  a.w1 = (const bf16_t*)w1;
+  a.b1 = b1;
+  a.w2 = (const bf16_t*)w2;
+  a.b2 = b2;
+  a.y = (bf16_t*)y;
+  a.hout = (bf16_t*)h;
+  a.M = M;
   if (h != nullptr) {
-    MSU_DISPATCH16(dtype, T, return launch_mlp<T, true>(x, w1, b1, w2, b2, y, h, M, st));
+    MSU_DISPATCH16(dtype, T, return launch_mlp<T, true>(a, st));
   } else {
-    MSU_DISPATCH16(dtype, T, return launch_mlp<T, false>(x, w1, b1, w2, b2, y, h, M, st));
+    MSU_DISPATCH16(dtype, T, return launch_mlp<T, false>(a, st));
   }
+  return -3;
+}
+
+// No-grad second half of a stage-0 Swin block in one kernel: s = a + bscale[sample] * br
+// (rounded to 16 bits; bscale null = 1), y = mlp(LN2(s)) -- msu_layernorm_fwd's residual-add mode
+// followed by msu_mlp_fused_fwd, without the normalised rows in HBM.  a, br, s_out, y [M][96];
+// rows_per_sample splits the rows into samples for bscale; gamma / beta / eps of norm2.
+int msu_add_ln_mlp_fwd(int dtype, const void* a, const void* br, const float* bscale, long rows_per_sample,
+                       const float* gamma, const float* beta, float eps, const void* w1, const float* b1,
+                       const void* w2, const float* b2, void* s_out, void* y, long M, int C, int Hd, void* stream) {
+  if (!msu_is16(dtype) || !msu_mlp_fused_supported(C, Hd) || M < 0 || rows_per_sample <= 0) return -2;
+  if ((((uintptr_t)a | (uintptr_t)br | (uintptr_t)s_out | (uintptr_t)y | (uintptr_t)w1 | (uintptr_t)w2 |
+        (uintptr_t)b1 | (uintptr_t)b2 | (uintptr_t)gamma | (uintptr_t)beta) & 15) != 0)
+    return -2;
+  if (M == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  MlpArgs p{};
+  p.x = (const bf16_t*)a;
+  p.br = (const bf16_t*)br;
+  p.bscale = bscale;
+  p.rps = rows_per_sample;
+  p.g2 = gamma;
+  p.be2 = beta;
+  p.eps = eps;
+  p.s_out = (bf16_t*)s_out;
+  p.w1 = (const bf16_t*)w1;
+  p.b1 = b1;
+  p.w2 = (const bf16_t*)w2;
+  p.b2 = b2;
+  p.y = (bf16_t*)y;
+  p.M = M;
+  MSU_DISPATCH16(dtype, T, return (launch_mlp<T, false, true>(p, st)));
   return -3;
 }
 

@@ -198,9 +198,17 @@ class SwinTransformerBlock(nn.Module):
         B = x.shape[0]
         a = self.attn(xn)
         sc1 = _drop_path_scale(self.stochastic_depth_prob, self.training, B, x.device)
-        x1, xn2 = ops.add_layer_norm(x, a, sc1, self.norm2.weight, self.norm2.bias, self.norm2.eps)
         fc1, fc2 = self.mlp[0], self.mlp[3]
         drop = self.dropout > 0 and self.training
+        if not drop and not torch.is_grad_enabled():
+            # no-grad blocks (the reference's discarded branches): norm2's residual-add LayerNorm
+            # and the MLP in one kernel when covered
+            r = ops.add_layer_norm_mlp(x, a, sc1, self.norm2.weight, self.norm2.bias, self.norm2.eps,
+                                       fc1.weight, fc1.bias, fc2.weight, fc2.bias)
+            if r is not None:
+                sc2 = _drop_path_scale(self.stochastic_depth_prob, self.training, B, x.device)
+                return (r[0], r[1], sc2)
+        x1, xn2 = ops.add_layer_norm(x, a, sc1, self.norm2.weight, self.norm2.bias, self.norm2.eps)
         if not drop and fc1.bias is not None and fc2.bias is not None and \
                 ops.mlp_fusable(xn2, fc1.weight, fc2.weight):
             m = ops.mlp(xn2, fc1.weight, fc1.bias, fc2.weight, fc2.bias)

@@ -1242,6 +1242,37 @@ _mlp = _define("mlp", "(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2, bo
                _mlp_impl, _mlp_fake, _mlp_setup, _mlp_backward)
 
 
+_MLP_LN = switches.on("MSU_MLP_LN")
+add_ln_mlp_calls = 0
+
+
+def add_layer_norm_mlp(a, branch, scale, ln_weight, ln_bias, eps, fc1_weight, fc1_bias, fc2_weight, fc2_bias):
+    """No-grad (s, mlp(LN(s))) with s = a + scale[sample] * branch in one kernel
+    (csrc/mlp_fused.hip), or None when not covered (autograd on, widths, dtype, alignment)."""
+    global add_ln_mlp_calls
+    dt = act_dtype()
+    if torch.is_grad_enabled() or not (_MLP_LN and _MLP_INFER) or dt not in _LOW or not a.is_cuda:
+        return None
+    C = a.shape[-1]
+    Hd = fc1_weight.shape[0]
+    if fc1_bias is None or fc2_bias is None or not _mlp_fused_ok(C, Hd) or fc2_weight.shape != (C, Hd):
+        return None
+    a, branch = _as(a, dt), _as(branch, dt)
+    W1, W2 = _shadow(fc1_weight, dt), _shadow(fc2_weight, dt)
+    B1, B2, G, Bt = _f32(fc1_bias), _f32(fc2_bias), _f32(ln_weight), _f32(ln_bias)
+    sc = None if scale is None else _f32(scale)
+    ts = [a, branch, W1, W2, B1, B2, G, Bt]
+    if not all(t.data_ptr() % 16 == 0 for t in ts) or not (W1.is_contiguous() and W2.is_contiguous()):
+        return None
+    rows = a.numel() // C
+    s = torch.empty_like(a)
+    y = torch.empty_like(a)
+    add_ln_mlp_calls += 1
+    _lib.call("msu_add_ln_mlp_fwd", _dt(a), _p(a), _p(branch), _p(sc), rows // a.shape[0], _p(G), _p(Bt),
+              float(eps), _p(W1), _p(B1), _p(W2), _p(B2), _p(s), _p(y), rows, C, Hd, _s(a))
+    return s, y
+
+
 def mlp(x, fc1_weight, fc1_bias, fc2_weight, fc2_bias):
     """Fused torchvision MLP forward/backward (16-bit; see ``mlp_fusable``)."""
     _need_cuda(x)

@@ -29,6 +29,8 @@ SWITCHES = {
                  "DESIGN 7 (r05i: +0.5 %, host -4 ms/step)"),
     "MSU_MLP_INFER": ("1", "0: no-grad stage-0 MLPs on the token-GEMM pair instead of the fused kernel",
                       "DESIGN 7 (r05am: +1.3 %)"),
+    "MSU_MLP_LN": ("1", "0: no-grad stage-0 blocks run norm2's residual-add LayerNorm as its own kernel before the "
+                   "fused MLP", "DESIGN 7 (r05at)"),
     "MSU_MLP_TRAIN": ("1", "0: training stage-0 MLPs on the token-GEMM pair (H and GELU(H) stored) instead of "
                       "the fused kernel storing H only", "DESIGN 7 (r05ao)"),
     "MSU_GRAPH": ("auto", "HIP-graph replay of the step: 1 / 0 / auto (replay when launch-bound)",

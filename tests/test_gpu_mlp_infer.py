@@ -111,12 +111,15 @@ def test_dead_branches_take_fused_mlp():
         fusable = ops.mlp_fusable(probe, blk.mlp[0].weight, blk.mlp[3].weight)
     if blk.dropout > 0 or not fusable:
         pytest.skip("stage-0 MLP not on the fused path in this configuration")
-    n0 = ops.mlp_infer_calls
+    n0, l0 = ops.mlp_infer_calls, ops.add_ln_mlp_calls
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y = model(x)
     torch.cuda.synchronize()
     assert torch.isfinite(y.float()).all()
-    assert ops.mlp_infer_calls - n0 == 4, ops.mlp_infer_calls - n0  # 2 + 2 dead stage-0 blocks
+    fused = (ops.mlp_infer_calls - n0) + (ops.add_ln_mlp_calls - l0)
+    assert fused == 4, fused  # 2 + 2 dead stage-0 blocks
+    if ops._MLP_LN:
+        assert ops.add_ln_mlp_calls - l0 == 4  # norm2 folded in
 
 
 def test_linbwd_gelu_from_h_matches_explicit_gelu(low):
@@ -149,3 +152,40 @@ def test_linbwd_gelu_from_h_matches_explicit_gelu(low):
         assert torch.equal(a, b), name
     ref_dw = dy.float().t() @ F.gelu(h.float()).to(low).float()
     assert ((out[1][1] - ref_dw).norm() / ref_dw.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("with_scale", [False, True])
+def test_add_ln_mlp_matches_two_kernels(with_scale, low):
+    """No-grad norm2 residual-add LayerNorm + MLP in one kernel vs msu_layernorm_fwd (add mode)
+    followed by the fused MLP: s bitwise (the same fma and rounding), y within rel. L2 2e-3 (the
+    row statistics summed in a different order)."""
+    ops = _ops()
+    w1, b1, w2, b2 = _params(21, low)
+    g = torch.Generator().manual_seed(22)
+    B, R = 2, 97  # M = 18818 tokens: a ragged last tile
+    x = torch.randn(B, R, R, 96, generator=g).to(DEV, low)
+    a = torch.randn(B, R, R, 96, generator=g).to(DEV, low)
+    lw = torch.nn.Parameter((1 + 0.1 * torch.randn(96, generator=g)).to(DEV))
+    lb = torch.nn.Parameter((0.1 * torch.randn(96, generator=g)).to(DEV))
+    sc = torch.tensor([1.25, 0.0], device=DEV) if with_scale else None
+    with torch.no_grad(), torch.autocast("cuda", dtype=low):
+        l0 = ops.add_ln_mlp_calls
+        r = ops.add_layer_norm_mlp(x, a, sc, lw, lb, 1e-5, w1, b1, w2, b2)
+        assert r is not None and ops.add_ln_mlp_calls == l0 + 1
+        s_ref, xn = ops.add_layer_norm(x, a, sc, lw, lb, 1e-5)
+        y_ref = ops.mlp(xn, w1, b1, w2, b2)
+    torch.cuda.synchronize()
+    s, y = r
+    assert torch.equal(s, s_ref)
+    rel = ((y.float() - y_ref.float()).norm() / y_ref.float().norm()).item()
+    assert rel <= 2e-3, rel
+
+
+def test_add_ln_mlp_not_under_autograd():
+    ops = _ops()
+    w1, b1, w2, b2 = _params(23, torch.bfloat16)
+    x = torch.randn(2, 64, 64, 96, device=DEV, dtype=torch.bfloat16)
+    lw = torch.nn.Parameter(torch.ones(96, device=DEV))
+    lb = torch.nn.Parameter(torch.zeros(96, device=DEV))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        assert ops.add_layer_norm_mlp(x, x, None, lw, lb, 1e-5, w1, b1, w2, b2) is None

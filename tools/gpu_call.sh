@@ -156,6 +156,7 @@ for s in "$@"; do
         python3 $R/tools/kstats.py $d/p_kernel_stats.csv mlp I$X >> $O/${TAG}_mlp_kern.log
       done
       cat $O/${TAG}_mlp_kern.log ;;
+    ab_mlp_ln) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlpln "" "MSU_MLP_LN=0" "" "MSU_MLP_LN=0" "" "MSU_MLP_LN=0" || exit 3 ;;
     ab_mlp_train) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlptrain "" "MSU_MLP_TRAIN=0" "" "MSU_MLP_TRAIN=0" "" "MSU_MLP_TRAIN=0" || exit 3 ;;
     ab_mlp) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlp "" "MSU_MLP_INFER=0" "" "MSU_MLP_INFER=0" "" "MSU_MLP_INFER=0" || exit 3 ;;
     ab_tail) bash $R/tools/gpu_bench_ab.sh ${TAG}_tail "" "MSU_TAIL=0" "" "MSU_TAIL=0" "" "MSU_TAIL=0" || exit 3 ;;
