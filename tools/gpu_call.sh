@@ -156,6 +156,15 @@ for s in "$@"; do
         python3 $R/tools/kstats.py $d/p_kernel_stats.csv mlp I$X >> $O/${TAG}_mlp_kern.log
       done
       cat $O/${TAG}_mlp_kern.log ;;
+    mlp_pmc)
+      # counters of the fused MLP (no-grad, 8 x 256^2 tokens): HBM bytes, VALU / MFMA / LDS activity
+      d=$O/${TAG}_mlppmc
+      for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA GRBM_GUI_ACTIVE"; do
+        tagc=$(echo $c | cut -d' ' -f1)
+        timeout -s KILL 90 rocprofv3 --pmc $c -d $d -o $tagc --output-format csv -- python3 $R/tools/mlp_one.py 3 > /dev/null 2>&1 || exit 3
+      done
+      for f in $d/*_counter_collection.csv; do python3 $R/tools/pmc_sum.py mlp_fused $f; done > $O/${TAG}_mlp_pmc.log
+      cat $O/${TAG}_mlp_pmc.log ;;
     ab_mlp_ln) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlpln "" "MSU_MLP_LN=0" "" "MSU_MLP_LN=0" "" "MSU_MLP_LN=0" || exit 3 ;;
     ab_mlp_train) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlptrain "" "MSU_MLP_TRAIN=0" "" "MSU_MLP_TRAIN=0" "" "MSU_MLP_TRAIN=0" || exit 3 ;;
     ab_mlp) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlp "" "MSU_MLP_INFER=0" "" "MSU_MLP_INFER=0" "" "MSU_MLP_INFER=0" || exit 3 ;;
