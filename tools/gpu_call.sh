@@ -155,6 +155,11 @@ for s in "$@"; do
         python3 $R/tools/kstats.py $d/p_kernel_stats.csv gemm I$X >> $O/${TAG}_mlp_kern.log
         python3 $R/tools/kstats.py $d/p_kernel_stats.csv mlp I$X >> $O/${TAG}_mlp_kern.log
       done
+      if [ -n "$AB_LIB" ]; then
+        d=$O/${TAG}_mlpk_B
+        MSU_LIB_OVERRIDE=$AB_LIB timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $d -o p --output-format csv -- python3 $R/tools/mlp_one.py 5 > /dev/null 2>&1 || exit 3
+        python3 $R/tools/kstats.py $d/p_kernel_stats.csv mlp B >> $O/${TAG}_mlp_kern.log
+      fi
       cat $O/${TAG}_mlp_kern.log ;;
     mlp_pmc)
       # counters of the fused MLP (no-grad, 8 x 256^2 tokens): HBM bytes, VALU / MFMA / LDS activity
