@@ -100,7 +100,10 @@ int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const fl
  * runs on param_stream, ordered after the backward kernel by an event (null: on stream).
  * dqkv is complete when `stream` is; dtable / dqkv_bias_pad when `param_stream` is.
  * param_stream == (void*)-1: only the backward kernel is launched; the caller orders its own
- * stream after `stream` and issues msu_win_attn_bwd_tail (the HIP-graph-safe split). */
+ * stream after `stream` and issues msu_win_attn_bwd_tail (the HIP-graph-safe split).
+ * 16-bit dtypes: table == null means the workspace is the forward's (msu_win_attn_fwd /
+ * msu_win_attn_qkv_fwd2 with a workspace of max(fwd, bwd) floats), whose relative-bias image and
+ * bias rows, built from the same table and qkv bias, are reused instead of rebuilt. */
 int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const float* table,
                       const void* dout, void* dqkv, float* dtable, float* dqkv_bias_pad,
                       float* workspace, int B, int H, int W, int C, int nh, int shift,

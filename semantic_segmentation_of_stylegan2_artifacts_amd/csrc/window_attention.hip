@@ -477,6 +477,7 @@ int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const f
   if (msu_is16(dtype))
     return msu_attn_mfma_bwd(dtype, qkv, qkv_bias, table, dout, dqkv, dtable, dqkv_bias_pad, workspace, B, H, W,
                              C, nh, shift, p_drop, seed, seed_dev, keep, st, pst);
+  if (table == nullptr) return -2;  // the f32 kernel reads the table itself
   const int nblk = f32_bwd_blocks(g.nwin, nh);
   const float scale = 1.0f / sqrtf((float)HD);
   float* dB_part = workspace;

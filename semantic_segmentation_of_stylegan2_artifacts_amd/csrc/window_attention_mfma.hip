@@ -966,9 +966,12 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
   float* qb_part = dB_part + parts * nh * 169;
   const int hpw = bwd_hpw(nh);
   const dim3 grid(nblk, nh / hpw);
+  // table null: the workspace's aux region (bias image, bias / zero rows) is the forward's, built
+  // from the same table and qkv bias (one aux launch per layer and step instead of two)
   MSU_DISPATCH16(dtype, T,
-    hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
-                       1.0f / scale, img, brow, zrow);
+    if (table != nullptr)
+      hipLaunchKernelGGL(aux_kernel<T>, dim3((nh * 4096 + 255) / 256), dim3(256), 0, st, table, qkv_bias, nh, 3 * C,
+                         1.0f / scale, img, brow, zrow);
     if (hpw == 2) launch_bwd<T, 2>(grid, st, qkv, aux, dout, dqkv, dB_part, qb_part, g, scale, p_drop, seed, seed_dev, keep, nblk);
     else launch_bwd<T, 1>(grid, st, qkv, aux, dout, dqkv, dB_part, qb_part, g, scale, p_drop, seed, seed_dev, keep, nblk));
   if (pst == (hipStream_t)(intptr_t)-1) return MSU_CHECK_LAUNCH();  // tail issued by the caller

@@ -444,6 +444,24 @@ def d2s_layer_norm(x, weight, bias, eps=1e-5):
 # xorshift streams, r02c -- the stored form is the default, the re-hash stays for the tests)
 _ATTN_KEEP = True
 
+_ATTN_AUX = switches.on("MSU_ATTN_AUX")
+
+
+def _attn_ws_numel(dt, B, H, W, C, nh):
+    """Workspace floats of a 16-bit attention forward that its backward reuses: the forward's aux
+    region (relative-bias image, bias / zero rows) stays valid for the backward, which then skips
+    its own aux launch (msu_win_attn_bwd2 with table = null); f32: the forward's only."""
+    L = _lib.lib()
+    n = L.msu_win_attn_fwd_workspace(_dt_code(dt), C, nh)
+    if dt in _LOW and _ATTN_AUX:
+        n = max(n, L.msu_win_attn_bwd_workspace(_dt_code(dt), B, H, W, C, nh))
+    return n
+
+
+def _dt_code(dt):
+    return _DT[dt]
+
+
 def _attn_impl(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
     _need_cuda(qkv)
     qkv = qkv.contiguous()
@@ -451,28 +469,29 @@ def _attn_impl(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
     C = C3 // 3
     out = torch.empty(B, H, W, C, device=qkv.device, dtype=qkv.dtype)
     L = _lib.lib()
-    ws = torch.empty(L.msu_win_attn_fwd_workspace(_dt(qkv), C, num_heads), device=qkv.device,
-                     dtype=torch.float32)
+    ws = torch.empty(_attn_ws_numel(qkv.dtype, B, H, W, C, num_heads), device=qkv.device, dtype=torch.float32)
     # the dropout keep bits, written by the forward for the backward (16-bit dtypes)
     keep = torch.empty(L.msu_win_attn_keep_words(_dt(qkv), B, H, W, num_heads) if p_drop > 0 and _ATTN_KEEP else 0,
                        device=qkv.device, dtype=torch.int32)
     _lib.call("msu_win_attn_fwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(out), _p(ws), B, H, W,
               C, num_heads, shift, float(p_drop), seed, _p(seed_dev), _p(keep) if keep.numel() else None,
               _s(qkv))
-    return out, keep
+    return out, keep, ws
 
 
 def _attn_fake(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
     B, H, W, C3 = qkv.shape
     nwin = B * (-(-H // 7)) * (-(-W // 7))
     kw = nwin * num_heads * 128 if (p_drop > 0 and _ATTN_KEEP and qkv.dtype in _LOW) else 0
-    return qkv.new_empty(B, H, W, C3 // 3), qkv.new_empty(kw, dtype=torch.int32)
+    return (qkv.new_empty(B, H, W, C3 // 3), qkv.new_empty(kw, dtype=torch.int32),
+            qkv.new_empty(_attn_ws_numel(qkv.dtype, B, H, W, C3 // 3, num_heads), dtype=torch.float32))
 
 
 def _attn_setup(ctx, inputs, output):
     qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev = inputs
     keep = output[1]
-    ctx.mark_non_differentiable(keep)
+    ctx.mark_non_differentiable(keep, output[2])
+    ctx.aux_ws = output[2]
     ctx.set_materialize_grads(False)
     ctx.save_for_backward(qkv.contiguous(), qkv_bias, table, seed_dev, keep)
     # the parameter itself when it reached us uncast (trainer flat buffers: direct .grad)
@@ -481,7 +500,7 @@ def _attn_setup(ctx, inputs, output):
     ctx.cfg = (num_heads, shift, float(p_drop), seed)
 
 
-def _attn_backward(ctx, dout, _dkeep):
+def _attn_backward(ctx, dout, _dkeep, _dws=None):
     qkv, qkv_bias, table, seed_dev, keep = ctx.saved_tensors
     if dout is None:
         return None, None, None, None, None, None, None, None
@@ -491,8 +510,13 @@ def _attn_backward(ctx, dout, _dkeep):
     C = C3 // 3
     dout = _as(dout, qkv.dtype)
     L = _lib.lib()
-    ws = torch.empty(L.msu_win_attn_bwd_workspace(_dt(qkv), B, H, W, C, nh), device=qkv.device,
-                     dtype=torch.float32)
+    need = L.msu_win_attn_bwd_workspace(_dt(qkv), B, H, W, C, nh)
+    ws = getattr(ctx, "aux_ws", None)
+    if ws is not None and _ATTN_AUX and qkv.dtype in _LOW and ws.numel() >= need:
+        tbl = None  # the forward's aux region is still in ws: no second aux launch
+    else:
+        ws = torch.empty(need, device=qkv.device, dtype=torch.float32)
+        tbl = _p(table)
     dqkv = torch.empty_like(qkv)
     bp, tp = ctx.bias_param, ctx.table_param
     if bp is not None and tp is not None and _side_enabled and _side_attn_tail and _direct(bp, tp):
@@ -506,7 +530,7 @@ def _attn_backward(ctx, dout, _dkeep):
         # every record / wait pair into its own edge)
         main = torch.cuda.current_stream(qkv.device)
         side = _side_stream_for(qkv.device)
-        _lib.call("msu_win_attn_bwd2", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
+        _lib.call("msu_win_attn_bwd2", _dt(qkv), _p(qkv), _p(qkv_bias), tbl, _p(dout), _p(dqkv),
                   None, None, _p(ws), B, H, W, C, nh, shift, p_drop, seed, _p(seed_dev), kp,
                   main.cuda_stream, -1)
         side.wait_stream(main)
@@ -528,7 +552,7 @@ def _attn_backward(ctx, dout, _dkeep):
         return dqkv, None, None, None, None, None, None, None
     dtable = torch.empty_like(table)
     dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
-    _lib.call("msu_win_attn_bwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(dout), _p(dqkv),
+    _lib.call("msu_win_attn_bwd", _dt(qkv), _p(qkv), _p(qkv_bias), tbl, _p(dout), _p(dqkv),
               _p(dtable), _p(dbias), _p(ws), B, H, W, C, nh, shift, p_drop, seed, _p(seed_dev), kp, _s(qkv))
     return dqkv, dbias, dtable, None, None, None, None, None
 
@@ -536,7 +560,7 @@ def _attn_backward(ctx, dout, _dkeep):
 _window_attention = _define(
     "window_attention",
     "(Tensor qkv, Tensor qkv_bias, Tensor table, int num_heads, int shift, float p_drop, int seed, Tensor? seed_dev)"
-    " -> (Tensor, Tensor)",
+    " -> (Tensor, Tensor, Tensor)",
     _attn_impl, _attn_fake, _attn_setup, _attn_backward)
 
 
@@ -589,7 +613,8 @@ def _attn_qkv_impl(x, weight, bias, table, proj_weight, proj_bias, num_heads, sh
     y = torch.empty(B, H, W, C, device=x.device, dtype=dt)
     o = torch.empty(B, H, W, C, device=x.device, dtype=dt) if (proj and store) else x.new_empty(0)
     qkv = torch.empty(B, H, W, 3 * C, device=x.device, dtype=dt) if store else x.new_empty(0)
-    ws = torch.empty(L.msu_win_attn_fwd_workspace(_dt(x), C, num_heads), device=x.device, dtype=torch.float32)
+    ws = torch.empty(_attn_ws_numel(dt, B, H, W, C, num_heads) if store else
+                     L.msu_win_attn_fwd_workspace(_dt(x), C, num_heads), device=x.device, dtype=torch.float32)
     keep = torch.empty(L.msu_win_attn_keep_words(_dt(x), B, H, W, num_heads) if p_drop > 0 and _ATTN_KEEP else 0,
                        device=x.device, dtype=torch.int32)
     fused_qkv_calls += 1
@@ -597,22 +622,27 @@ def _attn_qkv_impl(x, weight, bias, table, proj_weight, proj_bias, num_heads, sh
               _p(proj_bias) if proj else None, _p(y), _p(o) if o.numel() else None, _p(qkv) if store else None,
               _p(keep) if keep.numel() else None, _p(ws), B, H, W, C, num_heads, shift, float(p_drop), seed,
               _p(seed_dev), _s(x))
-    return y, o, qkv, keep
+    return y, o, qkv, keep, ws
 
 
 def _attn_qkv_fake(x, weight, bias, table, proj_weight, proj_bias, num_heads, shift, p_drop, seed, seed_dev, store):
     B, H, W, C = x.shape
     nwin = B * (-(-H // 7)) * (-(-W // 7))
     kw = nwin * num_heads * 128 if (p_drop > 0 and _ATTN_KEEP) else 0
+    L = _lib.lib()
+    nws = _attn_ws_numel(x.dtype, B, H, W, C, num_heads) if store else L.msu_win_attn_fwd_workspace(
+        _dt_code(x.dtype), C, num_heads)
     return (x.new_empty(B, H, W, C),
             x.new_empty(B, H, W, C) if (proj_weight is not None and store) else x.new_empty(0),
-            x.new_empty(B, H, W, 3 * C) if store else x.new_empty(0), x.new_empty(kw, dtype=torch.int32))
+            x.new_empty(B, H, W, 3 * C) if store else x.new_empty(0), x.new_empty(kw, dtype=torch.int32),
+            x.new_empty(nws, dtype=torch.float32))
 
 
 def _attn_qkv_setup(ctx, inputs, output):
     x, weight, bias, table, proj_weight, proj_bias, num_heads, shift, p_drop, seed, seed_dev, store = inputs
-    _, o, qkv, keep = output
-    ctx.mark_non_differentiable(o, qkv, keep)
+    _, o, qkv, keep, ws = output
+    ctx.mark_non_differentiable(o, qkv, keep, ws)
+    ctx.aux_ws = ws
     ctx.set_materialize_grads(False)
     ctx.save_for_backward(x.contiguous(), o, qkv, bias, table, seed_dev, keep)
     ctx.params = (weight, bias, proj_weight, proj_bias)
@@ -621,7 +651,7 @@ def _attn_qkv_setup(ctx, inputs, output):
     ctx.cfg = (num_heads, shift, float(p_drop), seed)
 
 
-def _attn_qkv_backward(ctx, dy, _do, _dqkv, _dkeep):
+def _attn_qkv_backward(ctx, dy, _do, _dqkv, _dkeep, _dws=None):
     x, o, qkv, bias, table, seed_dev, keep = ctx.saved_tensors
     if dy is None:
         return (None,) * 12
@@ -636,7 +666,7 @@ def _attn_qkv_backward(ctx, dy, _do, _dqkv, _dkeep):
     else:
         dout = dy
     actx = _Ctx((qkv, bias, table, seed_dev, keep), cfg=ctx.cfg, bias_param=ctx.bias_param,
-                table_param=ctx.table_param)
+                table_param=ctx.table_param, aux_ws=ctx.aux_ws)
     dqkv, dbias_pad, dtable = _attn_backward(actx, dout, None)[:3]
     lctx = _Ctx((x,), params=(weight, bias),
                 needs_input_grad=(ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]))
@@ -651,7 +681,7 @@ def _attn_qkv_backward(ctx, dy, _do, _dqkv, _dkeep):
 _window_attention_qkv = _define(
     "window_attention_qkv",
     "(Tensor x, Tensor weight, Tensor bias, Tensor table, Tensor? proj_weight, Tensor? proj_bias, int num_heads,"
-    " int shift, float p_drop, int seed, Tensor? seed_dev, bool store) -> (Tensor, Tensor, Tensor, Tensor)",
+    " int shift, float p_drop, int seed, Tensor? seed_dev, bool store) -> (Tensor, Tensor, Tensor, Tensor, Tensor)",
     _attn_qkv_impl, _attn_qkv_fake, _attn_qkv_setup, _attn_qkv_backward)
 
 

@@ -27,6 +27,8 @@ SWITCHES = {
                       "DESIGN 7 (r04s: side +0.2 %)"),
     "MSU_TAIL": ("1", "0: LayerNorm parameter-gradient partials summed by a colsum launch, not in the kernel",
                  "DESIGN 7 (r05i: +0.5 %, host -4 ms/step)"),
+    "MSU_ATTN_AUX": ("1", "0: each attention backward rebuilds its relative-bias image instead of reusing the "
+                     "forward's workspace", "DESIGN 7 (r05az)"),
     "MSU_MLP_INFER": ("1", "0: no-grad stage-0 MLPs on the token-GEMM pair instead of the fused kernel",
                       "DESIGN 7 (r05am: +1.3 %)"),
     "MSU_MLP_LN": ("1", "0: no-grad stage-0 blocks run norm2's residual-add LayerNorm as its own kernel before the "

@@ -79,11 +79,11 @@ def test_torch_library_ops_registered():
         assert str(op._schema).startswith(f"msunet::{name}(")
     with FakeTensorMode():
         qkv = torch.empty(2, 10, 12, 3 * 64, device="cuda", dtype=torch.float16)
-        out, keep = torch.ops.msunet.window_attention(qkv, torch.empty(192, device="cuda"),
+        out, keep, _ = torch.ops.msunet.window_attention(qkv, torch.empty(192, device="cuda"),
                                                       torch.empty(169, 2, device="cuda"), 2, 3, 0.0, 0, None)
         assert out.shape == (2, 10, 12, 64) and out.dtype == torch.float16 and keep.numel() == 0
         # with dropout the forward also returns its keep bits (128 words per window x head)
-        _, keep = torch.ops.msunet.window_attention(qkv, torch.empty(192, device="cuda"),
+        _, keep, _ = torch.ops.msunet.window_attention(qkv, torch.empty(192, device="cuda"),
                                                     torch.empty(169, 2, device="cuda"), 2, 3, 0.1, 0, None)
         assert keep.shape == (2 * 2 * 2 * 2 * 128,) and keep.dtype == torch.int32
         y, mean, rstd = torch.ops.msunet.layer_norm(torch.empty(5, 96, device="cuda"), torch.empty(96, device="cuda"),

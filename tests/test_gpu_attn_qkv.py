@@ -75,7 +75,7 @@ def test_fused_forward_matches_fp32(B, H, W, shift, p_drop, proj, low):
     wp, bp = _proj(B + H) if proj else (None, None)
     with torch.no_grad(), torch.autocast("cuda", dtype=low):
         assert ops.window_attention_qkv_fusable(x, NH, b)
-        y, o, qkv, keep = torch.ops.msunet.window_attention_qkv(x, w, b, table, wp, bp, NH, shift, p_drop, 99, None,
+        y, o, qkv, keep, _ = torch.ops.msunet.window_attention_qkv(x, w, b, table, wp, bp, NH, shift, p_drop, 99, None,
                                                                 True)
     torch.cuda.synchronize()
     nwin = B * ((H + 6) // 7) * ((W + 6) // 7)
@@ -102,11 +102,11 @@ def test_fused_equals_unfused_including_backward(B, H, W, shift, low):
         wg, bg, tg, wpg, bpg = [t.clone().requires_grad_(True) for t in (w, b, table, wp0, bp0)]
         with torch.autocast("cuda", dtype=low):
             if fused:
-                y, _, qkv, keep = torch.ops.msunet.window_attention_qkv(xg, wg, bg, tg, wpg, bpg, NH, shift, 0.1, 1234,
+                y, _, qkv, keep, _ = torch.ops.msunet.window_attention_qkv(xg, wg, bg, tg, wpg, bpg, NH, shift, 0.1, 1234,
                                                                         None, True)
             else:
                 qkv = ops.linear(xg, wg, bg)
-                o, keep = torch.ops.msunet.window_attention(qkv, bg, tg, NH, shift, 0.1, 1234, None)
+                o, keep, _ = torch.ops.msunet.window_attention(qkv, bg, tg, NH, shift, 0.1, 1234, None)
                 y = ops.linear(o, wpg, bpg)
         y.backward(dy)
         torch.cuda.synchronize()
@@ -154,7 +154,7 @@ def test_fused_inference_keeps_no_qkv():
     wp, bp = _proj(5)
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
         y1 = ops.window_attention_qkv(x, w, b, table, NH, 3, proj_weight=wp, proj_bias=bp)
-        _, o, qkv, _ = torch.ops.msunet.window_attention_qkv(x, w, b, table, wp, bp, NH, 3, 0.0, 0, None, False)
+        _, o, qkv, _, _ = torch.ops.msunet.window_attention_qkv(x, w, b, table, wp, bp, NH, 3, 0.0, 0, None, False)
         y2 = ops.linear(ops.window_attention(ops.linear(x, w, b), b, table, NH, 3), wp, bp)
     assert qkv.numel() == 0 and o.numel() == 0
     _check(y1, y2, 1.5e-2, "no-grad fused vs unfused")

@@ -252,7 +252,7 @@ def test_window_attention_keep_bits_equal_rehash(low, shift):
     table = (torch.randn(169, nh, generator=g) * 0.1).to(DEV)
     dout = torch.randn(B, H, W, C, generator=g).to(DEV, low)
     p, seed = 0.3, 4321
-    y, keep = torch.ops.msunet.window_attention(qkv, qb, table, nh, shift, p, seed, None)
+    y, keep, _ = torch.ops.msunet.window_attention(qkv, qb, table, nh, shift, p, seed, None)
     nwin = B * ((H + 6) // 7) * ((W + 6) // 7)
     assert keep.numel() == nwin * nh * 128
     # bit b of word [item][it][lane]: query i = 32 it + (lane & 31), key j = 32 (b >> 4) + crow(b & 15)

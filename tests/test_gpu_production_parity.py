@@ -77,7 +77,7 @@ def test_window_attention_production_size(B, H, W, nh, shift, p_drop, low):
     qg = qkv.clone().requires_grad_(True)
     qbg, tg = qb.clone().requires_grad_(True), table.clone().requires_grad_(True)
     with torch.autocast("cuda", dtype=low):
-        y, keep = torch.ops.msunet.window_attention(qg, qbg, tg, nh, shift, p_drop, seed, None)
+        y, keep, _ = torch.ops.msunet.window_attention(qg, qbg, tg, nh, shift, p_drop, seed, None)
     assert y.dtype == low
     y.backward(dy)
     torch.cuda.synchronize()

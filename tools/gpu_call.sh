@@ -170,6 +170,7 @@ for s in "$@"; do
       done
       for f in $d/*_counter_collection.csv; do python3 $R/tools/pmc_sum.py mlp_fused $f; done > $O/${TAG}_mlp_pmc.log
       cat $O/${TAG}_mlp_pmc.log ;;
+    ab_aux) bash $R/tools/gpu_bench_ab.sh ${TAG}_aux "" "MSU_ATTN_AUX=0" "" "MSU_ATTN_AUX=0" "" "MSU_ATTN_AUX=0" || exit 3 ;;
     ab_mlp_ln) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlpln "" "MSU_MLP_LN=0" "" "MSU_MLP_LN=0" "" "MSU_MLP_LN=0" || exit 3 ;;
     ab_mlp_train) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlptrain "" "MSU_MLP_TRAIN=0" "" "MSU_MLP_TRAIN=0" "" "MSU_MLP_TRAIN=0" || exit 3 ;;
     ab_mlp) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlp "" "MSU_MLP_INFER=0" "" "MSU_MLP_INFER=0" "" "MSU_MLP_INFER=0" || exit 3 ;;
