@@ -514,8 +514,8 @@ int msu_nt_gemm_plan(long M, int N) {
   return 64 * c.wm * 1000 + c.bn;
 }
 
-// 1: the ping-pong kernel where the shape tiles exactly (default), 0: the persistent 2-barrier
-// kernel everywhere.  Returns the previous mode.
+// 1: the ping-pong kernel where the shape tiles exactly, 0 (the default, MSU_NT_PP=0): the
+// persistent 2-barrier kernel everywhere.  Returns the previous mode.
 int msu_nt_gemm_mode(int mode) {
   const int prev = g_nt_pp;
   g_nt_pp = mode ? 1 : 0;

@@ -189,12 +189,16 @@ class SwinTransformerBlock(nn.Module):
     def forward_fused(self, state):
         """state: a residual-stream tensor [B, H, W, C] or a pending ``(x, branch, scale)``
         whose add is fused into this block's norm1.  Returns this block's pending state."""
+        hk = 0
         if isinstance(state, tuple):
             x, br, sc = state
             x, xn = ops.add_layer_norm(x, br, sc, self.norm1.weight, self.norm1.bias, self.norm1.eps)
         else:
+            # x's two readers (norm1, norm2's residual add) sum their gradients inside norm1's
+            # LayerNorm backward (ops.residual_handoff_key), not in an autograd add
             x = state
-            xn = ops.layer_norm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps)
+            hk = ops.residual_handoff_key()
+            xn = ops.layer_norm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, handoff=hk)
         B = x.shape[0]
         a = self.attn(xn)
         sc1 = _drop_path_scale(self.stochastic_depth_prob, self.training, B, x.device)
@@ -208,7 +212,7 @@ class SwinTransformerBlock(nn.Module):
             if r is not None:
                 sc2 = _drop_path_scale(self.stochastic_depth_prob, self.training, B, x.device)
                 return (r[0], r[1], sc2)
-        x1, xn2 = ops.add_layer_norm(x, a, sc1, self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        x1, xn2 = ops.add_layer_norm(x, a, sc1, self.norm2.weight, self.norm2.bias, self.norm2.eps, handoff=hk)
         if not drop and fc1.bias is not None and fc2.bias is not None and \
                 ops.mlp_fusable(xn2, fc1.weight, fc2.weight):
             m = ops.mlp(xn2, fc1.weight, fc1.bias, fc2.weight, fc2.bias)

@@ -173,9 +173,29 @@ _side_keep = []
 _side_event_params = []
 
 
+# Residual-gradient handoff.  A Swin block whose input x is a plain tensor (a stage's first
+# block) feeds x to two ops: norm1's LayerNorm and norm2's residual-add LayerNorm (x + attn).
+# Autograd would sum the two gradients of x with an ATen add (14 launches per Swin-T step, 50 M
+# elements each at stage 0).  Both ops carry the same handoff key instead: norm2's backward --
+# which always runs first (attn(norm1(x)) feeds norm2) -- parks its gradient of x here and
+# returns none for it, and norm1's backward pops it and adds it inside the LayerNorm backward
+# kernel (the add-mode residual-gradient input).  Cleared at the end of every backward.
+_RES_HANDOFF = switches.on("MSU_RES_HANDOFF")
+_res_handoff = {}
+_res_keys = iter(range(1, 1 << 62))
+res_handoff_calls = 0  # LayerNorm backwards that took a parked gradient (tests)
+
+
+def residual_handoff_key():
+    """A fresh key pairing a plain layer_norm with the add_layer_norm over the same input, or 0
+    (no pairing: autograd sums the gradients)."""
+    return next(_res_keys) if (_RES_HANDOFF and torch.is_grad_enabled()) else 0
+
+
 def _end_of_backward():
     global _join_queued
     _join_queued = False
+    _res_handoff.clear()
     join_side_streams()
     _side_keep.clear()  # the main stream now waits for every side-stream read
     for p in _side_event_params:
@@ -226,7 +246,7 @@ def _stats(x, rows):
 
 
 # ----------------------------------------------------------------------------- LayerNorm
-def _ln_impl(x, w, b, eps):
+def _ln_impl(x, w, b, eps, handoff=0):
     _need_cuda(x)
     x = x.contiguous()
     C = x.shape[-1]
@@ -238,46 +258,59 @@ def _ln_impl(x, w, b, eps):
     return y, mean, rstd
 
 
-def _ln_fake(x, w, b, eps):
+def _ln_fake(x, w, b, eps, handoff=0):
     rows = x.numel() // x.shape[-1]
     return torch.empty_like(x), x.new_empty(rows, dtype=torch.float32), x.new_empty(rows, dtype=torch.float32)
 
 
 def _ln_setup(ctx, inputs, output):
-    x, w, b, eps = inputs
+    x, w, b = inputs[:3]  # layer_norm (+ handoff), merge_layer_norm, d2s_layer_norm
     ctx.save_for_backward(x.contiguous(), w, output[1], output[2])
     ctx.affine = (w, b)
+    ctx.handoff = inputs[4] if len(inputs) > 4 else 0
     ctx.set_materialize_grads(False)
 
 
 def _ln_backward(ctx, dy, _dm, _dr):
+    global res_handoff_calls
     x, w, mean, rstd = ctx.saved_tensors
+    res = _res_handoff.pop(ctx.handoff, None) if ctx.handoff else None  # the paired add-LN's dx
     if dy is None:
-        return None, None, None, None
+        return res, None, None, None, None
     dy = _as(dy, x.dtype)
     C = x.shape[-1]
     rows = x.numel() // C
     dx = torch.empty_like(x)
     dw, db, acc, direct = _ln_grads(ctx, C, x.device)
     n, part = _ln_parts(rows, C, x.device)
-    _lib.call("msu_layernorm_bwd", _dt(x), IN_PLAIN, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
-              _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, C, 0, 0, 0, acc, _s(x))
+    if res is not None:
+        # the add-mode backward: dx = LN'(dy) + res in one pass (no branch output: scale null)
+        res_handoff_calls += 1
+        _lib.call("msu_layernorm_bwd", _dt(x), IN_ADD, _p(dy), _p(x), _p(_as(res, x.dtype).contiguous()), _p(w),
+                  _p(mean), _p(rstd), _p(dx), None, None, rows // x.shape[0], _p(part), n, _p(dw), _p(db), rows, C,
+                  0, 0, 0, acc, _s(x))
+    else:
+        _lib.call("msu_layernorm_bwd", _dt(x), IN_PLAIN, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
+                  _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, C, 0, 0, 0, acc, _s(x))
     if direct:
         _notify(*ctx.affine)
-        return dx, None, None, None
-    return dx, dw, db, None
+        return dx, None, None, None, None
+    return dx, dw, db, None, None
 
 
-_layer_norm = _define("layer_norm", "(Tensor x, Tensor weight, Tensor bias, float eps) -> (Tensor, Tensor, Tensor)",
+_layer_norm = _define("layer_norm",
+                      "(Tensor x, Tensor weight, Tensor bias, float eps, int handoff=0) -> (Tensor, Tensor, Tensor)",
                       _ln_impl, _ln_fake, _ln_setup, _ln_backward)
 
 
-def layer_norm(x, weight, bias, eps=1e-5):
-    """nn.LayerNorm(C) over the last dim; x keeps its (autocast) dtype."""
-    return _layer_norm(_as(x, act_dtype()), _f32(weight), _f32(bias), float(eps))[0]
+def layer_norm(x, weight, bias, eps=1e-5, handoff=0):
+    """nn.LayerNorm(C) over the last dim; x keeps its (autocast) dtype.  handoff: a
+    ``residual_handoff_key()`` shared with the add_layer_norm that also reads x (its gradient of
+    x is added inside this op's backward kernel)."""
+    return _layer_norm(_as(x, act_dtype()), _f32(weight), _f32(bias), float(eps), int(handoff))[0]
 
 
-def _add_ln_impl(a, branch, scale, w, b, eps):
+def _add_ln_impl(a, branch, scale, w, b, eps, handoff=0):
     """s = a + scale[sample] * branch ; y = LN(s)."""
     _need_cuda(a, branch)
     a, branch = a.contiguous(), branch.contiguous()
@@ -292,18 +325,19 @@ def _add_ln_impl(a, branch, scale, w, b, eps):
     return s, y, mean, rstd
 
 
-def _add_ln_fake(a, branch, scale, w, b, eps):
+def _add_ln_fake(a, branch, scale, w, b, eps, handoff=0):
     rows = a.numel() // a.shape[-1]
     return (torch.empty_like(a), torch.empty_like(a), a.new_empty(rows, dtype=torch.float32),
             a.new_empty(rows, dtype=torch.float32))
 
 
 def _add_ln_setup(ctx, inputs, output):
-    a, branch, scale, w, b, eps = inputs
+    a, branch, scale, w, b, eps, handoff = inputs
     s, y, mean, rstd = output
     ctx.save_for_backward(s, w, mean, rstd, scale)
     ctx.rps = (a.numel() // a.shape[-1]) // a.shape[0]
     ctx.affine = (w, b)
+    ctx.handoff = handoff
     ctx.set_materialize_grads(False)
 
 
@@ -324,21 +358,31 @@ def _add_ln_backward(ctx, ds, dy, _dm, _dr):
     if direct:
         _notify(*ctx.affine)
         dw = dbb = None
-    return da, (dbr if dbr is not None else da), None, dw, dbb, None
+    dbr = dbr if dbr is not None else da
+    if ctx.handoff:
+        # a's other reader is the paired plain LayerNorm, whose backward runs later and adds da
+        # in its kernel: park it, autograd sees no gradient for a here
+        _res_handoff[ctx.handoff] = da
+        _join_at_end_of_backward()  # clears the mailbox at the end of this backward
+        return None, dbr, None, dw, dbb, None, None
+    return da, dbr, None, dw, dbb, None, None
 
 
 _add_layer_norm = _define(
     "add_layer_norm",
-    "(Tensor a, Tensor branch, Tensor? scale, Tensor weight, Tensor bias, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
+    "(Tensor a, Tensor branch, Tensor? scale, Tensor weight, Tensor bias, float eps, int handoff=0)"
+    " -> (Tensor, Tensor, Tensor, Tensor)",
     _add_ln_impl, _add_ln_fake, _add_ln_setup, _add_ln_backward)
 
 
-def add_layer_norm(a, branch, scale, weight, bias, eps=1e-5):
+def add_layer_norm(a, branch, scale, weight, bias, eps=1e-5, handoff=0):
     """(s, LN(s)) with s = a + scale[sample] * branch (torchvision block residual with
-    StochasticDepth 'row', fused with the next norm)."""
+    StochasticDepth 'row', fused with the next norm).  handoff: the key of the plain layer_norm
+    that also reads ``a`` (see ``residual_handoff_key``)."""
     dt = act_dtype()
     sc = None if scale is None else _f32(scale)
-    s, y, _, _ = _add_layer_norm(_as(a, dt), _as(branch, dt), sc, _f32(weight), _f32(bias), float(eps))
+    s, y, _, _ = _add_layer_norm(_as(a, dt), _as(branch, dt), sc, _f32(weight), _f32(bias), float(eps),
+                                 int(handoff))
     return s, y
 
 
@@ -447,19 +491,45 @@ _ATTN_KEEP = True
 _ATTN_AUX = switches.on("MSU_ATTN_AUX")
 
 
+def _attn_fwd_ws(dt, C, nh):
+    """msu_win_attn_fwd_workspace restated (window_attention_mfma.hip aux_floats): the 16-bit
+    forward's aux region -- relative-bias image nh x 4096 f32, the 16-bit qkv-bias row, a zero
+    row; f32 kernels 1.  Python-side so fake kernels propagate shapes without the library
+    (tests/test_capi.py checks it against the library over a grid of shapes)."""
+    return nh * 4096 + (6 * C + 1) // 2 + 4 if dt in _LOW else 1
+
+
+def _nwin(B, H, W):
+    return B * (-(-H // 7)) * (-(-W // 7))
+
+
+def _attn_bwd_ws(dt, B, H, W, C, nh):
+    """msu_win_attn_bwd_workspace restated: 16-bit -- aux region + per-block partials of the
+    relative-table gradient (169 x nh) and the qkv-bias gradient (3C), over head_blocks(nwin,
+    1024 / nh) blocks (a multiple of 8); f32 -- min(2048 / nh, nwin) blocks of nh x 49^2 + 3C
+    partials and one nh x 49^2 image."""
+    nwin = _nwin(B, H, W)
+    if dt in _LOW:
+        cap = max(8, (1024 // nh) // 8 * 8)
+        parts = (min(nwin, cap) + 7) // 8 * 8
+        return _attn_fwd_ws(dt, C, nh) + parts * nh * 169 + parts * 3 * C
+    nblk = max(1, min(2048 // nh, nwin))
+    return nblk * nh * 49 * 49 + nh * 49 * 49 + nblk * 3 * C
+
+
+def _attn_keep_words(dt, B, H, W, nh):
+    """msu_win_attn_keep_words restated: 128 keep-bit words per window x head (16-bit kernels)."""
+    return _nwin(B, H, W) * nh * 128 if dt in _LOW else 0
+
+
 def _attn_ws_numel(dt, B, H, W, C, nh):
     """Workspace floats of a 16-bit attention forward that its backward reuses: the forward's aux
     region (relative-bias image, bias / zero rows) stays valid for the backward, which then skips
     its own aux launch (msu_win_attn_bwd2 with table = null); f32: the forward's only."""
-    L = _lib.lib()
-    n = L.msu_win_attn_fwd_workspace(_dt_code(dt), C, nh)
+    n = _attn_fwd_ws(dt, C, nh)
     if dt in _LOW and _ATTN_AUX:
-        n = max(n, L.msu_win_attn_bwd_workspace(_dt_code(dt), B, H, W, C, nh))
+        n = max(n, _attn_bwd_ws(dt, B, H, W, C, nh))
     return n
-
-
-def _dt_code(dt):
-    return _DT[dt]
 
 
 def _attn_impl(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
@@ -468,10 +538,9 @@ def _attn_impl(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
     B, H, W, C3 = qkv.shape
     C = C3 // 3
     out = torch.empty(B, H, W, C, device=qkv.device, dtype=qkv.dtype)
-    L = _lib.lib()
     ws = torch.empty(_attn_ws_numel(qkv.dtype, B, H, W, C, num_heads), device=qkv.device, dtype=torch.float32)
     # the dropout keep bits, written by the forward for the backward (16-bit dtypes)
-    keep = torch.empty(L.msu_win_attn_keep_words(_dt(qkv), B, H, W, num_heads) if p_drop > 0 and _ATTN_KEEP else 0,
+    keep = torch.empty(_attn_keep_words(qkv.dtype, B, H, W, num_heads) if p_drop > 0 and _ATTN_KEEP else 0,
                        device=qkv.device, dtype=torch.int32)
     _lib.call("msu_win_attn_fwd", _dt(qkv), _p(qkv), _p(qkv_bias), _p(table), _p(out), _p(ws), B, H, W,
               C, num_heads, shift, float(p_drop), seed, _p(seed_dev), _p(keep) if keep.numel() else None,
@@ -481,8 +550,7 @@ def _attn_impl(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
 
 def _attn_fake(qkv, qkv_bias, table, num_heads, shift, p_drop, seed, seed_dev):
     B, H, W, C3 = qkv.shape
-    nwin = B * (-(-H // 7)) * (-(-W // 7))
-    kw = nwin * num_heads * 128 if (p_drop > 0 and _ATTN_KEEP and qkv.dtype in _LOW) else 0
+    kw = _attn_keep_words(qkv.dtype, B, H, W, num_heads) if (p_drop > 0 and _ATTN_KEEP) else 0
     return (qkv.new_empty(B, H, W, C3 // 3), qkv.new_empty(kw, dtype=torch.int32),
             qkv.new_empty(_attn_ws_numel(qkv.dtype, B, H, W, C3 // 3, num_heads), dtype=torch.float32))
 
@@ -509,8 +577,7 @@ def _attn_backward(ctx, dout, _dkeep, _dws=None):
     B, H, W, C3 = qkv.shape
     C = C3 // 3
     dout = _as(dout, qkv.dtype)
-    L = _lib.lib()
-    need = L.msu_win_attn_bwd_workspace(_dt(qkv), B, H, W, C, nh)
+    need = _attn_bwd_ws(qkv.dtype, B, H, W, C, nh)
     ws = getattr(ctx, "aux_ws", None)
     if ws is not None and _ATTN_AUX and qkv.dtype in _LOW and ws.numel() >= need:
         tbl = None  # the forward's aux region is still in ws: no second aux launch
@@ -609,13 +676,12 @@ def _attn_qkv_impl(x, weight, bias, table, proj_weight, proj_bias, num_heads, sh
     w = _shadow(weight, dt)
     proj = proj_weight is not None
     wp = _shadow(proj_weight, dt) if proj else None
-    L = _lib.lib()
     y = torch.empty(B, H, W, C, device=x.device, dtype=dt)
     o = torch.empty(B, H, W, C, device=x.device, dtype=dt) if (proj and store) else x.new_empty(0)
     qkv = torch.empty(B, H, W, 3 * C, device=x.device, dtype=dt) if store else x.new_empty(0)
-    ws = torch.empty(_attn_ws_numel(dt, B, H, W, C, num_heads) if store else
-                     L.msu_win_attn_fwd_workspace(_dt(x), C, num_heads), device=x.device, dtype=torch.float32)
-    keep = torch.empty(L.msu_win_attn_keep_words(_dt(x), B, H, W, num_heads) if p_drop > 0 and _ATTN_KEEP else 0,
+    ws = torch.empty(_attn_ws_numel(dt, B, H, W, C, num_heads) if store else _attn_fwd_ws(dt, C, num_heads),
+                     device=x.device, dtype=torch.float32)
+    keep = torch.empty(_attn_keep_words(dt, B, H, W, num_heads) if p_drop > 0 and _ATTN_KEEP else 0,
                        device=x.device, dtype=torch.int32)
     fused_qkv_calls += 1
     _lib.call("msu_win_attn_qkv_fwd2", _dt(x), _p(x), _p(w), _p(bias), _p(table), _p(wp),
@@ -627,11 +693,8 @@ def _attn_qkv_impl(x, weight, bias, table, proj_weight, proj_bias, num_heads, sh
 
 def _attn_qkv_fake(x, weight, bias, table, proj_weight, proj_bias, num_heads, shift, p_drop, seed, seed_dev, store):
     B, H, W, C = x.shape
-    nwin = B * (-(-H // 7)) * (-(-W // 7))
-    kw = nwin * num_heads * 128 if (p_drop > 0 and _ATTN_KEEP) else 0
-    L = _lib.lib()
-    nws = _attn_ws_numel(x.dtype, B, H, W, C, num_heads) if store else L.msu_win_attn_fwd_workspace(
-        _dt_code(x.dtype), C, num_heads)
+    kw = _attn_keep_words(x.dtype, B, H, W, num_heads) if (p_drop > 0 and _ATTN_KEEP) else 0
+    nws = _attn_ws_numel(x.dtype, B, H, W, C, num_heads) if store else _attn_fwd_ws(x.dtype, C, num_heads)
     return (x.new_empty(B, H, W, C),
             x.new_empty(B, H, W, C) if (proj_weight is not None and store) else x.new_empty(0),
             x.new_empty(B, H, W, 3 * C) if store else x.new_empty(0), x.new_empty(kw, dtype=torch.int32),
@@ -1175,15 +1238,15 @@ _MLP_INFER = switches.on("MSU_MLP_INFER")
 _MLP_TRAIN = switches.on("MSU_MLP_TRAIN")
 mlp_infer_calls = 0  # fused MLP launches without H (tests assert which path a no-grad forward took)
 mlp_train_calls = 0  # fused MLP launches storing H
-_mlp_fused_cache = {}
+
+
+# the one (C, hidden) the fused MLP kernel is built for: msu_mlp_fused_supported restated (MC, MH
+# in csrc/mlp_fused.hip; tests/test_capi.py checks the two agree), so fake kernels need no library
+MLP_FUSED_SHAPE = (96, 384)
 
 
 def _mlp_fused_ok(C, Hd):
-    key = (int(C), int(Hd))
-    r = _mlp_fused_cache.get(key)
-    if r is None:
-        r = _mlp_fused_cache[key] = bool(_lib.lib().msu_mlp_fused_supported(*key))
-    return r
+    return (int(C), int(Hd)) == MLP_FUSED_SHAPE
 
 
 def _mlp_impl(x, w1, b1, w2, b2, keep):
@@ -1197,7 +1260,8 @@ def _mlp_impl(x, w1, b1, w2, b2, keep):
     W1 = _shadow(w1, x.dtype)
     W2 = _shadow(w2, x.dtype)
     Hd, C = W1.shape
-    if (_MLP_TRAIN if keep else _MLP_INFER) and x.dtype in _LOW and _mlp_fused_ok(C, Hd):
+    fused = _mlp_fused_route(x, w1, keep)
+    if fused:
         # one kernel, the hidden activation on chip (csrc/mlp_fused.hip); training keeps H only
         # (the backward re-derives GELU(H)).  Operands 16-B aligned (weight shadows are views
         # into one flat buffer).
@@ -1217,12 +1281,21 @@ def _mlp_impl(x, w1, b1, w2, b2, keep):
     y = _gemm(g, W2, _f32(b2))
     if not keep:
         return y, x.new_empty(0), x.new_empty(0)
-    return y, h, g
+    # the fused route's output contract (G empty: the backward re-derives it) also when an
+    # unaligned operand sent the call to the GEMM pair -- the fake kernel can't see alignment
+    return y, h, (x.new_empty(0) if fused else g)
+
+
+def _mlp_fused_route(x, w1, keep):
+    """Whether an mlp call takes the fused kernel's output contract: H kept, G empty (training)."""
+    Hd, C = w1.shape
+    return bool((_MLP_TRAIN if keep else _MLP_INFER) and x.dtype in _LOW and _mlp_fused_ok(C, Hd))
 
 
 def _mlp_fake(x, w1, b1, w2, b2, keep):
     hid = x.new_empty(*x.shape[:-1], w1.shape[0]) if keep else x.new_empty(0)
-    return x.new_empty(*x.shape[:-1], w2.shape[0]), hid, torch.empty_like(hid)
+    g = x.new_empty(0) if (not keep or _mlp_fused_route(x, w1, keep)) else torch.empty_like(hid)
+    return x.new_empty(*x.shape[:-1], w2.shape[0]), hid, g
 
 
 def _mlp_setup(ctx, inputs, output):

@@ -92,3 +92,52 @@ def test_torch_library_ops_registered():
     # a CPU tensor has no kernel (no silent CPU fallback)
     with pytest.raises(NotImplementedError):
         torch.ops.msunet.gelu(torch.zeros(8))
+
+
+def test_python_workspace_sizes_match_the_library():
+    """The fake kernels size the attention workspaces / keep bits and pick the mlp route from
+    Python restatements (no library needed for shape propagation); they equal the library's
+    own msu_win_attn_*_workspace / keep_words / msu_mlp_fused_supported."""
+    import torch
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built")
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    L = _lib.lib()
+    for dt, code in ((torch.bfloat16, 1), (torch.float16, 2), (torch.float32, 0)):
+        for B, H, W, nh in ((1, 7, 7, 1), (2, 10, 12, 2), (8, 256, 256, 3), (8, 128, 128, 6), (8, 64, 64, 12),
+                            (8, 32, 32, 24), (1, 56, 56, 3), (3, 15, 9, 4), (8, 16, 16, 32)):
+            C = 32 * nh
+            assert ops._attn_fwd_ws(dt, C, nh) == L.msu_win_attn_fwd_workspace(code, C, nh)
+            assert ops._attn_bwd_ws(dt, B, H, W, C, nh) == L.msu_win_attn_bwd_workspace(code, B, H, W, C, nh)
+            assert ops._attn_keep_words(dt, B, H, W, nh) == L.msu_win_attn_keep_words(code, B, H, W, nh)
+    for C, Hd in ((96, 384), (192, 768), (96, 192), (384, 96)):
+        assert ops._mlp_fused_ok(C, Hd) == bool(L.msu_mlp_fused_supported(C, Hd))
+
+
+def test_mlp_fake_matches_the_route_contract():
+    """ADVICE r5: msunet::mlp's fake kernel reports the outputs the real kernel returns -- with
+    keep (training) on the fused route H is [..., Hd] and G is empty (the backward re-derives
+    GELU(H)); on the GEMM-pair route (f32, other widths) G is [..., Hd] too; without keep both
+    are empty."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    with FakeTensorMode():
+        for dt, C, Hd, fused in ((torch.bfloat16, 96, 384, ops._MLP_TRAIN), (torch.float16, 96, 384, ops._MLP_TRAIN),
+                                 (torch.bfloat16, 192, 768, False), (torch.float32, 96, 384, False)):
+            x = torch.empty(4, 7, C, device="cuda", dtype=dt)
+            w1, w2 = torch.empty(Hd, C, device="cuda"), torch.empty(C, Hd, device="cuda")
+            b1, b2 = torch.empty(Hd, device="cuda"), torch.empty(C, device="cuda")
+            y, h, g = torch.ops.msunet.mlp(x, w1, b1, w2, b2, True)
+            assert y.shape == (4, 7, C) and h.shape == (4, 7, Hd)
+            assert g.numel() == 0 if fused else g.shape == (4, 7, Hd)
+            y, h, g = torch.ops.msunet.mlp(x, w1, b1, w2, b2, False)
+            assert y.shape == (4, 7, C) and h.numel() == 0 and g.numel() == 0
+        # the fused stage-0 attention unit's fake sizes its workspace without the library
+        x = torch.empty(2, 14, 14, 96, device="cuda", dtype=torch.bfloat16)
+        out = torch.ops.msunet.window_attention_qkv(
+            x, torch.empty(288, 96, device="cuda"), torch.empty(288, device="cuda"), torch.empty(169, 3, device="cuda"),
+            torch.empty(96, 96, device="cuda"), torch.empty(96, device="cuda"), 3, 3, 0.1, 0, None, True)
+        assert out[0].shape == (2, 14, 14, 96) and out[2].shape == (2, 14, 14, 288)
+        assert out[3].numel() == 2 * 2 * 2 * 3 * 128
+        assert out[4].numel() == ops._attn_ws_numel(torch.bfloat16, 2, 14, 14, 96, 3)

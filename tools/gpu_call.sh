@@ -22,11 +22,17 @@ step() {  # name seconds cmd...
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
 for s in "$@"; do
   case $s in
-    tests_new) step tests_new 600 $PYT -m gpu $R/tests/test_gpu_attn_qkv.py $R/tests/test_gpu_ln_side.py \
-                 $R/tests/test_gpu_rccl.py ;;
+    tests_new) step tests_new 900 $PYT -m gpu $R/tests/test_gpu_handoff.py $R/tests/test_gpu_mlp_infer.py \
+                 $R/tests/test_gpu_model.py $R/tests/test_gpu_ln_side.py ;;
     parity) step parity 900 $PYT -s -m gpu $R/tests/test_gpu_step_parity.py ;;
     nt_tests) step nt_tests 600 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py $R/tests/test_routing.py ;;
     nt_ab) step nt_ab 300 python -u $R/tools/nt_ab.py 3 20 ;;
+    nt_shapes)
+      # NT GEMM kernel times per stage 1-3 shape: this build (A) vs AB_LIB (B), interleaved twice
+      for L in "" "$AB_LIB" "" "$AB_LIB"; do
+        MSU_LIB_OVERRIDE=$L timeout -k 10 200 python -u $R/tools/nt_shapes.py 20 ${L:+B} >> $O/${TAG}_nt_shapes.log 2>&1 || exit 3
+      done
+      python3 $R/tools/ab_table.py $O/${TAG}_nt_shapes.log ;;
     nt_exp)
       for X in 4 8; do
         echo "== MSU_EXP=$X (1: no DMA, 2: no fragment reads, 4: no MFMA, 8: no epilogue)" >> $O/${TAG}_nt_exp.log
