@@ -228,6 +228,13 @@ MSU_DEV int xcd_remap(int b, int nb) {
   return start + local;
 }
 
+// opaque copy of a value: stops the compiler from hoisting per-chunk index math out of a
+// persistent tile loop (it would keep ~5 registers per chunk live across the whole loop)
+MSU_DEV int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // ------------------------------------------------------------------ LDS-DMA helpers
 // global_load_lds_dwordx4: each lane's 16 B land at lds_base + 16 * lane (lds_base is
 // wave-uniform); counted by vmcnt like any global load.

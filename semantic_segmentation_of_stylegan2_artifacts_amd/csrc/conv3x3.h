@@ -59,13 +59,6 @@ MSU_DEV int pix_off32(int b, int y, int x, int H, int W, int C) {
   }
 }
 
-// opaque copy of a value: stops the compiler from hoisting per-chunk index math out of the
-// persistent tile loop (it would keep ~5 registers per chunk live across the whole loop)
-MSU_DEV int opaque(int v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-
 // Stage rows [y_first, y_first + nrows) x cols [x0 - 1, x0 + TW + 1) of the transformed
 // input image (GELU optional) into LDS sX[(row * (TW+2) + col) * PS + c]; zero outside.
 template <typename T, bool D2S, bool GELU>

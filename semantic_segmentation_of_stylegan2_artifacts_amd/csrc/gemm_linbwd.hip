@@ -93,13 +93,6 @@ constexpr int ring_depth() {
   return GG ? MSU_LB_DGG : ts_of(K, N) == 64 ? 2 : (K == 96 && N == 96 ? MSU_LB_D96 : 3);
 }
 
-// opaque copy of a value: keeps the compiler from hoisting per-chunk / per-tile index math out
-// of the step loop (it would pin registers for the whole kernel)
-MSU_DEV int opaque(int v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-
 MSU_DEV v4s tr_read(const bf16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)p); }
 
 // 16-B global loads of the staged token rows.  Plain (compiler-tracked) loads: the compiler

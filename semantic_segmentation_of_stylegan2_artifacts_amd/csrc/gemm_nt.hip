@@ -361,6 +361,9 @@ namespace {
 // default): the persistent 2-barrier kernel everywhere.  A/B switch MSU_NT_PP, set by the Python
 // side at import: the ping-pong kernel measured 0.72-0.98x of the persistent one (r05g)
 int g_nt_pp = 0;
+// tile-form override for kernel-timing tools (msu_nt_gemm_mode bits 1-2): 0 = the cost model,
+// 1 = 128 x 192 (two workgroups per CU), 2 = 256 x 128 (three-stage ring), 3 = 128 x 128
+int g_nt_force = 0;
 
 int num_cus_nt();
 
@@ -411,6 +414,9 @@ struct NtCfg {
 };
 
 NtCfg nt_cfg(long M, int N, bool wkn) {
+  if (g_nt_force == 1 && !wkn && N % 192 == 0) return NtCfg{2, 192};
+  if (g_nt_force == 2) return NtCfg{4, 128};
+  if (g_nt_force == 3) return NtCfg{2, 128};
   const long cus = num_cus_nt();
   const NtCfg cands[4] = {{4, 128}, {2, 128}, {4, 192}, {2, 192}};
   NtCfg best = cands[0];
@@ -514,11 +520,13 @@ int msu_nt_gemm_plan(long M, int N) {
   return 64 * c.wm * 1000 + c.bn;
 }
 
-// 1: the ping-pong kernel where the shape tiles exactly, 0 (the default, MSU_NT_PP=0): the
-// persistent 2-barrier kernel everywhere.  Returns the previous mode.
+// bit 0 -- 1: the ping-pong kernel where the shape tiles exactly, 0 (the default, MSU_NT_PP=0): the
+// persistent 2-barrier kernel everywhere; bits 1-2: a forced tile form for kernel-timing tools
+// (0: the cost model; 1: 128 x 192, 2: 256 x 128, 3: 128 x 128).  Returns the previous mode.
 int msu_nt_gemm_mode(int mode) {
-  const int prev = g_nt_pp;
-  g_nt_pp = mode ? 1 : 0;
+  const int prev = g_nt_pp | (g_nt_force << 1);
+  g_nt_pp = mode & 1;
+  g_nt_force = (mode >> 1) & 3;
   return prev;
 }
 

@@ -302,14 +302,20 @@ int launch_mlp(const MlpArgs& a, hipStream_t st) {
 
 }  // namespace
 
+// mlp_s1.hip: the stage-1 form (C = 192, hidden 768, weights streamed through an LDS ring)
+int msu_mlp_s1_launch(int dtype, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                      void* y, void* h, long M, void* stream);
+
 extern "C" {
 
-// Whether msu_mlp_fused_fwd covers a (channels, hidden) shape: the stage-0 MLP, 96 -> 384 -> 96.
-int msu_mlp_fused_supported(int C, int Hd) { return C == MC && Hd == MH ? 1 : 0; }
+// Whether msu_mlp_fused_fwd covers a (channels, hidden) shape: the stage-0 MLP, 96 -> 384 -> 96,
+// and the stage-1 MLP, 192 -> 768 -> 192 (msu_add_ln_mlp_fwd: stage 0 only).
+int msu_mlp_fused_supported(int C, int Hd) { return (C == MC && Hd == MH) || (C == 192 && Hd == 768) ? 1 : 0; }
 
 // y = fc2(GELU(fc1(x))) with the hidden activation kept on chip; h (nullable) receives the
-// 16-bit pre-activation fc1(x) [M][384] for the backward.  dtype bf16 / f16; x, y [M][96]
-// (16-B aligned rows), w1 [384][96], w2 [96][384] in x's format, b1 [384] / b2 [96] f32.
+// 16-bit pre-activation fc1(x) [M][Hd] for the backward.  dtype bf16 / f16; x, y [M][C] (16-B
+// aligned rows), w1 [Hd][C], w2 [C][Hd] in x's format, b1 [Hd] / b2 [C] f32; (C, Hd) = (96, 384)
+// or (192, 768).
 int msu_mlp_fused_fwd(int dtype, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
                       void* y, void* h, long M, int C, int Hd, void* stream) {
   if (!msu_is16(dtype) || !msu_mlp_fused_supported(C, Hd) || M < 0) return -2;
@@ -317,6 +323,7 @@ int msu_mlp_fused_fwd(int dtype, const void* x, const void* w1, const float* b1,
        15) != 0)
     return -2;
   if (M == 0) return 0;
+  if (C != MC) return msu_mlp_s1_launch(dtype, x, w1, b1, w2, b2, y, h, M, stream);
   hipStream_t st = (hipStream_t)stream;
   MlpArgs a{};
   a.x = (const bf16_t*)x;
@@ -342,7 +349,7 @@ int msu_mlp_fused_fwd(int dtype, const void* x, const void* w1, const float* b1,
 int msu_add_ln_mlp_fwd(int dtype, const void* a, const void* br, const float* bscale, long rows_per_sample,
                        const float* gamma, const float* beta, float eps, const void* w1, const float* b1,
                        const void* w2, const float* b2, void* s_out, void* y, long M, int C, int Hd, void* stream) {
-  if (!msu_is16(dtype) || !msu_mlp_fused_supported(C, Hd) || M < 0 || rows_per_sample <= 0) return -2;
+  if (!msu_is16(dtype) || C != MC || Hd != MH || M < 0 || rows_per_sample <= 0) return -2;
   if ((((uintptr_t)a | (uintptr_t)br | (uintptr_t)s_out | (uintptr_t)y | (uintptr_t)w1 | (uintptr_t)w2 |
         (uintptr_t)b1 | (uintptr_t)b2 | (uintptr_t)gamma | (uintptr_t)beta) & 15) != 0)
     return -2;

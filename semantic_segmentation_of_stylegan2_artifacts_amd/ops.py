@@ -866,23 +866,35 @@ def _gemm_dx(dy, w, epi=TOK_PLAIN, h=None, param=None):
     return _gemm(dy, _wt(w) if wt is None else wt, None, epi, h)
 
 
-def _wgrad(dy, x, weight, bias, M, N, K):
+def _gelu16(h):
+    """GELU(h) in h's 16-bit format on the current stream (msu_gelu_fwd: the fused epilogues'
+    arithmetic and rounding)."""
+    g = torch.empty_like(h)
+    _lib.call("msu_gelu_fwd", _dt(h), _p(h), _p(g), h.numel(), _s(h))
+    return g
+
+
+def _wgrad(dy, x, weight, bias, M, N, K, x_gelu_of=None):
     """Linear weight/bias gradients on msu_linear_wgrad; (None, None) when accumulated
-    straight into the trainer's flat .grad views."""
+    straight into the trainer's flat .grad views.  x None: x = GELU(x_gelu_of), derived on the
+    stream the weight gradient runs on."""
     L = _lib.lib()
     if _direct(weight) and (bias is None or _direct(bias)):
         if _side_enabled and _side_wgrad:
-            main = torch.cuda.current_stream(x.device)
-            side = _side_stream_for(x.device)
+            src = x if x is not None else x_gelu_of
+            main = torch.cuda.current_stream(src.device)
+            side = _side_stream_for(src.device)
             side.wait_stream(main)  # dy and x are ready
             with torch.cuda.stream(side):
+                if x is None:
+                    x = _gelu16(x_gelu_of)  # allocated on the side stream, used there only
                 ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
                 _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(weight.grad),
                           _p(None if bias is None else bias.grad), _p(ws), M, N, K, 1, side.cuda_stream)
             dy.record_stream(side)  # their memory is not reused by the main stream meanwhile
-            x.record_stream(side)
+            src.record_stream(side)
             _side_keep.append(dy)  # ... nor accumulated into in place (see _side_keep)
-            _side_keep.append(x)
+            _side_keep.append(src)
             ev = torch.cuda.Event()
             ev.record(side)
             _guard_side_write(weight, ev)
@@ -890,11 +902,15 @@ def _wgrad(dy, x, weight, bias, M, N, K):
                 _guard_side_write(bias, ev)
             _join_at_end_of_backward()
         else:
+            if x is None:
+                x = _gelu16(x_gelu_of)
             ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
             _lib.call("msu_linear_wgrad", _dt(x), _p(dy), _p(x), _p(weight.grad),
                       _p(None if bias is None else bias.grad), _p(ws), M, N, K, 1, _s(x))
         _notify(weight, bias)
         return None, None
+    if x is None:
+        x = _gelu16(x_gelu_of)
     ws = torch.empty(L.msu_wgrad_workspace(M, N, K), device=x.device, dtype=torch.float32)
     dw = torch.empty(N, K, device=x.device, dtype=torch.float32)
     db = torch.empty(N, device=x.device, dtype=torch.float32) if bias is not None else None
@@ -1240,13 +1256,17 @@ mlp_infer_calls = 0  # fused MLP launches without H (tests assert which path a n
 mlp_train_calls = 0  # fused MLP launches storing H
 
 
-# the one (C, hidden) the fused MLP kernel is built for: msu_mlp_fused_supported restated (MC, MH
-# in csrc/mlp_fused.hip; tests/test_capi.py checks the two agree), so fake kernels need no library
-MLP_FUSED_SHAPE = (96, 384)
+# the (C, hidden) shapes the fused MLP kernels are built for: msu_mlp_fused_supported restated
+# (stage 0: csrc/mlp_fused.hip, weights resident in LDS; stage 1: csrc/mlp_s1.hip, weights streamed
+# through an LDS ring; tests/test_capi.py checks the two agree), so fake kernels need no library
+MLP_KERNEL_SHAPES = ((96, 384), (192, 768))
+# MSU_MLP_S1=0: the stage-1 MLPs on the GEMM pair (A/B switch)
+_MLP_S1 = switches.on("MSU_MLP_S1")
+MLP_FUSED_SHAPES = MLP_KERNEL_SHAPES if _MLP_S1 else MLP_KERNEL_SHAPES[:1]
 
 
 def _mlp_fused_ok(C, Hd):
-    return (int(C), int(Hd)) == MLP_FUSED_SHAPE
+    return (int(C), int(Hd)) in MLP_FUSED_SHAPES
 
 
 def _mlp_impl(x, w1, b1, w2, b2, keep):
@@ -1322,13 +1342,12 @@ def _mlp_backward(ctx, dy, _dh, _dg):
     dy = dy.contiguous()
     if g.numel() == 0:  # fused forward: H only; mlp.3's pass re-derives GELU(H) while staging
         dh = _linbwd(dy, h, w2, b2, M, C, Hd, h=h, gelu_x=True)
-        if dh is None:  # the two-kernel path reads GELU(H): derive it in H's 16-bit format
-            g = torch.empty_like(h)
-            _lib.call("msu_gelu_fwd", _dt(h), _p(h), _p(g), h.numel(), _s(h))
     else:
         dh = _linbwd(dy, g, w2, b2, M, C, Hd, h=h)  # mlp.3 in one pass (dh through GELU')
     if dh is None:
-        dw2, db2 = _wgrad(dy, g, w2, b2, M, C, Hd)
+        # two kernels: the weight gradient reads GELU(H) -- after a fused forward it is derived
+        # from H (in H's 16-bit format) where that weight gradient runs, the side stream
+        dw2, db2 = _wgrad(dy, g if g.numel() else None, w2, b2, M, C, Hd, x_gelu_of=h)
         dh = _gemm_dx(dy, W2, TOK_GELU_GRAD, h=h, param=w2)
     else:
         dw2 = db2 = None
@@ -1358,7 +1377,7 @@ def add_layer_norm_mlp(a, branch, scale, ln_weight, ln_bias, eps, fc1_weight, fc
         return None
     C = a.shape[-1]
     Hd = fc1_weight.shape[0]
-    if fc1_bias is None or fc2_bias is None or not _mlp_fused_ok(C, Hd) or fc2_weight.shape != (C, Hd):
+    if fc1_bias is None or fc2_bias is None or (C, Hd) != MLP_FUSED_SHAPES[0] or fc2_weight.shape != (C, Hd):
         return None
     a, branch = _as(a, dt), _as(branch, dt)
     W1, W2 = _shadow(fc1_weight, dt), _shadow(fc2_weight, dt)

@@ -110,8 +110,10 @@ def test_python_workspace_sizes_match_the_library():
             assert ops._attn_fwd_ws(dt, C, nh) == L.msu_win_attn_fwd_workspace(code, C, nh)
             assert ops._attn_bwd_ws(dt, B, H, W, C, nh) == L.msu_win_attn_bwd_workspace(code, B, H, W, C, nh)
             assert ops._attn_keep_words(dt, B, H, W, nh) == L.msu_win_attn_keep_words(code, B, H, W, nh)
-    for C, Hd in ((96, 384), (192, 768), (96, 192), (384, 96)):
-        assert ops._mlp_fused_ok(C, Hd) == bool(L.msu_mlp_fused_supported(C, Hd))
+    for C, Hd in ((96, 384), (192, 768), (96, 192), (384, 96), (384, 1536)):
+        assert ((C, Hd) in ops.MLP_KERNEL_SHAPES) == bool(L.msu_mlp_fused_supported(C, Hd))
+        if ops._mlp_fused_ok(C, Hd):
+            assert (C, Hd) in ops.MLP_KERNEL_SHAPES
 
 
 def test_mlp_fake_matches_the_route_contract():
@@ -124,7 +126,8 @@ def test_mlp_fake_matches_the_route_contract():
     from semantic_segmentation_of_stylegan2_artifacts_amd import ops
     with FakeTensorMode():
         for dt, C, Hd, fused in ((torch.bfloat16, 96, 384, ops._MLP_TRAIN), (torch.float16, 96, 384, ops._MLP_TRAIN),
-                                 (torch.bfloat16, 192, 768, False), (torch.float32, 96, 384, False)):
+                                 (torch.bfloat16, 192, 768, ops._MLP_TRAIN and ops._MLP_S1),
+                                 (torch.bfloat16, 384, 1536, False), (torch.float32, 96, 384, False)):
             x = torch.empty(4, 7, C, device="cuda", dtype=dt)
             w1, w2 = torch.empty(Hd, C, device="cuda"), torch.empty(C, Hd, device="cuda")
             b1, b2 = torch.empty(Hd, device="cuda"), torch.empty(C, device="cuda")

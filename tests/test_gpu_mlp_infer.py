@@ -28,12 +28,13 @@ def low(request):
     return request.param
 
 
-def _params(seed, low):
+def _params(seed, low, C=96):
     g = torch.Generator().manual_seed(seed)
-    w1 = torch.nn.Parameter((torch.randn(384, 96, generator=g) / 96 ** 0.5).to(DEV))
-    b1 = torch.nn.Parameter((torch.randn(384, generator=g) * 0.1).to(DEV))
-    w2 = torch.nn.Parameter((torch.randn(96, 384, generator=g) / 384 ** 0.5).to(DEV))
-    b2 = torch.nn.Parameter((torch.randn(96, generator=g) * 0.1).to(DEV))
+    Hd = 4 * C
+    w1 = torch.nn.Parameter((torch.randn(Hd, C, generator=g) / C ** 0.5).to(DEV))
+    b1 = torch.nn.Parameter((torch.randn(Hd, generator=g) * 0.1).to(DEV))
+    w2 = torch.nn.Parameter((torch.randn(C, Hd, generator=g) / Hd ** 0.5).to(DEV))
+    b2 = torch.nn.Parameter((torch.randn(C, generator=g) * 0.1).to(DEV))
     return w1, b1, w2, b2
 
 
@@ -43,17 +44,19 @@ def _ref(x, w1, b1, w2, b2, low):
     return g @ w2.detach().to(low).float().t() + b2.detach()
 
 
-# M: ragged tails (tile 32), one wave's worth, several tiles per wave, production (8 x 256^2)
-@pytest.mark.parametrize("M", [1, 33, 1000, 8192 + 17, 524288])
-def test_mlp_infer_matches_fp32(M, low):
+# M: ragged tails (tile 32 / 256), one wave's worth, several tiles per wave, production (stage 0:
+# 8 x 256^2 tokens; stage 1, C = 192: 8 x 128^2)
+@pytest.mark.parametrize("M,C", [(1, 96), (33, 96), (1000, 96), (8192 + 17, 96), (524288, 96),
+                                 (1, 192), (33, 192), (1000, 192), (8192 + 17, 192), (131072, 192)])
+def test_mlp_infer_matches_fp32(M, C, low):
     ops = _ops()
-    w1, b1, w2, b2 = _params(M, low)
-    x = torch.randn(M, 96, generator=torch.Generator().manual_seed(M + 1)).to(DEV, low)
+    w1, b1, w2, b2 = _params(M, low, C)
+    x = torch.randn(M, C, generator=torch.Generator().manual_seed(M + 1)).to(DEV, low)
     n0 = ops.mlp_infer_calls
     with torch.no_grad(), torch.autocast("cuda", dtype=low):
         y = ops.mlp(x, w1, b1, w2, b2)
     assert ops.mlp_infer_calls == n0 + 1, "the no-grad MLP did not take the fused kernel"
-    assert y.dtype == low and y.shape == (M, 96)
+    assert y.dtype == low and y.shape == (M, C)
     ref = _ref(x, w1, b1, w2, b2, low)
     scale = ref.abs().max().item()
     err = (y.float() - ref).abs() - 1e-2 * ref.abs()
@@ -87,18 +90,21 @@ def test_mlp_infer_matches_training_path(low, monkeypatch):
         assert rel <= 2e-3, (name, rel)
 
 
-# M: ragged (one partial tile), several tiles + a ragged tail, production (8 x 256^2 tokens)
-@pytest.mark.parametrize("M", [33, 8209, 524288])
-def test_mlp_train_matches_fp32(M, low):
-    """VERDICT r5 item 4: the training form of the fused MLP (mlp_fused_kernel with H stored;
-    mlp.3's one-pass backward re-deriving GELU(H) from H) under autograd against fp32 PyTorch on
+# M: ragged (one partial tile), several tiles + a ragged tail, production (stage 0: 8 x 256^2
+# tokens, stage 1: 8 x 128^2)
+@pytest.mark.parametrize("M,C", [(33, 96), (8209, 96), (524288, 96), (33, 192), (8209, 192), (131072, 192)])
+def test_mlp_train_matches_fp32(M, C, low):
+    """the training form of the fused MLP (stage 0: mlp_fused_kernel with H
+    stored, mlp.3's one-pass backward re-deriving GELU(H) from H; stage 1: mlp_s1_kernel, mlp.3's
+    weight gradient on GELU(H) derived on the side stream) under autograd against fp32 PyTorch on
     the same 16-bit operands: y and the stored H with the token-GEMM tolerance, dx / dW1 / db1 /
     dW2 / db2 within 3e-2 of the largest entry (16-bit H, GELU(H) and dH in between), as
     tests/test_gpu_tok_gemm.py::test_fused_mlp_matches_fp32."""
     ops = _ops()
     if not ops._MLP_TRAIN:
         pytest.skip("MSU_MLP_TRAIN=0")
-    w1, b1, w2, b2 = _params(M + 3, low)
+    w1, b1, w2, b2 = _params(M + 3, low, C)
+    Hd = 4 * C
     # trainer-style parameters (flat .grad, 16-bit shadows, direct accumulation): the backward
     # takes the production route -- at M >= the one-pass threshold mlp.3's pass re-derives
     # GELU(H) from H (msu_linear_bwd with X = null), then mlp.0's pass
@@ -110,8 +116,8 @@ def test_mlp_train_matches_fp32(M, low):
             p_._msu_shadow_t = p_.detach().t().contiguous().to(low)
         p_._msu_shadow_ver = p_._version
     g = torch.Generator().manual_seed(M + 4)
-    x = torch.randn(M, 96, generator=g).to(DEV, low)
-    dy = torch.randn(M, 96, generator=g).to(DEV, low)
+    x = torch.randn(M, C, generator=g).to(DEV, low)
+    dy = torch.randn(M, C, generator=g).to(DEV, low)
     # fp32 reference on the 16-bit operands (inputs, weights, upstream gradient)
     xr = x.float().requires_grad_(True)
     pr = [t.detach().to(low).float().requires_grad_(True) if t.dim() == 2 else t.detach().clone().requires_grad_(True)
@@ -124,11 +130,11 @@ def test_mlp_train_matches_fp32(M, low):
     with torch.autocast("cuda", dtype=low):
         y, h, gg = torch.ops.msunet.mlp(xg, w1, b1, w2, b2, True)
     assert ops.mlp_train_calls == t0 + 1, "the training MLP did not take the fused kernel"
-    assert gg.numel() == 0 and h.shape == (M, 384) and h.dtype == low
+    assert gg.numel() == 0 and h.shape == (M, Hd) and h.dtype == low
     l0 = ops.linbwd_calls
     y.backward(dy)
     torch.cuda.synchronize()
-    if M >= ops._LINBWD_MIN_M:
+    if M >= ops._LINBWD_MIN_M and C == 96:
         assert ops.linbwd_calls == l0 + 2, "the backward did not take the one-pass route"
     for name, a, r in (("y", y, yr), ("H", h, hr)):
         r = r.detach()
@@ -142,18 +148,18 @@ def test_mlp_train_matches_fp32(M, low):
 
 
 def test_mlp_infer_other_widths_keep_token_gemm_pair():
-    """Stage-1 widths (192 -> 768) are not covered: the no-grad MLP keeps the GEMM pair."""
+    """Stage-2 widths (384 -> 1536) are not covered: the no-grad MLP keeps the GEMM pair."""
     ops = _ops()
     g = torch.Generator().manual_seed(5)
-    w1 = torch.nn.Parameter((torch.randn(768, 192, generator=g) / 192 ** 0.5).to(DEV))
-    b1 = torch.nn.Parameter((torch.randn(768, generator=g) * 0.1).to(DEV))
-    w2 = torch.nn.Parameter((torch.randn(192, 768, generator=g) / 768 ** 0.5).to(DEV))
-    b2 = torch.nn.Parameter((torch.randn(192, generator=g) * 0.1).to(DEV))
-    x = torch.randn(4096, 192, generator=g).to(DEV, torch.bfloat16)
+    w1 = torch.nn.Parameter((torch.randn(1536, 384, generator=g) / 384 ** 0.5).to(DEV))
+    b1 = torch.nn.Parameter((torch.randn(1536, generator=g) * 0.1).to(DEV))
+    w2 = torch.nn.Parameter((torch.randn(384, 1536, generator=g) / 1536 ** 0.5).to(DEV))
+    b2 = torch.nn.Parameter((torch.randn(384, generator=g) * 0.1).to(DEV))
+    x = torch.randn(4096, 384, generator=g).to(DEV, torch.bfloat16)
     with torch.autocast("cuda", dtype=torch.bfloat16):
         fusable = ops.mlp_fusable(x, w1, w2)
     if not fusable:
-        pytest.skip("stage-1 MLP not on the fused GEMM pair")
+        pytest.skip("stage-2 MLP not on the fused GEMM pair")
     n0 = ops.mlp_infer_calls
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
         y = ops.mlp(x, w1, b1, w2, b2)

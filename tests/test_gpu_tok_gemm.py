@@ -138,7 +138,7 @@ def test_fused_mlp_matches_fp32(M, C, low):
 @pytest.mark.parametrize("M,C", [(4096, 96), (1000, 96), (2048, 192), (1000, 384)])
 def test_mlp_no_grad_keeps_nothing_and_equals_grad_path(M, C, route, monkeypatch, low):
     """Under no_grad (the reference's discarded branches) ops.mlp keeps neither H nor G.  At
-    C = 96 it runs the fused inference MLP (csrc/mlp_fused.hip: same roundings of H and GELU(H),
+    C = 96 / 192 it runs the fused inference MLP (csrc/mlp_fused.hip, mlp_s1.hip: same roundings of H and GELU(H),
     biases added in f32 rather than as a hi / lo k-block): within rel. L2 2e-3 of the grad path.
     Elsewhere the GELU store overwrites the pre-activation in one buffer and the output is
     bitwise the grad path's (same kernels, same rounding of H before GELU)."""
@@ -160,7 +160,7 @@ def test_mlp_no_grad_keeps_nothing_and_equals_grad_path(M, C, route, monkeypatch
         y1, h1, g1 = torch.ops.msunet.mlp(x, w1, b1, w2, b2, True)
     torch.cuda.synchronize()
     assert h.numel() == 0 and gg.numel() == 0 and h1.shape == (M, 4 * C)
-    if C == 96 and ops._MLP_INFER:
+    if (C, 4 * C) in ops.MLP_FUSED_SHAPES and ops._MLP_INFER:
         assert ops.mlp_infer_calls == n0 + 2
         rel = ((y0.float() - y1.float()).norm() / y1.float().norm()).item()
         assert rel <= 2e-3, rel

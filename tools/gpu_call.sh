@@ -33,6 +33,12 @@ for s in "$@"; do
         MSU_LIB_OVERRIDE=$L timeout -k 10 200 python -u $R/tools/nt_shapes.py 20 ${L:+B} >> $O/${TAG}_nt_shapes.log 2>&1 || exit 3
       done
       python3 $R/tools/ab_table.py $O/${TAG}_nt_shapes.log ;;
+    nt_force)
+      # NT GEMM kernel times per shape under each forced tile form (tools/nt_shapes.py NT_FORCE)
+      for F in 0 1 2 3 0 1; do
+        NT_FORCE=$F timeout -k 10 200 python -u $R/tools/nt_shapes.py 20 >> $O/${TAG}_nt_force.log 2>&1 || exit 3
+      done
+      for F in F1 F2 F3; do python3 $R/tools/ab_table.py $O/${TAG}_nt_force.log cur $F; done ;;
     nt_exp)
       for X in 4 8; do
         echo "== MSU_EXP=$X (1: no DMA, 2: no fragment reads, 4: no MFMA, 8: no epilogue)" >> $O/${TAG}_nt_exp.log
@@ -76,6 +82,8 @@ for s in "$@"; do
       cat $O/${TAG}_kern.log ;;
     gelu_tests) step gelu_tests 900 $PYT -m gpu $R/tests/test_gpu_tok_gemm.py $R/tests/test_gpu_nt_gemm.py \
                   $R/tests/test_gpu_linbwd.py $R/tests/test_gpu_ln_side.py $R/tests/test_gpu_ops.py ;;
+    mlp_s1) step mlp_s1 200 python -u $R/tools/mlp_s1_one.py 20 ;;
+    ab_mlp_s1) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlps1 "" "MSU_MLP_S1=0" "" "MSU_MLP_S1=0" "" "MSU_MLP_S1=0" || exit 3 ;;
     mlp_tests) step mlp_tests 600 $PYT -m gpu $R/tests/test_gpu_mlp_infer.py $R/tests/test_gpu_tok_gemm.py ;;
     attn_tests) step attn_tests 900 $PYT -m gpu $R/tests/test_gpu_attn_qkv.py $R/tests/test_gpu_production_parity.py \
                   $R/tests/test_gpu_ops.py -k "attn or attention or window" ;;

@@ -19,6 +19,12 @@ SHAPES = [(131072, 576, 192, 0, 0), (131072, 192, 192, 0, 0), (131072, 768, 192,
           (32768, 384, 1152, 0, 1), (131072, 192, 576, 0, 1)]
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 tag = sys.argv[2] if len(sys.argv) > 2 else os.path.basename(os.environ.get("MSU_LIB_OVERRIDE", "") or "cur")
+# NT_FORCE=1/2/3: a forced tile form (msu_nt_gemm_mode bits 1-2) for this run
+force = int(os.environ.get("NT_FORCE", "0"))
+if force:
+    from semantic_segmentation_of_stylegan2_artifacts_amd import _lib  # noqa: E402
+    _lib.lib().msu_nt_gemm_mode(force << 1)
+    tag = f"F{force}"
 tot = 0.0
 for M, N, K, epi, kn in SHAPES:
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
