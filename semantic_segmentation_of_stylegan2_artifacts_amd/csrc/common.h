@@ -156,6 +156,30 @@ MSU_DEV float gelu_grad_fast(float x) {
   return fmaf(x * 0.39894228040143268f, e, cdf);
 }
 
+// The same on a register pair: every multiply / fma / add of erf_fast as one v_pk_*_f32 (the same
+// IEEE operations in the same order: bitwise equal to two scalar calls); the v_rcp / v_exp and the
+// sign copies stay per element.  For the VALU-bound fused MLPs (the epilogues of the GEMMs and
+// convs are store-bound: packed there measured neutral, r05ai).
+MSU_DEV f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+MSU_DEV f32x2 splat2(float v) { return f32x2{v, v}; }
+MSU_DEV f32x2 erf_fast2(f32x2 x, f32x2& e_neg_x2) {
+  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
+  const f32x2 d = pk_fma(splat2(0.3275911f), ax, splat2(1.0f));
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = pk_fma(splat2(1.061405429f), t, splat2(-1.453152027f));
+  p = pk_fma(p, t, splat2(1.421413741f));
+  p = pk_fma(p, t, splat2(-0.284496736f));
+  p = pk_fma(p, t, splat2(0.254829592f)) * t;
+  const f32x2 q = -ax * ax;
+  e_neg_x2 = f32x2{__expf(q.x), __expf(q.y)};
+  const f32x2 r = pk_fma(-p, e_neg_x2, splat2(1.0f));
+  return f32x2{copysignf(r.x, x.x), copysignf(r.y, x.y)};
+}
+MSU_DEV f32x2 gelu_fast2(f32x2 x) {
+  f32x2 e;
+  return splat2(0.5f) * x * (splat2(1.0f) + erf_fast2(x * splat2(0.70710678118654752f), e));
+}
+
 // ------------------------------------------------------------------ counter-based RNG
 // Philox-free 32-bit hash (splitmix-style) of (seed, index): uniform in [0, 1).
 MSU_DEV float hash_uniform(uint64_t seed, uint64_t idx) {

@@ -30,19 +30,33 @@
 
 namespace {
 
-constexpr int SC = 192, SH = 768, SCH = 32, NCH = SH / SCH, SW = 8, STT = 32 * SW, SNS = 6;
-constexpr int W1S = SCH * SC;          // elements of a slot's W1 image
-constexpr int W2S = SC * SCH;          // elements of a slot's W2 image
-constexpr int SLOT = W1S + W2S;        // 24 KB
-constexpr int DMA_PER_CHUNK = SLOT * 2 / 1024;  // 1-KB DMA instructions per chunk (24)
-constexpr int DMA_PER_WAVE = DMA_PER_CHUNK / SW;         // 3
-static_assert(DMA_PER_WAVE * SW == DMA_PER_CHUNK, "whole DMA instructions per wave");
+// MSU_EXP: ablation / variant bits for timing experiments only (tools/build_exp.sh); 0 in every
+// real build.  2: fragment reads one MFMA ahead instead of three; 4: waves 4-7 staggered by half a
+// chunk (measured slower: 169 vs 160 us, r06h); 8: no GELU (identity); 16: no H stores; 32: no fc2
+// MFMAs; 64: no fc1 MFMAs (results wrong by design for 8 / 16 / 32 / 64)
+#ifndef MSU_EXP
+#define MSU_EXP 0
+#endif
+
+constexpr int SC = 192, SH = 768, SW = 8, STT = 32 * SW;
+constexpr int UH = 32;                      // hidden units per chunk (one barrier per chunk)
+constexpr int NU = SH / UH;                 // chunks per token tile (24)
+constexpr int SNS = 6;                      // ring slots (147 KB)
+constexpr int FD = (MSU_EXP & 2) ? 1 : 3;   // fragment reads in flight ahead of the MFMA using one
+constexpr bool STAG = (MSU_EXP & 4) != 0;   // waves 4-7 run half a chunk behind waves 0-3
+constexpr int W1S = UH * SC;                // elements of a slot's W1 image [32][192]
+constexpr int W2S = SC * UH;                // elements of a slot's W2 image [192][32]
+constexpr int SLOT = W1S + W2S;
+constexpr int DMA_PER_UNIT = SLOT * 2 / 1024;  // 1-KB DMA instructions per chunk (24)
+constexpr int DMA_PER_WAVE = DMA_PER_UNIT / SW;
+static_assert(DMA_PER_WAVE * SW == DMA_PER_UNIT, "whole DMA instructions per wave");
 
 struct S1Lds {
   bf16_t ring[SNS * SLOT];
   float b1[SH];
   float b2[SC];
 };
+static_assert(sizeof(S1Lds) <= 160 * 1024, "LDS");
 
 struct S1Args {
   const bf16_t* x;
@@ -55,8 +69,10 @@ struct S1Args {
   long M;
 };
 
-// hidden unit (within the chunk) held by slot row rho: bits 2 and 3 swapped
+// hidden unit (within a chunk) held by slot row rho: bits 2 and 3 swapped
 MSU_DEV constexpr int s1_pi(int rho) { return (rho & ~12) | ((rho & 4) << 1) | ((rho & 8) >> 1); }
+// 16-B chunk swizzle of a W2 slot row (4 chunks per row)
+MSU_DEV constexpr int w2_swz(int row) { return (row >> 2) & 3; }
 
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (capped: waiting for more is always safe)
 MSU_DEV void wait_vmcnt_le(int n) {
@@ -78,53 +94,51 @@ MSU_DEV bf16x8 ds_b128_untracked(uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
   return v;
 }
-// 8 consecutive f32 (bias values) from LDS, untracked, after lgkmcnt(0)
-MSU_DEV void ds_f32x8_untracked(uint32_t addr, float (&v)[8]) {
-  u32x4 a, b;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(a) : "v"(addr));
-  asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(b) : "v"(addr));
-  lds_wait_tie<0>(a, b);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[i] = __uint_as_float(a[i]);
-    v[4 + i] = __uint_as_float(b[i]);
-  }
-}
 
+// Per chunk a wave runs three phases: fc1 (12 MFMAs), the epilogue (b1, H, GELU: VALU), fc2 (12
+// MFMAs).  With one barrier per chunk the two waves of a SIMD (w, w + 4) would run them in phase --
+// both on MFMAs, then both on VALU.  So waves 4-7 are STAGGERED: in the interval after chunk j's
+// barrier waves 0-3 run fc1(j), epi(j), fc2(j) while waves 4-7 run epi(j - 1), fc2(j - 1), fc1(j)
+// (their fc1 accumulator crosses the barrier): each SIMD pairs one wave's MFMAs with the other's
+// VALU.  Chunk j - 1's slot is then read up to the end of interval j, so the ring prefetches
+// SNS - 2 chunks ahead and interval j refills chunk j - 2's slot; one extra interval at the end
+// lets waves 4-7 finish the last chunk.
 template <typename T, bool H_OUT>
 __global__ void __launch_bounds__(64 * SW) mlp_s1_kernel(S1Args A) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   S1Lds& L = *reinterpret_cast<S1Lds*>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, tl = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool late = STAG && wave >= 4;  // wave-uniform
   const long M = A.M;
   const long ntiles = (M + STT - 1) / STT;
   const int G = gridDim.x;
   const long first = blockIdx.x;
   if (first >= ntiles) return;
   const long mine = (ntiles - 1 - first) / G + 1;
-  const long nchunks = mine * NCH;
+  const long nunits = mine * NU;
 
   for (int s = tid; s < SH; s += 64 * SW) L.b1[s] = A.b1[s];
   for (int s = tid; s < SC; s += 64 * SW) L.b2[s] = A.b2[s];
   __syncthreads();  // before any LDS-DMA is in flight (this barrier drains nothing)
 
-  // chunk q (0 .. 23) of the weights into ring slot `slot`: this wave's 3 of the 24 1-KB DMA
-  // instructions (W1 rows permuted by pi and chunk-swizzled; W2 columns chunk-swizzled)
-  auto dma_chunk = [&](int q, int slot) __attribute__((always_inline)) {
+  // chunk q (0 .. 23) of the weights into ring slot `slot`: this wave's 3 of the chunk's 24 1-KB
+  // DMA instructions (W1 rows permuted by pi and chunk-swizzled; W2 columns chunk-swizzled)
+  auto dma_unit = [&](int q, int slot) __attribute__((always_inline)) {
     bf16_t* base = L.ring + slot * SLOT;
     const int ln = opaque(lane);
 #pragma unroll
     for (int r = 0; r < DMA_PER_WAVE; ++r) {
-      const int i = wave + SW * r;  // instruction 0 .. 23 (wave-uniform)
+      const int i = wave + SW * r;  // instruction (wave-uniform)
       if (i < 12) {
         const int p = 64 * i + ln, rho = p / 24, pos = p - (p / 24) * 24;
         const int gc = pos ^ ((rho >> 1) & 7);
-        glds16(A.w1 + (long)(SCH * q + s1_pi(rho)) * SC + 8 * gc, base + 512 * i);
+        glds16(A.w1 + (long)(UH * q + s1_pi(rho)) * SC + 8 * gc, base + 512 * i);
       } else {
-        const int p = 64 * (i - 12) + ln, row = p >> 2, pos = p & 3;
-        const int gc = pos ^ ((row >> 2) & 3);
-        glds16(A.w2 + (long)row * SH + SCH * q + 8 * gc, base + W1S + 512 * (i - 12));
+        const int i2 = i - 12;
+        const int p = 64 * i2 + ln, row = p >> 2, pos = p & 3;
+        const int gc = pos ^ w2_swz(row);
+        glds16(A.w2 + (long)row * SH + UH * q + 8 * gc, base + W1S + 512 * i2);
       }
     }
   };
@@ -142,19 +156,18 @@ __global__ void __launch_bounds__(64 * SW) mlp_s1_kernel(S1Args A) {
   };
 
   // vector-memory ops this wave issued (wave-uniform), and the count right after each pending
-  // chunk's DMA (a queue of SNS - 1: the chunk waited for next first): the vmcnt waits let every
+  // chunk's DMA (a queue of SNS - 2: the chunk waited for next first): the vmcnt waits let every
   // younger op stay in flight.  Stores are counted only when the whole wave issues them (full
   // tile rows): an uncounted op only makes a wait stricter.
   int issued = 0;
-  int mark[SNS - 1];
-  long tile = first;
-  load_x(tile);
+  int mark[SNS - 2];
+  load_x(first);
   issued += 12;
   int mark_x = issued;
 #pragma unroll
-  for (int s = 0; s < SNS - 1; ++s) {
-    if (s < nchunks) {
-      dma_chunk(s % NCH, s);
+  for (int s = 0; s < SNS - 2; ++s) {
+    if (s < nunits) {
+      dma_unit(s % NU, s);
       issued += DMA_PER_WAVE;
     }
     mark[s] = issued;
@@ -163,108 +176,97 @@ __global__ void __launch_bounds__(64 * SW) mlp_s1_kernel(S1Args A) {
   f32x16 yacc[6];
 #pragma unroll
   for (int ct = 0; ct < 6; ++ct) yacc[ct] = f32x16{0};
-  // untracked-read lane addresses (bytes) within a slot
+  f32x16 h = f32x16{0};  // fc1 accumulator (waves 4-7: carried to the next interval)
+  // untracked-read lane addresses (bytes)
   const uint32_t ring0 = lds_u32(L.ring);
   const uint32_t a1_lane = (uint32_t)(tl * SC * 2);              // + slot, + 16 * pos(ks)
   const int w1sw = (tl >> 1) & 7;
-  const uint32_t a2_lane = (uint32_t)(W1S * 2 + tl * SCH * 2);   // + slot, + 2048 ct, + 16 * pos(s)
-  const int w2sw = (tl >> 2) & 3;
-  // bias reads (untracked: a visible ds_read would wait for the ring) -- lane offsets
+  const uint32_t a2_lane = (uint32_t)(W1S * 2 + tl * UH * 2);    // + slot, + 2048 ct, + 16 * pos
+  const int w2sw = w2_swz(tl);                                   // (32 ct + tl: same swizzle)
   const uint32_t b1_lane = lds_u32(L.b1) + 4u * (uint32_t)(8 * hh);
   const uint32_t b2_lane = lds_u32(L.b2) + 4u * (uint32_t)(4 * hh);
 
-  // chunk j: weights chunk q = j % 24 in slot j % SNS; the DMA issued at chunk j is chunk
-  // j + SNS - 1 (weights qn, slot sn)
-  int q = 0, slot = 0, qn = (SNS - 1) % NCH, sn = SNS - 1;
-  for (long j = 0; j < nchunks; ++j) {
-    // chunk j's DMA (every wave's share, after the barrier) has landed; every wave is done with
-    // chunk j - 1's slot, which is refilled next
-    {
-      // steady state (full tiles, no tile boundary among the younger ops): a constant count
-      constexpr int STEADY = (SNS - 2) * DMA_PER_WAVE + (H_OUT ? 2 * (SNS - 1) : 0);
-      const int younger = issued - mark[0];
-      if (younger >= STEADY) wait_vmcnt<STEADY>();
-      else wait_vmcnt_le(younger);
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int s = 0; s < SNS - 2; ++s) mark[s] = mark[s + 1];
-    if (j + SNS - 1 < nchunks) {
-      dma_chunk(qn, sn);
-      issued += DMA_PER_WAVE;
-    }
-    mark[SNS - 2] = issued;
-    qn = qn + 1 == NCH ? 0 : qn + 1;
-    sn = sn + 1 == SNS ? 0 : sn + 1;
-    if (q == 0) wait_vmcnt_le(issued - mark_x);  // the tile's x rows
-    const long row0 = tile * STT + 32 * wave;
-    const bool full = row0 + 32 <= M;
-    // ---- fc1: C1^T[rho][t] for the chunk's 32 hidden units (slot rows rho)
+  // ---- the three phases of a chunk
+  auto fc1 = [&](int slot) __attribute__((always_inline)) {
     const uint32_t a1 = ring0 + (uint32_t)(slot * SLOT * 2) + a1_lane;
-    f32x16 h = f32x16{0};
-    bf16x8 wf[2];
-    // fragment reads two k steps apart in flight: (2 ks + hh) ^ w1sw is the slot chunk
+    h = f32x16{0};
+    bf16x8 wf[FD + 1];
     auto addr1 = [&](int ks) { return a1 + 16u * (uint32_t)((2 * ks + hh) ^ w1sw); };
-    wf[0] = ds_b128_untracked<0>(addr1(0));
+    unroll_for<FD>([&](auto KS) { wf[decltype(KS)::value] = ds_b128_untracked<0>(addr1(decltype(KS)::value)); });
     unroll_for<12>([&](auto KS) {
       constexpr int ks = decltype(KS)::value;
-      if constexpr (ks + 1 < 12) {
-        wf[(ks + 1) & 1] = ds_b128_untracked<0>(addr1(ks + 1));
-        lds_wait_tie<1>(wf[ks & 1]);
-      } else {
-        lds_wait_tie<0>(wf[ks & 1]);
-      }
-      h = Fmt16<T>::mma32(wf[ks & 1], __builtin_bit_cast(bf16x8, xc[ks]), h);
+      if constexpr (ks + FD < 12) wf[(ks + FD) % (FD + 1)] = ds_b128_untracked<0>(addr1(ks + FD));
+      lds_wait_tie<(ks + FD < 12 ? FD : 11 - ks)>(wf[ks % (FD + 1)]);
+      if constexpr (MSU_EXP & 64) {
+        const bf16x8 wv = wf[ks % (FD + 1)];
+        const u32x4 xv = xc[ks];
+        asm volatile("" ::"v"(wv), "v"(xv));
+      } else h = Fmt16<T>::mma32(wf[ks % (FD + 1)], __builtin_bit_cast(bf16x8, xc[ks]), h);
     });
-    if (q == NCH - 1 && tile + G < ntiles) {
-      // the next tile's x rows: xc is free once the last chunk's fc1 has issued
-      load_x(tile + G);
-      issued += 12;
-      mark_x = issued;
-    }
-    // ---- + b1, 16-bit H (stored), GELU, 16-bit GELU(H): registers 8s + e <-> hidden
-    // 32 q + 16 s + 8 hh + e
-    u32x4 g[2];
-    const long hrow = row0 + tl;
+  };
+  // + b1, 16-bit H (stored), GELU, 16-bit GELU(H): registers 8s + e <-> hidden 32 q + 16 s + 8 hh + e
+  auto epi = [&](int q, long t, u32x4 (&g)[2]) __attribute__((always_inline)) {
+    u32x4 bq[4];
+    unroll_for<4>([&](auto BI) {
+      constexpr int bi = decltype(BI)::value;
+      bq[bi] = __builtin_bit_cast(u32x4, ds_b128_untracked<(bi >> 1) * 64 + (bi & 1) * 16>(
+                                             b1_lane + 4u * (uint32_t)(UH * q)));
+    });
+    lds_wait_tie<0>(bq[0], bq[1], bq[2], bq[3]);
+    const long hrow = t * STT + 32 * wave + tl;
     const bool hok = hrow < M;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      float bv[8];
-      ds_f32x8_untracked(b1_lane + 4u * (uint32_t)(SCH * q + 16 * s), bv);
-      float u[8];
+      float uu[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) u[e] = round16<T>(h[8 * s + e] + bv[e]);
-      if constexpr (H_OUT) {
-        const u32x4 hv = {pack2<T>(u[0], u[1]), pack2<T>(u[2], u[3]), pack2<T>(u[4], u[5]), pack2<T>(u[6], u[7])};
-        if (hok) *reinterpret_cast<u32x4*>(A.hout + hrow * SH + SCH * q + 16 * s + 8 * hh) = hv;
+      for (int e = 0; e < 4; ++e) {
+        uu[e] = round16<T>(h[8 * s + e] + __uint_as_float(bq[2 * s][e]));
+        uu[4 + e] = round16<T>(h[8 * s + 4 + e] + __uint_as_float(bq[2 * s + 1][e]));
       }
-      g[s] = u32x4{pack2<T>(gelu_fast(u[0]), gelu_fast(u[1])), pack2<T>(gelu_fast(u[2]), gelu_fast(u[3])),
-                   pack2<T>(gelu_fast(u[4]), gelu_fast(u[5])), pack2<T>(gelu_fast(u[6]), gelu_fast(u[7]))};
+      if constexpr (H_OUT) {
+        const u32x4 hv = {pack2<T>(uu[0], uu[1]), pack2<T>(uu[2], uu[3]), pack2<T>(uu[4], uu[5]),
+                          pack2<T>(uu[6], uu[7])};
+        if constexpr (MSU_EXP & 16) {
+          const u32x4 hv2 = hv;
+          asm volatile("" ::"v"(hv2));
+        }
+        else if (hok) *reinterpret_cast<u32x4*>(A.hout + hrow * SH + UH * q + 16 * s + 8 * hh) = hv;
+      }
+      uint32_t gp[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const f32x2 gv = (MSU_EXP & 8) ? f32x2{uu[2 * e], uu[2 * e + 1]}
+                                       : gelu_fast2(f32x2{uu[2 * e], uu[2 * e + 1]});  // bitwise two gelu_fast
+        gp[e] = pack2<T>(gv.x, gv.y);
+      }
+      g[s] = u32x4{gp[0], gp[1], gp[2], gp[3]};
     }
-    if (H_OUT && full) issued += 2;
-    // ---- fc2: y^T[c][t] += W2[c][chunk] . GELU(H)^T, six 32-channel tiles, two 16-deep k steps
+    if (H_OUT && !(MSU_EXP & 16) && t * STT + 32 * wave + 32 <= M) issued += 2;
+  };
+  // y^T[c][t] += W2[c][chunk] . GELU(H)^T: six 32-channel tiles, two 16-deep k steps
+  auto fc2 = [&](int slot, const u32x4 (&g)[2]) __attribute__((always_inline)) {
     const uint32_t a2 = ring0 + (uint32_t)(slot * SLOT * 2) + a2_lane;
-    auto addr2 = [&](int ct, int s) { return a2 + 2048u * (uint32_t)ct + 16u * (uint32_t)((2 * s + hh) ^ w2sw); };
-    bf16x8 af[2];
-    af[0] = ds_b128_untracked<0>(addr2(0, 0));
+    auto addr2 = [&](int ct, int s) { return a2 + (uint32_t)(ct * 32 * UH * 2) + 16u * (uint32_t)((2 * s + hh) ^ w2sw); };
+    bf16x8 af[FD + 1];
+    unroll_for<FD>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      af[i] = ds_b128_untracked<0>(addr2(i % 6, i / 6));
+    });
     unroll_for<12>([&](auto I) {
       constexpr int i = decltype(I)::value, s = i / 6, ct = i % 6;
-      if constexpr (i + 1 < 12) {
-        af[(i + 1) & 1] = ds_b128_untracked<0>(addr2((i + 1) % 6, (i + 1) / 6));
-        lds_wait_tie<1>(af[i & 1]);
-      } else {
-        lds_wait_tie<0>(af[i & 1]);
-      }
-      yacc[ct] = Fmt16<T>::mma32(af[i & 1], __builtin_bit_cast(bf16x8, g[s]), yacc[ct]);
+      if constexpr (i + FD < 12) af[(i + FD) % (FD + 1)] = ds_b128_untracked<0>(addr2((i + FD) % 6, (i + FD) / 6));
+      lds_wait_tie<(i + FD < 12 ? FD : 11 - i)>(af[i % (FD + 1)]);
+      if constexpr (MSU_EXP & 32) {
+        const bf16x8 av = af[i % (FD + 1)];
+        const u32x4 gv = g[s];
+        asm volatile("" ::"v"(av), "v"(gv));
+      } else yacc[ct] = Fmt16<T>::mma32(af[i % (FD + 1)], __builtin_bit_cast(bf16x8, g[s]), yacc[ct]);
     });
-    const bool tile_end = q == NCH - 1;
-    q = tile_end ? 0 : q + 1;
-    slot = slot + 1 == SNS ? 0 : slot + 1;
-    if (!tile_end) continue;
-    // ---- tile epilogue: y = y^T + b2; lane (token tl) holds channels 32 ct + 8 r4 + 4 hh + i in
-    // register 4 r4 + i; a permlane32 swap pairs the halves into 8 consecutive channels per lane
-    const long row = row0 + tl;
+  };
+  // tile epilogue: y = y^T + b2; lane (token tl) holds channels 32 ct + 8 r4 + 4 hh + i in
+  // register 4 r4 + i; a permlane32 swap pairs the halves into 8 consecutive channels per lane
+  auto y_out = [&](long t) __attribute__((always_inline)) {
+    const long row = t * STT + 32 * wave + tl;
     const bool ok = row < M;
     bf16_t* yr = A.y + (ok ? row : 0) * SC;
 #pragma unroll
@@ -288,8 +290,68 @@ __global__ void __launch_bounds__(64 * SW) mlp_s1_kernel(S1Args A) {
       }
       yacc[ct] = f32x16{0};
     }
-    if (full) issued += 12;
-    tile += G;
+    if (t * STT + 32 * wave + 32 <= M) issued += 12;
+  };
+  // fc1 of chunk (q, slot) of tile t, after which the last chunk of a tile loads the next tile's x
+  auto fc1_step = [&](int q, int slot, long t) __attribute__((always_inline)) {
+    if (q == 0) wait_vmcnt_le(issued - mark_x);  // the tile's x rows
+    fc1(slot);
+    if (q == NU - 1 && t + G < ntiles) {  // xc is free once the tile's last fc1 has issued
+      load_x(t + G);
+      issued += 12;
+      mark_x = issued;
+    }
+  };
+
+  // interval j (0 .. nunits): chunk j = weights chunk q in ring slot `slot` of tile `tile`;
+  // (qp, slotp, tilep) the previous chunk; the DMA issued in interval j is chunk j + SNS - 2
+  int q = 0, slot = 0, qn = (SNS - 2) % NU, sn = SNS - 2, qp = 0, slotp = 0;
+  long tile = first, tilep = first;
+  for (long j = 0; j <= nunits; ++j) {
+    const bool cur = j < nunits;
+    if (cur) {
+      // steady state (full tiles, no tile boundary among the younger ops): a constant count
+      constexpr int STEADY = (SNS - 3) * DMA_PER_WAVE + (H_OUT && !(MSU_EXP & 16) ? 2 * (SNS - 2) : 0);
+      const int younger = issued - mark[0];
+      if (younger >= STEADY) wait_vmcnt<STEADY>();
+      else wait_vmcnt_le(younger);
+    }
+    // chunk j's DMA (every wave's share) has landed; every wave is done with chunk j - 2's slot
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int s = 0; s < SNS - 3; ++s) mark[s] = mark[s + 1];
+    if (j + SNS - 2 < nunits) {
+      dma_unit(qn, sn);
+      issued += DMA_PER_WAVE;
+    }
+    mark[SNS - 3] = issued;
+    qn = qn + 1 == NU ? 0 : qn + 1;
+    sn = sn + 1 == SNS ? 0 : sn + 1;
+    // one straight sequence for both wave groups (two branch-separated copies of the phases
+    // made the register allocator keep both copies' operands: 300+ VGPRs of spills)
+    const bool second = late ? j > 0 : cur;  // the epi + fc2 of this interval exists
+    const int qe = late ? qp : q, se = late ? slotp : slot;
+    const long te = late ? tilep : tile;
+    if (late && second) {
+      u32x4 g[2];
+      epi(qe, te, g);
+      fc2(se, g);
+      if (qe == NU - 1) y_out(te);
+    }
+    if (cur) fc1_step(q, slot, tile);
+    if (!late && second) {
+      u32x4 g[2];
+      epi(qe, te, g);
+      fc2(se, g);
+      if (qe == NU - 1) y_out(te);
+    }
+    qp = q;
+    slotp = slot;
+    tilep = tile;
+    if (q == NU - 1) tile += G;
+    q = q + 1 == NU ? 0 : q + 1;
+    slot = slot + 1 == SNS ? 0 : slot + 1;
   }
   wait_vmcnt<0>();  // no LDS-DMA outstanding when the workgroup retires
 }

@@ -196,6 +196,7 @@ def _end_of_backward():
     global _join_queued
     _join_queued = False
     _res_handoff.clear()
+    _flush_deferred()  # anything still held back runs now, before the join
     join_side_streams()
     _side_keep.clear()  # the main stream now waits for every side-stream read
     for p in _side_event_params:
@@ -274,6 +275,7 @@ def _ln_setup(ctx, inputs, output):
 def _ln_backward(ctx, dy, _dm, _dr):
     global res_handoff_calls
     x, w, mean, rstd = ctx.saved_tensors
+    _flush_deferred(x.shape[-1])
     res = _res_handoff.pop(ctx.handoff, None) if ctx.handoff else None  # the paired add-LN's dx
     if dy is None:
         return res, None, None, None, None
@@ -344,6 +346,7 @@ def _add_ln_setup(ctx, inputs, output):
 def _add_ln_backward(ctx, ds, dy, _dm, _dr):
     s, w, mean, rstd, scale = ctx.saved_tensors
     C = s.shape[-1]
+    _flush_deferred(C)
     rows = s.numel() // C
     if dy is None:
         dy = torch.zeros_like(s)
@@ -1553,6 +1556,22 @@ def _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout):
 # A/B switch MSU_CONV_SIDE=0: the refine convs' weight gradients on the main stream.  (Holding
 # them back to the next side-stream fork measured equal, r04z: gone.)
 _CONV_SIDE = switches.on("MSU_CONV_SIDE")
+# MSU_CONV_WGRAD_AT=C (> 0): the refine convs' side-stream weight gradients are held back until the
+# first LayerNorm backward of width >= C (the stage-2 blocks at C = 384: the latency-bound part of
+# backward, whose kernels leave CUs free), instead of running beside the refine dgrads they cannot
+# share a CU with (both fill a CU's LDS / registers)
+_CONV_WGRAD_AT = int(switches.get("MSU_CONV_WGRAD_AT"))
+_deferred_side = []  # side-stream launches held back to that point of backward
+
+
+def _flush_deferred(C=None):
+    """Issue the held-back side-stream launches (at a LayerNorm backward of width C >= the
+    threshold, or unconditionally at the end of backward: C None)."""
+    if _deferred_side and (C is None or C >= _CONV_WGRAD_AT):
+        todo = list(_deferred_side)
+        _deferred_side.clear()
+        for fn in todo:
+            fn()
 
 
 def _conv_wgrad_param(a, dz, mode, B, H, W, Cin, Cout, weight, bias):
@@ -1579,7 +1598,10 @@ def _conv_wgrad_param(a, dz, mode, B, H, W, Cin, Cout, weight, bias):
         _guard_side_write(bias, ev)
         _notify(weight, bias)
 
-    launch()
+    if _CONV_WGRAD_AT > 0:
+        _deferred_side.append(launch)
+    else:
+        launch()
     _join_at_end_of_backward()
     return None, None
 

@@ -83,6 +83,14 @@ for s in "$@"; do
     gelu_tests) step gelu_tests 900 $PYT -m gpu $R/tests/test_gpu_tok_gemm.py $R/tests/test_gpu_nt_gemm.py \
                   $R/tests/test_gpu_linbwd.py $R/tests/test_gpu_ln_side.py $R/tests/test_gpu_ops.py ;;
     mlp_s1) step mlp_s1 200 python -u $R/tools/mlp_s1_one.py 20 ;;
+    mlp_s1_ab)
+      # stage-1 fused MLP: this build vs AB_LIB (kernel times twice each, then AB_LIB's MLP tests)
+      for L in "" "$AB_LIB" "" "$AB_LIB"; do
+        echo "== ${L:-cur}" >> $O/${TAG}_mlp_s1_ab.log
+        MSU_LIB_OVERRIDE=$L timeout -k 10 200 python -u $R/tools/mlp_s1_one.py 20 >> $O/${TAG}_mlp_s1_ab.log 2>&1 || exit 3
+      done
+      cat $O/${TAG}_mlp_s1_ab.log
+      MSU_LIB_OVERRIDE=$AB_LIB step mlp_tests_B 600 $PYT -m gpu $R/tests/test_gpu_mlp_infer.py ;;
     ab_mlp_s1) bash $R/tools/gpu_bench_ab.sh ${TAG}_mlps1 "" "MSU_MLP_S1=0" "" "MSU_MLP_S1=0" "" "MSU_MLP_S1=0" || exit 3 ;;
     mlp_tests) step mlp_tests 600 $PYT -m gpu $R/tests/test_gpu_mlp_infer.py $R/tests/test_gpu_tok_gemm.py ;;
     attn_tests) step attn_tests 900 $PYT -m gpu $R/tests/test_gpu_attn_qkv.py $R/tests/test_gpu_production_parity.py \
@@ -135,6 +143,14 @@ for s in "$@"; do
       done
       cat $O/${TAG}_conv_env.log ;;
     ab_env) bash $R/tools/gpu_bench_ab.sh ${TAG}_env "" "$AB_ENV" "" "$AB_ENV" "" "$AB_ENV" || exit 3 ;;
+    ab_env2) bash $R/tools/gpu_bench_ab.sh ${TAG}_env2 "" "$AB_ENV" "$AB_ENV2" "" "$AB_ENV" "$AB_ENV2" || exit 3 ;;
+    mlp_s1_var)
+      # stage-1 fused MLP variants (tools/build_exp.sh mlp_s1 1 2): kernel times, twice each
+      for r in 1 2; do for L in "" $R/tools/exp/libmsunet_mlp_s1_1.so $R/tools/exp/libmsunet_mlp_s1_2.so; do
+        echo "== ${L:-cur}" >> $O/${TAG}_mlp_s1_var.log
+        MSU_LIB_OVERRIDE=$L timeout -k 10 200 python -u $R/tools/mlp_s1_one.py 20 2>&1 | grep fused >> $O/${TAG}_mlp_s1_var.log || exit 3
+      done; done
+      cat $O/${TAG}_mlp_s1_var.log ;;
     ln_exp)
       for X in ${LN_EXP:-0 1 2 8}; do
         L=""; [ $X != 0 ] && L=$R/tools/exp/libmsunet_layernorm_$X.so
