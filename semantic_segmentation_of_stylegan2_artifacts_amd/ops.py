@@ -1538,8 +1538,9 @@ def _pad_to(t, dim, mult):
 
 
 # persistent workgroups of the refine-conv weight gradient (one 139 KB / 12-wave workgroup per
-# CU; 192 / 128 measured slower, r04ac)
-_CONV_WGRAD_BLOCKS = 256
+# CU; 192 / 128 measured slower beside the refine dgrads, r04ac -- the A/B switch pairs fewer of
+# them with the deferral below, MSU_CONV_WGRAD_AT)
+_CONV_WGRAD_BLOCKS = int(switches.get("MSU_CONV_WGRAD_BLOCKS"))
 
 
 def _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout):
