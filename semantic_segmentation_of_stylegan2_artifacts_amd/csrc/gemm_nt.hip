@@ -142,10 +142,17 @@ struct KnTile {
 // 256 x 128, i.e. 1.5 rounds); KN (input-gradient) form: 128 only.
 // KB: K step (64).  A 32-deep step with a four-stage ring (three steps in flight in the same LDS)
 // was 25-50 % slower on every stage 1-3 shape (r04u) and is gone.
+// NST = 4 (A3W2): the 256 x 192 tile with the A operand two K steps ahead -- a ring of THREE A
+// stages (32 KB each) beside TWO W stages (24 KB): 144 KB, where three whole stages (168 KB) do not
+// fit.  A streams from HBM (or a sibling N tile's L2 lines), W is a small L2-resident weight: the
+// operand with the long latency gets the deeper prefetch.  Per step s the waves issue W(s + 1), then
+// A(s + 2); the wait for step s lets A(s + 1) (and a preceding epilogue's stores) stay in flight.
 template <typename T, int EPI, int WM, int NST, bool WKN, int BNT, int KB>
 __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   constexpr int NTHR = 128 * WM, BM = 64 * WM, NI = BNT / 64;
+  constexpr bool A3 = NST == 4;
   static_assert(!WKN || (BNT == BN && KB == BK), "KN tiles are 128 wide, 64 deep");
+  static_assert(!A3 || (!WKN && WM == 4 && BNT == 192), "A3W2: the 256 x 192 NT tile");
   typedef RowTile<BM, NTHR, KB> TA;
   typedef RowTile<BNT, NTHR, KB> TW;
   typedef KnTile<NTHR> TK;
@@ -157,9 +164,11 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   static_assert(TA::FULLW * 64 == NTHR, "A rows: whole rounds");
   constexpr int DW0 = WKN ? 64 : TW::FULLW;
   constexpr int E = (EPI == EPI_GELU_DUAL ? 8 : 4) * NI;
-  static_assert(NST >= 2 && NST <= 3, "ring depth");
-  static_assert(NST == 2 || ((NST - 2) * D + E < 64), "vmcnt range");
-  __shared__ __attribute__((aligned(16))) bf16_t lds[NST * STG];
+  static_assert(NST >= 2 && NST <= 4, "ring depth");
+  static_assert(NST == 2 || ((A3 ? TA::PER + TW::PER : (NST - 2) * D) + E < 64), "vmcnt range");
+  static_assert(!A3 || TW::FULLW * 64 == NTHR, "A3W2: every wave issues all its W DMA");
+  constexpr int LDS_ELEMS = A3 ? 3 * BM * KB + 2 * BNT * KB : NST * STG;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % WM, wn = wave / WM;  // this wave's 64 x 64 piece (tokens, columns)
@@ -170,18 +179,29 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   const int mine = L < ntiles ? (ntiles - 1 - L) / G + 1 : 0;
   const int nsteps = mine * nk;
 
-  // K step s of this workgroup's sequence -> LDS stage `st`
-  auto issue = [&](int s, int st) __attribute__((always_inline)) {
+  // K step s of this workgroup's sequence: its A / W tiles -> LDS at dst
+  auto issue_a = [&](int s, bf16_t* dst) __attribute__((always_inline)) {
     const int ti = s / nk, kk = s - ti * nk;
     const int t = L + ti * G;
-    const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
-    bf16_t* dst = lds + st * STG;
+    const int mt = t / a.tiles_n;
     if (a.A2 == nullptr) TA::stage(a.A, mt * BM, a.M, a.K, kk * KB, dst, tid);
     else if (kk * KB < a.K1) TA::stage(a.A, mt * BM, a.M, a.K1, kk * KB, dst, tid);  // K1 % 64 == 0
     else TA::stage(a.A2, mt * BM, a.M, a.K - a.K1, kk * KB - a.K1, dst, tid);
-    if constexpr (WKN) TK::stage(a.W, nt * BNT, a.N, kk * KB, dst + BM * KB, tid);
-    else TW::stage(a.W, nt * BNT, a.N, a.K, kk * KB, dst + BM * KB, tid);
   };
+  auto issue_w = [&](int s, bf16_t* dst) __attribute__((always_inline)) {
+    const int ti = s / nk, kk = s - ti * nk;
+    const int t = L + ti * G;
+    const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
+    if constexpr (WKN) TK::stage(a.W, nt * BNT, a.N, kk * KB, dst, tid);
+    else TW::stage(a.W, nt * BNT, a.N, a.K, kk * KB, dst, tid);
+  };
+  // K step s -> ring stage `st` (NST = 2 / 3: A and W in one stage)
+  auto issue = [&](int s, int st) __attribute__((always_inline)) {
+    bf16_t* dst = lds + st * STG;
+    issue_a(s, dst);
+    issue_w(s, dst + BM * KB);
+  };
+  bf16_t* const ldsW = lds + 3 * BM * KB;  // A3W2: the W stages after the three A stages
 
   f32x16 acc[NI][2];  // [column tile ni][token tile mi]: C^T, W rows on the accumulator rows
 #pragma unroll
@@ -189,12 +209,22 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
 
+  if constexpr (A3) {
+    // A(0), W(0), A(1): step 0 waits for W(0) with A(1) in flight
+    if (nsteps > 0) {
+      issue_a(0, lds);
+      issue_w(0, ldsW);
+    }
+    if (nsteps > 1) issue_a(1, lds + BM * KB);
+  } else {
 #pragma unroll
-  for (int s = 0; s < NST - 1; ++s)
-    if (s < nsteps) issue(s, s);
+    for (int s = 0; s < NST - 1; ++s)
+      if (s < nsteps) issue(s, s);
+  }
   int kk = 0, ti = 0;  // K step within the tile, tile ordinal (within this workgroup)
   int cst = 0;         // LDS stage of step s
   int epi_age = 99;    // steps since the last epilogue (its stores follow that step's DMA issue)
+  bool a3_more_a = false;  // A3W2: this step also issued A(s + 2)
   bool epi_full = true;  // that epilogue issued all E stores of this wave (no ragged M / N edge)
   for (int s = 0; s < nsteps; ++s) {
     // step s's DMA landed; younger DMAs (step s + 1) and epilogue stores issued after step s's
@@ -204,7 +234,16 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     // past N), so it does not count them -- counting them let that wave pass the barrier with
     // its share of step s's DMA still in flight, and the other waves read stale LDS (found as
     // run-to-run differences of the eager step with the side stream on, round 3)
-    if constexpr (NST == 2) {
+    if constexpr (A3) {
+      // W(s) landed (and A(s), issued a step earlier); A(s + 1), issued after W(s), and the
+      // stores of an epilogue that followed them may stay in flight
+      const bool younger = s + 1 < nsteps;
+      const bool stores = epi_age == 0 && epi_full;
+      if (younger && stores) wait_vmcnt<TA::PER + E>();
+      else if (younger) wait_vmcnt<TA::PER>();
+      else if (stores) wait_vmcnt<E>();
+      else wait_vmcnt<0>();
+    } else if constexpr (NST == 2) {
       wait_vmcnt<0>();
     } else if constexpr (NST == 3) {
       const bool younger = s + 1 < nsteps;
@@ -246,11 +285,27 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
           }
         }
     }
-    const bool more = s + NST - 1 < nsteps;
-    if (more) issue(s + NST - 1, cst == 0 ? NST - 1 : cst - 1);
-    const bf16_t* ta = lds + cst * STG;
-    const bf16_t* tw = ta + BM * KB;
-    cst = cst + 1 == NST ? 0 : cst + 1;
+    const bf16_t* ta;
+    const bf16_t* tw;
+    bool more;  // DMA issued in this step (the epilogue's wait lets it stay in flight)
+    if constexpr (A3) {
+      // W(s + 1) into the W stage step s - 1 used, A(s + 2) into the A stage of step s - 1
+      const int wst = s & 1, ast = cst;  // cst: A stage of step s (s % 3)
+      const bool mw = s + 1 < nsteps, ma = s + 2 < nsteps;
+      if (mw) issue_w(s + 1, ldsW + (wst ^ 1) * BNT * KB);
+      if (ma) issue_a(s + 2, lds + (ast == 0 ? 2 : ast - 1) * BM * KB);
+      more = mw;
+      a3_more_a = ma;
+      ta = lds + ast * BM * KB;
+      tw = ldsW + wst * BNT * KB;
+      cst = cst + 1 == 3 ? 0 : cst + 1;
+    } else {
+      more = s + NST - 1 < nsteps;
+      if (more) issue(s + NST - 1, cst == 0 ? NST - 1 : cst - 1);
+      ta = lds + cst * STG;
+      tw = ta + BM * KB;
+      cst = cst + 1 == NST ? 0 : cst + 1;
+    }
     bf16x8 fw[2][NI], fx[2][2];
     auto rd = [&](int ks, int set) {
 #pragma unroll
@@ -287,7 +342,12 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     epi_full = m0 + 64 * wm + 64 <= a.M && n0 + WNC * wn + WNC <= a.N;
     // the epilogue operands (and every older DMA) have landed; the DMA just issued may stay
     // in flight (NST = 3).  One wait, not one per exec-masked store branch.
-    if (NST >= 3 && more) {
+    if constexpr (A3) {
+      // the epilogue operands were loaded before this step's W(s + 1) / A(s + 2) DMAs
+      if (more && a3_more_a) wait_vmcnt<TW::PER + TA::PER>();
+      else if (more) wait_vmcnt<TW::PER>();
+      else wait_vmcnt<0>();
+    } else if (NST >= 3 && more) {
       if (wave < DW0) wait_vmcnt<D>();
       else wait_vmcnt<D - 1>();
     } else {
@@ -364,6 +424,8 @@ int g_nt_pp = 0;
 // tile-form override for kernel-timing tools (msu_nt_gemm_mode bits 1-2): 0 = the cost model,
 // 1 = 128 x 192 (two workgroups per CU), 2 = 256 x 128 (three-stage ring), 3 = 128 x 128
 int g_nt_force = 0;
+// msu_nt_gemm_mode bit 3: the 256 x 192 tile on the A3W2 ring (gemm_nt_kernel NST = 4)
+int g_nt_a3 = 0;
 
 int num_cus_nt();
 
@@ -492,7 +554,8 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
   }
   MSU_DISPATCH16(dtype, T,
     if (cfg.bn == 192) {
-      if (cfg.wm == 4) launch_nt<T, 4, 2, false, 192>(epi, a, st);
+      if (cfg.wm == 4 && g_nt_a3) launch_nt<T, 4, 4, false, 192>(epi, a, st);
+      else if (cfg.wm == 4) launch_nt<T, 4, 2, false, 192>(epi, a, st);
       else launch_nt<T, 2, 2, false, 192>(epi, a, st);
     } else if (cfg.wm == 4) {
       if (wkn) launch_nt<T, 4, 3, true, 128>(epi, a, st);
@@ -522,11 +585,13 @@ int msu_nt_gemm_plan(long M, int N) {
 
 // bit 0 -- 1: the ping-pong kernel where the shape tiles exactly, 0 (the default, MSU_NT_PP=0): the
 // persistent 2-barrier kernel everywhere; bits 1-2: a forced tile form for kernel-timing tools
-// (0: the cost model; 1: 128 x 192, 2: 256 x 128, 3: 128 x 128).  Returns the previous mode.
+// (0: the cost model; 1: 128 x 192, 2: 256 x 128, 3: 128 x 128); bit 3: the 256 x 192 tile on the
+// A3W2 ring (A two K steps ahead).  Returns the previous mode.
 int msu_nt_gemm_mode(int mode) {
-  const int prev = g_nt_pp | (g_nt_force << 1);
+  const int prev = g_nt_pp | (g_nt_force << 1) | (g_nt_a3 << 3);
   g_nt_pp = mode & 1;
   g_nt_force = (mode >> 1) & 3;
+  g_nt_a3 = (mode >> 3) & 1;
   return prev;
 }
 

@@ -29,10 +29,11 @@ def _ops():
     return ops
 
 
-@pytest.fixture(params=[1, 0], ids=["pingpong", "persistent"], autouse=True)
+@pytest.fixture(params=[1, 0, 8], ids=["pingpong", "persistent", "a3w2"], autouse=True)
 def nt_mode(request):
-    """Every test runs with both NT kernels: the ping-pong one (gemm_pp.h, default where the shape
-    tiles exactly) and the persistent 2-barrier one (MSU_NT_PP=0)."""
+    """Every test runs with each NT kernel form: the ping-pong one (gemm_pp.h, MSU_NT_PP=1 where the
+    shape tiles exactly), the persistent 2-barrier one, and the persistent kernel's 256 x 192 tile
+    on the A3W2 ring (msu_nt_gemm_mode bit 3: A two K steps ahead)."""
     from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
     prev = _lib.lib().msu_nt_gemm_mode(request.param)
     yield request.param

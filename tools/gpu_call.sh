@@ -33,6 +33,14 @@ for s in "$@"; do
         MSU_LIB_OVERRIDE=$L timeout -k 10 200 python -u $R/tools/nt_shapes.py 20 ${L:+B} >> $O/${TAG}_nt_shapes.log 2>&1 || exit 3
       done
       python3 $R/tools/ab_table.py $O/${TAG}_nt_shapes.log ;;
+    nt_a3)
+      # the 256 x 192 NT tile on the A3W2 ring vs the two-stage ring, interleaved twice; then the NT
+      # tests with A3 on
+      for A in 0 1 0 1; do
+        NT_A3=$A timeout -k 10 200 python -u $R/tools/nt_shapes.py 20 >> $O/${TAG}_nt_a3.log 2>&1 || exit 3
+      done
+      python3 $R/tools/ab_table.py $O/${TAG}_nt_a3.log F0A0 F0A1
+      step nt_a3_tests 600 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py ;;
     nt_force)
       # NT GEMM kernel times per shape under each forced tile form (tools/nt_shapes.py NT_FORCE)
       for F in 0 1 2 3 0 1; do

@@ -21,10 +21,13 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 tag = sys.argv[2] if len(sys.argv) > 2 else os.path.basename(os.environ.get("MSU_LIB_OVERRIDE", "") or "cur")
 # NT_FORCE=1/2/3: a forced tile form (msu_nt_gemm_mode bits 1-2) for this run
 force = int(os.environ.get("NT_FORCE", "0"))
-if force:
+a3 = int(os.environ.get("NT_A3", "-1"))
+if force or a3 >= 0:
     from semantic_segmentation_of_stylegan2_artifacts_amd import _lib  # noqa: E402
-    _lib.lib().msu_nt_gemm_mode(force << 1)
-    tag = f"F{force}"
+    prev = _lib.lib().msu_nt_gemm_mode(0)
+    a3 = (prev >> 3) & 1 if a3 < 0 else a3
+    _lib.lib().msu_nt_gemm_mode((force << 1) | (a3 << 3))
+    tag = f"F{force}A{a3}"
 tot = 0.0
 for M, N, K, epi, kn in SHAPES:
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
