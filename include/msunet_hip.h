@@ -130,6 +130,11 @@ int msu_conv3x3_fwd2(int dtype, int in_mode, const void* X, const void* Wt, cons
  * Wflip [9][Cin][roundup(Cout,32)], Wflip[t][ci][co] = W[co][ci][8-t]. */
 int msu_conv3x3_dgrad(int dtype, int out_mode, const void* dY, const void* Wflip, const void* S,
                       void* dX, int B, int H, int W, int Cin, int Cout, void* stream);
+/* 1 (default): the 96-channel refine-conv kernel takes its tiles from a device queue (per-stream
+ * counter slot, reset by the launch's last workgroup), so workgroups that start late beside
+ * the side stream's kernels take fewer tiles; 0: the static schedule (A/B switch MSU_CONV_DYN).
+ * Returns the previous mode. */
+int msu_conv_mode(int mode);
 long msu_conv3x3_wgrad_workspace(int nchunk, int Cin, int Cout, int dtype, int unused);
 /* dW [Cout][Cin][3][3] f32, db [Cout] f32 (deterministic partial-sum reduction). */
 int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, float* dW, float* db,
@@ -296,6 +301,13 @@ int msu_adamw(float* p, const float* g, float* m, float* v, long n, float lr, fl
 int msu_adamw_dev(float* p, const float* g, float* m, float* v, long n, const double* hyper, double beta1,
                   double beta2, double eps, double weight_decay, const float* inv_scale, const float* found_inf,
                   void* stream);
+/* msu_adamw_dev that also writes the updated parameters' 16-bit shadow (shadow_dtype 1 bf16 /
+ * 2 f16; shadow null = none) and zeroes g after reading it (zero_grad; a skipped step zeroes it
+ * too): the step's gradient reset and shadow refresh in the optimizer's own pass
+ * (trainer.py:315-316 optimizer.step + zero_grad). */
+int msu_adamw_dev2(float* p, float* g, float* m, float* v, long n, const double* hyper, double beta1, double beta2,
+                   double eps, double weight_decay, const float* inv_scale, const float* found_inf, void* shadow,
+                   int shadow_dtype, int zero_grad, void* stream);
 /* hyper[1] += 1 unless found_inf[0] != 0 (the skipped step does not count, as torch's AdamW
  * `step` state is not advanced when GradScaler skips optimizer.step). */
 int msu_step_advance(double* hyper, const float* found_inf, void* stream);
@@ -304,6 +316,10 @@ int msu_step_advance(double* hyper, const float* found_inf, void* stream);
 int msu_nonfinite(const float* x, long n, float* flag, void* stream);
 int msu_nonfinite2(const float* x0, long n0, const float* x1, long n1, float* flag, void* stream);
 int msu_cast(int dtype, const float* x, void* y, long n, void* stream);
+/* The refine conv's f32 weight W [Cout][Cin][3][3] (model_parts.py:447-448) in the conv kernels'
+ * layouts, in the activation dtype: flip 0 -> Wt of msu_conv3x3_fwd/_fwd2 [9][Cout][roundup(Cin,32)];
+ * flip 1 -> Wflip of msu_conv3x3_dgrad [9][Cin][roundup(Cout,32)] (zero padding). */
+int msu_conv3x3_weight(int dtype, const float* W, void* out, int Cout, int Cin, int flip, void* stream);
 
 /* ---------------------------------------------------------------- input pipeline
  * The per-sample CPU transform of the reference's DataLoader workers (dataset/dataset.py:20-95

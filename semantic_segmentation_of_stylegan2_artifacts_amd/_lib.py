@@ -26,6 +26,7 @@ SIGNATURES = {
     "msu_layernorm_bwd": (I, [I, I, P, P, P, P, P, P, P, P, P, L, P, I, P, P, L, I, I, I, I, I, P]),
     "msu_reduce_rows": (I, [P, I, I, L, P, I, P]),
     "msu_tail_reduce_mode": (I, [I]),
+    "msu_conv_mode": (I, [I]),
     "msu_head_fwd": (I, [I, P, P, P, P, P, P, P, L, I, F, P]),
     "msu_head_bwd": (I, [I, P, P, P, P, P, P, P, P, P, I, P, P, P, L, I, P]),
     "msu_win_count": (L, [I, I, I]),
@@ -53,8 +54,10 @@ SIGNATURES = {
     "msu_nonfinite": (I, [P, L, P, P]),
     "msu_nonfinite2": (I, [P, L, P, L, P, P]),
     "msu_adamw_dev": (I, [P, P, P, P, L, P, D, D, D, D, P, P, P]),
+    "msu_adamw_dev2": (I, [P, P, P, P, L, P, D, D, D, D, P, P, P, I, I, P]),
     "msu_step_advance": (I, [P, P, P]),
     "msu_cast": (I, [I, P, P, L, P]),
+    "msu_conv3x3_weight": (I, [I, P, P, I, I, I, P]),
     "msu_transpose16_multi": (I, [P, P, P, I, I, P]),
     "msu_conv3x3_fwd": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),
     "msu_conv3x3_fwd2": (I, [I, I, P, P, P, P, P, I, I, I, I, I, P]),
@@ -107,6 +110,7 @@ def lib():
     # the library-side A/B switches (the C code reads no environment; switches.py does)
     h.msu_nt_gemm_mode(1 if switches.on("MSU_NT_PP") else 0)
     h.msu_tail_reduce_mode(1 if switches.on("MSU_TAIL") else 0)
+    h.msu_conv_mode(1 if switches.on("MSU_CONV_DYN") else 0)
     _lib = h
     return _lib
 

@@ -13,6 +13,7 @@
 // with ds_read_b64_tr_b16 (bf16) and writes deterministic per-block partials.
 #pragma once
 #include <cstdlib>
+#include <mutex>
 #include <utility>
 
 #include "common.h"
@@ -525,7 +526,9 @@ __global__ void __launch_bounds__(64 * NW) conv3x3_v2_kernel(const bf16_t* __res
 // Epilogue as v2 (bias, DUAL = GELU(Y) as a second output, GELU'(S) for the backward-data
 // launches with S prefetched at tap 7, 16-B stores after a permlane32 swap).
 constexpr int V3_HALO_TAP = 1;
-constexpr int SPRE = 12;  // GELU' operand loads per lane (dgrad), issued at tap 7
+constexpr int SPRE = 12;  // GELU' operand loads per lane (dgrad)
+// ablation bit 1024: all of them at tap 7 (the round-5 placement; spilled halo registers)
+constexpr bool SP_AT7 = (MSU_EXP & 1024) != 0;
 
 MSU_DEV int swz(int p) { return (p >> 2) & 3; }
 // M16 (16x16x32 MFMA) fragment reads: 16 consecutive rows, chunk (lane >> 4) of a 4-chunk group;
@@ -538,13 +541,24 @@ template <bool M16> MSU_DEV int swzv(int p) { return M16 ? (p >> 1) & 3 : (p >> 
 // where the wait for tap 3's weights also waited for the whole 117 KB halo.
 MSU_DEV constexpr int halo_part_lo(int t, int nhc) { return (t - 1) * nhc / 7; }  // t = 1..7
 
+// Tile queue of the persistent conv3x3_v3_kernel: a workgroup takes its
+// first tile statically (blockIdx.x) and claims every further tile from a device counter, one
+// tile ahead (the next tile's halo and weight prefetch need its index from tap 1 on), so the
+// workgroups that get a CU late -- beside the side stream's weight-gradient kernels, which hold
+// whole CUs -- take fewer tiles instead of running a fixed share past the others' end.  Slot:
+// {claim counter, finished workgroups} on a 128-B line per stream; the last workgroup to finish
+// resets both (no memset launch, graph-replay safe).  Results do not depend on which workgroup
+// computes a tile.
+constexpr int TQ_SLOTS = 16;
+__device__ int g_tile_queue[TQ_SLOTS * 32];
+
 template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL, bool SPREAD, bool M16>
 __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restrict__ X,
                                                          const bf16_t* __restrict__ Wt,
                                                          const float* __restrict__ bias,
                                                          const bf16_t* __restrict__ S,
                                                          bf16_t* __restrict__ Y, bf16_t* __restrict__ Y2,
-                                                         ConvGeom g, int ntiles) {
+                                                         ConvGeom g, int ntiles, int* __restrict__ tq) {
   constexpr int C = 96, CH = 12, NW = 8, MT = 2, TH = NW * MT, TWV = 32, HWD = TWV + 2;
   constexpr int HPIX = (TH + 2) * HWD;  // 612 halo pixels
   (void)HPIX;
@@ -561,6 +575,7 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
   bf16_t* sX = reinterpret_cast<bf16_t*>(smem_raw);
   bf16_t* sW = sX + HPIX * C;  // [2][96][96]
   float* sB = reinterpret_cast<float*>(sW + 2 * WIMG);  // [96] bias (BIAS)
+  int* sQ = reinterpret_cast<int*>(sB + C);              // the claimed next tile (tq)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tiles_x = (g.W + TWV - 1) / TWV, tiles_y = (g.H + TH - 1) / TH;
@@ -641,8 +656,26 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
   // DMA wave-instructions this wave issues per tap (wave-uniform)
   const int my_wdma = (WINS - wave + NW - 1) / NW;
 
+  // tq: claims count up from 0 (tile gridDim.x + count); the last workgroup out resets the slot
+  auto finish = [&]() {
+    if (tq != nullptr && tid == 0 && atomicInc((unsigned*)tq + 1, 0xffffffffu) == gridDim.x - 1) {
+      atomicExch(tq, 0);
+      atomicExch(tq + 1, 0);
+    }
+  };
+  // the tile thread 0 left in sQ (after a barrier); untracked read: a compiler-visible ds_read
+  // would wait for the weight DMA and output stores in flight here (vmcnt(0))
+  auto read_q = [&]() -> int {
+    uint32_t v = ds_b32_untracked<0>(lds_u32(sQ));
+    lds_wait_tie<0>(v);
+    return __builtin_amdgcn_readfirstlane((int)v) + (int)gridDim.x;
+  };
   int tile = blockIdx.x;
-  if (tile >= ntiles) return;
+  if (tile >= ntiles) {  // (the launch keeps the grid <= ntiles)
+    finish();
+    return;
+  }
+  if (tq != nullptr && tid == 0) sQ[0] = (int)atomicInc((unsigned*)tq, 0xffffffffu);
   if constexpr (BIAS) {
     if (tid < C) sB[tid] = bias[tid];  // read by every epilogue from LDS (no global load there)
   }
@@ -650,6 +683,7 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
   store_halo();
   dma_w(0, 0);
   __syncthreads();  // the halo's ds_writes land before any wave reads (the tap barriers are raw)
+  int next = tq != nullptr ? read_q() : tile + (int)gridDim.x;
   int wbuf = 0;
   // w1_early: this tile's W(1) was DMA'd by the previous tile's epilogue, ahead of its output
   // stores; st_full: those stores are all EST of them (a whole tile) and may stay in flight
@@ -666,8 +700,8 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
   const int l15 = lane & 15, g4 = lane >> 4;
   const int wk16 = l15 * C + ((g4 ^ swzv<true>(l15)) << 3);  // weight rows 16n + l15
 
-  for (; tile < ntiles; tile += gridDim.x) {
-    const int next = tile + gridDim.x;
+  for (;;) {
+    int nn = 0;  // thread 0 (tq): the tile after next, claimed at tap 1
     int b, y0, x0;
     coords(tile, b, y0, x0);
     const int xo = x0 + xl;
@@ -700,7 +734,8 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
       // part(s) of the next tile and (dgrad, tap 7) the GELU' operands
       constexpr int hprev = SPREAD ? (tap >= 2 ? halo_part_lo(tap, NHC) - halo_part_lo(tap - 1, NHC) : 0)
                                    : (tap == V3_HALO_TAP + 1 ? NHC : 0);
-      constexpr int sprev = (OUT_GGRAD && tap == 8) ? SPRE : 0;
+      // (32 x 32 form: only co tile 0's operands are issued at tap 7, see load_sp)
+      constexpr int sprev = (OUT_GGRAD && tap == 8) ? ((M16 || SP_AT7) ? SPRE : SPRE / 3) : 0;
       if constexpr (tap == 0) {
         // W(0) landed (DMA'd at the previous tile's tap 8); W(1) and the previous tile's output
         // stores, issued after it in that epilogue, may stay in flight
@@ -727,6 +762,22 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
       const bf16_t* wcur = sW + wbuf * WIMG;
       if constexpr (tap == 0) {
         if (!w1_early) dma_w(1, wbuf ^ 1);
+      } else if constexpr (tap == 1) {
+        // claim the tile after next (thread 0); older than W(2)'s DMA, so tap 2's counted wait
+        // covers it
+        // (atomicInc: the add form goes through the atomic optimizer, whose lane arithmetic
+        // on the result waits for it at once; the raw count is offset by gridDim.x on read)
+        if (tq != nullptr && tid == 0 && next < ntiles) nn = (int)atomicInc((unsigned*)tq, 0xffffffffu);
+        dma_w(2, wbuf ^ 1);
+      } else if constexpr (tap == 2) {
+        // the claim to sQ: every wave read this tile's entry before tap 0's barrier, the next
+        // read follows the tile's closing barrier.  Untracked write (a visible ds_write would
+        // wait for the weight DMA in flight).
+        if (tq != nullptr && tid == 0 && next < ntiles) {
+          asm volatile("ds_write_b32 %0, %1" ::"v"(lds_u32(sQ)), "v"(nn) : "memory");
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        dma_w(3, wbuf ^ 1);
       } else if constexpr (tap < 8) {
         dma_w(tap + 1, wbuf ^ 1);
       } else {
@@ -737,6 +788,14 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
       } else if constexpr (!SPREAD && tap == V3_HALO_TAP) {
         if (next < ntiles) load_halo(next, IC<0>{}, IC<NHC>{});
       }
+      // dgrad, 32 x 32 form: GELU' operands of co tile n for rows m (two 16-B loads per row)
+      auto load_sp = [&](int m, int y, int n) __attribute__((always_inline)) {
+        const int xs = min(xo, g.W - 1);
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp)
+          sp[m][n][pp] = *reinterpret_cast<const u32x4*>(S + pix_off32<OUT_D2S>(b, y, xs, g.H, g.W, C) + 32 * n +
+                                                         16 * pp + 8 * h);
+      };
       if constexpr (OUT_GGRAD && tap == 7) {
         // dgrad: the pre-activation S of this tile's outputs for the GELU' epilogue
 #pragma unroll
@@ -752,13 +811,11 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
                                                                16 * (g4 & 1) + 8 * (g4 >> 1));
             }
           } else {
-            const int xs = min(xo, g.W - 1);
-#pragma unroll
-            for (int n = 0; n < 3; ++n)
-#pragma unroll
-              for (int pp = 0; pp < 2; ++pp)
-                sp[m][n][pp] = *reinterpret_cast<const u32x4*>(S + pix_off32<OUT_D2S>(b, y, xs, g.H, g.W, C) + 32 * n +
-                                                               16 * pp + 8 * h);
+            load_sp(m, y, 0);
+            if constexpr (SP_AT7) {
+              load_sp(m, y, 1);
+              load_sp(m, y, 2);
+            }
           }
         }
       }
@@ -853,6 +910,18 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
         }, std::make_integer_sequence<int, 6>{});
       }
       if constexpr (tap == 8) {
+        if constexpr (OUT_GGRAD && !M16 && !SP_AT7) {
+          // co tiles 1-2's GELU' operands after the last MFMAs: held through taps 7-8 beside the
+          // full halo prefetch they pushed the kernel past 256 VGPRs (halo registers spilled,
+          // each spill store a vmcnt(0) at tap 1); their latency is exposed at the epilogue's
+          // wait instead
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            const int y = min(y0 + 2 * wave + m, g.H - 1);
+            load_sp(m, y, 1);
+            load_sp(m, y, 2);
+          }
+        }
         if (next < ntiles) {
           __syncthreads();  // every wave's last halo read done (s_barrier + lgkmcnt)
           store_halo();
@@ -864,7 +933,18 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
     // tap 8's weight buffer: every wave passed tap 8's barrier before the halo store) ahead of
     // this tile's output stores, so tap 1 of the next tile waits for it and not for the stores
     auto epi_start = [&]() __attribute__((always_inline)) {
-      if constexpr (OUT_GGRAD) wait_vmcnt<0>();
+      // the GELU' operands landed; pinned after the wait (an empty asm redefining them), or the
+      // compiler still counts them pending and puts a vmcnt(0) in front of each first use --
+      // behind the previous store group's stores
+      if constexpr (OUT_GGRAD) {
+        wait_vmcnt<0>();
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int n = 0; n < (M16 ? 2 : 3); ++n)
+#pragma unroll
+            for (int pp = 0; pp < (M16 ? 3 : 2); ++pp) vreg_pin(sp[m][n][pp]);
+      }
       w1_early = next < ntiles;
       st_full = w1_early && x0 + TWV <= g.W && y0 + TH <= g.H;
       if (w1_early) dma_w(1, wbuf ^ 1);
@@ -984,11 +1064,13 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
         }
     }
     }
-    if (next < ntiles) {
-      // the next tile's halo (stored after tap 8) visible to every wave before its tap 0
-      __syncthreads();
-    }
+    if (next >= ntiles) break;
+    // the next tile's halo (stored after tap 8) visible to every wave before its tap 0
+    __syncthreads();
+    tile = next;
+    next = tq != nullptr ? read_q() : next + (int)gridDim.x;
   }
+  finish();
 }
 
 // ------------------------------------------------------------------ wgrad kernel
@@ -1325,6 +1407,30 @@ int launch_conv(const ConvGeom& g, const T* X, const T* Wt, const float* bias, c
   return MSU_CHECK_LAUNCH();
 }
 
+// msu_conv_mode bit 0 (default on; A/B switch MSU_CONV_DYN): conv3x3_v3_kernel takes tiles
+// from the per-stream queue slot instead of the static blockIdx.x + k * gridDim.x schedule
+int g_conv_dyn = 1;
+
+// the queue slot of stream `st` (nullptr: the static schedule -- queue off, or more streams
+// than slots)
+int* tile_queue(hipStream_t st) {
+  if (!g_conv_dyn) return nullptr;
+  static std::mutex mu;
+  static int* base = nullptr;
+  static hipStream_t owner[TQ_SLOTS];
+  static int used = 0;
+  std::lock_guard<std::mutex> lock(mu);
+  if (base == nullptr && hipGetSymbolAddress((void**)&base, HIP_SYMBOL(g_tile_queue)) != hipSuccess) {
+    base = nullptr;
+    return nullptr;
+  }
+  for (int i = 0; i < used; ++i)
+    if (owner[i] == st) return base + 32 * i;
+  if (used == TQ_SLOTS) return nullptr;
+  owner[used] = st;
+  return base + 32 * used++;
+}
+
 int num_cus() {
   static int n = 0;
   if (n <= 0) {
@@ -1360,7 +1466,7 @@ int launch_v2(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float*
 template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL, bool SPREAD, bool M16>
 int launch_v3s(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float* bias, const bf16_t* S, bf16_t* Y,
                bf16_t* Y2, hipStream_t st) {
-  constexpr size_t lds = sizeof(bf16_t) * ((size_t)18 * 34 * 96 + 2 * 96 * 96) + 96 * sizeof(float);  // + bias
+  constexpr size_t lds = sizeof(bf16_t) * ((size_t)18 * 34 * 96 + 2 * 96 * 96) + 96 * sizeof(float) + 16;  // + bias, queue
   static_assert(lds <= 160 * 1024, "LDS");
   auto kern = conv3x3_v3_kernel<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, SPREAD, M16>;
   static bool attr_set = false;
@@ -1372,7 +1478,7 @@ int launch_v3s(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float
   if (ntiles == 0) return 0;
   if ((long)g.B * g.H * g.W * 96 >= (1L << 31)) return -2;
   const int grid = (int)(ntiles < num_cus() ? ntiles : num_cus());
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, X, Wt, bias, S, Y, Y2, g, (int)ntiles);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, X, Wt, bias, S, Y, Y2, g, (int)ntiles, tile_queue(st));
   return MSU_CHECK_LAUNCH();
 }
 

@@ -72,4 +72,11 @@ int msu_conv3x3_dgrad(int dtype, int out_mode, const void* dY, const void* Wflip
   return -3;
 }
 
+// bit 0: the refine-conv kernel's tile queue (g_conv_dyn); returns the previous mode
+int msu_conv_mode(int mode) {
+  const int prev = g_conv_dyn;
+  g_conv_dyn = mode & 1;
+  return prev;
+}
+
 }  // extern "C"

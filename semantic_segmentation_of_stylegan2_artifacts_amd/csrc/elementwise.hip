@@ -5,6 +5,8 @@
 // All HBM-bound: vectorised 4-wide, grid-stride, f32 math.  GELU: libm erff for f32 (the
 // parity path), the one-exp / one-rcp erf of common.h for bf16 (|error| <= 1.5e-7, far below
 // bf16 rounding; libm erff made the bf16 kernels VALU-bound).
+#include <type_traits>
+
 #include "common.h"
 
 #ifndef MSU_EXP
@@ -235,13 +237,21 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
 // formed in double and rounded once, and the update follows torch.optim.AdamW's operation
 // order (param.mul_(1 - lr*wd); exp_avg.lerp_(g, 1 - b1); exp_avg_sq.mul_(b2).addcmul_(g, g,
 // 1 - b2); param.addcdiv_(exp_avg, sqrt(exp_avg_sq) / sqrt(bc2) + eps, -lr / bc1)).
-__global__ void __launch_bounds__(256) adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
+// S: the 16-bit shadow written with the updated parameter (void: none); ZERO: the gradient is
+// zeroed after it was read (also on a skipped step) -- the step's gradient reset and bf16 shadow
+// refresh in the same pass instead of a fill and a re-read of the parameters
+template <typename S, bool ZERO>
+__global__ void __launch_bounds__(256) adamw_dev_kernel(float* __restrict__ p, float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v, long n,
                                                         const double* hyper, double b1, double b2, float eps,
                                                         double wd, const float* inv_scale,
-                                                        const float* found_inf) {
+                                                        const float* found_inf, S* __restrict__ shadow) {
 #pragma clang fp contract(off)
-  if (found_inf && found_inf[0] != 0.f) return;
+  if (found_inf && found_inf[0] != 0.f) {
+    if constexpr (ZERO)
+      for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) g[i] = 0.f;
+    return;
+  }
   const double lr = hyper[0];
   const double step = hyper[1];
   const float decay = (float)(1.0 - lr * wd);
@@ -259,7 +269,10 @@ __global__ void __launch_bounds__(256) adamw_dev_kernel(float* __restrict__ p, c
     m[i] = mi;
     v[i] = vi;
     const float denom = __fsqrt_rn(vi) / bc2_sqrt + eps;
-    p[i] = pi + neg_step_size * (mi / denom);
+    const float pn = pi + neg_step_size * (mi / denom);
+    p[i] = pn;
+    if constexpr (!std::is_void_v<S>) shadow[i] = from_f32<S>(pn);  // the cast copy_shadow made
+    if constexpr (ZERO) g[i] = 0.f;
   }
 }
 
@@ -289,6 +302,26 @@ template <typename T>
 __global__ void __launch_bounds__(256) cast_kernel(const float* x, T* y, long n) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
     y[i] = from_f32<T>(x[i]);
+}
+
+// Refine-conv weight in the layouts the implicit-GEMM conv reads (ops.py _refine_impl /
+// _refine_backward; the reference's nn.Conv2d weight [Cout][Cin][3][3], model_parts.py:447-448):
+// flip 0: out[t][co][ci] = W[co][ci][t], ci padded with zeros to P = roundup(Cin, 32);
+// flip 1: out[t][ci][co] = W[co][ci][8 - t], co padded to P = roundup(Cout, 32).
+// One thread per output element (<= 9 x 192 x 224 per conv: one launch, read once, L2-resident).
+template <typename T>
+__global__ void __launch_bounds__(256) conv_weight_kernel(const float* w, T* out, int Cout, int Cin,
+                                                          int flip, int P, long n) {
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int inner = (int)(i % P);
+  long r = i / P;
+  int outer = (int)(r % (flip ? Cin : Cout));
+  int t = (int)(r / (flip ? Cin : Cout));
+  int co = flip ? inner : outer, ci = flip ? outer : inner;
+  float v = 0.f;
+  if (co < Cout && ci < Cin) v = w[((long)co * Cin + ci) * 9 + (flip ? 8 - t : t)];
+  out[i] = from_f32<T>(v);
 }
 
 // Batched 16-bit transpose: entry e = {src offset, dst offset, N, K, first tile} (int64, in
@@ -424,8 +457,29 @@ int msu_adamw_dev(float* p, const float* g, float* m, float* v, long n, const do
                   void* stream) {
   if (n == 0) return 0;
   if (hyper == nullptr) return -2;
-  hipLaunchKernelGGL(adamw_dev_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream,
-                     p, g, m, v, n, hyper, beta1, beta2, (float)eps, weight_decay, inv_scale, found_inf);
+  hipLaunchKernelGGL((adamw_dev_kernel<void, false>), dim3(grid_for(n, 256, 16384)), dim3(256), 0,
+                     (hipStream_t)stream, p, const_cast<float*>(g), m, v, n, hyper, beta1, beta2, (float)eps,
+                     weight_decay, inv_scale, found_inf, (void*)nullptr);
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_adamw_dev2(float* p, float* g, float* m, float* v, long n, const double* hyper, double beta1, double beta2,
+                   double eps, double weight_decay, const float* inv_scale, const float* found_inf, void* shadow,
+                   int shadow_dtype, int zero_grad, void* stream) {
+  if (n == 0) return 0;
+  if (hyper == nullptr || (shadow != nullptr && !msu_is16(shadow_dtype))) return -2;
+  const dim3 grid(grid_for(n, 256, 16384));
+  hipStream_t st = (hipStream_t)stream;
+#define MSU_ADAMW(S, Z)                                                                                         \
+  hipLaunchKernelGGL((adamw_dev_kernel<S, Z>), grid, dim3(256), 0, st, p, g, m, v, n, hyper, beta1, beta2,      \
+                     (float)eps, weight_decay, inv_scale, found_inf, (S*)shadow)
+  if (shadow == nullptr) {
+    if (zero_grad) MSU_ADAMW(void, true);
+    else MSU_ADAMW(void, false);
+  } else {
+    MSU_DISPATCH16(shadow_dtype, T, if (zero_grad) MSU_ADAMW(T, true); else MSU_ADAMW(T, false));
+  }
+#undef MSU_ADAMW
   return MSU_CHECK_LAUNCH();
 }
 
@@ -451,6 +505,16 @@ int msu_nonfinite(const float* x, long n, float* flag, void* stream) {
 int msu_cast(int dtype, const float* x, void* y, long n, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(cast_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, x, (T*)y, n));
+  return MSU_CHECK_LAUNCH();
+}
+
+int msu_conv3x3_weight(int dtype, const float* W, void* out, int Cout, int Cin, int flip, void* stream) {
+  if (Cout <= 0 || Cin <= 0) return 0;
+  int P = ((flip ? Cout : Cin) + 31) / 32 * 32;
+  long n = 9L * (flip ? Cin : Cout) * P;
+  hipStream_t st = (hipStream_t)stream;
+  MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(conv_weight_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                                            st, W, (T*)out, Cout, Cin, flip, P, n));
   return MSU_CHECK_LAUNCH();
 }
 

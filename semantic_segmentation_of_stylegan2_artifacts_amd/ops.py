@@ -1527,16 +1527,6 @@ def head_norm_output(z, gamma, beta, out_weight, eps=1e-5):
 
 
 # ----------------------------------------------------------------------------- conv 3x3
-def _pad_to(t, dim, mult):
-    n = t.shape[dim]
-    p = (n + mult - 1) // mult * mult - n
-    if p == 0:
-        return t
-    shape = list(t.shape)
-    shape[dim] = p
-    return torch.cat([t, t.new_zeros(shape)], dim)
-
-
 # persistent workgroups of the refine-conv weight gradient (one 139 KB / 12-wave workgroup per
 # CU; 192 / 128 measured slower beside the refine dgrads, r04ac -- the A/B switch pairs fewer of
 # them with the deferral below, MSU_CONV_WGRAD_AT)
@@ -1607,6 +1597,18 @@ def _conv_wgrad_param(a, dz, mode, B, H, W, Cin, Cout, weight, bias):
     return None, None
 
 
+def _conv_weight(weight, dt, flip):
+    """The refine conv's weight in the conv kernels' layout (msu_conv3x3_weight; one launch in
+    place of the flip / permute / pad / cast chain of ATen kernels): flip 0 -> [9][Cout][Cin32],
+    flip 1 -> [9][Cin][Cout32]."""
+    Cout, Cin = weight.shape[0], weight.shape[1]
+    P = ((Cout if flip else Cin) + 31) // 32 * 32
+    out = torch.empty(9, Cin if flip else Cout, P, device=weight.device, dtype=dt)
+    w = weight.contiguous()
+    _lib.call("msu_conv3x3_weight", _dt(out), _p(w), _p(out), Cout, Cin, int(flip), _s(w))
+    return out
+
+
 def _refine_impl(x, weight, bias, d2s, H, W):
     """z = conv3x3(GELU(map(x)), W) + b, NHWC; map = identity or the 4x4 depth-to-space of
     FinalPatchExpand_X4_V2 (x: [B, H/4, W/4, 16*Cin])."""
@@ -1615,7 +1617,7 @@ def _refine_impl(x, weight, bias, d2s, H, W):
     Cout, Cin = weight.shape[0], weight.shape[1]
     B = x.shape[0]
     dt = x.dtype
-    wt = _pad_to(weight.permute(2, 3, 0, 1).reshape(9, Cout, Cin), 2, 32).to(dt).contiguous()
+    wt = _conv_weight(weight, dt, 0)
     z = torch.empty(B, H, W, Cout, device=x.device, dtype=dt)
     _lib.call("msu_conv3x3_fwd", _dt(x), 1 | (2 if d2s else 0), _p(x), _p(wt), _p(bias), _p(z),
               B, H, W, Cin, Cout, _s(x))
@@ -1638,8 +1640,7 @@ def _refine_backward(ctx, dz):
     mode = 1 | (2 if d2s else 0)
     dx = None
     if ctx.needs_input_grad[0]:
-        wf = _pad_to(weight.flip(2, 3).permute(2, 3, 1, 0).reshape(9, Cin, Cout), 2, 32)
-        wf = wf.to(x.dtype).contiguous()
+        wf = _conv_weight(weight, x.dtype, 1)
         dx = torch.empty_like(x)
         _lib.call("msu_conv3x3_dgrad", _dt(x), mode, _p(dz), _p(wf), _p(x), _p(dx), B, H, W, Cin, Cout, _s(x))
     dw, db = _conv_wgrad_param(x, dz, mode, B, H, W, Cin, Cout, *ctx.params)
@@ -1668,7 +1669,7 @@ def _refine_act_impl(x, a, weight, bias, d2s, H, W, dual):
     Cout, Cin = weight.shape[0], weight.shape[1]
     B = a.shape[0]
     dt = a.dtype
-    wt = _pad_to(weight.permute(2, 3, 0, 1).reshape(9, Cout, Cin), 2, 32).to(dt).contiguous()
+    wt = _conv_weight(weight, dt, 0)
     z = torch.empty(B, H, W, Cout, device=a.device, dtype=dt)
     z2 = torch.empty_like(z) if dual else z.new_empty(0)
     _lib.call("msu_conv3x3_fwd2", _dt(a), 2 if d2s else 0, _p(a), _p(wt), _p(bias), _p(z), _p(z2) if dual else None,
@@ -1700,8 +1701,7 @@ def _refine_act_backward(ctx, dz, _dz2):
     dz = _as(dz, a.dtype)
     dx = None
     if ctx.needs_input_grad[0]:
-        wf = _pad_to(weight.flip(2, 3).permute(2, 3, 1, 0).reshape(9, Cin, Cout), 2, 32)
-        wf = wf.to(a.dtype).contiguous()
+        wf = _conv_weight(weight, a.dtype, 1)
         dx = torch.empty_like(x)
         _lib.call("msu_conv3x3_dgrad", _dt(a), 1 | (2 if d2s else 0), _p(dz), _p(wf), _p(x), _p(dx),
                   B, H, W, Cin, Cout, _s(a))
@@ -1892,12 +1892,21 @@ def nonfinite_(x, flag, x2=None):
 
 
 def adamw_dev_(param, grad, exp_avg, exp_avg_sq, hyper, beta1, beta2, eps, weight_decay, inv_scale=None,
-               found_inf=None):
+               found_inf=None, shadow=None, zero_grad=False):
     """AdamW over flat f32 buffers with lr and step read from the device tensor
-    ``hyper = [lr, step]`` (f64); no update at all when found_inf[0] != 0."""
+    ``hyper = [lr, step]`` (f64); no update at all when found_inf[0] != 0.  shadow: a 16-bit
+    buffer of param's length receiving the updated values (the trainer's bf16 shadow);
+    zero_grad: grad is zeroed in the same pass (also on a skipped step)."""
     _need_cuda(param)
-    _lib.call("msu_adamw_dev", _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), _p(hyper),
-              beta1, beta2, eps, weight_decay, _p(inv_scale), _p(found_inf), _s(param))
+    if shadow is None and not zero_grad:
+        _lib.call("msu_adamw_dev", _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), _p(hyper),
+                  beta1, beta2, eps, weight_decay, _p(inv_scale), _p(found_inf), _s(param))
+        return
+    if shadow is not None and (shadow.numel() != param.numel() or shadow.dtype not in _LOW):
+        raise ValueError("adamw_dev_: the shadow must be a 16-bit buffer of the parameters' length")
+    _lib.call("msu_adamw_dev2", _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(), _p(hyper),
+              beta1, beta2, eps, weight_decay, _p(inv_scale), _p(found_inf), _p(shadow),
+              _DT[shadow.dtype] if shadow is not None else 0, int(bool(zero_grad)), _s(param))
 
 
 def step_advance_(hyper, found_inf=None):

@@ -37,6 +37,8 @@ SWITCHES = {
                       "the fused kernel storing H only", "DESIGN 7 (r05ao)"),
     "MSU_CONV_WGRAD_AT": ("0", "C > 0: the refine-conv side-stream weight gradients held back to the first LayerNorm "
                           "backward of width >= C (0: issued beside the refine dgrads)", "DESIGN 7 (r06)"),
+    "MSU_CONV_DYN": ("1", "0: the refine-conv kernel's static tile schedule (blockIdx.x + k * gridDim.x) instead "
+                     "of the device tile queue", "DESIGN 7 (r06)"),
     "MSU_CONV_WGRAD_BLOCKS": ("256", "persistent workgroups of the refine-conv weight gradient (one per CU by "
                               "default; fewer leave CUs to the main stream)", "DESIGN 7 (r04ac, r06)"),
     "MSU_MLP_S1": ("1", "0: the stage-1 training MLPs on the GEMM pair (H and GELU(H) stored) instead of the "

@@ -118,6 +118,10 @@ class FlatGroup:
 
     def copy_shadow(self):
         self.shadow.copy_(self.data)
+        self.transpose_shadow()
+
+    def transpose_shadow(self):
+        """The transposed shadow of the 2-D weights from the (refreshed) shadow."""
         if self.tshadow is not None and ops._SHADOW_T:
             ops.transpose16_multi(self.shadow, self.tshadow, self.ttable, self.ntiles)
 
@@ -556,11 +560,14 @@ class Trainer:
                 self.reducer.update_scale(found)
         ops.step_advance_(self.hyper, found)
         for g in self.groups:
+            # the gradient reset and (bf16) the shadow refresh ride in AdamW's pass: no fill and
+            # no re-read of the parameters for the cast (a skipped step leaves the shadow as is
+            # and zeroes the gradient too)
             ops.adamw_dev_(g.data, g.grad, g.exp_avg, g.exp_avg_sq, self.hyper, self.betas[0], self.betas[1],
-                           self.eps, g.weight_decay, inv_scale=inv, found_inf=found)
-            g.grad.zero_()
+                           self.eps, g.weight_decay, inv_scale=inv, found_inf=found,
+                           shadow=g.shadow if bf16 else None, zero_grad=True)
             if bf16:  # keeps evaluation between steps on the updated weights
-                g.copy_shadow()
+                g.transpose_shadow()
         return loss.detach()
 
     GRAPH_HOST_FRACTION = 0.9

@@ -325,6 +325,24 @@ def _conv_ref(x, w, b, d2s, H, W):
     return F.conv2d(x, w, b, padding=1).permute(0, 2, 3, 1)
 
 
+@pytest.mark.parametrize("Cout,Cin", [(96, 96), (5, 40), (33, 7), (192, 224)])
+@pytest.mark.parametrize("dtype", ALL)
+def test_conv_weight_layouts(Cout, Cin, dtype):
+    """msu_conv3x3_weight against the ATen expression it replaces (flip / permute / zero pad to
+    32 / cast), bit-exact, both layouts, ragged widths included."""
+    ops = _ops()
+    w = torch.randn(Cout, Cin, 3, 3, generator=_g(Cout * Cin)).to(DEV)
+
+    def pad32(t):
+        p = (-t.shape[2]) % 32
+        return torch.cat([t, t.new_zeros(t.shape[0], t.shape[1], p)], 2)
+
+    wt = pad32(w.permute(2, 3, 0, 1).reshape(9, Cout, Cin)).to(dtype)
+    wf = pad32(w.flip(2, 3).permute(2, 3, 1, 0).reshape(9, Cin, Cout)).to(dtype)
+    assert torch.equal(ops._conv_weight(w, dtype, 0), wt)
+    assert torch.equal(ops._conv_weight(w, dtype, 1), wf)
+
+
 @pytest.mark.parametrize("B,H,W,C,d2s", CONV_CASES)
 @pytest.mark.parametrize("dtype", ALL)
 def test_refine_conv(B, H, W, C, d2s, dtype):
@@ -660,3 +678,45 @@ def test_window_attention_param_tail_on_side_stream():
         res[direct] = (q.grad.float(), pb.grad.clone(), pt.grad.clone())
     for a, b, what in zip(res[True], res[False], ("dqkv", "dbias", "dtable")):
         torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7, msg=what)
+
+
+@pytest.mark.parametrize("d2s", [False, True])
+def test_conv_tile_queue_equals_static_schedule(d2s):
+    """The refine-conv kernel's device tile queue (msu_conv_mode 1, the default) against the
+    static schedule (mode 0): bit-identical forward (dual) and dgrad at 1024 tiles > one
+    workgroup per CU, over repeated launches (the queue slot resets itself at each launch's
+    end) and on a second stream (its own slot)."""
+    ops = _ops()
+    from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
+    B, H, W, C = 8, 256, 256, 96
+    g = _g(17 + d2s)
+    x = torch.randn((B, H // 4, W // 4, 16 * C) if d2s else (B, H, W, C), generator=g).to(DEV, torch.bfloat16)
+    a = torch.nn.functional.gelu(x.float()).to(torch.bfloat16)
+    w = (torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(DEV)
+    b = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    dz = torch.randn(B, H, W, C, generator=g).to(DEV, torch.bfloat16)
+
+    def run():
+        xg = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            z, z2 = ops.refine_conv_act(xg, a, w, b, d2s, (H, W), dual=True)
+        (dx,) = torch.autograd.grad(z, (xg,), dz)
+        return z, z2, dx
+
+    L = _lib.lib()
+    prev = L.msu_conv_mode(0)
+    try:
+        ref = run()
+        L.msu_conv_mode(1)
+        outs = [run() for _ in range(3)]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            outs.append(run())
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+    finally:
+        L.msu_conv_mode(prev)
+    for o in outs:
+        for u, r, name in zip(o, ref, ("z", "gelu(z)", "dx")):
+            assert torch.equal(u, r), name

@@ -186,3 +186,30 @@ def test_adamw_dev_skip_matches_torch_adamw():
     torch.testing.assert_close(p.cpu(), ref.detach(), rtol=4e-7, atol=1e-8)
     torch.testing.assert_close(m.cpu(), opt.state[ref]["exp_avg"], rtol=4e-7, atol=2e-8)
     torch.testing.assert_close(v.cpu(), opt.state[ref]["exp_avg_sq"], rtol=4e-7, atol=1e-12)
+
+
+@pytest.mark.parametrize("sdt", [torch.bfloat16, torch.float16, None], ids=["bf16", "f16", "noshadow"])
+def test_adamw_dev2_equals_adamw_zero_and_cast(sdt):
+    """msu_adamw_dev2 (the trainer's optimizer pass): bitwise msu_adamw_dev, then the gradient
+    zeroed and the 16-bit shadow cast from the updated parameters -- the three launches it
+    replaces; a skipped step (found_inf) still zeroes the gradient and leaves parameters and
+    shadow as they were."""
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    g = torch.Generator().manual_seed(3)
+    n = 100003
+    p0 = torch.randn(n, generator=g).to(DEV)
+    m0, v0 = (0.1 * torch.randn(n, generator=g)).to(DEV), torch.rand(n, generator=g).to(DEV)
+    g0 = torch.randn(n, generator=g).to(DEV)
+    for skip in (False, True):
+        hyper = torch.tensor([1e-3, 5.0], device=DEV, dtype=torch.float64)
+        found = torch.tensor([1.0 if skip else 0.0], device=DEV)
+        pa, ma, va, ga = p0.clone(), m0.clone(), v0.clone(), g0.clone()
+        ops.adamw_dev_(pa, ga, ma, va, hyper, 0.9, 0.999, 1e-8, 0.05, found_inf=found)
+        pb, mb, vb, gb = p0.clone(), m0.clone(), v0.clone(), g0.clone()
+        sh = p0.to(sdt) if sdt is not None else None
+        ops.adamw_dev_(pb, gb, mb, vb, hyper, 0.9, 0.999, 1e-8, 0.05, found_inf=found, shadow=sh, zero_grad=True)
+        torch.cuda.synchronize()
+        assert torch.equal(pa, pb) and torch.equal(ma, mb) and torch.equal(va, vb)
+        assert torch.count_nonzero(gb).item() == 0
+        if sdt is not None:
+            assert torch.equal(sh, pb.to(sdt))
