@@ -212,8 +212,10 @@ int msu_nt_gemm_supported(long M, int N, int K);
 /* Tile msu_nt_gemm picks for an M x N output (rows * 1000 + columns; 128/256 x 128/192/256),
  * + 1000000 when the ping-pong kernel (gemm_pp.h) takes it. */
 int msu_nt_gemm_plan(long M, int N);
-/* 1: the ping-pong kernel where the shape tiles exactly; 0 (default): the persistent 2-barrier
- * kernel everywhere (A/B switch MSU_NT_PP).  Returns the previous mode. */
+/* bit 0: the ping-pong kernel where the shape tiles exactly (default off: the persistent
+ * 2-barrier kernel everywhere; A/B switch MSU_NT_PP); bits 1-2: a forced tile form (timing
+ * tools); bit 3: the 256 x 192 A3W2 ring; bit 4: the two-stage kernel claims its tiles from a
+ * per-XCD device queue (opt-in MSU_NT_DYN=1: measured slower).  Returns the previous mode. */
 int msu_nt_gemm_mode(int mode);
 int msu_nt_gemm(int dtype, const void* A, const void* W, const float* bias, void* Y, void* Y2, const void* H,
                 long M, int N, int K, int epi, void* stream);

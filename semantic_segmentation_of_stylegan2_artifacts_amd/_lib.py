@@ -108,7 +108,7 @@ def lib():
         fn.restype = res
         fn.argtypes = args
     # the library-side A/B switches (the C code reads no environment; switches.py does)
-    h.msu_nt_gemm_mode(1 if switches.on("MSU_NT_PP") else 0)
+    h.msu_nt_gemm_mode((1 if switches.on("MSU_NT_PP") else 0) | (16 if switches.on("MSU_NT_DYN") else 0))
     h.msu_tail_reduce_mode(1 if switches.on("MSU_TAIL") else 0)
     h.msu_conv_mode(1 if switches.on("MSU_CONV_DYN") else 0)
     _lib = h

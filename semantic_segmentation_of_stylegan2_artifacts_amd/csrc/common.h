@@ -9,6 +9,8 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #define MSU_DEV __device__ __forceinline__
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -283,6 +285,49 @@ __device__ __attribute__((aligned(16))) uint32_t g_zero_region[1024];
 MSU_DEV const void* zero_src(int slot) { return g_zero_region + 4 * (slot & 255); }
 
 #define MSU_CHECK_LAUNCH() (hipGetLastError() == hipSuccess ? 0 : -1)
+
+// ------------------------------------------------------------------ tile queues
+// Persistent kernels beside the side stream: a workgroup takes its first
+// tile statically and claims the others from a device counter, so workgroups that get a CU late
+// (the side stream's weight-gradient kernels hold whole CUs) take fewer tiles instead of running
+// a fixed share past the others' end.  A slot = 8 claim counters (one per XCD, for kernels
+// that keep each XCD on its own tile range; others use counter 0) and a finished-workgroup
+// count, each on its own 128-B line; the launch's last workgroup resets the slot (no memset
+// launch; graph-replay safe).  One slot per stream and translation unit.
+namespace {
+constexpr int TQ_SLOTS = 16, TQ_LINE = 32, TQ_DONE = 8 * TQ_LINE, TQ_INTS = 9 * TQ_LINE;
+__device__ int g_tile_queue[TQ_SLOTS * TQ_INTS];
+
+// claim k = 0, 1, ... of counter `line` (atomicInc: the add form goes through the atomic
+// optimizer, whose lane arithmetic on the result makes the wave wait for it at once)
+MSU_DEV int tq_claim(int* tq, int line) { return (int)atomicInc((unsigned*)tq + TQ_LINE * line, 0xffffffffu); }
+
+// thread 0 of every workgroup once at its end: the last one out resets the slot
+MSU_DEV void tq_finish(int* tq) {
+  if (tq != nullptr && threadIdx.x == 0 && atomicInc((unsigned*)tq + TQ_DONE, 0xffffffffu) == gridDim.x - 1) {
+#pragma unroll
+    for (int i = 0; i <= 8; ++i) atomicExch(tq + TQ_LINE * i, 0);
+  }
+}
+
+// the queue slot of stream `st`, or nullptr (the static schedule: more streams than slots)
+inline int* tile_queue(hipStream_t st) {
+  static std::mutex mu;
+  static int* base = nullptr;
+  static hipStream_t owner[TQ_SLOTS];
+  static int used = 0;
+  std::lock_guard<std::mutex> lock(mu);
+  if (base == nullptr && hipGetSymbolAddress((void**)&base, HIP_SYMBOL(g_tile_queue)) != hipSuccess) {
+    base = nullptr;
+    return nullptr;
+  }
+  for (int i = 0; i < used; ++i)
+    if (owner[i] == st) return base + TQ_INTS * i;
+  if (used == TQ_SLOTS) return nullptr;
+  owner[used] = st;
+  return base + TQ_INTS * used++;
+}
+}  // namespace
 
 // Run a statement with T bound to the storage type of `dtype` (f32 / bf16 / f16).
 #define MSU_DISPATCH(dtype, T, ...)          \

@@ -13,7 +13,6 @@
 // with ds_read_b64_tr_b16 (bf16) and writes deterministic per-block partials.
 #pragma once
 #include <cstdlib>
-#include <mutex>
 #include <utility>
 
 #include "common.h"
@@ -541,17 +540,9 @@ template <bool M16> MSU_DEV int swzv(int p) { return M16 ? (p >> 1) & 3 : (p >> 
 // where the wait for tap 3's weights also waited for the whole 117 KB halo.
 MSU_DEV constexpr int halo_part_lo(int t, int nhc) { return (t - 1) * nhc / 7; }  // t = 1..7
 
-// Tile queue of the persistent conv3x3_v3_kernel: a workgroup takes its
-// first tile statically (blockIdx.x) and claims every further tile from a device counter, one
-// tile ahead (the next tile's halo and weight prefetch need its index from tap 1 on), so the
-// workgroups that get a CU late -- beside the side stream's weight-gradient kernels, which hold
-// whole CUs -- take fewer tiles instead of running a fixed share past the others' end.  Slot:
-// {claim counter, finished workgroups} on a 128-B line per stream; the last workgroup to finish
-// resets both (no memset launch, graph-replay safe).  Results do not depend on which workgroup
-// computes a tile.
-constexpr int TQ_SLOTS = 16;
-__device__ int g_tile_queue[TQ_SLOTS * 32];
-
+// Tile queue (tq, common.h): a workgroup takes its first tile statically (blockIdx.x) and claims
+// every further one from counter 0, one tile ahead (the next tile's halo and weight prefetch
+// need its index from tap 1 on).  Results do not depend on which workgroup computes a tile.
 template <typename T, bool IN_D2S, bool OUT_D2S, bool OUT_GGRAD, bool BIAS, bool DUAL, bool SPREAD, bool M16>
 __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restrict__ X,
                                                          const bf16_t* __restrict__ Wt,
@@ -656,13 +647,8 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
   // DMA wave-instructions this wave issues per tap (wave-uniform)
   const int my_wdma = (WINS - wave + NW - 1) / NW;
 
-  // tq: claims count up from 0 (tile gridDim.x + count); the last workgroup out resets the slot
-  auto finish = [&]() {
-    if (tq != nullptr && tid == 0 && atomicInc((unsigned*)tq + 1, 0xffffffffu) == gridDim.x - 1) {
-      atomicExch(tq, 0);
-      atomicExch(tq + 1, 0);
-    }
-  };
+  // tq: claims count up from 0 (tile gridDim.x + count)
+  auto finish = [&]() { tq_finish(tq); };
   // the tile thread 0 left in sQ (after a barrier); untracked read: a compiler-visible ds_read
   // would wait for the weight DMA and output stores in flight here (vmcnt(0))
   auto read_q = [&]() -> int {
@@ -675,7 +661,7 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
     finish();
     return;
   }
-  if (tq != nullptr && tid == 0) sQ[0] = (int)atomicInc((unsigned*)tq, 0xffffffffu);
+  if (tq != nullptr && tid == 0) sQ[0] = tq_claim(tq, 0);
   if constexpr (BIAS) {
     if (tid < C) sB[tid] = bias[tid];  // read by every epilogue from LDS (no global load there)
   }
@@ -765,9 +751,8 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
       } else if constexpr (tap == 1) {
         // claim the tile after next (thread 0); older than W(2)'s DMA, so tap 2's counted wait
         // covers it
-        // (atomicInc: the add form goes through the atomic optimizer, whose lane arithmetic
-        // on the result waits for it at once; the raw count is offset by gridDim.x on read)
-        if (tq != nullptr && tid == 0 && next < ntiles) nn = (int)atomicInc((unsigned*)tq, 0xffffffffu);
+        // (the raw count; offset by gridDim.x on read)
+        if (tq != nullptr && tid == 0 && next < ntiles) nn = tq_claim(tq, 0);
         dma_w(2, wbuf ^ 1);
       } else if constexpr (tap == 2) {
         // the claim to sQ: every wave read this tile's entry before tap 0's barrier, the next
@@ -1411,26 +1396,6 @@ int launch_conv(const ConvGeom& g, const T* X, const T* Wt, const float* bias, c
 // from the per-stream queue slot instead of the static blockIdx.x + k * gridDim.x schedule
 int g_conv_dyn = 1;
 
-// the queue slot of stream `st` (nullptr: the static schedule -- queue off, or more streams
-// than slots)
-int* tile_queue(hipStream_t st) {
-  if (!g_conv_dyn) return nullptr;
-  static std::mutex mu;
-  static int* base = nullptr;
-  static hipStream_t owner[TQ_SLOTS];
-  static int used = 0;
-  std::lock_guard<std::mutex> lock(mu);
-  if (base == nullptr && hipGetSymbolAddress((void**)&base, HIP_SYMBOL(g_tile_queue)) != hipSuccess) {
-    base = nullptr;
-    return nullptr;
-  }
-  for (int i = 0; i < used; ++i)
-    if (owner[i] == st) return base + 32 * i;
-  if (used == TQ_SLOTS) return nullptr;
-  owner[used] = st;
-  return base + 32 * used++;
-}
-
 int num_cus() {
   static int n = 0;
   if (n <= 0) {
@@ -1478,7 +1443,8 @@ int launch_v3s(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float
   if (ntiles == 0) return 0;
   if ((long)g.B * g.H * g.W * 96 >= (1L << 31)) return -2;
   const int grid = (int)(ntiles < num_cus() ? ntiles : num_cus());
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, X, Wt, bias, S, Y, Y2, g, (int)ntiles, tile_queue(st));
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, X, Wt, bias, S, Y, Y2, g, (int)ntiles,
+                     g_conv_dyn ? tile_queue(st) : nullptr);
   return MSU_CHECK_LAUNCH();
 }
 

@@ -49,6 +49,7 @@ struct NtArgs {
   const bf16_t* H;     // [M][N] (GELU_GRAD: pre-activation)
   int M, N, K, K1;
   int tiles_m, tiles_n;
+  int* tq;             // tile-queue slot (common.h; the two-stage kernel only) or null: static
 };
 
 // A ROWS x KB operand tile (K-contiguous rows, KB = 64 or 32) staged by NTHR threads.  A 256-B
@@ -178,28 +179,49 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
   const int nk = a.K / KB;  // K % 64 == 0 (nt_shape_ok)
   const int mine = L < ntiles ? (ntiles - 1 - L) / G + 1 : 0;
   const int nsteps = mine * nk;
+  // NST = 2 walks tiles (tcur, then tnext): statically L, L + G, ..., or with the tile queue
+  // claims of this XCD's counter -- the same tiles xcd_remap gives the XCD (first tile x0 +
+  // local, then rounds of qx tiles G apart), in round order, so a row block of A still stays on
+  // one XCD's L2.  The next tile is claimed by thread 0 at a tile's first K step (after its
+  // barrier), published at the second (after that step's vmcnt(0)) through sq[ti & 1] and read
+  // after its barrier -- before the last step issues the next tile's first DMA (nk >= 2: the
+  // launch passes no queue for single-step tiles).
+  int* const tq = NST == 2 ? a.tq : nullptr;
+  const int xcd = blockIdx.x & 7;
+  const int qx = (G >> 3) + (xcd < (G & 7) ? 1 : 0);
+  const int x0 = L - (int)(blockIdx.x >> 3);
+  __shared__ int sq[2];
 
-  // K step s of this workgroup's sequence: its A / W tiles -> LDS at dst
-  auto issue_a = [&](int s, bf16_t* dst) __attribute__((always_inline)) {
-    const int ti = s / nk, kk = s - ti * nk;
-    const int t = L + ti * G;
+  // K step kk of tile t: its A / W tiles -> LDS at dst
+  auto issue_a_t = [&](int t, int kk, bf16_t* dst) __attribute__((always_inline)) {
     const int mt = t / a.tiles_n;
     if (a.A2 == nullptr) TA::stage(a.A, mt * BM, a.M, a.K, kk * KB, dst, tid);
     else if (kk * KB < a.K1) TA::stage(a.A, mt * BM, a.M, a.K1, kk * KB, dst, tid);  // K1 % 64 == 0
     else TA::stage(a.A2, mt * BM, a.M, a.K - a.K1, kk * KB - a.K1, dst, tid);
   };
-  auto issue_w = [&](int s, bf16_t* dst) __attribute__((always_inline)) {
-    const int ti = s / nk, kk = s - ti * nk;
-    const int t = L + ti * G;
+  auto issue_w_t = [&](int t, int kk, bf16_t* dst) __attribute__((always_inline)) {
     const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
     if constexpr (WKN) TK::stage(a.W, nt * BNT, a.N, kk * KB, dst, tid);
     else TW::stage(a.W, nt * BNT, a.N, a.K, kk * KB, dst, tid);
   };
-  // K step s -> ring stage `st` (NST = 2 / 3: A and W in one stage)
-  auto issue = [&](int s, int st) __attribute__((always_inline)) {
+  // K step s of this workgroup's static sequence
+  auto issue_a = [&](int s, bf16_t* dst) __attribute__((always_inline)) {
+    const int ti = s / nk;
+    issue_a_t(L + ti * G, s - ti * nk, dst);
+  };
+  auto issue_w = [&](int s, bf16_t* dst) __attribute__((always_inline)) {
+    const int ti = s / nk;
+    issue_w_t(L + ti * G, s - ti * nk, dst);
+  };
+  // K step kk of tile t -> ring stage `st` (NST = 2 / 3: A and W in one stage)
+  auto issue_tk = [&](int t, int kk, int st) __attribute__((always_inline)) {
     bf16_t* dst = lds + st * STG;
-    issue_a(s, dst);
-    issue_w(s, dst + BM * KB);
+    issue_a_t(t, kk, dst);
+    issue_w_t(t, kk, dst + BM * KB);
+  };
+  auto issue = [&](int s, int st) __attribute__((always_inline)) {
+    const int ti = s / nk;
+    issue_tk(L + ti * G, s - ti * nk, st);
   };
   bf16_t* const ldsW = lds + 3 * BM * KB;  // A3W2: the W stages after the three A stages
 
@@ -222,11 +244,13 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
       if (s < nsteps) issue(s, s);
   }
   int kk = 0, ti = 0;  // K step within the tile, tile ordinal (within this workgroup)
+  int tcur = L, tnext = L + G;  // NST = 2: this tile, the next (tq: known from the tile's 2nd step)
+  int nn = 0;                   // thread 0 (tq): the claim in flight
   int cst = 0;         // LDS stage of step s
   int epi_age = 99;    // steps since the last epilogue (its stores follow that step's DMA issue)
   bool a3_more_a = false;  // A3W2: this step also issued A(s + 2)
   bool epi_full = true;  // that epilogue issued all E stores of this wave (no ragged M / N edge)
-  for (int s = 0; s < nsteps; ++s) {
+  for (int s = 0; NST == 2 ? tcur < ntiles : s < nsteps; ++s) {
     // step s's DMA landed; younger DMAs (step s + 1) and epilogue stores issued after step s's
     // DMA may stay in flight (NST = 3, tiles of >= 3 K steps); else everything retires.
     // The counts must never exceed the ops really issued after step s's DMA: a wave whose last
@@ -245,6 +269,10 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
       else wait_vmcnt<0>();
     } else if constexpr (NST == 2) {
       wait_vmcnt<0>();
+      if (tq != nullptr && kk == 1 && tid == 0) {
+        sq[ti & 1] = nn;  // (nothing in flight here)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // landed before the raw barrier
+      }
     } else if constexpr (NST == 3) {
       const bool younger = s + 1 < nsteps;
       const bool stores = epi_age <= 1 && nk >= 3 && epi_full;
@@ -258,7 +286,16 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     asm volatile("" ::: "memory");  // done reading step s-1's stage (refilled below)
     ++epi_age;
     const bool last = kk + 1 == nk;
-    const int t = L + ti * G;
+    if (NST == 2 && tq != nullptr) {
+      if (kk == 0) {
+        if (tid == 0) nn = tq_claim(tq, xcd);
+      } else if (kk == 1) {
+        // read before this step's DMA issue: no LDS-DMA in flight
+        const int c = __builtin_amdgcn_readfirstlane(sq[ti & 1]);
+        tnext = x0 + G * (1 + c / qx) + c % qx;
+      }
+    }
+    const int t = NST == 2 ? tcur : L + ti * G;
     const int mt = t / a.tiles_n, nt = t - mt * a.tiles_n;
     const int m0 = mt * BM, n0 = nt * BNT;
     const int hh = lane >> 5;
@@ -299,6 +336,12 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
       ta = lds + ast * BM * KB;
       tw = ldsW + wst * BNT * KB;
       cst = cst + 1 == 3 ? 0 : cst + 1;
+    } else if constexpr (NST == 2) {
+      more = !last || tnext < ntiles;
+      if (more) issue_tk(last ? tnext : tcur, last ? 0 : kk + 1, cst ^ 1);
+      ta = lds + cst * STG;
+      tw = ta + BM * KB;
+      cst ^= 1;
     } else {
       more = s + NST - 1 < nsteps;
       if (more) issue(s + NST - 1, cst == 0 ? NST - 1 : cst - 1);
@@ -338,6 +381,10 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
     }
     kk = 0;
     ++ti;
+    if constexpr (NST == 2) {
+      tcur = tnext;
+      tnext = tcur + G;  // (static; tq: replaced at the next tile's first step)
+    }
     epi_age = 0;
     epi_full = m0 + 64 * wm + 64 <= a.M && n0 + WNC * wn + WNC <= a.N;
     // the epilogue operands (and every older DMA) have landed; the DMA just issued may stay
@@ -409,6 +456,7 @@ __global__ void __launch_bounds__(128 * WM) gemm_nt_kernel(NtArgs a) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{0};
   }
+  tq_finish(tq);
 }
 
 }  // namespace
@@ -426,6 +474,9 @@ int g_nt_pp = 0;
 int g_nt_force = 0;
 // msu_nt_gemm_mode bit 3: the 256 x 192 tile on the A3W2 ring (gemm_nt_kernel NST = 4)
 int g_nt_a3 = 0;
+// msu_nt_gemm_mode bit 4: the two-stage kernel's tile queue (opt-in MSU_NT_DYN=1: the claim's
+// round trip costs 2-3 us on the short stage-2/3 launches and the step did not gain, r06q/r06r)
+int g_nt_dyn = 0;
 
 int num_cus_nt();
 
@@ -509,10 +560,12 @@ void launch_nt(int epi, const NtArgs& a, hipStream_t st) {
   const long cap = (long)num_cus_nt() * (WM == 2 ? 2 : 1);
   const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
   const dim3 blk(128 * WM);
+  NtArgs q = a;
+  q.tq = NST == 2 && g_nt_dyn && a.K >= 2 * KB ? tile_queue(st) : nullptr;
   switch (epi) {
-    case EPI_PLAIN: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_PLAIN, WM, NST, WKN, BNT, KB>), dim3(grid), blk, 0, st, a); break;
-    case EPI_GELU_DUAL: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_DUAL, WM, NST, WKN, BNT, KB>), dim3(grid), blk, 0, st, a); break;
-    default: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_GRAD, WM, NST, WKN, BNT, KB>), dim3(grid), blk, 0, st, a); break;
+    case EPI_PLAIN: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_PLAIN, WM, NST, WKN, BNT, KB>), dim3(grid), blk, 0, st, q); break;
+    case EPI_GELU_DUAL: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_DUAL, WM, NST, WKN, BNT, KB>), dim3(grid), blk, 0, st, q); break;
+    default: hipLaunchKernelGGL((gemm_nt_kernel<T, EPI_GELU_GRAD, WM, NST, WKN, BNT, KB>), dim3(grid), blk, 0, st, q); break;
   }
 }
 
@@ -524,6 +577,7 @@ int nt_launch(int dtype, const void* A, const void* W, const float* bias, void* 
   if (epi == EPI_GELU_GRAD && (H == nullptr || bias != nullptr)) return -3;
   if (epi < 0 || epi > 2) return -3;
   NtArgs a;
+  a.tq = nullptr;
   if (A2 != nullptr && (wkn || epi != EPI_PLAIN || K1 <= 0 || K1 >= K || K1 % 64)) return -3;
   a.A = (const bf16_t*)A;
   a.A2 = (const bf16_t*)A2;
@@ -588,10 +642,11 @@ int msu_nt_gemm_plan(long M, int N) {
 // (0: the cost model; 1: 128 x 192, 2: 256 x 128, 3: 128 x 128); bit 3: the 256 x 192 tile on the
 // A3W2 ring (A two K steps ahead).  Returns the previous mode.
 int msu_nt_gemm_mode(int mode) {
-  const int prev = g_nt_pp | (g_nt_force << 1) | (g_nt_a3 << 3);
+  const int prev = g_nt_pp | (g_nt_force << 1) | (g_nt_a3 << 3) | (g_nt_dyn << 4);
   g_nt_pp = mode & 1;
   g_nt_force = (mode >> 1) & 3;
   g_nt_a3 = (mode >> 3) & 1;
+  g_nt_dyn = (mode >> 4) & 1;
   return prev;
 }
 

@@ -37,6 +37,8 @@ SWITCHES = {
                       "the fused kernel storing H only", "DESIGN 7 (r05ao)"),
     "MSU_CONV_WGRAD_AT": ("0", "C > 0: the refine-conv side-stream weight gradients held back to the first LayerNorm "
                           "backward of width >= C (0: issued beside the refine dgrads)", "DESIGN 7 (r06)"),
+    "MSU_NT_DYN": ("0", "1: the NT GEMM's two-stage kernel claims tiles from a per-XCD device queue (measured "
+                   "-0.3 % step, 1.8 % slower standalone: r06q/r06r)", "DESIGN 7 (r06)"),
     "MSU_CONV_DYN": ("1", "0: the refine-conv kernel's static tile schedule (blockIdx.x + k * gridDim.x) instead "
                      "of the device tile queue", "DESIGN 7 (r06)"),
     "MSU_CONV_WGRAD_BLOCKS": ("256", "persistent workgroups of the refine-conv weight gradient (one per CU by "

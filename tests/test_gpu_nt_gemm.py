@@ -29,11 +29,12 @@ def _ops():
     return ops
 
 
-@pytest.fixture(params=[1, 0, 8], ids=["pingpong", "persistent", "a3w2"], autouse=True)
+@pytest.fixture(params=[17, 16, 0, 8], ids=["pingpong", "persistent", "static", "a3w2"], autouse=True)
 def nt_mode(request):
     """Every test runs with each NT kernel form: the ping-pong one (gemm_pp.h, MSU_NT_PP=1 where the
-    shape tiles exactly), the persistent 2-barrier one, and the persistent kernel's 256 x 192 tile
-    on the A3W2 ring (msu_nt_gemm_mode bit 3: A two K steps ahead)."""
+    shape tiles exactly), the persistent 2-barrier one with its per-XCD tile queue (bit 4, the
+    default) and with the static schedule, and the persistent kernel's 256 x 192 tile on the A3W2
+    ring (msu_nt_gemm_mode bit 3: A two K steps ahead)."""
     from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
     prev = _lib.lib().msu_nt_gemm_mode(request.param)
     yield request.param
@@ -128,7 +129,7 @@ def test_nt_gemm_wide_tile_is_chosen_and_exact(M, N, K, nt_mode):
     ops = _ops()
     wm, bn, pp = _lib.plan_nt(M, N)
     assert bn == 192, (M, N, wm, bn)
-    assert pp == (nt_mode == 1 and M % 256 == 0), (M, N, pp)
+    assert pp == (bool(nt_mode & 1) and M % 256 == 0), (M, N, pp)
     a, w, b = _inputs(M, N, K, 11 * M + N, torch.bfloat16)
     y = ops.nt_gemm(a, w, b)
     _check(y, F.linear(a.float(), w.float(), b), "y")
@@ -159,7 +160,7 @@ def test_nt_gemm_production_shapes(M, N, K, nt_mode, low):
     from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
     ops = _ops()
     _, bn, pp = _lib.plan_nt(M, N)
-    if nt_mode == 1:
+    if nt_mode & 1:
         assert pp, (M, N)
     a, w, b = _inputs(M, N, K, 13 * M + N + K, low)
     y = ops.nt_gemm(a, w, b)
@@ -232,3 +233,37 @@ def test_linear_routes_stage_shapes_to_nt_and_matches(M, N, K, monkeypatch):
     gw = wg.grad.float().cpu()
     wref = dy.bfloat16().float().t() @ xr.detach()
     assert ((gw - wref).norm() / wref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(32768, 384, 384), (131072, 576, 192), (32000 + 77, 384, 192), (8192, 2304, 768)])
+def test_tile_queue_equals_static(M, N, K, nt_mode):
+    """The two-stage kernel's per-XCD tile queue against its static schedule: bit-identical
+    outputs (plain, GELU dual, GELU' epilogues) over repeated launches (the slot resets itself)
+    and on a second stream (its own slot).  Grids of 256 (or 512) workgroups over >= 2 tiles each."""
+    if nt_mode != 16:
+        pytest.skip("queue vs static: one run")
+    from semantic_segmentation_of_stylegan2_artifacts_amd import _lib
+    ops = _ops()
+    a, w, b = _inputs(M, N, K, M + N, torch.bfloat16)
+    h = torch.randn(M, N, generator=torch.Generator().manual_seed(5)).to(DEV, torch.bfloat16)
+
+    def run():
+        return (ops.nt_gemm(a, w, b, 0), ops.nt_gemm(a, w, b, 1), ops.nt_gemm(a, w, None, 2, h=h))
+
+    L = _lib.lib()
+    L.msu_nt_gemm_mode(0)
+    ref = run()
+    L.msu_nt_gemm_mode(16)
+    outs = [run() for _ in range(3)]
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        outs.append(run())
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    def flat(o):
+        return [o[0], *o[1], o[2]]  # y (plain), (H, GELU(H)) (dual), y (GELU')
+
+    for o in outs:
+        for u, r in zip(flat(o), flat(ref)):
+            assert torch.equal(u, r)

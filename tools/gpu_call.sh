@@ -41,6 +41,12 @@ for s in "$@"; do
       done
       python3 $R/tools/ab_table.py $O/${TAG}_nt_a3.log F0A0 F0A1
       step nt_a3_tests 600 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py ;;
+    nt_dyn)
+      # NT GEMM kernel times per shape: the tile queue (default) vs MSU_NT_DYN=0, interleaved twice
+      for E in 1 0 1 0; do
+        MSU_NT_DYN=$E timeout -k 10 200 python -u $R/tools/nt_shapes.py 20 dyn$E >> $O/${TAG}_nt_dyn.log 2>&1 || exit 3
+      done
+      python3 $R/tools/ab_table.py $O/${TAG}_nt_dyn.log dyn1 dyn0 ;;
     nt_force)
       # NT GEMM kernel times per shape under each forced tile form (tools/nt_shapes.py NT_FORCE)
       for F in 0 1 2 3 0 1; do

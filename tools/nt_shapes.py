@@ -26,7 +26,7 @@ if force or a3 >= 0:
     from semantic_segmentation_of_stylegan2_artifacts_amd import _lib  # noqa: E402
     prev = _lib.lib().msu_nt_gemm_mode(0)
     a3 = (prev >> 3) & 1 if a3 < 0 else a3
-    _lib.lib().msu_nt_gemm_mode((force << 1) | (a3 << 3))
+    _lib.lib().msu_nt_gemm_mode((prev & 17) | (force << 1) | (a3 << 3))
     tag = f"F{force}A{a3}"
 tot = 0.0
 for M, N, K, epi, kn in SHAPES:
