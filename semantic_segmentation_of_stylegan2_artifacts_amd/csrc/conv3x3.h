@@ -1215,7 +1215,9 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
           const int y = y0 + dp / TWV, x = x0 + dp % TWV;
           if (y < g.H && x < g.W) src = DY + pix_off32<false>(b, y, x, g.H, g.W, C) + ch * 8;
         }
-        __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(lds + buf * BUF + 64 * 8 * k), 16, 0, 0);
+        // ablation 4096: no DMA (the LDS images stay stale; results wrong)
+        if constexpr (!(MSU_EXP & 4096))
+          __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)(lds + buf * BUF + 64 * 8 * k), 16, 0, 0);
       }
     }
   };
@@ -1260,8 +1262,8 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
     const bf16_t* sD = sX + HPIX * PS;
     // All LDS reads of the tile are untracked (inline asm): a compiler-visible ds_read would
     // be preceded by vmcnt(0) for the next tile's pending LDS-DMA and serialise the two.
-    // bias gradient: 16 groups x 48 channel pairs, 8 pixels each
-    {
+    // bias gradient: 16 groups x 48 channel pairs, 8 pixels each (ablation 65536: none)
+    if constexpr (!(MSU_EXP & 65536)) {
       const uint32_t ba = lds_u32(sD + dbg * PS + dbc);
       uint32_t v[DPIX / 16];
       unroll_for<DPIX / 16>([&](auto P) {
@@ -1286,18 +1288,22 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
     unroll_for<TH>([&](auto R) {
       constexpr int r = decltype(R)::value;
       // the dY fragments of row r serve all three dx (read once per row, not once per dx:
-      // 12 instead of 18 fragment reads per 27 MFMAs -- the LDS reads bound this loop)
+      // 12 instead of 18 fragment reads per 27 MFMAs -- the LDS reads bound this loop).
+      // (Reading group g + 1's X fragments before group g's MFMAs measured no faster, r06x:
+      // the loop is bound by its operand traffic, ablations r06w.)
       bf16x8 af[3];
       unroll_for<3>([&](auto I) {
         constexpr int o = 2 * (r * TWV * PS + 16 * decltype(I)::value);
-        af[decltype(I)::value] = tr8_untracked<o, o + 32 * PS>(da);
+        if constexpr (MSU_EXP & 32768) af[decltype(I)::value] = bf16x8{};  // ablation: no fragment reads
+        else af[decltype(I)::value] = tr8_untracked<o, o + 32 * PS>(da);
       });
       unroll_for<3>([&](auto D) {
         constexpr int d = decltype(D)::value;
         bf16x8 bf[3];
         unroll_for<3>([&](auto J) {
           constexpr int o = 2 * ((r * HWD + d) * PS + 16 * decltype(J)::value);
-          bf[decltype(J)::value] = tr8_untracked<o, o + 32 * PS>(xa);
+          if constexpr (MSU_EXP & 32768) bf[decltype(J)::value] = bf16x8{};
+          else bf[decltype(J)::value] = tr8_untracked<o, o + 32 * PS>(xa);
         });
         if constexpr (d == 0)
           lds_wait_tie<0>(bf[0], bf[1], bf[2], af[0], af[1], af[2]);
@@ -1307,7 +1313,8 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
         for (int i = 0; i < 3; ++i)
 #pragma unroll
           for (int j = 0; j < 3; ++j)
-            acc[d][i][j] = Fmt16<T>::mma16(af[i], bf[j], acc[d][i][j]);
+            if constexpr (MSU_EXP & 16384) asm volatile("" ::"v"(af[i]), "v"(bf[j]));  // ablation: no MFMA
+            else acc[d][i][j] = Fmt16<T>::mma16(af[i], bf[j], acc[d][i][j]);
         __builtin_amdgcn_sched_barrier(0);
       });
     });

@@ -1,5 +1,5 @@
 """Run one refine-conv forward shape repeatedly (for rocprofv3 counter passes).
-    python tools/conv_one.py [d2s 0|1] [reps] [bwd]"""
+    python tools/conv_one.py [d2s 0|1] [reps] [fwd|bwd] [act]"""
 import os
 import sys
 
@@ -20,7 +20,8 @@ act = len(sys.argv) > 4 and sys.argv[4] == "act"  # the model's path: activation
 with torch.autocast("cuda", dtype=torch.bfloat16):
     if bwd:
         xq, wq = x.requires_grad_(True), w.requires_grad_(True)
-        z = ops.refine_conv(xq, wq, b, d2s, (H, H))
+        # act: the model's path (activation from the producer; the weight gradient reads it as is)
+        z = ops.refine_conv_act(xq, a, wq, b, d2s, (H, H)) if act else ops.refine_conv(xq, wq, b, d2s, (H, H))
         dz = torch.randn_like(z)
     for _ in range(reps):
         if bwd:

@@ -125,7 +125,8 @@ for s in "$@"; do
       # refine-conv kernel times with ablation builds (tools/build_exp.sh conv3x3 64 128 256 512)
       for X in ${CONV_EXP:-0 64 128 256 512}; do
         L=""; [ $X != 0 ] && L=$R/tools/exp/libmsunet_conv3x3_$X.so
-        for args in "1 6 bwd" "0 6 fwd act"; do
+        IFS=';' read -ra CARGS <<< "${CONV_EXP_ARGS:-1 6 bwd;0 6 fwd act}"
+        for args in "${CARGS[@]}"; do
           d=$O/${TAG}_convexp_${X}_${args// /_}
           MSU_LIB_OVERRIDE=$L timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $d -o p --output-format csv -- python3 $R/tools/conv_one.py $args > /dev/null 2>&1 || exit 3
           python3 $R/tools/kstats.py $d/p_kernel_stats.csv conv3x3 $X >> $O/${TAG}_conv_exp.log
