@@ -49,6 +49,15 @@ int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const 
                       void* db, const float* bscale, long rows_per_sample, float* part,
                       int nparts, float* dgamma, float* dbeta, long rows, int C, int H, int W,
                       int Cin, int accumulate, void* stream);
+/* As msu_layernorm_bwd with up to two more extra gradients (dres2, then dres3; null = none;
+ * only with dres, plain / add modes) summed with dres in f32 before the one rounding of dx: a
+ * stage input's other readers (skip fusion, PatchExpand Linear) hand their input gradients
+ * to its first block's norm1 backward instead of autograd adds (model_parts.py:775-815). */
+int msu_layernorm_bwd3(int dtype, int mode, const void* dy, const void* x, const void* dres,
+                       const void* dres2, const void* dres3, const float* gamma, const float* mean,
+                       const float* rstd, void* dx, void* db, const float* bscale, long rows_per_sample,
+                       float* part, int nparts, float* dgamma, float* dbeta, long rows, int C, int H, int W,
+                       int Cin, int accumulate, void* stream);
 int msu_ln_part_blocks(long rows, int C);
 /* 1 (default): the partial-row reductions of msu_layernorm_bwd / msu_head_bwd run inside the
  * kernel (its last blocks, in a fixed order); 0: a separate column-sum launch after it (A/B switch

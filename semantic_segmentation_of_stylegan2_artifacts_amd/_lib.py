@@ -24,6 +24,7 @@ SIGNATURES = {
     "msu_ln_part_blocks": (I, [L, I]),
     "msu_layernorm_fwd": (I, [I, I, P, P, P, L, P, P, P, P, P, P, L, I, I, I, I, F, P]),
     "msu_layernorm_bwd": (I, [I, I, P, P, P, P, P, P, P, P, P, L, P, I, P, P, L, I, I, I, I, I, P]),
+    "msu_layernorm_bwd3": (I, [I, I, P, P, P, P, P, P, P, P, P, P, P, L, P, I, P, P, L, I, I, I, I, I, P]),
     "msu_reduce_rows": (I, [P, I, I, L, P, I, P]),
     "msu_tail_reduce_mode": (I, [I]),
     "msu_conv_mode": (I, [I]),

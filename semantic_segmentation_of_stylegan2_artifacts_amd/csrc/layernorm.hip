@@ -266,6 +266,10 @@ struct LnBwdArgs {
   int accumulate = 0;
   float* dgamma = nullptr;
   float* dbeta = nullptr;
+  // more extra gradients into s, summed with dres in f32 before the one rounding (only with
+  // dres; the skip-gradient handoff: a stage input's other readers)
+  const void* dres2 = nullptr;
+  const void* dres3 = nullptr;
 };
 
 template <typename T, int MODE, int TPR, int KMAX, bool PFB = true>
@@ -299,7 +303,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
     if (act) load_f32<VW>(a.gamma + ch * VW, gg);
     const long stride = (long)gridDim.x * GPB;
     long r = (long)blockIdx.x * GPB + grp;
-    uint4 qx{}, qd{}, qr{};
+    uint4 qx{}, qd{}, qr{}, qr2{}, qr3{};
     float mu = 0.f, rs = 0.f;
     auto fetch = [&](long rr) __attribute__((always_inline)) {
       mu = a.mean[rr];
@@ -310,12 +314,14 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
         qd = *reinterpret_cast<const uint4*>(DY + rr * (long)a.C + ch * VW);
         if constexpr (HAS_RES) {
           if (a.dres) qr = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dres) + off);
+          if (a.dres2) qr2 = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dres2) + off);
+          if (a.dres3) qr3 = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dres3) + off);
         }
       }
     };
     if (r < a.rows) fetch(r);
     for (; r < a.rows; r += stride) {
-      const uint4 cx = qx, cd = qd, cr = qr;
+      const uint4 cx = qx, cd = qd, cr = qr, cr2 = qr2, cr3 = qr3;
       const float cmu = mu, crs = rs;
       if (r + stride < a.rows) fetch(r + stride);
       float xh[VW], g[VW];
@@ -352,6 +358,16 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
           unpack16<T>(cr, dr);
 #pragma unroll
           for (int e = 0; e < VW; ++e) o[e] = __builtin_fmaf(crs, o[e], dr[e]);
+          if (a.dres2) {
+            unpack16<T>(cr2, dr);
+#pragma unroll
+            for (int e = 0; e < VW; ++e) o[e] += dr[e];
+          }
+          if (a.dres3) {
+            unpack16<T>(cr3, dr);
+#pragma unroll
+            for (int e = 0; e < VW; ++e) o[e] += dr[e];
+          }
         } else {
 #pragma unroll
           for (int e = 0; e < VW; ++e) o[e] *= crs;
@@ -415,6 +431,16 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
         if (res) {
 #pragma unroll
           for (int e = 0; e < VW; ++e) o[e] = __builtin_fmaf(rs, o[e], dr[k][e]);
+          const void* more[2] = {a.dres2, a.dres3};
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            if (more[q]) {
+              float d2[VW];
+              VecW<T>::load(reinterpret_cast<const T*>(more[q]) + off, d2);
+#pragma unroll
+              for (int e = 0; e < VW; ++e) o[e] += d2[e];
+            }
+          }
         } else {
 #pragma unroll
           for (int e = 0; e < VW; ++e) o[e] *= rs;
@@ -933,6 +959,26 @@ int msu_layernorm_bwd(int dtype, int mode, const void* dy, const void* x, const 
                       int Cin, int accumulate, void* stream) {
   LnBwdArgs a{dy, x, dres, gamma, mean, rstd, dx, db, bscale, part, rows, C, H, W, Cin,
               rows_per_sample > 0 ? rows_per_sample : 1};
+  hipStream_t st = (hipStream_t)stream;
+  switch (mode) {
+    case IN_PLAIN: return bwd_dispatch<IN_PLAIN>(dtype, a, dgamma, dbeta, nparts, accumulate, st);
+    case IN_ADD: return bwd_dispatch<IN_ADD>(dtype, a, dgamma, dbeta, nparts, accumulate, st);
+    case IN_MERGE: return bwd_dispatch<IN_MERGE>(dtype, a, dgamma, dbeta, nparts, accumulate, st);
+    case IN_D2S2: return bwd_dispatch<IN_D2S2>(dtype, a, dgamma, dbeta, nparts, accumulate, st);
+  }
+  return -3;
+}
+
+int msu_layernorm_bwd3(int dtype, int mode, const void* dy, const void* x, const void* dres,
+                       const void* dres2, const void* dres3, const float* gamma, const float* mean,
+                       const float* rstd, void* dx, void* db, const float* bscale, long rows_per_sample,
+                       float* part, int nparts, float* dgamma, float* dbeta, long rows, int C, int H, int W,
+                       int Cin, int accumulate, void* stream) {
+  if ((dres2 || dres3) && (!dres || (mode != IN_PLAIN && mode != IN_ADD) || (dres3 && !dres2))) return -3;
+  LnBwdArgs a{dy, x, dres, gamma, mean, rstd, dx, db, bscale, part, rows, C, H, W, Cin,
+              rows_per_sample > 0 ? rows_per_sample : 1};
+  a.dres2 = dres2;
+  a.dres3 = dres3;
   hipStream_t st = (hipStream_t)stream;
   switch (mode) {
     case IN_PLAIN: return bwd_dispatch<IN_PLAIN>(dtype, a, dgamma, dbeta, nparts, accumulate, st);

@@ -186,10 +186,11 @@ class SwinTransformerBlock(nn.Module):
                 if m.bias is not None:
                     nn.init.normal_(m.bias, std=1e-6)
 
-    def forward_fused(self, state):
+    def forward_fused(self, state, hk=0):
         """state: a residual-stream tensor [B, H, W, C] or a pending ``(x, branch, scale)``
-        whose add is fused into this block's norm1.  Returns this block's pending state."""
-        hk = 0
+        whose add is fused into this block's norm1.  Returns this block's pending state.  hk:
+        the handoff key of a plain-tensor state shared with its other readers outside the block
+        (MSUNetSys.forward_features), else 0 (a fresh key pairs norm1 and norm2 only)."""
         if isinstance(state, tuple):
             x, br, sc = state
             x, xn = ops.add_layer_norm(x, br, sc, self.norm1.weight, self.norm1.bias, self.norm1.eps)
@@ -197,7 +198,7 @@ class SwinTransformerBlock(nn.Module):
             # x's two readers (norm1, norm2's residual add) sum their gradients inside norm1's
             # LayerNorm backward (ops.residual_handoff_key), not in an autograd add
             x = state
-            hk = ops.residual_handoff_key()
+            hk = hk or ops.residual_handoff_key()
             xn = ops.layer_norm(x, self.norm1.weight, self.norm1.bias, self.norm1.eps, handoff=hk)
         B = x.shape[0]
         a = self.attn(xn)
@@ -289,16 +290,18 @@ class BasicLayer(nn.Module):
             for i in range(depth)])
         self.downsample = downsample(input_resolution, dim=dim, norm_layer=norm_layer) if downsample is not None else None
 
-    def forward(self, x):
+    def forward(self, x, hk=0):
+        """hk: x's handoff key (its other readers' gradients are added in the first block's
+        norm1 backward; only without checkpointing, see MSUNetSys._key_for)."""
         B, N, C = x.shape
         H, W = self.input_resolution
         assert H * W == N, f"{N=} passt nicht zu {H}x{W}"
         state = x.view(B, H, W, C)
-        for blk in self.blocks:
+        for i, blk in enumerate(self.blocks):
             if self.use_checkpoint and torch.is_grad_enabled():
                 state = torch.utils.checkpoint.checkpoint(blk, materialize(state), use_reentrant=False)
             else:
-                state = blk.forward_fused(state)
+                state = blk.forward_fused(state, hk if i == 0 else 0)
         x = materialize(state)
         if self.downsample is not None:
             x = self.downsample(x)
@@ -348,7 +351,8 @@ class PatchExpand(nn.Module):
         self.expand = nn.Linear(dim, 2 * dim, bias=False) if dim_scale == 2 else nn.Identity()
         self.norm = norm_layer(dim // dim_scale)
 
-    def forward(self, x):
+    def forward(self, x, hk=0):
+        """hk: x's handoff key (the Linear's input gradient goes to the keyed LayerNorm)."""
         if x.dim() == 4:
             B, H, W, C_in = x.shape
         elif x.dim() == 3:
@@ -359,7 +363,7 @@ class PatchExpand(nn.Module):
         else:
             raise ValueError(f"Unexpected dimensionality: x.dim()={x.dim()}")
         x = x.reshape(B, H, W, C_in)
-        x = self.expand(x) if isinstance(self.expand, nn.Identity) else ops.linear(x, self.expand.weight)
+        x = self.expand(x) if isinstance(self.expand, nn.Identity) else ops.linear(x, self.expand.weight, handoff=hk)
         C = x.shape[-1]
         if C % 4 != 0:
             raise ValueError(f"channels C={C} are not divisible by 4 (required for ×2 upsampling).")
@@ -425,26 +429,29 @@ class BasicLayer_up(nn.Module):
             for i in range(depth)])
         self.upsample = PatchExpand(input_resolution, dim=dim, dim_scale=2, norm_layer=norm_layer) if upsample is not None else None
 
-    def forward(self, x):
+    def forward(self, x, hk=0):
+        """hk: as BasicLayer.forward."""
         B, N, C = x.shape
         H, W = self.input_resolution
         assert H * W == N, f"{N=} passt nicht zu {H}x{W}"
         state = x.view(B, H, W, C)
-        for blk in self.blocks:
+        for i, blk in enumerate(self.blocks):
             if self.use_checkpoint and torch.is_grad_enabled():
                 state = torch.utils.checkpoint.checkpoint(blk, materialize(state), use_reentrant=False)
             else:
-                state = blk.forward_fused(state)
+                state = blk.forward_fused(state, hk if i == 0 else 0)
         x = materialize(state)
         if self.upsample is not None:
             x = self.upsample(x)
         return x
 
 
-def _skip_fuse(lin, x, skip):
-    """``torch.cat([x, skip], -1)`` -> ``concat_back_dim[k]`` (model_parts.py:792-793 etc.)."""
+def _skip_fuse(lin, x, skip, hk=0):
+    """``torch.cat([x, skip], -1)`` -> ``concat_back_dim[k]`` (model_parts.py:792-793 etc.);
+    hk: the skip's handoff key."""
     B = x.shape[0]
-    return ops.linear_cat(x.reshape(B, -1, x.shape[-1]), skip.reshape(B, -1, skip.shape[-1]), lin.weight, lin.bias)
+    return ops.linear_cat(x.reshape(B, -1, x.shape[-1]), skip.reshape(B, -1, skip.shape[-1]), lin.weight, lin.bias,
+                          handoff=hk)
 
 
 # ============================================================================ MSUNetSys
@@ -566,56 +573,63 @@ class MSUNetSys(nn.Module):
             mod(x)
         x.record_stream(side)
 
+    @staticmethod
+    def _key_for(layer):
+        """A handoff key for a tensor whose first-block reader is `layer` (a Swin stage): its
+        other readers -- skip fusions, the central decoders' PatchExpand Linears -- hand their
+        input gradients to that block's norm1 backward kernel (ops.residual_handoff_key; 0
+        under checkpointing, where the blocks make their own keys)."""
+        return 0 if layer.use_checkpoint else ops.residual_handoff_key()
+
     def forward_features(self, x):
         """``model_parts.py:775-815``."""
+        x, xd, self._skip_keys = self._forward_features(x)
+        return x, xd
+
+    def _forward_features(self, x):
         x = self.patch_embed(x)
         if self.ape:
             x = x + self.absolute_pos_embed
         x = self.pos_drop(x)
-        xd = []
-        L = self.num_layers
+        xd, xk = [], []  # the skip tensors and their handoff keys
         dead = []  # issued after the stage's own blocks: the main stream is not starved while
         # the host launches a branch nobody reads
         for i, layer in enumerate(self.layers):
-            if i == 1:
-                x2 = x
-                for k, mod in enumerate(self.layers_cent2):
+            kx = self._key_for(layer)  # x's readers: this stage, a central branch, a skip fusion
+            # the central decoders: layers_cent2 before stage 1, layers_cent1 before stage 2, each
+            # ending in a branch the reference discards (model_parts.py:795, :807)
+            for cent, cat0, start in ((self.layers_cent2, 2, 1), (self.layers_cent1, 1, 2)):
+                if i != start:
+                    continue
+                xc = x
+                for k, mod in enumerate(cent):
                     if k == 0:
-                        x2 = mod(x2)
+                        xc = mod(xc, kx)
                     else:
-                        x2 = _skip_fuse(self.concat_back_dim[k + 2], x2, xd[i - k])
-                        xd[i - k] = x2
-                        if k == L - 3:
-                            dead.append((mod, x2))
+                        xc = _skip_fuse(self.concat_back_dim[k + cat0], xc, xd[i - k], xk[i - k])
+                        xd[i - k] = xc
+                        if k == len(cent) - 1:
+                            xk[i - k] = 0  # read by the discarded branch (no gradient) and a skip
+                            dead.append((mod, xc))
                         else:
-                            x2 = mod(x2)
-            if i == 2:
-                x1 = x
-                for k, mod in enumerate(self.layers_cent1):
-                    if k == 0:
-                        x1 = mod(x1)
-                    else:
-                        x1 = _skip_fuse(self.concat_back_dim[k + 1], x1, xd[i - k])
-                        xd[i - k] = x1
-                        if k == L - 2:
-                            dead.append((mod, x1))
-                        else:
-                            x1 = mod(x1)
+                            xk[i - k] = self._key_for(mod)
+                            xc = mod(xc, xk[i - k])
             xd.append(x)
-            x = layer(x)
+            xk.append(kx)
+            x = layer(x, kx)
             for mod, xin in dead:
                 self._run_dead(mod, xin)
             dead.clear()
         x = ops.layer_norm(x, self.norm.weight, self.norm.bias, self.norm.eps)
-        return x, xd
+        return x, xd, xk
 
-    def forward_up_features(self, x, xd):
-        """``model_parts.py:818-829``."""
+    def forward_up_features(self, x, xd, keys=None):
+        """``model_parts.py:818-829``; keys: the skips' handoff keys (forward_features')."""
         for k, layer_up in enumerate(self.layers_up):
             if k == 0:
                 x = layer_up(x)
             else:
-                x = _skip_fuse(self.concat_back_dim[k], x, xd[3 - k])
+                x = _skip_fuse(self.concat_back_dim[k], x, xd[3 - k], keys[3 - k] if keys else 0)
                 x = layer_up(x)
         return ops.layer_norm(x, self.norm_up.weight, self.norm_up.bias, self.norm_up.eps)
 
@@ -639,8 +653,8 @@ class MSUNetSys(nn.Module):
         return ops.linear(y, self.output.weight.reshape(self.num_classes, -1)).permute(0, 3, 1, 2)
 
     def forward(self, x):
-        x, xd = self.forward_features(x)
-        x = self.forward_up_features(x, xd)
+        x, xd, xk = self._forward_features(x)
+        x = self.forward_up_features(x, xd, xk)
         return self.up_x4(x)
 
     def freeze_encoder(self, freeze=True):

@@ -16,6 +16,8 @@ modules in ``network/`` call.  They cast the activation to the autocast dtype an
 registered op.  (A plain ``autograd.Function`` route around the dispatcher measured equal on
 the GPU-bound 1024^2 step, r02c 50.50 vs 50.57 ms: gone.)
 """
+import functools
+
 import torch
 
 from . import _lib, switches
@@ -180,22 +182,55 @@ _side_event_params = []
 # which always runs first (attn(norm1(x)) feeds norm2) -- parks its gradient of x here and
 # returns none for it, and norm1's backward pops it and adds it inside the LayerNorm backward
 # kernel (the add-mode residual-gradient input).  Cleared at the end of every backward.
+# The same key extends to a stage input's other readers (MSUNetSys.forward_features: the skip
+# fusions' skip halves and the central decoders' PatchExpand Linears, model_parts.py:775-829):
+# their backwards, which run before the stage's first block, park their input gradients too
+# (up to three per key: msu_layernorm_bwd3's dres / dres2 / dres3).  A reader whose backward
+# comes after the adder's (key closed) returns its gradient to autograd as usual, so the sum
+# is right in any order.
 _RES_HANDOFF = switches.on("MSU_RES_HANDOFF")
-_res_handoff = {}
+_res_handoff = {}  # key -> parked gradients of the keyed tensor, in park order
+_res_closed = set()  # keys whose adder (the plain LayerNorm) ran in this backward
 _res_keys = iter(range(1, 1 << 62))
-res_handoff_calls = 0  # LayerNorm backwards that took a parked gradient (tests)
+res_handoff_calls = 0  # LayerNorm backwards that took parked gradients (tests)
+res_parked = 0  # gradients parked (tests)
+res_dropped = 0  # parked gradients no adder took (its tensor's gradient was not needed; tests)
 
 
 def residual_handoff_key():
-    """A fresh key pairing a plain layer_norm with the add_layer_norm over the same input, or 0
-    (no pairing: autograd sums the gradients)."""
+    """A fresh key pairing a plain layer_norm with the other readers of its input (the
+    add_layer_norm over it; skip fusions / Linears given the same key), or 0 (no pairing:
+    autograd sums the gradients)."""
     return next(_res_keys) if (_RES_HANDOFF and torch.is_grad_enabled()) else 0
 
 
+def _park(key, g):
+    """A reader's gradient of the keyed tensor, handed to the adder; False when there is no key
+    or the adder already ran (the caller returns g to autograd)."""
+    global res_parked
+    if not key or key in _res_closed:
+        return False
+    _res_handoff.setdefault(key, []).append(g)
+    res_parked += 1
+    _join_at_end_of_backward()  # clears the mailbox at the end of this backward
+    return True
+
+
+def _take(key):
+    """The adder's side: the parked gradients of key (and the key closed)."""
+    if not key:
+        return []
+    _res_closed.add(key)
+    _join_at_end_of_backward()
+    return _res_handoff.pop(key, [])
+
+
 def _end_of_backward():
-    global _join_queued
+    global _join_queued, res_dropped
     _join_queued = False
+    res_dropped += sum(len(v) for v in _res_handoff.values())
     _res_handoff.clear()
+    _res_closed.clear()
     _flush_deferred()  # anything still held back runs now, before the join
     join_side_streams()
     _side_keep.clear()  # the main stream now waits for every side-stream read
@@ -276,19 +311,26 @@ def _ln_backward(ctx, dy, _dm, _dr):
     global res_handoff_calls
     x, w, mean, rstd = ctx.saved_tensors
     _flush_deferred(x.shape[-1])
-    res = _res_handoff.pop(ctx.handoff, None) if ctx.handoff else None  # the paired add-LN's dx
+    res = _take(ctx.handoff)  # the other readers' gradients of x (the paired add-LN's first)
     if dy is None:
-        return res, None, None, None, None
+        return (functools.reduce(torch.add, res) if res else None), None, None, None, None
     dy = _as(dy, x.dtype)
     C = x.shape[-1]
     rows = x.numel() // C
     dx = torch.empty_like(x)
     dw, db, acc, direct = _ln_grads(ctx, C, x.device)
     n, part = _ln_parts(rows, C, x.device)
-    if res is not None:
-        # the add-mode backward: dx = LN'(dy) + res in one pass (no branch output: scale null)
+    if res:
+        # the add-mode backward: dx = LN'(dy) + res (+ res2 + res3) in one pass, one rounding
+        # (no branch output: scale null; a fourth reader's gradient, not on the model's path, is
+        # folded in by an add first)
+        res = [_as(r, x.dtype).contiguous() for r in res]
+        if len(res) > 3:
+            res = res[:2] + [functools.reduce(torch.add, res[2:])]
         res_handoff_calls += 1
-        _lib.call("msu_layernorm_bwd", _dt(x), IN_ADD, _p(dy), _p(x), _p(_as(res, x.dtype).contiguous()), _p(w),
+        r2 = res[1] if len(res) > 1 else None
+        r3 = res[2] if len(res) > 2 else None
+        _lib.call("msu_layernorm_bwd3", _dt(x), IN_ADD, _p(dy), _p(x), _p(res[0]), _p(r2), _p(r3), _p(w),
                   _p(mean), _p(rstd), _p(dx), None, None, rows // x.shape[0], _p(part), n, _p(dw), _p(db), rows, C,
                   0, 0, 0, acc, _s(x))
     else:
@@ -362,11 +404,9 @@ def _add_ln_backward(ctx, ds, dy, _dm, _dr):
         _notify(*ctx.affine)
         dw = dbb = None
     dbr = dbr if dbr is not None else da
-    if ctx.handoff:
+    if _park(ctx.handoff, da):
         # a's other reader is the paired plain LayerNorm, whose backward runs later and adds da
-        # in its kernel: park it, autograd sees no gradient for a here
-        _res_handoff[ctx.handoff] = da
-        _join_at_end_of_backward()  # clears the mailbox at the end of this backward
+        # in its kernel: autograd sees no gradient for a here
         return None, dbr, None, dw, dbb, None, None
     return da, dbr, None, dw, dbb, None, None
 
@@ -728,7 +768,7 @@ def _attn_qkv_backward(ctx, dy, _do, _dqkv, _dkeep, _dws=None):
     if wp is not None:
         # proj Linear first: do = dy . W_proj, dW_proj / db_proj from (dy, o)
         pctx = _Ctx((o,), params=(wp, bp), needs_input_grad=(True, ctx.needs_input_grad[4], ctx.needs_input_grad[5]))
-        dout, dwp, dbp = _linear_backward(pctx, dy)
+        dout, dwp, dbp = _linear_grads(pctx, dy)
     else:
         dout = dy
     actx = _Ctx((qkv, bias, table, seed_dev, keep), cfg=ctx.cfg, bias_param=ctx.bias_param,
@@ -736,7 +776,7 @@ def _attn_qkv_backward(ctx, dy, _do, _dqkv, _dkeep, _dws=None):
     dqkv, dbias_pad, dtable = _attn_backward(actx, dout, None)[:3]
     lctx = _Ctx((x,), params=(weight, bias),
                 needs_input_grad=(ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]))
-    dx, dw, db = _linear_backward(lctx, dqkv)
+    dx, dw, db = _linear_grads(lctx, dqkv)
     if db is not None and dbias_pad is not None:
         db = db + dbias_pad
     elif dbias_pad is not None:
@@ -1007,7 +1047,7 @@ def _mm(a, w, bias=None):
 
 
 # ----------------------------------------------------------------------------- Linear
-def _linear_impl(x, weight, bias):
+def _linear_impl(x, weight, bias, handoff=0):
     """Y = x . W^T + b in x's dtype; the f32 master weight / bias are cast inside the op so
     that the parameter gradients are the f32 ones of the weight-gradient kernel."""
     _need_cuda(x)
@@ -1022,14 +1062,15 @@ def _linear_impl(x, weight, bias):
         return torch.nn.functional.linear(x, w, b)
 
 
-def _linear_fake(x, weight, bias):
+def _linear_fake(x, weight, bias, handoff=0):
     return x.new_empty(*x.shape[:-1], weight.shape[0])
 
 
 def _linear_setup(ctx, inputs, output):
-    x, weight, bias = inputs
+    x, weight, bias = inputs[:3]
     ctx.save_for_backward(x)
     ctx.params = (weight, bias)
+    ctx.handoff = inputs[3] if len(inputs) > 3 else 0
 
 
 # One-pass Linear backward (csrc/gemm_linbwd.hip) for the stage-0 block Linears: dX, dW and db
@@ -1075,9 +1116,12 @@ def _linbwd(dy, x, weight, bias, M, N, K, h=None, gelu_x=False):
     return dx
 
 
-def _linear_backward(ctx, dy):
+def _linear_grads(ctx, dy):
+    """(dx, dW, db) of a Linear; dx is None when it went to x's keyed LayerNorm (ctx.handoff,
+    absent on the hand-made contexts of the fused units' backwards)."""
     (x,) = ctx.saved_tensors
     weight, bias = ctx.params
+    key = getattr(ctx, "handoff", 0)
     w = _shadow(weight, x.dtype)
     dy = _as(dy, x.dtype)
     N, K = w.shape
@@ -1085,7 +1129,7 @@ def _linear_backward(ctx, dy):
     if ctx.needs_input_grad[0]:
         dx = _linbwd(dy.contiguous(), x, weight, bias, M, N, K)
         if dx is not None:
-            return dx, None, None
+            return (None if _park(key, dx) else dx), None, None
     dx = None
     if ctx.needs_input_grad[0]:
         if x.dtype in _LOW and gemm_route(M, K, N) != "lib":
@@ -1093,26 +1137,34 @@ def _linear_backward(ctx, dy):
         else:
             with torch.autocast("cuda", enabled=False):
                 dx = dy.matmul(w)
+    if dx is not None and _park(key, dx):
+        dx = None  # x's gradient goes to its keyed LayerNorm's backward kernel
     if not (ctx.needs_input_grad[1] or (bias is not None and ctx.needs_input_grad[2])):
         return dx, None, None  # frozen weight and bias: no weight-gradient work at all
     dw, db = _wgrad(dy, x, weight, bias, M, N, K)
     return dx, dw, db
 
 
-_linear = _define("linear", "(Tensor x, Tensor weight, Tensor? bias) -> Tensor",
+def _linear_backward(ctx, dy):
+    return (*_linear_grads(ctx, dy), None)
+
+
+_linear = _define("linear", "(Tensor x, Tensor weight, Tensor? bias, int handoff=0) -> Tensor",
                   _linear_impl, _linear_fake, _linear_setup, _linear_backward)
 
 
-def linear(x, weight, bias=None):
+def linear(x, weight, bias=None, handoff=0):
     """nn.functional.linear with the HIP weight-gradient kernel (activation dtype per autocast);
-    16-bit forward / input-gradient GEMMs on the token GEMM where it covers the shape."""
+    16-bit forward / input-gradient GEMMs on the token GEMM where it covers the shape.
+    handoff: a ``residual_handoff_key()`` of x (its gradient is added in the keyed LayerNorm's
+    backward kernel)."""
     _need_cuda(x)
     dt = act_dtype()
     x = _as(x, dt)
     N, K = weight.shape
     if K % 8 or N % 8:
         return torch.nn.functional.linear(x, weight.to(dt), None if bias is None else bias.to(dt))
-    return _linear(x, weight, bias)
+    return _linear(x, weight, bias, int(handoff))
 
 
 # ----------------------------------------------------------------------------- skip fusion
@@ -1137,7 +1189,7 @@ def _cat_route(M, N, K, C1):
     return None
 
 
-def _linear_cat_impl(x, skip, weight, bias):
+def _linear_cat_impl(x, skip, weight, bias, handoff=0):
     W = _shadow(weight, x.dtype)
     N, K = W.shape
     C1 = x.shape[-1]
@@ -1146,14 +1198,15 @@ def _linear_cat_impl(x, skip, weight, bias):
     return tok_gemm(x, W, _f32(bias), a2=skip)
 
 
-def _linear_cat_fake(x, skip, weight, bias):
+def _linear_cat_fake(x, skip, weight, bias, handoff=0):
     return x.new_empty(*x.shape[:-1], weight.shape[0])
 
 
 def _linear_cat_setup(ctx, inputs, output):
-    x, skip, weight, bias = inputs
+    x, skip, weight, bias = inputs[:4]
     ctx.save_for_backward(x, skip)
     ctx.params = (weight, bias)
+    ctx.handoff = inputs[4] if len(inputs) > 4 else 0
 
 
 def _wgrad_into(dy, x, dw, db, M, N, K, acc):
@@ -1179,6 +1232,8 @@ def _linear_cat_backward(ctx, dy):
     wt = _shadow_t(weight, W.dtype)  # W^T [K, N]: the halves are row ranges, no copies
     for lo, hi in ((0, C1), (C1, C1 + C2)):
         outs.append(_gemm(dy, W[:, lo:hi].t().contiguous() if wt is None else wt[lo:hi]))
+    if _park(ctx.handoff, outs[1]):
+        outs[1] = None  # the skip's gradient goes to its keyed LayerNorm's backward kernel
     # weight gradient per half straight into the column slices of dW (bias with the first):
     # the trainer's flat .grad (accumulate) or a fresh [N, C1 + C2] gradient
     direct = _direct(weight, bias)
@@ -1201,7 +1256,7 @@ def _linear_cat_backward(ctx, dy):
         _guard_side_write(bias, ev)
         _join_at_end_of_backward()
         _notify(weight, bias)
-        return outs[0], outs[1], None, None
+        return outs[0], outs[1], None, None, None
     if direct:
         dw, db, acc = weight.grad, bias.grad, 1
     else:
@@ -1212,19 +1267,21 @@ def _linear_cat_backward(ctx, dy):
     _wgrad_into(dy, skip, dw[:, C1:], None, M, N, C2, acc)
     if direct:
         _notify(weight, bias)
-        return outs[0], outs[1], None, None
-    return outs[0], outs[1], dw, db
+        return outs[0], outs[1], None, None, None
+    return outs[0], outs[1], dw, db, None
 
 
-_linear_cat = _define("linear_cat", "(Tensor x, Tensor skip, Tensor weight, Tensor bias) -> Tensor",
+_linear_cat = _define("linear_cat", "(Tensor x, Tensor skip, Tensor weight, Tensor bias, int handoff=0) -> Tensor",
                       _linear_cat_impl, _linear_cat_fake, _linear_cat_setup, _linear_cat_backward)
 
 
-def linear_cat(x, skip, weight, bias):
+def linear_cat(x, skip, weight, bias, handoff=0):
     """``F.linear(torch.cat([x, skip], -1), weight, bias)`` (skip fusion, model_parts.py:792-794,
     :804-806, :823-824); x / skip: [..., C1] / [..., C2] with equal leading dims.  16-bit: the
     concatenation is folded into the A loads of the routed GEMM (token GEMM or NT GEMM: no
-    concatenated copy) and split back out of the input gradient (two GEMMs over W's halves)."""
+    concatenated copy) and split back out of the input gradient (two GEMMs over W's halves).
+    handoff: the skip's ``residual_handoff_key()`` (its gradient is added in the keyed
+    LayerNorm's backward kernel)."""
     _need_cuda(x)
     dt = act_dtype()
     x, skip = _as(x, dt), _as(skip, dt)
@@ -1232,7 +1289,7 @@ def linear_cat(x, skip, weight, bias):
     C1, C2 = x.shape[-1], skip.shape[-1]
     M = x.numel() // C1
     if dt in _LOW and bias is not None and C1 + C2 == K and _cat_route(M, N, K, C1) is not None:
-        return _linear_cat(x, skip, weight, bias)
+        return _linear_cat(x, skip, weight, bias, int(handoff))
     return linear(torch.cat([x, skip], -1), weight, bias)
 
 
