@@ -596,12 +596,18 @@ class MSUNetSys(nn.Module):
         # the host launches a branch nobody reads
         for i, layer in enumerate(self.layers):
             kx = self._key_for(layer)  # x's readers: this stage, a central branch, a skip fusion
-            # the central decoders: layers_cent2 before stage 1, layers_cent1 before stage 2, each
-            # ending in a branch the reference discards (model_parts.py:795, :807)
+            xd.append(x)
+            xk.append(kx)
+            xs, x = x, layer(x, kx)
+            # the central decoders: layers_cent2 on stage 1's input, layers_cent1 on stage 2's,
+            # each ending in a branch the reference discards (model_parts.py:795, :807).  Run
+            # after the stage (independent of it; the reference runs them before): their nodes
+            # are then newer than the stage's, so autograd runs their backwards first and their
+            # input gradients reach the stage's first norm1 through the handoff, not an add
             for cent, cat0, start in ((self.layers_cent2, 2, 1), (self.layers_cent1, 1, 2)):
                 if i != start:
                     continue
-                xc = x
+                xc = xs
                 for k, mod in enumerate(cent):
                     if k == 0:
                         xc = mod(xc, kx)
@@ -614,9 +620,6 @@ class MSUNetSys(nn.Module):
                         else:
                             xk[i - k] = self._key_for(mod)
                             xc = mod(xc, xk[i - k])
-            xd.append(x)
-            xk.append(kx)
-            x = layer(x, kx)
             for mod, xin in dead:
                 self._run_dead(mod, xin)
             dead.clear()
