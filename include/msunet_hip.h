@@ -59,6 +59,13 @@ int msu_layernorm_bwd3(int dtype, int mode, const void* dy, const void* x, const
                        float* part, int nparts, float* dgamma, float* dbeta, long rows, int C, int H, int W,
                        int Cin, int accumulate, void* stream);
 int msu_ln_part_blocks(long rows, int C);
+/* nseg independent partial-row reductions in as few launches as fit (48 segments each):
+ * out[j][i] (+)= sum over q < nparts[j] of part[j][q * stride[j] + i], i < n[j], in a fixed order.
+ * Host arrays; n, stride multiples of 4, 16-B aligned rows.  With dgamma = dbeta = null,
+ * msu_layernorm_bwd / _bwd3 write only their [nparts][2C] partials (dgamma row, then dbeta),
+ * for such a batched reduction later (the deferred LayerNorm parameter gradients). */
+int msu_colsum_batch(int nseg, const float* const* part, const long* stride, const int* nparts, const int* n,
+                     float* const* out, int accumulate, void* stream);
 /* 1 (default): the partial-row reductions of msu_layernorm_bwd / msu_head_bwd run inside the
  * kernel (its last blocks, in a fixed order); 0: a separate column-sum launch after it (A/B switch
  * MSU_TAIL).  Returns the previous mode. */

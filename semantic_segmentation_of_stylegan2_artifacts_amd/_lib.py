@@ -58,6 +58,7 @@ SIGNATURES = {
     "msu_adamw_dev2": (I, [P, P, P, P, L, P, D, D, D, D, P, P, P, I, I, P]),
     "msu_step_advance": (I, [P, P, P]),
     "msu_cast": (I, [I, P, P, L, P]),
+    "msu_colsum_batch": (I, [I, P, P, P, P, P, I, P]),
     "msu_conv3x3_weight": (I, [I, P, P, I, I, I, P]),
     "msu_transpose16_multi": (I, [P, P, P, I, I, P]),
     "msu_conv3x3_fwd": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),

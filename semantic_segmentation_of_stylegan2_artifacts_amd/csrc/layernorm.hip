@@ -303,36 +303,34 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
     if (act) load_f32<VW>(a.gamma + ch * VW, gg);
     const long stride = (long)gridDim.x * GPB;
     long r = (long)blockIdx.x * GPB + grp;
-    uint4 qx{}, qd{}, qr{}, qr2{}, qr3{};
-    float mu = 0.f, rs = 0.f;
-    auto fetch = [&](long rr) __attribute__((always_inline)) {
-      mu = a.mean[rr];
-      rs = a.rstd[rr];
+    struct RowSet {
+      uint4 x{}, d{}, r{}, r2{}, r3{};
+      float mu = 0.f, rs = 0.f;
+    };
+    auto fetch = [&](RowSet& q, long rr) __attribute__((always_inline)) {
+      q.mu = a.mean[rr];
+      q.rs = a.rstd[rr];
       if (act) {
         const long off = src_off<MODE>(fa, rr, ch * VW);
-        qx = *reinterpret_cast<const uint4*>(X + off);
-        qd = *reinterpret_cast<const uint4*>(DY + rr * (long)a.C + ch * VW);
+        q.x = *reinterpret_cast<const uint4*>(X + off);
+        q.d = *reinterpret_cast<const uint4*>(DY + rr * (long)a.C + ch * VW);
         if constexpr (HAS_RES) {
-          if (a.dres) qr = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dres) + off);
-          if (a.dres2) qr2 = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dres2) + off);
-          if (a.dres3) qr3 = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dres3) + off);
+          if (a.dres) q.r = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dres) + off);
+          if (a.dres2) q.r2 = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dres2) + off);
+          if (a.dres3) q.r3 = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dres3) + off);
         }
       }
     };
-    if (r < a.rows) fetch(r);
-    for (; r < a.rows; r += stride) {
-      const uint4 cx = qx, cd = qd, cr = qr, cr2 = qr2, cr3 = qr3;
-      const float cmu = mu, crs = rs;
-      if (r + stride < a.rows) fetch(r + stride);
+    auto work = [&](const RowSet& c, long r) __attribute__((always_inline)) {
       float xh[VW], g[VW];
       float s1 = 0.f, s2 = 0.f;
       if (act) {
         float xv[VW], dv[VW];
-        unpack16<T>(cx, xv);
-        unpack16<T>(cd, dv);
+        unpack16<T>(c.x, xv);
+        unpack16<T>(c.d, dv);
 #pragma unroll
         for (int e = 0; e < VW; ++e) {
-          xh[e] = (xv[e] - cmu) * crs;
+          xh[e] = (xv[e] - c.mu) * c.rs;
           g[e] = dv[e] * gg[e];
           s1 += g[e];
           s2 = __builtin_fmaf(g[e], xh[e], s2);
@@ -355,22 +353,22 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
         if constexpr (HAS_RES) res = a.dres != nullptr;
         if (res) {
           float dr[VW];
-          unpack16<T>(cr, dr);
+          unpack16<T>(c.r, dr);
 #pragma unroll
-          for (int e = 0; e < VW; ++e) o[e] = __builtin_fmaf(crs, o[e], dr[e]);
+          for (int e = 0; e < VW; ++e) o[e] = __builtin_fmaf(c.rs, o[e], dr[e]);
           if (a.dres2) {
-            unpack16<T>(cr2, dr);
+            unpack16<T>(c.r2, dr);
 #pragma unroll
             for (int e = 0; e < VW; ++e) o[e] += dr[e];
           }
           if (a.dres3) {
-            unpack16<T>(cr3, dr);
+            unpack16<T>(c.r3, dr);
 #pragma unroll
             for (int e = 0; e < VW; ++e) o[e] += dr[e];
           }
         } else {
 #pragma unroll
-          for (int e = 0; e < VW; ++e) o[e] *= crs;
+          for (int e = 0; e < VW; ++e) o[e] *= c.rs;
         }
         VecW<T>::store(reinterpret_cast<T*>(a.dx) + off, o);
         if constexpr (MODE == IN_ADD) {
@@ -380,6 +378,27 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
             VecW<T>::store(reinterpret_cast<T*>(a.db) + off, o);
           }
         }
+      }
+    };
+    if constexpr ((MSU_EXP & 256) != 0) {
+      // ablation: two rows ahead (two register sets, the loop unrolled by two)
+      RowSet q0, q1;
+      if (r < a.rows) fetch(q0, r);
+      if (r + stride < a.rows) fetch(q1, r + stride);
+      for (; r < a.rows; r += 2 * stride) {
+        work(q0, r);
+        if (r + 2 * stride < a.rows) fetch(q0, r + 2 * stride);
+        if (r + stride >= a.rows) break;
+        work(q1, r + stride);
+        if (r + 3 * stride < a.rows) fetch(q1, r + 3 * stride);
+      }
+    } else {
+      RowSet nxt;
+      if (r < a.rows) fetch(nxt, r);
+      for (; r < a.rows; r += stride) {
+        const RowSet cur = nxt;
+        if (r + stride < a.rows) fetch(nxt, r + stride);
+        work(cur, r);
       }
     }
   } else
@@ -576,8 +595,12 @@ int bwd_dispatch(int dtype, const LnBwdArgs& a, float* dgamma, float* dbeta, int
   b.accumulate = accumulate;
   b.dgamma = dgamma;
   b.dbeta = dbeta;
+  // dgamma and dbeta null: only the [nparts][2C] partials are written (the caller reduces them
+  // later, msu_colsum_batch: the deferred LayerNorm parameter gradients)
+  const bool partials_only = dgamma == nullptr && dbeta == nullptr;
+  if (partials_only || (MSU_EXP & 128) != 0) b.tail = -1;  // (128: ablation, no reduction)
   MSU_DISPATCH(dtype, T, rc = launch_bwd<T, MODE>(b, st, nparts));
-  if (rc || b.tail >= 0) return rc;
+  if (rc || b.tail >= 0 || partials_only || (MSU_EXP & 128)) return rc;
   if (dbeta == dgamma + a.C) {  // contiguous [dgamma | dbeta]: one reduction launch
     colsum(a.part, nparts, 2L * a.C, 2L * a.C, dgamma, accumulate, st);
   } else {
@@ -993,6 +1016,33 @@ int msu_tail_reduce_mode(int mode) {
   const int prev = g_msu_tail_on;
   g_msu_tail_on = mode ? 1 : 0;
   return prev;
+}
+
+int msu_colsum_batch(int nseg, const float* const* part, const long* stride, const int* nparts, const int* n,
+                     float* const* out, int accumulate, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  for (int j0 = 0; j0 < nseg; j0 += CB_MAX) {
+    ColBatch cb{};
+    cb.nseg = nseg - j0 < CB_MAX ? nseg - j0 : CB_MAX;
+    cb.accumulate = accumulate;
+    int blocks = 0;
+    for (int j = 0; j < cb.nseg; ++j) {
+      const int k = j0 + j;
+      if (n[k] % 4 || stride[k] % 4 || ((uintptr_t)part[k] & 15) || ((uintptr_t)out[k] & 15) || nparts[k] < 1) return -3;
+      cb.part[j] = part[k];
+      cb.out[j] = out[k];
+      cb.stride[j] = stride[k];
+      cb.n[j] = n[k];
+      cb.nparts[j] = nparts[k];
+      blocks += (n[k] / 4 + CB_NC - 1) / CB_NC;
+      cb.bend[j] = blocks;
+    }
+    if (blocks == 0) continue;
+    hipLaunchKernelGGL(colsum_batch_kernel, dim3(blocks), dim3(256), 0, st, cb);
+    const int rc = MSU_CHECK_LAUNCH();
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 int msu_reduce_rows(const float* part, int nparts, int n, long stride, float* out,

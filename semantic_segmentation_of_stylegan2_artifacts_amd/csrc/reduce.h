@@ -124,6 +124,61 @@ inline void colsum(const float* part, int nparts, long n, long stride, float* ou
   colsum_multi(&s, 1, nparts, accumulate, st);
 }
 
+// ------------------------------------------------------------------ batched reductions
+// Many independent partial-row reductions in one launch (deferred LayerNorm parameter
+// gradients: a stage's worth of LayerNorm backwards hand over their [nparts][2C] partials instead
+// of each summing them in its own tail): segment j sums part_j[q * stride_j + i] over q in
+// [0, nparts_j) for i < n_j into out_j (+= with accumulate), in a fixed order (deterministic).
+// Block = 32 part-lanes x 8 float4 column lanes (32 columns).
+constexpr int CB_MAX = 48, CB_PL = 32, CB_NC = 8;
+struct ColBatch {
+  const float* part[CB_MAX];
+  float* out[CB_MAX];
+  long stride[CB_MAX];
+  int n[CB_MAX];
+  int nparts[CB_MAX];
+  int bend[CB_MAX];  // prefix sums of the segments' block counts
+  int nseg;
+  int accumulate;
+};
+
+__global__ void __launch_bounds__(256) colsum_batch_kernel(ColBatch cb) {
+  int seg = 0;
+  while (seg + 1 < cb.nseg && (int)blockIdx.x >= cb.bend[seg]) ++seg;
+  const int b0 = seg == 0 ? 0 : cb.bend[seg - 1];
+  const float* __restrict__ part = cb.part[seg];
+  const long stride = cb.stride[seg];
+  const int n = cb.n[seg], np = cb.nparts[seg];
+  const int lx = threadIdx.x % CB_NC, ly = threadIdx.x / CB_NC;
+  const int i = (((int)blockIdx.x - b0) * CB_NC + lx) * 4;
+  float4 s = {0.f, 0.f, 0.f, 0.f};
+  if (i < n) {
+    int q = ly;
+    for (; q + 3 * CB_PL < np; q += 4 * CB_PL) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(part + (long)(q + u * CB_PL) * stride + i);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+    }
+    for (; q < np; q += CB_PL) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (long)q * stride + i);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  __shared__ float4 red[CB_PL][CB_NC];
+  red[ly][lx] = s;
+  __syncthreads();
+  if (ly == 0 && i < n) {
+    float4 t = red[0][lx];
+#pragma unroll
+    for (int k = 1; k < CB_PL; ++k) { t.x += red[k][lx].x; t.y += red[k][lx].y; t.z += red[k][lx].z; t.w += red[k][lx].w; }
+    float4* o = reinterpret_cast<float4*>(cb.out[seg] + i);
+    if (cb.accumulate) { const float4 v = *o; t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w; }
+    *o = t;
+  }
+}
+
 // ------------------------------------------------------------------ in-kernel tail reduction
 // The partial rows a kernel's blocks write, summed by the kernel itself instead of a colsum
 // launch.  A colsum launch queued behind the other stream's kernels waited for free CUs: the

@@ -16,6 +16,7 @@ modules in ``network/`` call.  They cast the activation to the autocast dtype an
 registered op.  (A plain ``autograd.Function`` route around the dispatcher measured equal on
 the GPU-bound 1024^2 step, r02c 50.50 vs 50.57 ms: gone.)
 """
+import ctypes
 import functools
 
 import torch
@@ -228,10 +229,10 @@ def _take(key):
 def _end_of_backward():
     global _join_queued, res_dropped
     _join_queued = False
+    _flush_ln()
     res_dropped += sum(len(v) for v in _res_handoff.values())
     _res_handoff.clear()
     _res_closed.clear()
-    _flush_deferred()  # anything still held back runs now, before the join
     join_side_streams()
     _side_keep.clear()  # the main stream now waits for every side-stream read
     for p in _side_event_params:
@@ -260,12 +261,67 @@ def _notify(*params):
 
 
 def _ln_grads(ctx, C, device):
-    """(dgamma, dbeta, accumulate, direct) buffers for a LayerNorm backward."""
+    """(dgamma, dbeta, accumulate, direct) buffers for a LayerNorm backward; (None, None, ...)
+    with direct parameters under MSU_LN_DEFER: the kernel writes only its partial rows, summed
+    into .grad later by _ln_finish's batch."""
     w, b = ctx.affine
+    ctx.ln_deferred = False
     if _direct(w, b):
+        if _LN_DEFER and C % 4 == 0 and w.grad.data_ptr() % 16 == 0 and b.grad.data_ptr() % 16 == 0:
+            ctx.ln_deferred = True  # (16-B rows and outputs: msu_colsum_batch's float4 sums)
+            return None, None, 1, True
         return w.grad, b.grad, 1, True
     dw, db = torch.empty(2, C, device=device, dtype=torch.float32)  # contiguous: one reduction
     return dw, db, 0, False
+
+
+# Deferred LayerNorm parameter gradients (MSU_LN_DEFER): a LayerNorm backward with trainer-
+# direct gamma / beta writes its [nparts][2C] partial rows and ends there; the partials of the
+# LayerNorms of one width (a stage) are summed into .grad by one msu_colsum_batch launch when the
+# width changes, and the rest at the end of backward.  Each kernel's in-kernel tail reduction
+# (last-arriving blocks summing ~1 MB of partials, 8-15 us at the end of every launch, r06ac)
+# leaves its critical path; the parameters are notified to the gradient bucketer after the batch.
+_LN_DEFER = switches.on("MSU_LN_DEFER")
+_ln_pending = []  # (part, nparts, C, gamma, beta)
+ln_batches = 0  # batched reductions launched (tests)
+
+
+def _flush_ln():
+    """Sum the pending LayerNorm partials into their parameters' .grad (one launch per 48 rows
+    of segments), then notify the parameters."""
+    global ln_batches
+    if not _ln_pending:
+        return
+    parts, strides, nps, ns, outs = [], [], [], [], []
+    for part, n, C, w, b in _ln_pending:
+        for off, g in ((0, w.grad), (C, b.grad)):
+            parts.append(part.data_ptr() + 4 * off)
+            strides.append(2 * C)
+            nps.append(n)
+            ns.append(C)
+            outs.append(g.data_ptr())
+    k = len(parts)
+    P = ctypes.c_void_p * k
+    _lib.call("msu_colsum_batch", k, P(*parts), (ctypes.c_long * k)(*strides), (ctypes.c_int * k)(*nps),
+              (ctypes.c_int * k)(*ns), P(*outs), 1, _s(_ln_pending[0][0]))
+    ln_batches += 1
+    pend = list(_ln_pending)
+    _ln_pending.clear()
+    for _, _, _, w, b in pend:
+        _notify(w, b)
+
+
+def _ln_finish(ctx, part, n, C):
+    """After a LayerNorm backward with direct parameters: register its partials (deferred) or
+    notify (reduced in the kernel)."""
+    w, b = ctx.affine
+    if not ctx.ln_deferred:
+        _notify(w, b)
+        return
+    if _ln_pending and _ln_pending[-1][2] != C:
+        _flush_ln()
+    _ln_pending.append((part, n, C, w, b))
+    _join_at_end_of_backward()
 
 
 def _ln_parts(rows, C, device):
@@ -310,7 +366,6 @@ def _ln_setup(ctx, inputs, output):
 def _ln_backward(ctx, dy, _dm, _dr):
     global res_handoff_calls
     x, w, mean, rstd = ctx.saved_tensors
-    _flush_deferred(x.shape[-1])
     res = _take(ctx.handoff)  # the other readers' gradients of x (the paired add-LN's first)
     if dy is None:
         return (functools.reduce(torch.add, res) if res else None), None, None, None, None
@@ -337,7 +392,7 @@ def _ln_backward(ctx, dy, _dm, _dr):
         _lib.call("msu_layernorm_bwd", _dt(x), IN_PLAIN, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
                   _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, C, 0, 0, 0, acc, _s(x))
     if direct:
-        _notify(*ctx.affine)
+        _ln_finish(ctx, part, n, C)
         return dx, None, None, None, None
     return dx, dw, db, None, None
 
@@ -388,7 +443,6 @@ def _add_ln_setup(ctx, inputs, output):
 def _add_ln_backward(ctx, ds, dy, _dm, _dr):
     s, w, mean, rstd, scale = ctx.saved_tensors
     C = s.shape[-1]
-    _flush_deferred(C)
     rows = s.numel() // C
     if dy is None:
         dy = torch.zeros_like(s)
@@ -401,7 +455,7 @@ def _add_ln_backward(ctx, ds, dy, _dm, _dr):
     _lib.call("msu_layernorm_bwd", _dt(s), IN_ADD, _p(dy), _p(s), _p(ds), _p(w), _p(mean), _p(rstd),
               _p(da), _p(dbr), _p(scale), ctx.rps, _p(part), n, _p(dw), _p(dbb), rows, C, 0, 0, 0, acc, _s(s))
     if direct:
-        _notify(*ctx.affine)
+        _ln_finish(ctx, part, n, C)
         dw = dbb = None
     dbr = dbr if dbr is not None else da
     if _park(ctx.handoff, da):
@@ -461,7 +515,7 @@ def _merge_ln_backward(ctx, dy, _dm, _dr):
     _lib.call("msu_layernorm_bwd", _dt(x), IN_MERGE, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
               _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, 4 * C, H, W, C, acc, _s(x))
     if direct:
-        _notify(*ctx.affine)
+        _ln_finish(ctx, part, n, 4 * C)
         return dx, None, None, None
     return dx, dw, db, None
 
@@ -510,7 +564,7 @@ def _d2s_ln_backward(ctx, dy, _dm, _dr):
     _lib.call("msu_layernorm_bwd", _dt(x), IN_D2S2, _p(dy), _p(x), None, _p(w), _p(mean), _p(rstd),
               _p(dx), None, None, 1, _p(part), n, _p(dw), _p(db), rows, c, H, W, 0, acc, _s(x))
     if direct:
-        _notify(*ctx.affine)
+        _ln_finish(ctx, part, n, c)
         return dx, None, None, None
     return dx, dw, db, None
 
@@ -1585,8 +1639,8 @@ def head_norm_output(z, gamma, beta, out_weight, eps=1e-5):
 
 # ----------------------------------------------------------------------------- conv 3x3
 # persistent workgroups of the refine-conv weight gradient (one 139 KB / 12-wave workgroup per
-# CU; 192 / 128 measured slower beside the refine dgrads, r04ac -- the A/B switch pairs fewer of
-# them with the deferral below, MSU_CONV_WGRAD_AT)
+# CU; 192 / 128 measured slower beside the refine dgrads, r04ac; fewer of them held back to the
+# stage-2 LayerNorm backward, neutral / slower: r06k, r06t, removed)
 _CONV_WGRAD_BLOCKS = int(switches.get("MSU_CONV_WGRAD_BLOCKS"))
 
 
@@ -1604,22 +1658,6 @@ def _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout):
 # A/B switch MSU_CONV_SIDE=0: the refine convs' weight gradients on the main stream.  (Holding
 # them back to the next side-stream fork measured equal, r04z: gone.)
 _CONV_SIDE = switches.on("MSU_CONV_SIDE")
-# MSU_CONV_WGRAD_AT=C (> 0): the refine convs' side-stream weight gradients are held back until the
-# first LayerNorm backward of width >= C (the stage-2 blocks at C = 384: the latency-bound part of
-# backward, whose kernels leave CUs free), instead of running beside the refine dgrads they cannot
-# share a CU with (both fill a CU's LDS / registers)
-_CONV_WGRAD_AT = int(switches.get("MSU_CONV_WGRAD_AT"))
-_deferred_side = []  # side-stream launches held back to that point of backward
-
-
-def _flush_deferred(C=None):
-    """Issue the held-back side-stream launches (at a LayerNorm backward of width C >= the
-    threshold, or unconditionally at the end of backward: C None)."""
-    if _deferred_side and (C is None or C >= _CONV_WGRAD_AT):
-        todo = list(_deferred_side)
-        _deferred_side.clear()
-        for fn in todo:
-            fn()
 
 
 def _conv_wgrad_param(a, dz, mode, B, H, W, Cin, Cout, weight, bias):
@@ -1628,28 +1666,21 @@ def _conv_wgrad_param(a, dz, mode, B, H, W, Cin, Cout, weight, bias):
     them: off the activation-gradient chain, 2 x 1.3 ms per step on the main stream before)."""
     if not (_CONV_SIDE and _side_enabled and _direct(weight, bias)):
         return _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout)
-
-    def launch():
-        main = torch.cuda.current_stream(a.device)
-        side = _side_stream_for(a.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            dw, db = _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout)
-            weight.grad.add_(dw)
-            bias.grad.add_(db)
-        for t in (a, dz):
-            t.record_stream(side)
-            _side_keep.append(t)
-        ev = torch.cuda.Event()
-        ev.record(side)
-        _guard_side_write(weight, ev)
-        _guard_side_write(bias, ev)
-        _notify(weight, bias)
-
-    if _CONV_WGRAD_AT > 0:
-        _deferred_side.append(launch)
-    else:
-        launch()
+    main = torch.cuda.current_stream(a.device)
+    side = _side_stream_for(a.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        dw, db = _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout)
+        weight.grad.add_(dw)
+        bias.grad.add_(db)
+    for t in (a, dz):
+        t.record_stream(side)
+        _side_keep.append(t)
+    ev = torch.cuda.Event()
+    ev.record(side)
+    _guard_side_write(weight, ev)
+    _guard_side_write(bias, ev)
+    _notify(weight, bias)
     _join_at_end_of_backward()
     return None, None
 

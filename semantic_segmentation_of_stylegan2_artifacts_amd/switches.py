@@ -35,8 +35,8 @@ SWITCHES = {
                    "fused MLP", "DESIGN 7 (r05at)"),
     "MSU_MLP_TRAIN": ("1", "0: training stage-0 MLPs on the token-GEMM pair (H and GELU(H) stored) instead of "
                       "the fused kernel storing H only", "DESIGN 7 (r05ao)"),
-    "MSU_CONV_WGRAD_AT": ("0", "C > 0: the refine-conv side-stream weight gradients held back to the first LayerNorm "
-                          "backward of width >= C (0: issued beside the refine dgrads)", "DESIGN 7 (r06)"),
+    "MSU_LN_DEFER": ("1", "0: each LayerNorm backward sums its parameter-gradient partials itself (in-kernel "
+                     "tail) instead of one batched reduction per width", "DESIGN 7 (r06)"),
     "MSU_NT_DYN": ("0", "1: the NT GEMM's two-stage kernel claims tiles from a per-XCD device queue (measured "
                    "-0.3 % step, 1.8 % slower standalone: r06q/r06r)", "DESIGN 7 (r06)"),
     "MSU_CONV_DYN": ("1", "0: the refine-conv kernel's static tile schedule (blockIdx.x + k * gridDim.x) instead "

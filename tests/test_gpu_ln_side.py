@@ -1,7 +1,8 @@
 """GPU: parameter gradients written straight into trainer-style ``.grad`` (direct parameters) equal
 the plain autograd gradients bitwise -- the same partials summed in the same order:
 
-* the LayerNorm parameter gradients accumulated into ``.grad`` by the backward's reduction, for
+* the LayerNorm parameter gradients accumulated into ``.grad`` by the backward's reduction (or, deferred,
+  by the batched reduction at the end of backward: to f32 rounding), for
   the four LayerNorm forms of the path (torchvision block norms, the fused residual + norm,
   PatchMerging's gather + norm, PatchExpand's rearrange + norm; model_parts.py:87-94, :403-405);
 * the refine convs' weight / bias gradients added into ``.grad`` on the side stream
@@ -31,9 +32,15 @@ def _params(C, seed, direct):
     return w, b
 
 
+@pytest.mark.parametrize("defer", [False, True], ids=["tail", "deferred"])
 @pytest.mark.parametrize("form", ["plain", "add", "merge", "d2s"])
-def test_ln_param_grads_direct_equal_autograd(form):
+def test_ln_param_grads_direct_equal_autograd(form, defer, monkeypatch):
+    """In-kernel tail reduction: bitwise the autograd gradients.  Deferred (MSU_LN_DEFER: the
+    partials summed by a batched reduction at the end of backward, another fixed order): to f32
+    rounding; dx bitwise either way."""
     ops = _ops()
+    monkeypatch.setattr(ops, "_LN_DEFER", defer)
+    batches = ops.ln_batches
     g = torch.Generator().manual_seed(3)
     B, H, W, C = 2, 32, 32, 96
     x = torch.randn(B, H, W, C, generator=g).to(DEV, torch.bfloat16)
@@ -58,8 +65,13 @@ def test_ln_param_grads_direct_equal_autograd(form):
         ops.join_side_streams()
         torch.cuda.synchronize()
         res[direct] = (xg.grad.clone(), w.grad.clone(), b.grad.clone())
+    assert ops.ln_batches - batches == (1 if defer else 0)
+    assert not ops._ln_pending
     for name, a, r in zip(("dx", "dgamma", "dbeta"), res[True], res[False]):
-        assert torch.equal(a, r), name
+        if defer and name != "dx":
+            assert ((a - r).norm() / r.norm()).item() <= 1e-6, name
+        else:
+            assert torch.equal(a, r), name
 
 
 @pytest.mark.parametrize("d2s", [False, True])
