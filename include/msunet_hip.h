@@ -129,6 +129,10 @@ int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const f
  * workspace partials its backward kernel left, on `stream`. */
 int msu_win_attn_bwd_tail(int dtype, float* workspace, float* dtable, float* dqkv_bias_pad, int B, int H, int W,
                           int C, int nh, void* stream);
+/* As msu_win_attn_bwd_tail; accumulate != 0 adds into dtable / dqkv_bias_pad (a trainer's .grad)
+ * instead of overwriting them. */
+int msu_win_attn_bwd_tail2(int dtype, float* workspace, float* dtable, float* dqkv_bias_pad, int B, int H, int W,
+                           int C, int nh, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------- refine convs
  * FinalPatchExpand_X4_V2.refine1 / refine2 (model_parts.py:447-448, :468-471): 3x3, pad 1,

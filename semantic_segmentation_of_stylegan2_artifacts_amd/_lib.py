@@ -38,6 +38,7 @@ SIGNATURES = {
     "msu_win_attn_bwd": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P, P]),
     "msu_win_attn_bwd2": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P, P, P]),
     "msu_win_attn_bwd_tail": (I, [I, P, P, P, I, I, I, I, I, P]),
+    "msu_win_attn_bwd_tail2": (I, [I, P, P, P, I, I, I, I, I, I, P]),
     "msu_win_attn_qkv_supported": (I, [I, I]),
     "msu_win_attn_qkv_fwd": (I, [I, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P]),
     "msu_win_attn_qkv_fwd2": (I, [I, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, U64, P, P]),

@@ -365,7 +365,8 @@ __global__ void __launch_bounds__(64, 2) win_attn_bwd_kernel(
 
 
 // dB [nh, 49*49] -> d_table [169, nh]: gather the (i, j) pairs of each relative offset
-__global__ void __launch_bounds__(256) rel_table_grad_kernel(const float* dB, int nh, float* dtable) {
+__global__ void __launch_bounds__(256) rel_table_grad_kernel(const float* dB, int nh, float* dtable,
+                                                             int accumulate = 0) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= 169 * nh) return;
   const int idx = e / nh, h = e - (e / nh) * nh;
@@ -380,7 +381,7 @@ __global__ void __launch_bounds__(256) rel_table_grad_kernel(const float* dB, in
       s += dB[(long)h * NT * NT + (ih * WS + iw) * NT + jh * WS + jw];
     }
   }
-  dtable[e] = s;
+  dtable[e] = accumulate ? dtable[e] + s : s;
 }
 
 WinGeom make_geom(int B, int H, int W, int C, int nh, int shift) {
@@ -407,7 +408,7 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
                       const unsigned long long* seed_dev, const void* keep, hipStream_t st, hipStream_t pst);
 long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh);
 int msu_attn_mfma_bwd_tail(float* ws, float* dtable, float* dqkv_bias_pad, long nwin, int C, int nh,
-                           hipStream_t st);
+                           hipStream_t st, int accumulate = 0);
 long msu_attn_mfma_fwd_workspace(int C, int nh);
 
 namespace {
@@ -492,22 +493,28 @@ int msu_win_attn_bwd2(int dtype, const void* qkv, const float* qkv_bias, const f
   return msu_win_attn_bwd_tail(dtype, workspace, dtable, dqkv_bias_pad, B, H, W, C, nh, pst);
 }
 
-int msu_win_attn_bwd_tail(int dtype, float* workspace, float* dtable, float* dqkv_bias_pad, int B, int H, int W,
-                          int C, int nh, void* stream) {
+int msu_win_attn_bwd_tail2(int dtype, float* workspace, float* dtable, float* dqkv_bias_pad, int B, int H, int W,
+                           int C, int nh, int accumulate, void* stream) {
   if (C != nh * HD) return -2;
   const WinGeom g = make_geom(B, H, W, C, nh, 0);
   hipStream_t st = (hipStream_t)stream;
   if (g.nwin == 0) return 0;
-  if (msu_is16(dtype)) return msu_attn_mfma_bwd_tail(workspace, dtable, dqkv_bias_pad, g.nwin, C, nh, st);
+  if (msu_is16(dtype)) return msu_attn_mfma_bwd_tail(workspace, dtable, dqkv_bias_pad, g.nwin, C, nh, st, accumulate);
   const int nblk = f32_bwd_blocks(g.nwin, nh);
   float* dB_part = workspace;
   float* dB = dB_part + (long)nblk * nh * NT * NT;
   float* qb_part = dB + (long)nh * NT * NT;
   const long nB = (long)nh * NT * NT;
   colsum(dB_part, nblk, nB, nB, dB, 0, st);
-  hipLaunchKernelGGL(rel_table_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, st, dB, nh, dtable);
-  colsum(qb_part, nblk, 3L * C, 3L * C, dqkv_bias_pad, 0, st);
+  hipLaunchKernelGGL(rel_table_grad_kernel, dim3((169 * nh + 255) / 256), dim3(256), 0, st, dB, nh, dtable,
+                     accumulate);
+  colsum(qb_part, nblk, 3L * C, 3L * C, dqkv_bias_pad, accumulate, st);
   return MSU_CHECK_LAUNCH();
+}
+
+int msu_win_attn_bwd_tail(int dtype, float* workspace, float* dtable, float* dqkv_bias_pad, int B, int H, int W,
+                          int C, int nh, void* stream) {
+  return msu_win_attn_bwd_tail2(dtype, workspace, dtable, dqkv_bias_pad, B, H, W, C, nh, 0, stream);
 }
 
 int msu_win_attn_bwd(int dtype, const void* qkv, const float* qkv_bias, const float* table,

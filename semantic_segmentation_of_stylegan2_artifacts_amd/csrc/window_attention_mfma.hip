@@ -919,7 +919,7 @@ void launch_bwd(dim3 grid, hipStream_t st, const void* qkv, const Aux& aux, cons
 
 // entry points used by window_attention.hip for the 16-bit dtypes
 int msu_attn_mfma_bwd_tail(float* ws, float* dtable, float* dqkv_bias_pad, long nwin, int C, int nh,
-                           hipStream_t st);
+                           hipStream_t st, int accumulate = 0);
 long msu_attn_mfma_fwd_workspace(int C, int nh) { return aux_floats(C, nh); }
 
 long msu_attn_mfma_bwd_workspace(long nwin, int C, int nh) {
@@ -983,13 +983,13 @@ int msu_attn_mfma_bwd(int dtype, const void* qkv, const float* qkv_bias, const f
 
 // the parameter-gradient reductions of msu_attn_mfma_bwd from its workspace partials
 int msu_attn_mfma_bwd_tail(float* ws, float* dtable, float* dqkv_bias_pad, long nwin, int C, int nh,
-                           hipStream_t st) {
+                           hipStream_t st, int accumulate) {
   if (nwin == 0) return 0;
   const long parts = (long)bwd_blocks(nwin, nh);
   float* dB_part = ws + aux_floats(C, nh);
   float* qb_part = dB_part + parts * nh * 169;
   const ColSeg segs[2] = {{dB_part, 169L * nh, 169L * nh, dtable}, {qb_part, 3L * C, 3L * C, dqkv_bias_pad}};
-  colsum_multi(segs, 2, (int)parts, 0, st);
+  colsum_multi(segs, 2, (int)parts, accumulate, st);
   return MSU_CHECK_LAUNCH();
 }
 

@@ -701,12 +701,9 @@ def _attn_backward(ctx, dout, _dkeep, _dws=None):
         ws.record_stream(side)
         _side_keep.append(ws)
         with torch.cuda.stream(side):
-            dtable = torch.empty_like(table)
-            dbias = torch.empty(3 * C, device=qkv.device, dtype=torch.float32)
-            _lib.call("msu_win_attn_bwd_tail", _dt(qkv), _p(ws), _p(dtable), _p(dbias), B, H, W, C, nh,
+            # the reductions add straight into .grad (no .grad adds behind them)
+            _lib.call("msu_win_attn_bwd_tail2", _dt(qkv), _p(ws), _p(tp.grad), _p(bp.grad), B, H, W, C, nh, 1,
                       side.cuda_stream)
-            bp.grad.add_(dbias)
-            tp.grad.add_(dtable)
         ev = torch.cuda.Event()
         ev.record(side)
         _guard_side_write(bp, ev)
