@@ -720,8 +720,8 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
       // part(s) of the next tile and (dgrad, tap 7) the GELU' operands
       constexpr int hprev = SPREAD ? (tap >= 2 ? halo_part_lo(tap, NHC) - halo_part_lo(tap - 1, NHC) : 0)
                                    : (tap == V3_HALO_TAP + 1 ? NHC : 0);
-      // (32 x 32 form: only co tile 0's operands are issued at tap 7, see load_sp)
-      constexpr int sprev = (OUT_GGRAD && tap == 8) ? ((M16 || SP_AT7) ? SPRE : SPRE / 3) : 0;
+      // (only a third of them are issued at tap 7, see load_sp / load_sp16)
+      constexpr int sprev = (OUT_GGRAD && tap == 8) ? (SP_AT7 ? SPRE : SPRE / 3) : 0;
       if constexpr (tap == 0) {
         // W(0) landed (DMA'd at the previous tile's tap 8); W(1) and the previous tile's output
         // stores, issued after it in that epilogue, may stay in flight
@@ -781,19 +781,25 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
           sp[m][n][pp] = *reinterpret_cast<const u32x4*>(S + pix_off32<OUT_D2S>(b, y, xs, g.H, g.W, C) + 32 * n +
                                                          16 * pp + 8 * h);
       };
+      // dgrad, 16 x 16 form: the operands of channel group q (32 q .. 32 q + 31) of rows m
+      auto load_sp16 = [&](int m, int y, int q) __attribute__((always_inline)) {
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) {
+          const int xs = min(x0 + 16 * pt + l15, g.W - 1);
+          sp[m][pt][q] = *reinterpret_cast<const u32x4*>(S + pix_off32<OUT_D2S>(b, y, xs, g.H, g.W, C) + 32 * q +
+                                                         16 * (g4 & 1) + 8 * (g4 >> 1));
+        }
+      };
       if constexpr (OUT_GGRAD && tap == 7) {
         // dgrad: the pre-activation S of this tile's outputs for the GELU' epilogue
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           const int y = min(y0 + 2 * wave + m, g.H - 1);
           if constexpr (M16) {
-#pragma unroll
-            for (int pt = 0; pt < 2; ++pt) {
-              const int xs = min(x0 + 16 * pt + l15, g.W - 1);
-#pragma unroll
-              for (int q = 0; q < 3; ++q)
-                sp[m][pt][q] = *reinterpret_cast<const u32x4*>(S + pix_off32<OUT_D2S>(b, y, xs, g.H, g.W, C) + 32 * q +
-                                                               16 * (g4 & 1) + 8 * (g4 >> 1));
+            load_sp16(m, y, 0);
+            if constexpr (SP_AT7) {
+              load_sp16(m, y, 1);
+              load_sp16(m, y, 2);
             }
           } else {
             load_sp(m, y, 0);
@@ -895,7 +901,7 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
         }, std::make_integer_sequence<int, 6>{});
       }
       if constexpr (tap == 8) {
-        if constexpr (OUT_GGRAD && !M16 && !SP_AT7) {
+        if constexpr (OUT_GGRAD && !SP_AT7) {
           // co tiles 1-2's GELU' operands after the last MFMAs: held through taps 7-8 beside the
           // full halo prefetch they pushed the kernel past 256 VGPRs (halo registers spilled,
           // each spill store a vmcnt(0) at tap 1); their latency is exposed at the epilogue's
@@ -903,8 +909,13 @@ __global__ void __launch_bounds__(512) conv3x3_v3_kernel(const bf16_t* __restric
 #pragma unroll
           for (int m = 0; m < MT; ++m) {
             const int y = min(y0 + 2 * wave + m, g.H - 1);
-            load_sp(m, y, 1);
-            load_sp(m, y, 2);
+            if constexpr (M16) {
+              load_sp16(m, y, 1);
+              load_sp16(m, y, 2);
+            } else {
+              load_sp(m, y, 1);
+              load_sp(m, y, 2);
+            }
           }
         }
         if (next < ntiles) {
@@ -1465,7 +1476,8 @@ int launch_v3(const ConvGeom& g, const bf16_t* X, const bf16_t* Wt, const float*
   // GELU' operands held from tap 7 the 16x16 form spills 260 B per lane.  Halo loads spread over
   // taps 1..7 (SPREAD; all at tap 1 measured equal, r03).  v4 (one wave per SIMD, 4 rows per
   // wave) was 7-10 % slower on every launch (r03l/m) and is gone.
-  if constexpr (!OUT_GGRAD)
+  // (ablation 2048: the dgrad on 16 x 16 x 32 too)
+  if constexpr (!OUT_GGRAD || (MSU_EXP & 2048) != 0)
     return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, true, true>(g, X, Wt, bias, S, Y, Y2, st);
   return launch_v3s<T, IN_D2S, OUT_D2S, OUT_GGRAD, BIAS, DUAL, true, false>(g, X, Wt, bias, S, Y, Y2, st);
 }
