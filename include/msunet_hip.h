@@ -82,6 +82,11 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
                  const float* beta, const float* w, const float* mean, const float* rstd,
                  void* dz, float* part, int nparts, float* dgamma, float* dbeta, float* dw,
                  long rows, int C, void* stream);
+/* accumulate != 0: dgamma / dbeta / dw are added to (the trainer's .grad: no autograd adds) */
+int msu_head_bwd2(int dtype, const float* dlogit, const void* z, const float* gamma,
+                  const float* beta, const float* w, const float* mean, const float* rstd,
+                  void* dz, float* part, int nparts, float* dgamma, float* dbeta, float* dw,
+                  long rows, int C, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------- window attention
  * torchvision shifted_window_attention core (called from SwinTransformerBlock at
@@ -160,6 +165,11 @@ long msu_conv3x3_wgrad_workspace(int nchunk, int Cin, int Cout, int dtype, int u
 int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, float* dW, float* db,
                       float* workspace, void* unused, int nchunk, int B, int H, int W, int Cin,
                       int Cout, void* stream);
+/* The same with accumulate != 0: dW and db are added to (the trainer's .grad on the side stream:
+ * no separate adds). */
+int msu_conv3x3_wgrad2(int dtype, int in_mode, const void* X, const void* dY, float* dW, float* db,
+                       float* workspace, int nchunk, int B, int H, int W, int Cin, int Cout, int accumulate,
+                       void* stream);
 
 /* ---------------------------------------------------------------- fused qkv Linear + window attention
  * Stage 0 of the Swin block (C = 96, 3 heads; model_parts.py:166-170 -> torchvision's qkv Linear and
@@ -300,6 +310,14 @@ int msu_dynloss_fwd(int dtype, const void* logits, const float* target, int B, l
 int msu_dynloss_bwd(int dtype, const void* logits, const float* target, const float* coef,
                     const float* loss, const float* gout, int B, long N, float alpha, float beta,
                     float mix, float* dlogits, void* stream);
+/* The same with the binarised flag in its own float (flag[0]): the loss is then a 1-element
+ * buffer of its own (the 0-dim autograd output, no select and its backward's fill + copy). */
+int msu_dynloss_fwd2(int dtype, const void* logits, const float* target, int B, long N,
+                     float alpha, float beta, float mix, float* part, int nblk, float* loss, float* flag,
+                     float* coef, void* stream);
+int msu_dynloss_bwd2(int dtype, const void* logits, const float* target, const float* coef,
+                     const float* flag, const float* gout, int B, long N, float alpha, float beta,
+                     float mix, float* dlogits, void* stream);
 
 /* Validation metrics (scripts/validation_functions.py:37-309): per image, p = sigmoid(logit),
  * pred_bin = p > threshold (:106-107), gt = label > 0 (:108).  out [B][12] f64 = sum(p g),

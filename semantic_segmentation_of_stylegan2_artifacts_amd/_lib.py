@@ -30,6 +30,7 @@ SIGNATURES = {
     "msu_conv_mode": (I, [I]),
     "msu_head_fwd": (I, [I, P, P, P, P, P, P, P, L, I, F, P]),
     "msu_head_bwd": (I, [I, P, P, P, P, P, P, P, P, P, I, P, P, P, L, I, P]),
+    "msu_head_bwd2": (I, [I, P, P, P, P, P, P, P, P, P, I, P, P, P, L, I, I, P]),
     "msu_win_count": (L, [I, I, I]),
     "msu_win_attn_fwd_workspace": (L, [I, I, I]),
     "msu_win_attn_keep_words": (L, [I, I, I, I, I]),
@@ -52,6 +53,8 @@ SIGNATURES = {
     "msu_dynloss_nblk": (I, [L]),
     "msu_dynloss_fwd": (I, [I, P, P, I, L, F, F, F, P, I, P, P, P]),
     "msu_dynloss_bwd": (I, [I, P, P, P, P, P, I, L, F, F, F, P, P]),
+    "msu_dynloss_fwd2": (I, [I, P, P, I, L, F, F, F, P, I, P, P, P, P]),
+    "msu_dynloss_bwd2": (I, [I, P, P, P, P, P, I, L, F, F, F, P, P]),
     "msu_adamw": (I, [P, P, P, P, L, F, F, F, F, F, I, P, P, P]),
     "msu_nonfinite": (I, [P, L, P, P]),
     "msu_nonfinite2": (I, [P, L, P, L, P, P]),
@@ -67,6 +70,7 @@ SIGNATURES = {
     "msu_conv3x3_dgrad": (I, [I, I, P, P, P, P, I, I, I, I, I, P]),
     "msu_conv3x3_wgrad_workspace": (L, [I, I, I, I, I]),
     "msu_conv3x3_wgrad": (I, [I, I, P, P, P, P, P, P, I, I, I, I, I, I, P]),
+    "msu_conv3x3_wgrad2": (I, [I, I, P, P, P, P, P, I, I, I, I, I, I, I, P]),
     "msu_wgrad_splits": (I, [L, I, I]),
     "msu_wgrad_workspace": (L, [L, I, I]),
     "msu_linear_wgrad": (I, [I, P, P, P, P, P, L, I, I, I, P]),

@@ -1366,14 +1366,15 @@ __global__ void __launch_bounds__(768) conv3x3_wgrad_v2_kernel(const bf16_t* __r
 
 // chunk-summed partial [dy][co][dx][ci] -> dW[co][ci][3][3] (torch Conv2d layout)
 __global__ void __launch_bounds__(256) wgrad_permute_kernel(const float* __restrict__ sum, int Cout, int Cin,
-                                                            int CinP, float* __restrict__ dW) {
+                                                            int CinP, float* __restrict__ dW, int accumulate) {
   const long n = (long)Cout * Cin * 9;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i < n) {
     const int co = (int)(i / (Cin * 9));
     const int rem = (int)(i - (long)co * Cin * 9);
     const int ci = rem / 9, tap = rem % 9, dy = tap / 3, dx = tap % 3;
-    dW[i] = sum[((long)dy * Cout * 3 + (long)co * 3 + dx) * CinP + ci];
+    const float v = sum[((long)dy * Cout * 3 + (long)co * 3 + dx) * CinP + ci];
+    dW[i] = accumulate ? dW[i] + v : v;
   }
 }
 

@@ -10,11 +10,11 @@ long msu_conv3x3_wgrad_workspace(int nchunk, int Cin, int Cout, int dtype, int u
   return (long)(nchunk + 1) * 3 * Cout * 3 * CinP + (long)nchunk * Cout;
 }
 
-// dW [Cout][Cin][3][3] f32 and db [Cout] f32 (db may be null).  in_mode as in fwd.
-int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, float* dW, float* db,
-                      float* workspace, void* unused, int nchunk, int B, int H, int W, int Cin,
-                      int Cout, void* stream) {
-  (void)unused;
+// dW [Cout][Cin][3][3] f32 and db [Cout] f32 (db may be null), overwritten or (accumulate != 0)
+// added to.  in_mode as in fwd.
+int msu_conv3x3_wgrad2(int dtype, int in_mode, const void* X, const void* dY, float* dW, float* db,
+                       float* workspace, int nchunk, int B, int H, int W, int Cin, int Cout, int accumulate,
+                       void* stream) {
   if (Cout % 16 || Cin % 8 || Cout > 128 || Cin > 128 || nchunk < 1) return -2;
   const ConvGeom g = make_geom(B, H, W, Cin, Cout, msu_is16(dtype) ? 2 : 4);
   hipStream_t st = (hipStream_t)stream;
@@ -54,11 +54,19 @@ int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, flo
   const long slab = 3L * Cout * 3 * g.CinP;
   float* sum = dbpart + (long)nchunk * Cout;
   const ColSeg segs[2] = {{part, slab, slab, sum}, {dbpart, Cout, Cout, db}};
-  colsum_multi(segs, db ? 2 : 1, nchunk, 0, st);
+  // (the slab sum is workspace, always overwritten; db and the permuted dW accumulate)
+  colsum_multi(segs, db ? 2 : 1, nchunk, 0, st, accumulate ? 2 : 0);
   const long n = (long)Cout * Cin * 9;
   hipLaunchKernelGGL(wgrad_permute_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, sum, Cout, Cin,
-                     g.CinP, dW);
+                     g.CinP, dW, accumulate);
   return MSU_CHECK_LAUNCH();
+}
+
+int msu_conv3x3_wgrad(int dtype, int in_mode, const void* X, const void* dY, float* dW, float* db,
+                      float* workspace, void* unused, int nchunk, int B, int H, int W, int Cin,
+                      int Cout, void* stream) {
+  (void)unused;
+  return msu_conv3x3_wgrad2(dtype, in_mode, X, dY, dW, db, workspace, nchunk, B, H, W, Cin, Cout, 0, stream);
 }
 
 }  // extern "C"

@@ -134,7 +134,8 @@ MSU_DEV double wave_sum_d(double v) {
 
 __global__ void __launch_bounds__(512) dynloss_final_kernel(const float* part, int B, int nblk, long N,
                                                             float alpha, float beta, float mix,
-                                                            float smooth, float* loss, float* coef) {
+                                                            float smooth, float* loss, float* flag,
+                                                            float* coef) {
   __shared__ int binarise;
   __shared__ double sums[64][5];  // B <= 64
   __shared__ float wmax[8];
@@ -180,18 +181,18 @@ __global__ void __launch_bounds__(512) dynloss_final_kernel(const float* part, i
       }
     }
     loss[0] = (float)(total / B);
-    loss[1] = (float)binarise;
+    flag[0] = (float)binarise;
   }
 }
 
 template <typename T>
 __global__ void __launch_bounds__(256) dynloss_bwd_kernel(const T* logits, const float* target,
-                                                          const float* coef, const float* flags,
+                                                          const float* coef, const float* flag,
                                                           const float* gout, long N, int B,
                                                           float alpha, float beta, float mix,
                                                           float* dlogits) {
   const long total = N * B;
-  const bool bin = flags[1] != 0.f;
+  const bool bin = flag[0] != 0.f;
   const float g = gout ? gout[0] / B : 1.f / B;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const int b = (int)(i / N);
@@ -416,28 +417,41 @@ int msu_dynloss_nblk(long N) {
   return (int)(nb < 1 ? 1 : nb);
 }
 
-// loss[0] = loss value, loss[1] = binarised flag; coef [B*4]; part [B*nblk*12]
-int msu_dynloss_fwd(int dtype, const void* logits, const float* target, int B, long N,
-                    float alpha, float beta, float mix, float* part, int nblk, float* loss,
-                    float* coef, void* stream) {
+// loss[0] = loss value, flag[0] = binarised flag; coef [B*4]; part [B*nblk*12]
+int msu_dynloss_fwd2(int dtype, const void* logits, const float* target, int B, long N,
+                     float alpha, float beta, float mix, float* part, int nblk, float* loss, float* flag,
+                     float* coef, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(dynloss_partial_kernel<T>, dim3(nblk, B), dim3(256), 0, st,
                                             (const T*)logits, target, N, nblk, part));
   if (B > 64) return -2;
   hipLaunchKernelGGL(dynloss_final_kernel, dim3(1), dim3(512), 0, st, part, B, nblk, N, alpha, beta,
-                     mix, 1e-6f, loss, coef);
+                     mix, 1e-6f, loss, flag, coef);
+  return MSU_CHECK_LAUNCH();
+}
+
+// loss[0] = loss value, loss[1] = binarised flag
+int msu_dynloss_fwd(int dtype, const void* logits, const float* target, int B, long N,
+                    float alpha, float beta, float mix, float* part, int nblk, float* loss,
+                    float* coef, void* stream) {
+  return msu_dynloss_fwd2(dtype, logits, target, B, N, alpha, beta, mix, part, nblk, loss, loss + 1, coef, stream);
+}
+
+int msu_dynloss_bwd2(int dtype, const void* logits, const float* target, const float* coef,
+                     const float* flag, const float* gout, int B, long N, float alpha, float beta,
+                     float mix, float* dlogits, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long n = (long)B * N;
+  MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(dynloss_bwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st,
+                                            (const T*)logits, target, coef, flag, gout, N, B, alpha, beta, mix,
+                                            dlogits));
   return MSU_CHECK_LAUNCH();
 }
 
 int msu_dynloss_bwd(int dtype, const void* logits, const float* target, const float* coef,
                     const float* loss, const float* gout, int B, long N, float alpha, float beta,
                     float mix, float* dlogits, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-  const long n = (long)B * N;
-  MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(dynloss_bwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st,
-                                            (const T*)logits, target, coef, loss, gout, N, B, alpha, beta, mix,
-                                            dlogits));
-  return MSU_CHECK_LAUNCH();
+  return msu_dynloss_bwd2(dtype, logits, target, coef, loss + 1, gout, B, N, alpha, beta, mix, dlogits, stream);
 }
 
 int msu_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,

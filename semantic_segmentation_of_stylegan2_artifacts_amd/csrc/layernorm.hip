@@ -920,10 +920,10 @@ int msu_head_fwd(int dtype, const void* z, const float* gamma, const float* beta
 }
 
 // grads: dgamma, dbeta, dw (each [C]); part [nparts, 3, C]
-int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gamma,
-                 const float* beta, const float* w, const float* mean, const float* rstd, void* dz,
-                 float* part, int nparts, float* dgamma, float* dbeta, float* dw, long rows, int C,
-                 void* stream) {
+int msu_head_bwd2(int dtype, const float* dlogit, const void* z, const float* gamma,
+                  const float* beta, const float* w, const float* mean, const float* rstd, void* dz,
+                  float* part, int nparts, float* dgamma, float* dbeta, float* dw, long rows, int C,
+                  int accumulate, void* stream) {
   if (C % 4 || C > 256) return -2;
   if (rows == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
@@ -937,12 +937,20 @@ int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gam
       else hipLaunchKernelGGL((head_bwd_kernel<T, 8>), dim3(nparts), dim3(256), 0, st, dlogit, (const T*)z, gamma, beta, w, mean, rstd, (T*)dz, part, rows, C));
   }
   if (dbeta == dgamma + C && dw == dgamma + 2 * C) {  // contiguous [dgamma | dbeta | dw]
-    colsum(part, nparts, 3L * C, 3L * C, dgamma, 0, st);
+    colsum(part, nparts, 3L * C, 3L * C, dgamma, accumulate, st);
   } else {
     const ColSeg segs[3] = {{part, C, 3L * C, dgamma}, {part + C, C, 3L * C, dbeta}, {part + 2 * C, C, 3L * C, dw}};
-    colsum_multi(segs, 3, nparts, 0, st);
+    colsum_multi(segs, 3, nparts, accumulate, st);
   }
   return MSU_CHECK_LAUNCH();
+}
+
+int msu_head_bwd(int dtype, const float* dlogit, const void* z, const float* gamma,
+                 const float* beta, const float* w, const float* mean, const float* rstd, void* dz,
+                 float* part, int nparts, float* dgamma, float* dbeta, float* dw, long rows, int C,
+                 void* stream) {
+  return msu_head_bwd2(dtype, dlogit, z, gamma, beta, w, mean, rstd, dz, part, nparts, dgamma, dbeta, dw, rows, C,
+                       0, stream);
 }
 
 int msu_ln_part_blocks(long rows, int C) {

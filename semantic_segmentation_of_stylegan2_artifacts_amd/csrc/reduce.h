@@ -31,7 +31,7 @@ struct ColSegs {
 
 // V = floats per thread (4: 16-B loads; needs n, stride and pointers 16-B aligned)
 template <int PL, int V>
-__global__ void __launch_bounds__(256) colsum_kernel(ColSegs sg, int nparts, int accumulate) {
+__global__ void __launch_bounds__(256) colsum_kernel(ColSegs sg, int nparts, int accmask) {
   constexpr int NC = 256 / PL;
   typedef float vec __attribute__((ext_vector_type(V)));
   __shared__ vec red[PL][NC + (V == 1 ? 1 : 0)];
@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(256) colsum_kernel(ColSegs sg, int nparts, int
     const long rl = sg.rowlen[seg];
     const long oi = rl == n ? i : (i / rl) * sg.ldo[seg] + (i - (i / rl) * rl);
     vec* o = reinterpret_cast<vec*>(out + oi);
-    *o = accumulate ? *o + t : t;
+    *o = (accmask >> seg) & 1 ? *o + t : t;  // bit j: segment j adds to its output
   }
 }
 
@@ -78,7 +78,10 @@ struct ColSeg {
   long ldo = 0;
 };
 
-inline void colsum_multi(const ColSeg* segs, int nseg, int nparts, int accumulate, hipStream_t st) {
+// accumulate != 0: every segment adds to its output; acc_mask >= 0 instead picks them (bit j: segment j)
+inline void colsum_multi(const ColSeg* segs, int nseg, int nparts, int accumulate, hipStream_t st,
+                         int acc_mask = -1) {
+  const int accmask = acc_mask >= 0 ? acc_mask : (accumulate ? 7 : 0);
   bool v4 = true;
   long total = 0;
   for (int j = 0; j < nseg; ++j) {
@@ -108,13 +111,13 @@ inline void colsum_multi(const ColSeg* segs, int nseg, int nparts, int accumulat
   sg.nseg = nseg;
   if (blocks == 0) return;
   if (V == 4) {
-    if (PL == 128) hipLaunchKernelGGL((colsum_kernel<128, 4>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
-    else if (PL == 32) hipLaunchKernelGGL((colsum_kernel<32, 4>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
-    else hipLaunchKernelGGL((colsum_kernel<8, 4>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
+    if (PL == 128) hipLaunchKernelGGL((colsum_kernel<128, 4>), dim3(blocks), dim3(256), 0, st, sg, nparts, accmask);
+    else if (PL == 32) hipLaunchKernelGGL((colsum_kernel<32, 4>), dim3(blocks), dim3(256), 0, st, sg, nparts, accmask);
+    else hipLaunchKernelGGL((colsum_kernel<8, 4>), dim3(blocks), dim3(256), 0, st, sg, nparts, accmask);
   } else {
-    if (PL == 128) hipLaunchKernelGGL((colsum_kernel<128, 1>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
-    else if (PL == 32) hipLaunchKernelGGL((colsum_kernel<32, 1>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
-    else hipLaunchKernelGGL((colsum_kernel<8, 1>), dim3(blocks), dim3(256), 0, st, sg, nparts, accumulate);
+    if (PL == 128) hipLaunchKernelGGL((colsum_kernel<128, 1>), dim3(blocks), dim3(256), 0, st, sg, nparts, accmask);
+    else if (PL == 32) hipLaunchKernelGGL((colsum_kernel<32, 1>), dim3(blocks), dim3(256), 0, st, sg, nparts, accmask);
+    else hipLaunchKernelGGL((colsum_kernel<8, 1>), dim3(blocks), dim3(256), 0, st, sg, nparts, accmask);
   }
 }
 

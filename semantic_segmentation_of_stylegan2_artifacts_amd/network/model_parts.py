@@ -334,7 +334,7 @@ class PatchEmbed(nn.Module):
         if self.patch_size[0] != self.patch_size[1]:
             raise ValueError("square patches only")
         cols = ops.patchify(x, self.patch_size[0], ops.act_dtype())
-        t = ops.linear(cols, self.proj.weight.reshape(self.embed_dim, -1), self.proj.bias)
+        t = ops.linear(cols, ops.param_view(self.proj.weight, (self.embed_dim, -1)), self.proj.bias)
         t = t.view(B, self.num_patches, self.embed_dim)
         if self.norm is not None:
             t = ops.layer_norm(t, self.norm.weight, self.norm.bias, self.norm.eps)

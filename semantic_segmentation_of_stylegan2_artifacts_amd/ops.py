@@ -150,6 +150,7 @@ def _guard_side_write(p, ev):
     another gradient into p on the main stream (e.g. the qkv bias: its Linear adds db here,
     the attention op returns the padded tokens' share), that AccumulateGrad must wait for it:
     a tensor hook on p makes the current stream wait for the last such event first."""
+    p = getattr(p, "_msu_param", p)  # a param_view: guard its parameter
     p._msu_side_event = ev
     _side_event_params.append(p)
     if not getattr(p, "_msu_side_hooked", False):
@@ -257,7 +258,24 @@ def _notify(*params):
     if _grad_ready is not None:
         for p in params:
             if p is not None:
-                _grad_ready(p)
+                _grad_ready(getattr(p, "_msu_param", p))
+
+
+def param_view(param, shape):
+    """A reshaped view of a parameter that the ops treat as the parameter itself: a trainer-
+    direct parameter's view carries the viewed .grad (backward kernels add into it), the viewed
+    16-bit shadow and the owner (notified to the gradient bucketer, side-stream guards).  E.g.
+    PatchEmbed's [C, Cin, p, p] conv weight as the [C, Cin*p*p] Linear weight of its im2col GEMM."""
+    v = param.view(shape)
+    if _direct(param):
+        v.grad = param.grad.view(shape)
+        v._msu_direct = True
+        v._msu_param = param
+        sh = getattr(param, "_msu_shadow", None)
+        if sh is not None:
+            v._msu_shadow = sh.view(shape)
+            v._msu_shadow_ver = getattr(param, "_msu_shadow_ver", -1)
+    return v
 
 
 def _ln_grads(ctx, C, device):
@@ -1601,6 +1619,7 @@ def _head_fake(z, gamma, beta, w, eps):
 def _head_setup(ctx, inputs, output):
     z, gamma, beta, w, eps = inputs
     ctx.save_for_backward(z.contiguous(), gamma, beta, w, output[1], output[2])
+    ctx.params = (gamma, beta, w)
     ctx.set_materialize_grads(False)
 
 
@@ -1612,11 +1631,19 @@ def _head_backward(ctx, dlogit, _dm, _dr):
     rows = B * H * W
     dlogit = _f32(dlogit)
     dz = torch.empty_like(z)
-    dg, db, dw = torch.empty(3, C, device=z.device, dtype=torch.float32)  # contiguous: one reduction
+    # trainer-direct gamma / beta / output weight: summed straight into their .grad
+    direct = _direct(*ctx.params)
+    if direct:
+        dg, db, dw = (p.grad for p in ctx.params)
+    else:
+        dg, db, dw = torch.empty(3, C, device=z.device, dtype=torch.float32)  # contiguous: one reduction
     n, part = _ln_parts(rows, C, z.device)
-    _lib.call("msu_head_bwd", _dt(z), _p(dlogit), _p(z), _p(gamma), _p(beta), _p(w), _p(mean),
-              _p(rstd), _p(dz), _p(part), n, _p(dg), _p(db), _p(dw), rows, C, _s(z))
-    return dz, dg, db, dw, None
+    _lib.call("msu_head_bwd2", _dt(z), _p(dlogit), _p(z), _p(gamma), _p(beta), _p(w), _p(mean),
+              _p(rstd), _p(dz), _p(part), n, _p(dg), _p(db), _p(dw), rows, C, int(direct), _s(z))
+    if direct:
+        _notify(*ctx.params)
+        return dz, None, None, None, None
+    return dz, dg, db, dw.view(w.shape), None
 
 
 _head = _define("head_norm_output",
@@ -1629,8 +1656,9 @@ def head_norm_output(z, gamma, beta, out_weight, eps=1e-5):
     z: [B, H, W, C] -> f32 logits [B, 1, H, W]."""
     if out_weight.shape[0] != 1:
         raise ValueError("fused head supports num_classes == 1")
-    C = z.shape[-1]
-    w = _f32(out_weight.reshape(C))
+    # the [1, C, 1, 1] conv weight itself (contiguous: the kernel reads C floats), so a trainer-
+    # direct parameter's .grad is reachable from the backward
+    w = _f32(out_weight).contiguous()
     return _head(_as(z, act_dtype()), _f32(gamma), _f32(beta), w, float(eps))[0]
 
 
@@ -1641,14 +1669,18 @@ def head_norm_output(z, gamma, beta, out_weight, eps=1e-5):
 _CONV_WGRAD_BLOCKS = int(switches.get("MSU_CONV_WGRAD_BLOCKS"))
 
 
-def _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout):
+def _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout, into=None):
+    """(dW, db) of the refine conv; ``into`` = (weight, bias): added to their .grad instead."""
     L = _lib.lib()
     nchunk = _CONV_WGRAD_BLOCKS
     ws = torch.empty(L.msu_conv3x3_wgrad_workspace(nchunk, Cin, Cout, 0, 0), device=a.device, dtype=torch.float32)
-    dw = torch.empty(Cout, Cin, 3, 3, device=a.device, dtype=torch.float32)
-    db = torch.empty(Cout, device=a.device, dtype=torch.float32)
-    _lib.call("msu_conv3x3_wgrad", _dt(a), mode, _p(a), _p(dz), _p(dw), _p(db), _p(ws), None, nchunk,
-              B, H, W, Cin, Cout, _s(a))
+    if into is None:
+        dw = torch.empty(Cout, Cin, 3, 3, device=a.device, dtype=torch.float32)
+        db = torch.empty(Cout, device=a.device, dtype=torch.float32)
+    else:
+        dw, db = into[0].grad, into[1].grad
+    _lib.call("msu_conv3x3_wgrad2", _dt(a), mode, _p(a), _p(dz), _p(dw), _p(db), _p(ws), nchunk,
+              B, H, W, Cin, Cout, 0 if into is None else 1, _s(a))
     return dw, db
 
 
@@ -1667,9 +1699,7 @@ def _conv_wgrad_param(a, dz, mode, B, H, W, Cin, Cout, weight, bias):
     side = _side_stream_for(a.device)
     side.wait_stream(main)
     with torch.cuda.stream(side):
-        dw, db = _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout)
-        weight.grad.add_(dw)
-        bias.grad.add_(db)
+        _conv_wgrad(a, dz, mode, B, H, W, Cin, Cout, into=(weight, bias))
     for t in (a, dz):
         t.record_stream(side)
         _side_keep.append(t)
@@ -1907,15 +1937,17 @@ def _dynloss_impl(logits, target, alpha, beta, mix):
     L = _lib.lib()
     nblk = L.msu_dynloss_nblk(N)
     part = torch.empty(B * nblk * 12, device=logits.device, dtype=torch.float32)
-    out = torch.empty(2, device=logits.device, dtype=torch.float32)
-    coef = torch.empty(B * 4, device=logits.device, dtype=torch.float32)
-    _lib.call("msu_dynloss_fwd", _dt(logits), _p(logits), _p(target), B, N, alpha, beta, mix,
-              _p(part), nblk, _p(out), _p(coef), _s(logits))
+    # the loss is a 0-dim output of its own (no select after the op: its backward would fill and
+    # copy); coef [4B] plus the binarised flag in its last float
+    out = torch.empty((), device=logits.device, dtype=torch.float32)
+    coef = torch.empty(B * 4 + 1, device=logits.device, dtype=torch.float32)
+    _lib.call("msu_dynloss_fwd2", _dt(logits), _p(logits), _p(target), B, N, alpha, beta, mix,
+              _p(part), nblk, _p(out), coef.data_ptr() + 16 * B, _p(coef), _s(logits))
     return out, coef
 
 
 def _dynloss_fake(logits, target, alpha, beta, mix):
-    return logits.new_empty(2, dtype=torch.float32), logits.new_empty(logits.shape[0] * 4, dtype=torch.float32)
+    return logits.new_empty((), dtype=torch.float32), logits.new_empty(logits.shape[0] * 4 + 1, dtype=torch.float32)
 
 
 def _dynloss_setup(ctx, inputs, output):
@@ -1934,10 +1966,10 @@ def _dynloss_backward(ctx, g, _gc):
         return None, None, None, None, None
     B = logits.shape[0]
     N = logits[0].numel()
-    g = _f32(g.reshape(-1)[:1])  # d loss_vec: only element 0 (the loss) is used downstream
+    g = _f32(g.reshape(1))
     dl = torch.empty(logits.shape, device=logits.device, dtype=torch.float32)
-    _lib.call("msu_dynloss_bwd", _dt(logits), _p(logits), _p(target), _p(coef), _p(out), _p(g), B, N,
-              alpha, beta, mix, _p(dl), _s(logits))
+    _lib.call("msu_dynloss_bwd2", _dt(logits), _p(logits), _p(target), _p(coef), coef.data_ptr() + 16 * B,
+              _p(g), B, N, alpha, beta, mix, _p(dl), _s(logits))
     return dl.to(logits.dtype), None, None, None, None
 
 
@@ -1955,8 +1987,7 @@ def dynamic_loss(logits, target, alpha, beta, mix):
         raise ValueError(f"target shape {tuple(target.shape)} does not match output {tuple(logits.shape)}")
     if logits.dtype not in _DT:
         logits = logits.float()
-    out, _ = _dynamic_loss(logits, target, float(alpha), float(beta), float(mix))
-    return out[0]
+    return _dynamic_loss(logits, target, float(alpha), float(beta), float(mix))[0]
 
 
 # ----------------------------------------------------------------------------- optimizer

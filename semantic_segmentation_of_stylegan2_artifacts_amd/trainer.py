@@ -359,6 +359,15 @@ class Trainer:
         # reverse registration order ~ gradient-ready order during backward
         self.groups = [FlatGroup(decay[::-1], config.TRAIN.WEIGHT_DECAY, device),
                        FlatGroup(no_decay[::-1], 0.0, device)]
+        # the dead branches' parameters are never updated: one 16-bit shadow each for the run, so
+        # their no-grad forwards (side stream) read it instead of casting every weight every step
+        # (16 cast launches per step at Swin-T); a write through the parameter (load_state_dict)
+        # bumps its version and the ops cast it again (ops._shadow)
+        for m in (core.dead_modules() if hasattr(core, "dead_modules") else []):
+            for p in m.parameters():
+                if p.is_floating_point() and p.dim() >= 2 and p.device.type == "cuda":
+                    p._msu_shadow = p.detach().to(amp_dtype)
+                    p._msu_shadow_ver = p._version
         opt = config.TRAIN.OPTIMIZER
         self.betas = tuple(opt.BETAS)
         self.eps = float(opt.EPS)
@@ -370,6 +379,7 @@ class Trainer:
         # NaN leaves parameters and moments untouched
         self.skip_nonfinite = skip_nonfinite
         self.found_inf = torch.zeros(1, device=device, dtype=torch.float32)
+        self._one = torch.ones((), device=device, dtype=torch.float32)
         t = config.TRAIN
         self.loss_fn = DynamicLoss(alpha=t.TVERSKY_LOSS_ALPHA, beta=t.TVERSKY_LOSS_BETA,
                                    tversky_bce_mix=t.LOSS_TVERSKY_BCE_MIX)
@@ -536,7 +546,7 @@ class Trainer:
         if self.reducer is not None and torch.device(self.device).type == "cuda":
             self.reducer.main_stream = torch.cuda.current_stream(self.device)
         loss = self.forward_loss(images, labels)
-        loss.backward()
+        loss.backward(self._one)  # a persistent seed: no ones_like fill per step
         if self.reducer is not None:
             self.reducer.finish()
         ops.join_side_streams()  # weight gradients issued on the side stream

@@ -343,6 +343,28 @@ def test_conv_weight_layouts(Cout, Cin, dtype):
     assert torch.equal(ops._conv_weight(w, dtype, 1), wf)
 
 
+@pytest.mark.parametrize("mode", [0, 2], ids=["plain", "d2s"])
+@pytest.mark.parametrize("C", [96, 64])
+def test_conv_wgrad_accumulate_equals_add(C, mode):
+    """msu_conv3x3_wgrad2 with accumulate: dW / db added into existing f32 gradients bitwise equal
+    to the overwrite form followed by an f32 add (the side stream's .grad accumulation)."""
+    ops = _ops()
+    g = _g(C + mode)
+    B, H, W = 2, 32, 32
+    xs = (B, H // 4, W // 4, 16 * C) if mode == 2 else (B, H, W, C)
+    a = torch.randn(xs, generator=g).to(DEV, torch.bfloat16)
+    dz = torch.randn(B, H, W, C, generator=g).to(DEV, torch.bfloat16)
+    w0 = torch.randn(C, C, 3, 3, generator=g).to(DEV)
+    b0 = torch.randn(C, generator=g).to(DEV)
+    dw, db = ops._conv_wgrad(a, dz, mode, B, H, W, C, C)
+    w, b = torch.nn.Parameter(w0.clone()), torch.nn.Parameter(b0.clone())
+    w.grad, b.grad = w0.clone(), b0.clone()
+    ops._conv_wgrad(a, dz, mode, B, H, W, C, C, into=(w, b))
+    torch.cuda.synchronize()
+    assert torch.equal(w.grad, w0 + dw)
+    assert torch.equal(b.grad, b0 + db)
+
+
 @pytest.mark.parametrize("B,H,W,C,d2s", CONV_CASES)
 @pytest.mark.parametrize("dtype", ALL)
 def test_refine_conv(B, H, W, C, d2s, dtype):
@@ -476,6 +498,37 @@ def test_head_norm_output(dtype, C, W):
     _close(gg.grad, gr.grad, tol, tol, "dgamma")
     _close(bg.grad, btr.grad, tol, tol, "dbeta")
     _close(wg.grad, wr.grad, tol, tol, "dw_out")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_head_direct_params_accumulate_into_grad(dtype):
+    """Trainer-direct gamma / beta / output weight: the head backward adds its sums into the
+    existing .grad (msu_head_bwd2, accumulate) -- bitwise the autograd gradients added to it; dz
+    bitwise."""
+    ops = _ops()
+    g = _g(8)
+    B, H, W, C = 2, 16, 13, 96
+    z = torch.randn(B, H, W, C, generator=g).to(DEV, dtype)
+    p0 = [(1 + 0.1 * torch.randn(C, generator=g)).to(DEV), (0.1 * torch.randn(C, generator=g)).to(DEV),
+          (torch.randn(1, C, 1, 1, generator=g) / math.sqrt(C)).to(DEV)]
+    g0 = [torch.randn(t.shape, generator=g).to(DEV) for t in p0]
+    dl = torch.randn(B, 1, H, W, generator=g).to(DEV)
+    res = {}
+    for direct in (False, True):
+        ps = [torch.nn.Parameter(t.clone()) for t in p0]
+        if direct:
+            for p, g1 in zip(ps, g0):
+                p.grad = g1.clone()
+                p._msu_direct = True
+        zg = z.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=dtype):
+            y = ops.head_norm_output(zg, *ps)
+        y.backward(dl)
+        torch.cuda.synchronize()
+        res[direct] = (zg.grad, [p.grad if direct else g1 + p.grad for p, g1 in zip(ps, g0)])
+    assert torch.equal(res[True][0], res[False][0])
+    for a, b in zip(res[True][1], res[False][1]):
+        assert torch.equal(a, b)
 
 
 def test_patchify_matches_conv():
