@@ -1840,6 +1840,22 @@ def refine_conv_act(x, a, weight, bias, d2s, out_hw, dual=False):
     return (z, z2) if dual else z
 
 
+_zero_bias_cache = {}
+
+
+def _zero_bias(N, device):
+    """A persistent f32 zero vector (the GELU-dual epilogue needs a bias; the expand Linear has
+    none): filled once, not per call.  Inside a graph capture the fill would only be recorded,
+    so a capture that finds none takes a fresh (captured) one instead of caching it."""
+    key = (N, str(device))
+    z = _zero_bias_cache.get(key)
+    if z is None:
+        z = torch.zeros(N, device=device, dtype=torch.float32)
+        if not torch.cuda.is_current_stream_capturing():
+            _zero_bias_cache[key] = z
+    return z
+
+
 def _linear_gelu_impl(x, weight):
     """y = x . W^T (no bias) and the non-differentiable GELU(y) from the same epilogue
     (FinalPatchExpand_X4_V2.expand -> act, model_parts.py:458-460); the activation gradient is
@@ -1850,7 +1866,7 @@ def _linear_gelu_impl(x, weight):
     N, K = w.shape
     M = x.numel() // K
     if dt in _LOW and gemm_route(M, N, K, TOK_GELU_DUAL) != "lib":
-        return _gemm(x, w, torch.zeros(N, device=x.device, dtype=torch.float32), TOK_GELU_DUAL)
+        return _gemm(x, w, _zero_bias(N, x.device), TOK_GELU_DUAL)
     with torch.autocast("cuda", enabled=False):
         y = torch.nn.functional.linear(x, w)
     g = torch.empty_like(y)
