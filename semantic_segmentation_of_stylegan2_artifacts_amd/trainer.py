@@ -631,6 +631,13 @@ class Trainer:
         self._sx = images.detach().clone()
         self._sy = labels.detach().clone()
         torch.cuda.synchronize(self.device)
+        if self.reducer is not None and dist.is_initialized():
+            # the process group's watchdog thread polls its eager works' events every ~100 ms;
+            # one it has not retired yet, queried while the capture below holds the RCCL stream,
+            # can fail with hipErrorCapturedEvent and terminate the process (seen once in the
+            # r06ah suite, in a process's third capture).  The warmup's works are complete
+            # (synchronize above): give the watchdog a few polls to drop them first
+            time.sleep(0.3)
         graph = torch.cuda.CUDAGraph()
         # The captured step is single-stream: with the weight-gradient / dead-branch side
         # stream forked into the capture, the ROCm 7.2 graph executor's parallel branches gave
