@@ -69,6 +69,13 @@ for s in "$@"; do
     # single-stream graph replay; the profile must show the eager step the bench line measures
     prof) MSU_GRAPH=0 step prof 420 rocprofv3 --kernel-trace --stats -d $O/${TAG}_prof -o p --output-format csv -- \
             python3 $R/bench.py --steps 8 --warmup 4 --no-roofline --no-cpu-baseline --no-input-pipeline ;;
+    # the bench command itself under the profiler (roofline included): the roofline kernel's
+    # launches in the trace against the bench line's HIP-event time
+    bprof) step bprof 600 rocprofv3 --kernel-trace --stats -d $O/${TAG}_bprof -o p --output-format csv -- \
+             python3 $R/bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-input-pipeline
+           grep '^{' $O/${TAG}_bprof.log > $O/${TAG}_bprof.json
+           python3 $R/tools/roofline_trace.py $O/${TAG}_bprof/p_kernel_trace.csv $O/${TAG}_bprof.json > $O/${TAG}_roofline_trace.txt
+           cat $O/${TAG}_roofline_trace.txt ;;
     conv_pmc)
       timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $O/${TAG}_pmcconv -o conv_fetch --output-format csv -- python3 $R/tools/conv_one.py 0 3 fwd act > /dev/null 2>&1 || exit 3
       timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d $O/${TAG}_pmcconv -o conv_write --output-format csv -- python3 $R/tools/conv_one.py 0 3 fwd act > /dev/null 2>&1 || exit 3
