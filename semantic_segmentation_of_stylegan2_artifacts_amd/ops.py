@@ -2023,6 +2023,13 @@ def nonfinite_(x, flag, x2=None):
         _lib.call("msu_nonfinite2", _p(x), x.numel(), _p(x2), x2.numel(), _p(flag), _s(x))
 
 
+def nonfinite_set_(x, flag, x2=None):
+    """flag[0] = 1. if x (or x2) holds an inf / NaN, else 0. (written by the check itself: no
+    zeroing launch before it)."""
+    n2 = 0 if x2 is None else x2.numel()
+    _lib.call("msu_nonfinite_set", _p(x), x.numel(), _p(x2), n2, _p(flag), _s(x))
+
+
 def adamw_dev_(param, grad, exp_avg, exp_avg_sq, hyper, beta1, beta2, eps, weight_decay, inv_scale=None,
                found_inf=None, shadow=None, zero_grad=False):
     """AdamW over flat f32 buffers with lr and step read from the device tensor
