@@ -355,9 +355,6 @@ int msu_step_advance(double* hyper, const float* found_inf, void* stream);
  * (GradScaler's non-finite check, torch._amp_foreach_non_finite_check_and_unscale_). */
 int msu_nonfinite(const float* x, long n, float* flag, void* stream);
 int msu_nonfinite2(const float* x0, long n0, const float* x1, long n1, float* flag, void* stream);
-/* The same, writing flag[0] = 1 or 0 itself (no zeroing before it): the launch's last block sets it.
- * One such launch at a time per device (a device-wide block counter). */
-int msu_nonfinite_set(const float* x0, long n0, const float* x1, long n1, float* flag, void* stream);
 int msu_cast(int dtype, const float* x, void* y, long n, void* stream);
 /* The refine conv's f32 weight W [Cout][Cin][3][3] (model_parts.py:447-448) in the conv kernels'
  * layouts, in the activation dtype: flip 0 -> Wt of msu_conv3x3_fwd/_fwd2 [9][Cout][roundup(Cin,32)];

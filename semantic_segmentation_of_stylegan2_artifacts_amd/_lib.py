@@ -58,7 +58,6 @@ SIGNATURES = {
     "msu_adamw": (I, [P, P, P, P, L, F, F, F, F, F, I, P, P, P]),
     "msu_nonfinite": (I, [P, L, P, P]),
     "msu_nonfinite2": (I, [P, L, P, L, P, P]),
-    "msu_nonfinite_set": (I, [P, L, P, L, P, P]),
     "msu_adamw_dev": (I, [P, P, P, P, L, P, D, D, D, D, P, P, P]),
     "msu_adamw_dev2": (I, [P, P, P, P, L, P, D, D, D, D, P, P, P, I, I, P]),
     "msu_step_advance": (I, [P, P, P]),

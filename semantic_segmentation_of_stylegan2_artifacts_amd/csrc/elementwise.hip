@@ -291,36 +291,6 @@ __global__ void __launch_bounds__(256) nonfinite2_kernel(const float* x0, long n
   if (__any(bad) && (threadIdx.x & 63) == 0) flag[0] = 1.f;
 }
 
-// flag[0] = 1.f / 0.f: whether x0 / x1 hold an inf or NaN, written (not or-ed) by the launch's
-// last block, so no zeroing launch is needed before it.  Blocks that saw a non-finite value bump
-// a device counter; the last block to finish reads it, writes the flag and resets both counters
-// (one launch at a time per device: the trainer's main stream).
-__device__ unsigned g_nonfinite_cnt[2];  // [blocks finished, blocks that saw a non-finite]
-
-__global__ void __launch_bounds__(256) nonfinite_set_kernel(const float* x0, long n0, const float* x1, long n1,
-                                                            float* flag) {
-  __shared__ int sbad;
-  if (threadIdx.x == 0) sbad = 0;
-  __syncthreads();
-  bool bad = false;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n0 + n1; i += (long)gridDim.x * 256)
-    bad |= !isfinite(i < n0 ? x0[i] : x1[i - n0]);
-  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&sbad, 1);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (sbad) atomicAdd(&g_nonfinite_cnt[1], 1u);
-    __threadfence();
-    const unsigned done = atomicAdd(&g_nonfinite_cnt[0], 1u);
-    if (done == gridDim.x - 1) {
-      __threadfence();
-      const unsigned nbad = atomicAdd(&g_nonfinite_cnt[1], 0u);
-      flag[0] = nbad ? 1.f : 0.f;
-      atomicExch(&g_nonfinite_cnt[1], 0u);
-      atomicExch(&g_nonfinite_cnt[0], 0u);
-    }
-  }
-}
-
 // any non-finite in x -> flag[0] = 1 (flag must be zeroed by the caller)
 __global__ void __launch_bounds__(256) nonfinite_kernel(const float* x, long n, float* flag) {
   bool bad = false;
@@ -536,16 +506,6 @@ int msu_step_advance(double* hyper, const float* found_inf, void* stream) {
 int msu_nonfinite2(const float* x0, long n0, const float* x1, long n1, float* flag, void* stream) {
   if (n0 + n1 == 0) return 0;
   hipLaunchKernelGGL(nonfinite2_kernel, dim3(grid_for(n0 + n1, 256, 16384)), dim3(256), 0, (hipStream_t)stream,
-                     x0, n0, x1, n1, flag);
-  return MSU_CHECK_LAUNCH();
-}
-
-int msu_nonfinite_set(const float* x0, long n0, const float* x1, long n1, float* flag, void* stream) {
-  if (n0 + n1 == 0) {
-    (void)hipMemsetAsync(flag, 0, sizeof(float), (hipStream_t)stream);
-    return MSU_CHECK_LAUNCH();
-  }
-  hipLaunchKernelGGL(nonfinite_set_kernel, dim3(grid_for(n0 + n1, 256, 16384)), dim3(256), 0, (hipStream_t)stream,
                      x0, n0, x1, n1, flag);
   return MSU_CHECK_LAUNCH();
 }

@@ -986,13 +986,16 @@ def _gelu16(h):
     return g
 
 
-def _wgrad(dy, x, weight, bias, M, N, K, x_gelu_of=None):
+def _wgrad(dy, x, weight, bias, M, N, K, x_gelu_of=None, side_ok=True):
     """Linear weight/bias gradients on msu_linear_wgrad; (None, None) when accumulated
     straight into the trainer's flat .grad views.  x None: x = GELU(x_gelu_of), derived on the
-    stream the weight gradient runs on."""
+    stream the weight gradient runs on.  side_ok False: on the main stream even with direct
+    parameters (a Linear whose input needs no gradient -- PatchEmbed's, the last node of backward:
+    nothing is left on the main stream to overlap it, and behind the side stream's queue it would
+    only delay the end-of-backward join)."""
     L = _lib.lib()
     if _direct(weight) and (bias is None or _direct(bias)):
-        if _side_enabled and _side_wgrad:
+        if _side_enabled and _side_wgrad and side_ok:
             src = x if x is not None else x_gelu_of
             main = torch.cuda.current_stream(src.device)
             side = _side_stream_for(src.device)
@@ -1210,7 +1213,7 @@ def _linear_grads(ctx, dy):
         dx = None  # x's gradient goes to its keyed LayerNorm's backward kernel
     if not (ctx.needs_input_grad[1] or (bias is not None and ctx.needs_input_grad[2])):
         return dx, None, None  # frozen weight and bias: no weight-gradient work at all
-    dw, db = _wgrad(dy, x, weight, bias, M, N, K)
+    dw, db = _wgrad(dy, x, weight, bias, M, N, K, side_ok=ctx.needs_input_grad[0])
     return dx, dw, db
 
 
@@ -2021,13 +2024,6 @@ def nonfinite_(x, flag, x2=None):
         _lib.call("msu_nonfinite", _p(x), x.numel(), _p(flag), _s(x))
     else:
         _lib.call("msu_nonfinite2", _p(x), x.numel(), _p(x2), x2.numel(), _p(flag), _s(x))
-
-
-def nonfinite_set_(x, flag, x2=None):
-    """flag[0] = 1. if x (or x2) holds an inf / NaN, else 0. (written by the check itself: no
-    zeroing launch before it)."""
-    n2 = 0 if x2 is None else x2.numel()
-    _lib.call("msu_nonfinite_set", _p(x), x.numel(), _p(x2), n2, _p(flag), _s(x))
 
 
 def adamw_dev_(param, grad, exp_avg, exp_avg_sq, hyper, beta1, beta2, eps, weight_decay, inv_scale=None,

@@ -564,7 +564,8 @@ class Trainer:
             # after the all-reduce: an inf on any rank reaches every rank's sum, so all ranks
             # skip together (an f16-wire overflow included: it must never reach AdamW)
             found = self.found_inf
-            ops.nonfinite_set_(self.groups[0].grad, found, self.groups[1].grad)  # writes 0 or 1
+            found.zero_()
+            ops.nonfinite_(self.groups[0].grad, found, self.groups[1].grad)
             if wire_scaled:
                 self.reducer.update_scale(found)
         ops.step_advance_(self.hyper, found)
