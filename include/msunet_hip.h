@@ -318,6 +318,11 @@ int msu_dynloss_fwd2(int dtype, const void* logits, const float* target, int B, 
 int msu_dynloss_bwd2(int dtype, const void* logits, const float* target, const float* coef,
                      const float* flag, const float* gout, int B, long N, float alpha, float beta,
                      float mix, float* dlogits, void* stream);
+/* fwd2 that also sets zero_out[0] = 0 (nullable) from its single-block final launch: the trainer's
+ * non-finite flag is reset there each step, before the check after backward (no fill launch). */
+int msu_dynloss_fwd3(int dtype, const void* logits, const float* target, int B, long N,
+                     float alpha, float beta, float mix, float* part, int nblk, float* loss, float* flag,
+                     float* coef, float* zero_out, void* stream);
 
 /* Validation metrics (scripts/validation_functions.py:37-309): per image, p = sigmoid(logit),
  * pred_bin = p > threshold (:106-107), gt = label > 0 (:108).  out [B][12] f64 = sum(p g),

@@ -54,6 +54,7 @@ SIGNATURES = {
     "msu_dynloss_fwd": (I, [I, P, P, I, L, F, F, F, P, I, P, P, P]),
     "msu_dynloss_bwd": (I, [I, P, P, P, P, P, I, L, F, F, F, P, P]),
     "msu_dynloss_fwd2": (I, [I, P, P, I, L, F, F, F, P, I, P, P, P, P]),
+    "msu_dynloss_fwd3": (I, [I, P, P, I, L, F, F, F, P, I, P, P, P, P, P]),
     "msu_dynloss_bwd2": (I, [I, P, P, P, P, P, I, L, F, F, F, P, P]),
     "msu_adamw": (I, [P, P, P, P, L, F, F, F, F, F, I, P, P, P]),
     "msu_nonfinite": (I, [P, L, P, P]),

@@ -135,7 +135,7 @@ MSU_DEV double wave_sum_d(double v) {
 __global__ void __launch_bounds__(512) dynloss_final_kernel(const float* part, int B, int nblk, long N,
                                                             float alpha, float beta, float mix,
                                                             float smooth, float* loss, float* flag,
-                                                            float* coef) {
+                                                            float* coef, float* zero_out) {
   __shared__ int binarise;
   __shared__ double sums[64][5];  // B <= 64
   __shared__ float wmax[8];
@@ -182,6 +182,7 @@ __global__ void __launch_bounds__(512) dynloss_final_kernel(const float* part, i
     }
     loss[0] = (float)(total / B);
     flag[0] = (float)binarise;
+    if (zero_out) zero_out[0] = 0.f;  // the trainer's non-finite flag, reset for this step
   }
 }
 
@@ -417,17 +418,25 @@ int msu_dynloss_nblk(long N) {
   return (int)(nb < 1 ? 1 : nb);
 }
 
-// loss[0] = loss value, flag[0] = binarised flag; coef [B*4]; part [B*nblk*12]
-int msu_dynloss_fwd2(int dtype, const void* logits, const float* target, int B, long N,
+// loss[0] = loss value, flag[0] = binarised flag; coef [B*4]; part [B*nblk*12]; zero_out (nullable)
+// is set to 0 by the same single-block launch
+int msu_dynloss_fwd3(int dtype, const void* logits, const float* target, int B, long N,
                      float alpha, float beta, float mix, float* part, int nblk, float* loss, float* flag,
-                     float* coef, void* stream) {
+                     float* coef, float* zero_out, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   MSU_DISPATCH(dtype, T, hipLaunchKernelGGL(dynloss_partial_kernel<T>, dim3(nblk, B), dim3(256), 0, st,
                                             (const T*)logits, target, N, nblk, part));
   if (B > 64) return -2;
   hipLaunchKernelGGL(dynloss_final_kernel, dim3(1), dim3(512), 0, st, part, B, nblk, N, alpha, beta,
-                     mix, 1e-6f, loss, flag, coef);
+                     mix, 1e-6f, loss, flag, coef, zero_out);
   return MSU_CHECK_LAUNCH();
+}
+
+int msu_dynloss_fwd2(int dtype, const void* logits, const float* target, int B, long N,
+                     float alpha, float beta, float mix, float* part, int nblk, float* loss, float* flag,
+                     float* coef, void* stream) {
+  return msu_dynloss_fwd3(dtype, logits, target, B, N, alpha, beta, mix, part, nblk, loss, flag, coef, nullptr,
+                          stream);
 }
 
 // loss[0] = loss value, loss[1] = binarised flag

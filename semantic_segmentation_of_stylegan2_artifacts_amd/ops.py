@@ -1947,6 +1947,23 @@ def patchify(img, patch, dtype):
 
 
 # ----------------------------------------------------------------------------- loss
+# A one-float f32 flag the loss forward zeroes every step (the trainer's non-finite flag: the
+# check after backward then only sets it, and no fill launch resets it).  None: nothing.
+_step_flag = [None, False]  # [flag, reset by a loss launch since it was registered]
+
+
+def set_step_flag(flag):
+    """Register (or clear, None) the trainer's non-finite flag for the DynamicLoss forward to
+    reset each step."""
+    _step_flag[0] = flag
+    _step_flag[1] = False
+
+
+def step_flag_reset():
+    """Whether a DynamicLoss launch reset the registered flag since it was registered."""
+    return _step_flag[1]
+
+
 def _dynloss_impl(logits, target, alpha, beta, mix):
     _need_cuda(logits, target)
     logits = logits.contiguous()
@@ -1960,8 +1977,11 @@ def _dynloss_impl(logits, target, alpha, beta, mix):
     # copy); coef [4B] plus the binarised flag in its last float
     out = torch.empty((), device=logits.device, dtype=torch.float32)
     coef = torch.empty(B * 4 + 1, device=logits.device, dtype=torch.float32)
-    _lib.call("msu_dynloss_fwd2", _dt(logits), _p(logits), _p(target), B, N, alpha, beta, mix,
-              _p(part), nblk, _p(out), coef.data_ptr() + 16 * B, _p(coef), _s(logits))
+    zero = _step_flag[0] if _step_flag[0] is not None and _step_flag[0].device == logits.device else None
+    if zero is not None:
+        _step_flag[1] = True
+    _lib.call("msu_dynloss_fwd3", _dt(logits), _p(logits), _p(target), B, N, alpha, beta, mix,
+              _p(part), nblk, _p(out), coef.data_ptr() + 16 * B, _p(coef), _p(zero), _s(logits))
     return out, coef
 
 

@@ -545,7 +545,14 @@ class Trainer:
         ops.set_grad_ready_callback(self.reducer._hook if self.reducer is not None else None)
         if self.reducer is not None and torch.device(self.device).type == "cuda":
             self.reducer.main_stream = torch.cuda.current_stream(self.device)
-        loss = self.forward_loss(images, labels)
+        # the DynamicLoss forward (msu_dynloss_fwd3) zeroes the non-finite flag for this step; a
+        # loss_fn swapped for something else leaves it to the fill below
+        ops.set_step_flag(self.found_inf)
+        try:
+            loss = self.forward_loss(images, labels)
+            self._flag_reset_by_loss = ops.step_flag_reset()
+        finally:
+            ops.set_step_flag(None)
         loss.backward(self._one)  # a persistent seed: no ones_like fill per step
         if self.reducer is not None:
             self.reducer.finish()
@@ -564,7 +571,8 @@ class Trainer:
             # after the all-reduce: an inf on any rank reaches every rank's sum, so all ranks
             # skip together (an f16-wire overflow included: it must never reach AdamW)
             found = self.found_inf
-            found.zero_()
+            if not self._flag_reset_by_loss:
+                found.zero_()
             ops.nonfinite_(self.groups[0].grad, found, self.groups[1].grad)
             if wire_scaled:
                 self.reducer.update_scale(found)

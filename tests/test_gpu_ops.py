@@ -558,6 +558,32 @@ def test_dynamic_loss_golden(golden_dir):
         _close(x.grad, torch.from_numpy(z[f"{name}.grad"]), 1e-4, 1e-9, name)
 
 
+def test_dynamic_loss_resets_the_registered_step_flag():
+    """ops.set_step_flag: the DynamicLoss forward's final launch zeroes the registered flag (the
+    trainer's non-finite flag) and reports it; the loss value is unchanged; unregistered: the flag
+    is left alone."""
+    import cases
+    from semantic_segmentation_of_stylegan2_artifacts_amd import ops
+    from semantic_segmentation_of_stylegan2_artifacts_amd.loss import DynamicLoss
+    logits, target, kw = cases.loss_cases()["mixed3d"]
+    lossf = DynamicLoss(alpha=kw["alpha"], beta=kw["beta"], tversky_bce_mix=kw["mix"])
+    x, t = logits.to(DEV), target.to(DEV)
+    ref = lossf(x, t).item()
+    flag = torch.ones(1, device=DEV)
+    ops.set_step_flag(flag)
+    try:
+        assert not ops.step_flag_reset()
+        out = lossf(x, t).item()
+        assert ops.step_flag_reset()
+    finally:
+        ops.set_step_flag(None)
+    assert out == ref
+    assert flag.item() == 0.0
+    flag.fill_(1.0)
+    lossf(x, t)
+    assert flag.item() == 1.0
+
+
 @pytest.mark.parametrize("low", LOW)
 def test_dynamic_loss_bf16_logits(low):
     from semantic_segmentation_of_stylegan2_artifacts_amd.loss import DynamicLoss

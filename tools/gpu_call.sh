@@ -27,6 +27,7 @@ for s in "$@"; do
     linbwd) step linbwd 600 $PYT -m gpu $R/tests/test_gpu_linbwd.py $R/tests/test_gpu_ln_side.py $R/tests/test_gpu_handoff.py ;;
     aten) step aten 600 $PYT -m gpu $R/tests/test_gpu_ops.py -k 'conv_wgrad or conv_weight or refine_conv' $R/tests/test_gpu_ln_side.py $R/tests/test_gpu_trainer.py $R/tests/test_gpu_mlp_infer.py ;;
     trainer) step trainer 900 $PYT -m gpu $R/tests/test_gpu_trainer.py $R/tests/test_gpu_graph.py $R/tests/test_gpu_rccl.py $R/tests/test_gpu_baseline_shapes.py $R/tests/test_gpu_step_parity.py ;;
+    flag) step flag 900 $PYT -m gpu $R/tests/test_gpu_trainer.py $R/tests/test_gpu_graph.py $R/tests/test_gpu_ops.py -k 'dynamic_loss or nonfinite or trainer or graph or adamw' ;;
     parity) step parity 900 $PYT -s -m gpu $R/tests/test_gpu_step_parity.py ;;
     nt_tests) step nt_tests 600 $PYT -m gpu $R/tests/test_gpu_nt_gemm.py $R/tests/test_routing.py ;;
     nt_ab) step nt_ab 300 python -u $R/tools/nt_ab.py 3 20 ;;
